@@ -1,0 +1,92 @@
+/*
+ * ppo_ext.h — libppo exports beyond the reference API (additive only).
+ *
+ * None of these exist in cube1324/ppo.c; they expose what the MI355X build
+ * adds: device selection and error reporting (SURVEY §8b "Errors"), the
+ * device-resident PPO update over an already-filled buffer (the hot path of
+ * reference ppo.cu:479-539 without the host rollout), the batched sampler,
+ * the env-sharded data-parallel communicator (RCCL over xGMI),
+ * a seeded synthetic rollout generator and kernel timing.
+ */
+#ifndef PPO_EXT_H
+#define PPO_EXT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* PPO / GaussianPolicy objects are passed as void* so this header stands alone. */
+
+/* ---------------- device & errors ---------------- */
+int         ppo_device_count(void);              /* HIP devices visible (0 without a GPU) */
+int         ppo_set_device(int device);          /* 0 on success */
+const char* ppo_last_error(void);                /* first HIP/RCCL error recorded, "" if none */
+void        ppo_synchronize(void);               /* drain libppo's stream */
+const char* ppo_build_info(void);                /* offload arch, compiler, kernel list */
+/* sizeof of the API structs, for FFI layout checks: Layer, NeuralNetwork,
+ * GaussianPolicy, TrajectoryBuffer, Adam, PPO, Env (no GPU needed) */
+int         ppo_struct_sizes(long* out, int n);
+
+/* raw device memory helpers (tests, bench) */
+void* ppo_dev_alloc(size_t bytes);
+void  ppo_dev_free(void* p);
+void  ppo_h2d(void* dst, const void* src, size_t bytes);
+void  ppo_d2h(void* dst, const void* src, size_t bytes);
+void  ppo_d2d(void* dst, const void* src, size_t bytes);
+void  ppo_dev_memset(void* dst, int value, size_t bytes);
+
+/* ---------------- data parallel (RCCL) ---------------- */
+int  ppo_comm_unique_id(unsigned char* out, int cap);   /* returns id size (128) */
+int  ppo_comm_init(int rank, int world, const unsigned char* id);  /* 0 on success */
+int  ppo_comm_rank(void);
+int  ppo_comm_world(void);
+void ppo_comm_finalize(void);
+/* sum-all-reduce of n floats in place on libppo's stream (no-op at world 1) */
+void ppo_comm_allreduce_f32(float* d_buf, long n);
+
+/* ---------------- the PPO update ---------------- */
+enum { PPO_SHUFFLE_HOST_RAND = 0,   /* reference shuffle_buffer: swap(i, rand()%N), host rand() */
+       PPO_SHUFFLE_DEVICE   = 1 };  /* device Feistel bijection, seeded, no host work */
+
+/* One PPO update over the device-resident buffer (limit = full ? capacity : idx):
+ * compute_gae_cuda, then n_epochs_value value epochs and n_epochs_policy policy
+ * epochs of ⌊limit/batch_size⌋ minibatches (reference ppo.cu:487-533).  With
+ * ppo_comm_world() > 1 every rank holds its own env shard; gradients are
+ * all-reduced (mean over the global minibatch) and advantage statistics are
+ * global.  Asynchronous: nothing is read back to the host. */
+void ppo_update(void* ppo, float gamma, int batch_size, int n_epochs_policy, int n_epochs_value,
+                int shuffle_mode, unsigned long long seed);
+
+/* stats accumulated by ppo_update since the last reset (synchronises):
+ * out[0]=Σ value loss, out[1]=#value steps, out[2]=Σ policy loss,
+ * out[3]=#policy steps, out[4]=entropy, out[5]=advantage mean, out[6]=advantage std */
+void ppo_read_stats(void* ppo, double* out, int n);
+void ppo_reset_stats(void* ppo);
+
+/* Batched policy sample on device: a = μ(s) + σ·ε, ε ~ N(0,1) (counter-based
+ * Philox + Box–Muller), log_prob per row.  d_* are device pointers. */
+void ppo_sample_action_device(void* policy, float* d_state, float* d_action, float* d_log_prob, int m,
+                              unsigned long long seed, unsigned long long offset);
+
+/* Seeded synthetic rollout written straight into the device buffer
+ * (SURVEY §8d): n_envs env-major segments of `horizon` steps, obs ~ U(−1,1),
+ * actions sampled from the current policy, rewards 0.1·N(0,1),
+ * terminated ~ Bernoulli(p_terminate), truncated at each segment end. */
+void ppo_fill_synthetic(void* ppo, int n_envs, int horizon, unsigned long long seed, float p_terminate);
+
+/* ---------------- kernel timing ---------------- */
+enum { PPO_K_GEMM = 0, PPO_K_GAE = 1, PPO_K_ADAM = 2, PPO_K_GATHER = 3, PPO_K_HEAD = 4,
+       PPO_K_COMM = 5, PPO_K_OTHER = 6, PPO_K_COUNT = 7 };
+void ppo_prof_enable(int on);      /* record HIP events around every launch on libppo's stream */
+void ppo_prof_reset(void);
+/* per class: out_ms[k] = Σ kernel time (ms), out_work[k] = Σ algorithmic FLOPs (GEMM) or bytes,
+ * out_launches[k] = launches.  Synchronises. */
+void ppo_prof_read(double* out_ms, double* out_work, long* out_launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PPO_EXT_H */

@@ -1,0 +1,124 @@
+// adam.hip — Adam as one streaming pass over a flat parameter span (HBM-bound, 28 B/param).
+//
+// Reference: adam_update (adam.cu:53-74) and adam_update_kernel (adam.cu:138-169, K10), which
+// finds each element's layer by a linear search over prefix lengths through a device float**.
+// libppo networks keep W and b of every layer in one contiguous buffer, so the update is a
+// single float4-vectorised kernel; a multi-tensor variant covers arbitrary tensor lists.
+//
+// Arithmetic is the reference's, operation for operation (compiled without FMA contraction):
+//   m = β1·m + (1−β1)·g;  v = β2·v + (1−β2)·g²;
+//   denom = (float)(sqrtf(v/bc2) + 1e-8)   (double add, as in C);   p −= step·m/denom
+// so that, given identical gradients, parameters match the oracle bit for bit.
+#include "dev.h"
+
+namespace {
+
+constexpr int TPB = 256;
+
+__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, float step, float b1, float b2,
+                                          float bc2, float scale) {
+    g = g * scale;
+    m = b1 * m + (1 - b1) * g;
+    v = b2 * v + (1 - b2) * (g * g);
+    const float denom = (float)((double)sqrtf(v / bc2) + 1e-8);
+    p -= step * m / denom;
+}
+
+__global__ void adam_flat_vec_kernel(float4* __restrict__ p, const float4* __restrict__ g, float4* __restrict__ m,
+                                     float4* __restrict__ v, long n4, float step, float b1, float b2, float bc2,
+                                     float scale) {
+    for (long i = blockIdx.x * (long)TPB + threadIdx.x; i < n4; i += (long)gridDim.x * TPB) {
+        float4 pp = p[i], gg = g[i], mm = m[i], vv = v[i];
+        adam_elem(pp.x, gg.x, mm.x, vv.x, step, b1, b2, bc2, scale);
+        adam_elem(pp.y, gg.y, mm.y, vv.y, step, b1, b2, bc2, scale);
+        adam_elem(pp.z, gg.z, mm.z, vv.z, step, b1, b2, bc2, scale);
+        adam_elem(pp.w, gg.w, mm.w, vv.w, step, b1, b2, bc2, scale);
+        p[i] = pp; m[i] = mm; v[i] = vv;
+    }
+}
+
+__global__ void adam_flat_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                                 float* __restrict__ v, long n, float step, float b1, float b2, float bc2,
+                                 float scale) {
+    for (long i = blockIdx.x * (long)TPB + threadIdx.x; i < n; i += (long)gridDim.x * TPB) {
+        float pp = p[i], mm = m[i], vv = v[i];
+        adam_elem(pp, g[i], mm, vv, step, b1, b2, bc2, scale);
+        p[i] = pp; m[i] = mm; v[i] = vv;
+    }
+}
+
+constexpr int MAXT = 24;
+struct TensorTable {
+    float* p[MAXT];
+    const float* g[MAXT];
+    long start[MAXT + 1];        // prefix offsets into the flat m / v
+    int count;
+};
+
+__global__ void adam_multi_kernel(TensorTable t, float* __restrict__ m, float* __restrict__ v, float step, float b1,
+                                  float b2, float bc2, float scale) {
+    const long total = t.start[t.count];
+    for (long i = blockIdx.x * (long)TPB + threadIdx.x; i < total; i += (long)gridDim.x * TPB) {
+        int k = 0;
+        while (i >= t.start[k + 1]) ++k;           // ≤ 24 tensors, uniform-ish
+        const long j = i - t.start[k];
+        float pp = t.p[k][j], mm = m[i], vv = v[i];
+        adam_elem(pp, t.g[k][j], mm, vv, step, b1, b2, bc2, scale);
+        t.p[k][j] = pp; m[i] = mm; v[i] = vv;
+    }
+}
+
+int grid_for(long n) {
+    long g = (n + TPB - 1) / TPB;
+    if (g < 1) g = 1;
+    if (g > 2048) g = 2048;
+    return (int)g;
+}
+
+}  // namespace
+
+extern "C" {
+
+void phip_adam_flat(float* p, const float* g, float* m, float* v, long n, float lr, float beta1, float beta2,
+                    float bias_correction1, float bias_correction2, float grad_scale) {
+    if (n <= 0) return;
+    const float step = lr / bias_correction1;
+    ppo::ProfScope ps(PPO_K_ADAM, 28.0 * n);
+    const bool vec = n % 4 == 0 && (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15u) == 0;
+    if (vec) {
+        hipLaunchKernelGGL(adam_flat_vec_kernel, dim3(grid_for(n / 4)), dim3(TPB), 0, ppo::stream(), (float4*)p,
+                           (const float4*)g, (float4*)m, (float4*)v, n / 4, step, beta1, beta2, bias_correction2,
+                           grad_scale);
+    } else {
+        hipLaunchKernelGGL(adam_flat_kernel, dim3(grid_for(n)), dim3(TPB), 0, ppo::stream(), p, g, m, v, n, step,
+                           beta1, beta2, bias_correction2, grad_scale);
+    }
+    PPO_LAUNCH_CHECK();
+}
+
+void phip_adam_multi(float* const* params, float* const* grads, const int* lengths, int num_tensors, float* m,
+                     float* v, float lr, float beta1, float beta2, float bias_correction1, float bias_correction2,
+                     float grad_scale) {
+    const float step = lr / bias_correction1;
+    long base = 0;
+    for (int t0 = 0; t0 < num_tensors; t0 += MAXT) {
+        TensorTable t{};
+        t.count = num_tensors - t0 < MAXT ? num_tensors - t0 : MAXT;
+        t.start[0] = 0;
+        for (int k = 0; k < t.count; ++k) {
+            t.p[k] = params[t0 + k];
+            t.g[k] = grads[t0 + k];
+            t.start[k + 1] = t.start[k] + lengths[t0 + k];
+        }
+        const long total = t.start[t.count];
+        if (total > 0) {
+            ppo::ProfScope ps(PPO_K_ADAM, 28.0 * total);
+            hipLaunchKernelGGL(adam_multi_kernel, dim3(grid_for(total)), dim3(TPB), 0, ppo::stream(), t, m + base,
+                               v + base, step, beta1, beta2, bias_correction2, grad_scale);
+            PPO_LAUNCH_CHECK();
+        }
+        base += total;
+    }
+}
+
+}  // extern "C"

@@ -1,0 +1,103 @@
+// buffer.hip — minibatch gather from the HBM-resident trajectory buffer.
+//
+// Reference: get_batch_kernel (trajectory_buffer.cu:168-200, K18): one thread per sample looping
+// over state_size — uncoalesced.  Here one wave owns one minibatch row, so every row copy is a
+// contiguous, coalesced read of state (S floats) and action (A floats).
+//
+// Row index of minibatch slot i:  list = (offset + i) mod limit, then either
+//   perm[list]                            — a permutation in HBM (host rand() shuffle, the
+//                                           reference's shuffle_buffer semantics), or
+//   feistel(list)                         — libppo's device shuffle: a 4-round Feistel
+//                                           bijection on 2^(2h) ≥ limit, cycle-walked into
+//                                           [0, limit); no storage, no host work.  Restated
+//                                           bit-exactly in oracle/ref_cpu.c (ref_feistel_index).
+#include "dev.h"
+
+namespace {
+
+constexpr int TPB = 256;
+
+struct Feistel { uint32_t k[4]; uint32_t half, mask, n; };
+
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+    return x;
+}
+
+__device__ __forceinline__ uint32_t feistel_index(uint32_t i, const Feistel& f) {
+    uint32_t x = i;
+    do {
+        uint32_t L = x >> f.half, R = x & f.mask;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t nl = R;
+            R = L ^ (mix32(R ^ f.k[r]) & f.mask);
+            L = nl;
+        }
+        x = (L << f.half) | R;
+    } while (x >= f.n);
+    return x;
+}
+
+__global__ void gather_kernel(const int* __restrict__ perm, Feistel f, int offset, int limit, int batch, int S,
+                              int A, const float* __restrict__ state, const float* __restrict__ action,
+                              const float* __restrict__ logprob, const float* __restrict__ advantage,
+                              const float* __restrict__ adv_target, float* __restrict__ states,
+                              float* __restrict__ actions, float* __restrict__ logprobs, float* __restrict__ advs,
+                              float* __restrict__ adv_targets) {
+    const int lane = threadIdx.x & 63;
+    const int waves = gridDim.x * (TPB / 64);
+    for (int i = blockIdx.x * (TPB / 64) + (threadIdx.x >> 6); i < batch; i += waves) {
+        const int list = (int)(((long)offset + i) % limit);
+        const int src = perm ? perm[list] : (int)feistel_index((uint32_t)list, f);
+        if (states) {
+            const float* sp = state + (long)src * S;
+            float* dp = states + (long)i * S;
+            for (int c = lane; c < S; c += 64) dp[c] = sp[c];
+        }
+        if (actions) {
+            const float* sp = action + (long)src * A;
+            float* dp = actions + (long)i * A;
+            for (int c = lane; c < A; c += 64) dp[c] = sp[c];
+        }
+        if (lane == 0) {
+            if (logprobs) logprobs[i] = logprob[src];
+            if (advs) advs[i] = advantage[src];
+            if (adv_targets) adv_targets[i] = adv_target[src];
+        }
+    }
+}
+
+uint64_t splitmix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+}  // namespace
+
+extern "C" {
+
+void phip_gather(const int* perm, uint64_t key, int offset, int limit, int batch, int S, int A,
+                 const float* state, const float* action, const float* logprob, const float* advantage,
+                 const float* adv_target, float* states, float* actions, float* logprobs, float* advs,
+                 float* adv_targets) {
+    if (batch <= 0) return;
+    PPO_REQUIRE(limit > 0, "phip_gather: empty buffer");
+    Feistel f{};
+    int bits = 2;
+    while ((1ULL << bits) < (unsigned long long)limit) bits++;
+    f.half = (uint32_t)((bits + 1) / 2);
+    f.mask = (1u << f.half) - 1u;
+    f.n = (uint32_t)limit;
+    for (int r = 0; r < 4; ++r) f.k[r] = (uint32_t)splitmix64(key + (uint64_t)r);
+    int grid = ppo_divup(batch, TPB / 64);
+    if (grid > 8192) grid = 8192;
+    ppo::ProfScope ps(PPO_K_GATHER, 8.0 * batch * (S + A + 3));
+    hipLaunchKernelGGL(gather_kernel, dim3(grid), dim3(TPB), 0, ppo::stream(), perm, f, offset, limit, batch, S, A,
+                       state, action, logprob, advantage, adv_target, states, actions, logprobs, advs, adv_targets);
+    PPO_LAUNCH_CHECK();
+}
+
+}  // extern "C"

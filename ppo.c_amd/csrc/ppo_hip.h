@@ -1,0 +1,115 @@
+/*
+ * ppo_hip.h — the thin C ABI between libppo's plain-C host code (ppo.c_amd/host)
+ * and its hand-written gfx950 HIP kernels (ppo.c_amd/csrc).
+ *
+ * All pointers named d_* / device arrays are HBM pointers; every launch goes to
+ * libppo's single stream and is asynchronous unless stated.  Shapes follow the
+ * reference (row-major, W is [out, in]).  No function here allocates per call.
+ */
+#ifndef PPO_HIP_H
+#define PPO_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------- runtime / memory ---------------- */
+void  phip_init(void);                     /* select device, create stream; abort without a GPU */
+void* phip_malloc(size_t bytes);           /* zero-filled, 256-B aligned */
+void  phip_free(void* p);
+void  phip_h2d(void* dst, const void* src, size_t bytes);   /* completes before return */
+void  phip_d2h(void* dst, const void* src, size_t bytes);   /* completes before return */
+void  phip_d2d(void* dst, const void* src, size_t bytes);   /* async */
+void  phip_memset(void* dst, int value, size_t bytes);      /* async */
+void  phip_sync(void);
+void  phip_record_error(const char* msg);
+
+/* ---------------- dense layers (gemm.hip) ---------------- */
+/* y[m,l] = x[m,n]·W[l,n]ᵀ + b[l], optional ReLU (mat_mul.cu:132-163 + K1/K5 fused) */
+void phip_linear_fwd(float* y, const float* x, const float* W, const float* b, int m, int n, int l, int relu);
+/* gx[m,n] = g[m,l]·W[l,n]; if mask: gx = (mask > 0) ? gx : 0 (K3 + K6 fused) */
+void phip_linear_bwd_x(float* gx, const float* g, const float* W, const float* mask, int m, int n, int l);
+/* gW[l,n] = g[m,l]ᵀ·x[m,n] and gb[l] = Σ_m g[m,l] (K4 + K7 fused); overwrites */
+void phip_linear_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, int n, int l);
+
+/* ---------------- element-wise / heads (kernels.hip) ---------------- */
+void phip_relu(float* x, long count);
+void phip_relu_bwd(const float* y, float* g, long count);
+/* y += x (host-pointer API: the reference's CPU backward accumulates, mat_mul.cu:67,79) */
+void phip_axpy(float* y, const float* x, long count);
+/* d_loss[0] = Σ(t−y)²/count (written), d_loss_accum[0] += same (if non-NULL);
+ * grad = 2(y−t)/count (if non-NULL).  loss.cu:25-83 fused, no host sync. */
+void phip_mse(const float* y, const float* t, long count, float* grad, float* d_loss, float* d_loss_accum);
+void phip_log_prob(const float* mu, const float* log_std, const float* action, float* out, int m, int A);
+void phip_log_prob_bwd(const float* mu, const float* log_std, const float* action, const float* grad_in,
+                       float* grad_mu, float* grad_log_std, int m, int A);
+/* d_out[0] = A·½(1+log 2π) + Σ log_std */
+void phip_entropy(const float* log_std, int A, float* d_out);
+/* clipped surrogate (ppo.cu:82-107): grad_lp[i], d_loss[0] = loss incl. −c·H (H from d_entropy) */
+void phip_policy_loss(const float* adv, const float* lp, const float* old_lp, float* grad_lp, int m,
+                      float epsilon, float ent_coeff, const float* d_entropy, float* d_loss, float* d_loss_accum);
+/* fused policy head for the update: log-prob, ratio/clip, grad_lp, grad_mu, grad_log_std
+ * (+ −ent_coeff, ppo.cu:436-438); loss accumulated into d_loss_accum. */
+void phip_policy_head(const float* mu, const float* log_std, const float* action, const float* adv,
+                      const float* old_lp, int m, int A, float epsilon, float ent_coeff,
+                      float* grad_mu, float* grad_log_std, float* d_loss_accum);
+
+/* ---------------- GAE + normalisation (gae.hip) ---------------- */
+/* advantages and targets by an exact segmented reverse scan; d_welford[0..2] =
+ * (n, mean, M2) in double for this shard.  Then normalise with the (global)
+ * statistics held in d_welford. */
+void phip_gae_scan(const float* v, const float* v_next, const float* reward, const uint8_t* term,
+                   const uint8_t* trunc, int n, float gamma, float lambda, float* adv, float* adv_target,
+                   double* d_welford);
+/* d_welford_all holds `world` triples; combine them into d_welford (3 doubles) */
+void phip_welford_combine(const double* d_welford_all, int world, double* d_welford);
+/* adv = (adv − mean)/(σ_pop + 1e-8); d_stats_out (optional) = {mean, std} as float */
+void phip_normalize(float* adv, int n, const double* d_welford, float* d_stats_out);
+
+/* ---------------- buffer (buffer.hip) ---------------- */
+/* minibatch gather: row i ← perm[(offset+i) % limit] (perm != NULL) or
+ * feistel((offset+i) % limit, limit, key) (perm == NULL).  Any dst may be NULL. */
+void phip_gather(const int* perm, uint64_t key, int offset, int limit, int batch, int S, int A,
+                 const float* state, const float* action, const float* logprob,
+                 const float* advantage, const float* adv_target,
+                 float* states, float* actions, float* logprobs, float* advs, float* adv_targets);
+
+/* ---------------- Adam (adam.hip) ---------------- */
+void phip_adam_flat(float* p, const float* g, float* m, float* v, long n, float lr, float beta1,
+                    float beta2, float bias_correction1, float bias_correction2, float grad_scale);
+/* multi-tensor: ptrs/lengths are HOST arrays describing device tensors; m/v are flat */
+void phip_adam_multi(float* const* params, float* const* grads, const int* lengths, int num_tensors,
+                     float* m, float* v, float lr, float beta1, float beta2,
+                     float bias_correction1, float bias_correction2, float grad_scale);
+
+/* ---------------- sampling / synthetic data (sample.hip) ---------------- */
+void phip_sample(const float* mu, const float* log_std, float* action, float* logprob, int m, int A,
+                 uint64_t seed, uint64_t offset);
+/* same with caller-supplied noise ε[m·A] (host rand() Box–Muller in the reference API path) */
+void phip_sample_noise(const float* mu, const float* log_std, const float* noise, float* action, float* logprob,
+                       int m, int A);
+void phip_fill_uniform(float* p, long n, uint64_t seed, float lo, float hi);
+void phip_fill_normal(float* p, long n, uint64_t seed, float scale);
+void phip_fill_rollout_flags(uint8_t* term, uint8_t* trunc, int n_envs, int horizon, float p_term, uint64_t seed);
+/* next_state[t] = state[t+1] inside an env segment when not terminated (else fresh U(−1,1)) */
+void phip_link_next_state(float* next_state, const float* state, const uint8_t* term, int n_envs,
+                          int horizon, int S, uint64_t seed);
+
+/* ---------------- data parallel (comm.hip, RCCL) ---------------- */
+int  phip_comm_world(void);
+int  phip_comm_rank(void);
+void phip_allreduce_sum_f32(float* d_buf, long n);
+void phip_allgather_f64(const double* d_send, double* d_recv, long n_per_rank);
+
+/* ---------------- profiling ---------------- */
+/* host C wrappers bracket launches: slot = phip_prof_begin(cls, work); ...; phip_prof_end(slot) */
+int  phip_prof_begin(int cls, double work);
+void phip_prof_end(int slot);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PPO_HIP_H */

@@ -1,0 +1,214 @@
+// runtime.hip — libppo device runtime: device/stream ownership, HBM allocation,
+// copies, error recording and per-launch event timing.
+//
+// One process drives one MI355X (data parallelism is one process per GPU,
+// SURVEY §8e).  All work is issued on a single non-blocking stream so the host
+// orchestration never blocks except where the reference API returns a value
+// that lives on the device (e.g. mean_squared_error_cuda).
+#include "dev.h"
+#include "../../include/ppo_ext.h"
+
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+namespace ppo {
+
+static int          g_device = -1;
+static hipStream_t  g_stream = nullptr;
+static char         g_err[512] = "";
+static std::once_flag g_init_once;
+
+void fail(const char* msg, const char* file, int line) {
+    if (!g_err[0]) snprintf(g_err, sizeof(g_err), "%s (%s:%d)", msg, file, line);
+    fprintf(stderr, "libppo: FATAL: %s (%s:%d)\n", msg, file, line);
+    fflush(stderr);
+    abort();
+}
+
+void check(hipError_t e, const char* what, const char* file, int line) {
+    if (e == hipSuccess) return;
+    char buf[400];
+    snprintf(buf, sizeof(buf), "%s failed: %s", what, hipGetErrorString(e));
+    fail(buf, file, line);
+}
+
+static void init_impl() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+        fail("no HIP device visible: libppo runs only on an AMD Instinct MI355X (gfx950)", __FILE__, __LINE__);
+    if (g_device < 0) {
+        const char* env = getenv("LOCAL_RANK");
+        g_device = env ? atoi(env) % n : 0;
+    }
+    PPO_CHECK(hipSetDevice(g_device));
+    hipDeviceProp_t prop;
+    PPO_CHECK(hipGetDeviceProperties(&prop, g_device));
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        char buf[256];
+        snprintf(buf, sizeof(buf), "device %d is %s; libppo is built for gfx950 (MI355X) only", g_device,
+                 prop.gcnArchName);
+        fail(buf, __FILE__, __LINE__);
+    }
+    PPO_CHECK(hipStreamCreateWithFlags(&g_stream, hipStreamNonBlocking));
+}
+
+void ensure_device() { std::call_once(g_init_once, init_impl); }
+
+hipStream_t stream() {
+    ensure_device();
+    return g_stream;
+}
+
+// ---------------- per-launch event timing ----------------
+struct ProfSlot { hipEvent_t a, b; int k; double work; };
+static bool                  g_prof_on = false;
+static std::vector<ProfSlot> g_slots;       // recorded, not yet harvested
+static std::vector<hipEvent_t> g_free_events;
+static double g_ms[PPO_K_COUNT], g_work[PPO_K_COUNT];
+static long   g_launches[PPO_K_COUNT];
+
+static hipEvent_t take_event() {
+    if (!g_free_events.empty()) { hipEvent_t e = g_free_events.back(); g_free_events.pop_back(); return e; }
+    hipEvent_t e;
+    PPO_CHECK(hipEventCreate(&e));
+    return e;
+}
+
+static void harvest() {
+    if (g_slots.empty()) return;
+    PPO_CHECK(hipStreamSynchronize(g_stream));
+    for (auto& s : g_slots) {
+        float ms = 0.f;
+        PPO_CHECK(hipEventElapsedTime(&ms, s.a, s.b));
+        g_ms[s.k] += ms;
+        g_work[s.k] += s.work;
+        g_launches[s.k] += 1;
+        g_free_events.push_back(s.a);
+        g_free_events.push_back(s.b);
+    }
+    g_slots.clear();
+}
+
+ProfScope::ProfScope(int k_, double work_) : k(k_), work(work_), slot(-1) { slot = phip_prof_begin(k, work); }
+ProfScope::~ProfScope() { phip_prof_end(slot); }
+
+}  // namespace ppo
+
+using namespace ppo;
+
+extern "C" {
+
+int phip_prof_begin(int cls, double work) {
+    if (!g_prof_on) return -1;
+    if (g_slots.size() >= (1u << 16)) harvest();
+    ProfSlot s{take_event(), take_event(), cls, work};
+    PPO_CHECK(hipEventRecord(s.a, stream()));
+    g_slots.push_back(s);
+    return (int)g_slots.size() - 1;
+}
+
+void phip_prof_end(int slot) {
+    if (slot < 0 || !g_prof_on || slot >= (int)g_slots.size()) return;
+    PPO_CHECK(hipEventRecord(g_slots[slot].b, stream()));
+}
+
+void phip_init(void) { ensure_device(); }
+
+void* phip_malloc(size_t bytes) {
+    ensure_device();
+    void* p = nullptr;
+    if (bytes == 0) bytes = 256;
+    PPO_CHECK(hipMalloc(&p, bytes));
+    PPO_CHECK(hipMemsetAsync(p, 0, bytes, g_stream));
+    return p;
+}
+
+void phip_free(void* p) {
+    if (!p) return;
+    PPO_CHECK(hipStreamSynchronize(stream()));
+    PPO_CHECK(hipFree(p));
+}
+
+void phip_h2d(void* dst, const void* src, size_t bytes) {
+    if (!bytes) return;
+    PPO_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream()));
+    PPO_CHECK(hipStreamSynchronize(g_stream));   // the host buffer may be reused right after
+}
+
+void phip_d2h(void* dst, const void* src, size_t bytes) {
+    if (!bytes) return;
+    PPO_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, stream()));
+    PPO_CHECK(hipStreamSynchronize(g_stream));
+}
+
+void phip_d2d(void* dst, const void* src, size_t bytes) {
+    if (!bytes || dst == src) return;
+    PPO_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, stream()));
+}
+
+void phip_memset(void* dst, int value, size_t bytes) {
+    if (!bytes) return;
+    PPO_CHECK(hipMemsetAsync(dst, value, bytes, stream()));
+}
+
+void phip_sync(void) { PPO_CHECK(hipStreamSynchronize(stream())); }
+
+void phip_record_error(const char* msg) {
+    if (!g_err[0]) snprintf(g_err, sizeof(g_err), "%s", msg);
+}
+
+// ---------------- ppo_ext.h: device & errors ----------------
+int ppo_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int ppo_set_device(int device) {
+    if (g_stream) {   // already initialised: only the same device is allowed
+        return device == g_device ? 0 : -1;
+    }
+    g_device = device;
+    ensure_device();
+    return 0;
+}
+
+const char* ppo_last_error(void) { return g_err; }
+void ppo_synchronize(void) { phip_sync(); }
+
+const char* ppo_build_info(void) {
+    return "libppo: hand-written HIP for gfx950 (MI355X); fp32 MFMA v_mfma_f32_32x32x2_f32 GEMMs; "
+           "kernels: gemm{NT,NN,TN}, relu, mse, policy_head, log_prob, gae_scan, welford, normalize, "
+           "gather, adam_flat/multi, sample, synthetic fill; comm: RCCL";
+}
+
+void* ppo_dev_alloc(size_t bytes) { return phip_malloc(bytes); }
+void  ppo_dev_free(void* p) { phip_free(p); }
+void  ppo_h2d(void* dst, const void* src, size_t bytes) { phip_h2d(dst, src, bytes); }
+void  ppo_d2h(void* dst, const void* src, size_t bytes) { phip_d2h(dst, src, bytes); }
+void  ppo_d2d(void* dst, const void* src, size_t bytes) { phip_d2d(dst, src, bytes); phip_sync(); }
+void  ppo_dev_memset(void* dst, int value, size_t bytes) { phip_memset(dst, value, bytes); phip_sync(); }
+
+// ---------------- ppo_ext.h: kernel timing ----------------
+void ppo_prof_enable(int on) {
+    if (!on && g_prof_on) harvest();
+    g_prof_on = on != 0;
+}
+
+void ppo_prof_reset(void) {
+    harvest();
+    for (int k = 0; k < PPO_K_COUNT; k++) { g_ms[k] = 0; g_work[k] = 0; g_launches[k] = 0; }
+}
+
+void ppo_prof_read(double* out_ms, double* out_work, long* out_launches) {
+    harvest();
+    for (int k = 0; k < PPO_K_COUNT; k++) {
+        if (out_ms) out_ms[k] = g_ms[k];
+        if (out_work) out_work[k] = g_work[k];
+        if (out_launches) out_launches[k] = g_launches[k];
+    }
+}
+
+}  // extern "C"

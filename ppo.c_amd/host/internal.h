@@ -1,0 +1,56 @@
+/*
+ * internal.h — helpers shared by libppo's plain-C host code.
+ *
+ * The host side is orchestration only: object lifetime, the reference's
+ * libc-rand() consumption order (weight init, shuffles, rollout noise) and
+ * launch sequencing.  Every numeric operation of the PPO path runs in a HIP
+ * kernel through ppo_hip.h; host-pointer entry points of the reference API
+ * stage their operands through HBM (stage_*) and run the same kernels.
+ */
+#ifndef PPO_HOST_INTERNAL_H
+#define PPO_HOST_INTERNAL_H
+
+#include <stdbool.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../include/ppo.h"
+#include "../csrc/ppo_hip.h"
+
+void* xmalloc(size_t n);
+void* xcalloc(size_t n, size_t sz);
+void  die(const char* msg);
+
+/* grow-only device scratch slots for host-pointer (staged) entry points */
+enum { ST_A = 0, ST_B, ST_C, ST_D, ST_E, ST_F, ST_G, ST_H, ST_COUNT };
+void* stage(int slot, size_t bytes);
+float* stage_up(int slot, const float* host, size_t count);   /* h2d into slot, returns device ptr */
+
+static inline long align4(long n) { return (n + 3) & ~3L; }
+
+/* neural_network.c internals used by policy.c / ppo.c */
+NeuralNetwork* nn_create_ex(int* layer_sizes, char** activation_functions, int num_layers, long extra_floats,
+                            int init_from_rand);
+int  nn_is_relu(const NeuralNetwork* nn, int layer);
+void nn_ensure_act(NeuralNetwork* nn, int m);
+void nn_ensure_grad(NeuralNetwork* nn, int m);
+/* device forward using d_x as layer-0 input (no copy) */
+void nn_forward_dev(NeuralNetwork* nn, const float* d_x, int m);
+/* device backward from d_grad_out (no copy unless the output activation needs masking) */
+void nn_backward_dev(NeuralNetwork* nn, const float* d_grad_out, int m, int want_grad_x0);
+
+NeuralNetwork* nn_load_ex(FILE* file, long extra_floats);
+
+/* trajectory_buffer.c */
+void buffer_point_device(TrajectoryBuffer* b);
+
+/* policy.c */
+GaussianPolicy* policy_create_ex(int* layer_sizes, char** activation_functions, int num_layers, float init_std,
+                                 int init_from_rand);
+
+/* ppo.c: GAE on the device buffer with explicit output of v / v_next scratch */
+void ppo_gae_device(NeuralNetwork* V, TrajectoryBuffer* buffer, float gamma, float lambda);
+
+#endif

@@ -1,0 +1,296 @@
+/*
+ * neural_network.c — MLP objects over flat HBM parameter/gradient buffers.
+ *
+ * Reference: /root/reference/src/neural_network.cu.  Construction consumes
+ * libc rand() in the reference's order and with its initialisers
+ * (neural_network.cu:40-51) so seeded runs start from the same weights; the
+ * forward/backward passes run the fused MFMA GEMMs of csrc/gemm.hip:
+ *   forward  : y_{i+1} = act_i(y_i·W_iᵀ + b_i)                 (one kernel per layer)
+ *   backward : gW_i, gb_i = g_{i+1}ᵀ·y_i, Σ g_{i+1}             (one kernel per layer)
+ *              g_i = (g_{i+1}·W_i) ⊙ 1[y_i > 0]                (one kernel per layer, skipped
+ *                                                               for layer 0 in the update)
+ */
+#include "internal.h"
+
+#include <math.h>
+
+int nn_is_relu(const NeuralNetwork* nn, int layer) {
+    const ActivationFunction* a = nn->layers[layer].d_activation_function;
+    return a && a->activation != NULL;
+}
+
+/* neural_network.cu:40-51 restated: He-uniform hidden layers, Xavier-uniform output layer. */
+static void init_layer_from_rand(Layer* ly, int is_last) {
+    const int in = ly->input_size, out = ly->output_size;
+    float gain = is_last ? 1 : sqrtf(2.0);
+    float std = gain * sqrtf(2.0 / (in + out));
+    for (long j = 0; j < (long)in * out; j++) ly->weights[j] = (2 * (float)rand() / RAND_MAX - 1) * sqrtf(3.0) * std;
+    for (int j = 0; j < out; j++) ly->biases[j] = (2 * (float)rand() / RAND_MAX - 1) * (1. / sqrtf(in));
+}
+
+NeuralNetwork* nn_create_ex(int* layer_sizes, char** activation_functions, int num_layers, long extra_floats,
+                            int init_from_rand) {
+    if (num_layers < 2) die("create_neural_network: need at least 2 layer sizes");
+    phip_init();
+    const int L = num_layers - 1;
+    NeuralNetwork* nn = (NeuralNetwork*)xcalloc(1, sizeof(NeuralNetwork));
+    nn->num_layers = num_layers;
+    nn->layers = (Layer*)xcalloc((size_t)num_layers, sizeof(Layer));
+    nn->activation_functions = (char**)xmalloc(sizeof(char*) * (size_t)L);
+    nn->param_offset = (long*)xmalloc(sizeof(long) * (size_t)L);
+    nn->bias_offset = (long*)xmalloc(sizeof(long) * (size_t)L);
+
+    long off = 0, packed = 0;
+    for (int i = 0; i < L; i++) {
+        Layer* ly = &nn->layers[i];
+        nn->activation_functions[i] = strdup(activation_functions[i]);
+        ly->input_size = layer_sizes[i];
+        ly->output_size = layer_sizes[i + 1];
+        const long nw = (long)ly->input_size * ly->output_size;
+        nn->param_offset[i] = off;
+        off += align4(nw);
+        nn->bias_offset[i] = off;
+        off += align4(ly->output_size);
+        packed += nw + ly->output_size;
+        ly->weights = (float*)xmalloc(sizeof(float) * (size_t)nw);
+        ly->biases = (float*)xmalloc(sizeof(float) * (size_t)ly->output_size);
+        ly->grad_weights = (float*)xcalloc((size_t)nw, sizeof(float));
+        ly->grad_biases = (float*)xcalloc((size_t)ly->output_size, sizeof(float));
+        ly->activation_function = build_activation_function(activation_functions[i]);
+        ly->d_activation_function = build_activation_function_cuda(activation_functions[i]);
+        if (init_from_rand) init_layer_from_rand(ly, i == L - 1);
+    }
+    nn->layers[L].input_size = layer_sizes[L];
+    nn->output_size = layer_sizes[L];
+    nn->num_params = off;
+    nn->num_params_packed = packed;
+    nn->extra_floats = extra_floats;
+
+    const size_t bytes = sizeof(float) * (size_t)(off + align4(extra_floats));
+    nn->d_params = (float*)phip_malloc(bytes);
+    nn->d_grads = (float*)phip_malloc(bytes);
+    for (int i = 0; i < L; i++) {
+        Layer* ly = &nn->layers[i];
+        ly->d_weights = nn->d_params + nn->param_offset[i];
+        ly->d_biases = nn->d_params + nn->bias_offset[i];
+        ly->d_grad_weights = nn->d_grads + nn->param_offset[i];
+        ly->d_grad_biases = nn->d_grads + nn->bias_offset[i];
+    }
+    if (init_from_rand) nn_write_weights_to_device(nn);
+    nn->cublas_handle = NULL;
+    return nn;
+}
+
+NeuralNetwork* create_neural_network(int* layer_sizes, char** activation_functions, int num_layers) {
+    return nn_create_ex(layer_sizes, activation_functions, num_layers, 0, 1);
+}
+
+void nn_ensure_act(NeuralNetwork* nn, int m) {
+    if (m <= nn->act_cap_m) return;
+    for (int i = 0; i < nn->num_layers; i++) {
+        phip_free(nn->layers[i].d_input);
+        nn->layers[i].d_input = (float*)phip_malloc(sizeof(float) * (size_t)m * nn->layers[i].input_size);
+    }
+    nn->act_cap_m = m;
+}
+
+void nn_ensure_grad(NeuralNetwork* nn, int m) {
+    if (m <= nn->grad_cap_m) return;
+    for (int i = 0; i < nn->num_layers; i++) {
+        phip_free(nn->layers[i].d_grad_x);
+        nn->layers[i].d_grad_x = (float*)phip_malloc(sizeof(float) * (size_t)m * nn->layers[i].input_size);
+    }
+    nn->grad_cap_m = m;
+}
+
+void nn_forward_dev(NeuralNetwork* nn, const float* d_x, int m) {
+    nn_ensure_act(nn, m);
+    const int L = nn->num_layers - 1;
+    nn->d_x0 = d_x;
+    const float* in = d_x;
+    for (int i = 0; i < L; i++) {
+        Layer* ly = &nn->layers[i];
+        float* out = nn->layers[i + 1].d_input;
+        phip_linear_fwd(out, in, ly->d_weights, ly->d_biases, m, ly->input_size, ly->output_size, nn_is_relu(nn, i));
+        in = out;
+    }
+    nn->cache_m_forward = m;
+    nn->d_output = nn->layers[L].d_input;
+}
+
+void nn_backward_dev(NeuralNetwork* nn, const float* d_grad_out, int m, int want_grad_x0) {
+    nn_ensure_grad(nn, m);
+    const int L = nn->num_layers - 1;
+    const float* g = d_grad_out;
+    if (nn_is_relu(nn, L - 1)) {      /* output activation: mask a copy (rare; the reference uses "none") */
+        float* top = nn->layers[L].d_grad_x;
+        if (top != d_grad_out) phip_d2d(top, d_grad_out, sizeof(float) * (size_t)m * nn->output_size);
+        phip_relu_bwd(nn->layers[L].d_input, top, (long)m * nn->output_size);
+        g = top;
+    }
+    for (int i = L - 1; i >= 0; i--) {
+        Layer* ly = &nn->layers[i];
+        const float* x = i == 0 ? nn->d_x0 : ly->d_input;
+        phip_linear_bwd_w(ly->d_grad_weights, ly->d_grad_biases, g, x, m, ly->input_size, ly->output_size);
+        if (i > 0 || want_grad_x0) {
+            const float* mask = (i > 0 && nn_is_relu(nn, i - 1)) ? ly->d_input : NULL;
+            phip_linear_bwd_x(ly->d_grad_x, g, ly->d_weights, mask, m, ly->input_size, ly->output_size);
+        }
+        g = ly->d_grad_x;
+    }
+    nn->cache_m_backward = m;
+}
+
+/* neural_network.cu:74-105: copies the input into layers[0].d_input first. */
+void forward_propagation_cuda(NeuralNetwork* nn, float* input, int m) {
+    nn_ensure_act(nn, m);
+    phip_d2d(nn->layers[0].d_input, input, sizeof(float) * (size_t)m * nn->layers[0].input_size);
+    nn_forward_dev(nn, nn->layers[0].d_input, m);
+}
+
+/* neural_network.cu:121-161: grad_in is copied into the last layer's d_grad_x;
+ * every layer's d_grad_x (including layer 0) is produced. */
+void backward_propagation_cuda(NeuralNetwork* nn, float* grad_in, int m) {
+    nn_ensure_grad(nn, m);
+    const int L = nn->num_layers - 1;
+    phip_d2d(nn->layers[L].d_grad_x, grad_in, sizeof(float) * (size_t)m * nn->output_size);
+    nn_backward_dev(nn, nn->layers[L].d_grad_x, m, 1);
+}
+
+/* Host-pointer entry points (reference CPU path, neural_network.cu:163-231): the host
+ * weight arrays are the source of truth, so they are uploaded first; the output and
+ * gradients come back into the host mirrors. */
+void forward_propagation(NeuralNetwork* nn, float* input, int m) {
+    nn_write_weights_to_device(nn);
+    nn_ensure_act(nn, m);
+    phip_h2d(nn->layers[0].d_input, input, sizeof(float) * (size_t)m * nn->layers[0].input_size);
+    nn_forward_dev(nn, nn->layers[0].d_input, m);
+    free(nn->output);
+    nn->output = (float*)xmalloc(sizeof(float) * (size_t)m * nn->output_size);
+    phip_d2h(nn->output, nn->d_output, sizeof(float) * (size_t)m * nn->output_size);
+}
+
+void backward_propagation(NeuralNetwork* nn, float* grad_in, int m) {
+    nn_ensure_grad(nn, m);
+    const int L = nn->num_layers - 1;
+    phip_h2d(nn->layers[L].d_grad_x, grad_in, sizeof(float) * (size_t)m * nn->output_size);
+    nn_backward_dev(nn, nn->layers[L].d_grad_x, m, 0);
+    for (int i = 0; i < L; i++) {
+        Layer* ly = &nn->layers[i];
+        phip_d2h(ly->grad_weights, ly->d_grad_weights, sizeof(float) * (size_t)ly->input_size * ly->output_size);
+        phip_d2h(ly->grad_biases, ly->d_grad_biases, sizeof(float) * (size_t)ly->output_size);
+    }
+}
+
+void nn_write_weights_to_device(NeuralNetwork* nn) {
+    for (int i = 0; i < nn->num_layers - 1; i++) {
+        Layer* ly = &nn->layers[i];
+        phip_h2d(ly->d_weights, ly->weights, sizeof(float) * (size_t)ly->input_size * ly->output_size);
+        phip_h2d(ly->d_biases, ly->biases, sizeof(float) * (size_t)ly->output_size);
+    }
+}
+
+void nn_write_weights_to_host(NeuralNetwork* nn) {
+    for (int i = 0; i < nn->num_layers - 1; i++) {
+        Layer* ly = &nn->layers[i];
+        phip_d2h(ly->weights, ly->d_weights, sizeof(float) * (size_t)ly->input_size * ly->output_size);
+        phip_d2h(ly->biases, ly->d_biases, sizeof(float) * (size_t)ly->output_size);
+    }
+}
+
+void free_neural_network(NeuralNetwork* nn) {
+    if (!nn) return;
+    const int L = nn->num_layers - 1;
+    for (int i = 0; i < L; i++) {
+        Layer* ly = &nn->layers[i];
+        free(ly->weights);
+        free(ly->biases);
+        free(ly->grad_weights);
+        free(ly->grad_biases);
+        free(ly->input);
+        free(ly->activation_function);
+        free(ly->d_activation_function);
+        free(nn->activation_functions[i]);
+    }
+    for (int i = 0; i < nn->num_layers; i++) {
+        phip_free(nn->layers[i].d_input);
+        phip_free(nn->layers[i].d_grad_x);
+    }
+    phip_free(nn->d_params);
+    phip_free(nn->d_grads);
+    free(nn->activation_functions);
+    free(nn->param_offset);
+    free(nn->bias_offset);
+    free(nn->layers);
+    free(nn->output);
+    free(nn);
+}
+
+/* neural_network.cu:284-300 byte layout: num_layers, output_size, per activation
+ * (len incl. NUL, chars), per layer (in, out, W[out·in], b[out]). */
+void save_neural_network(NeuralNetwork* nn, FILE* file) {
+    fwrite(&nn->num_layers, sizeof(int), 1, file);
+    fwrite(&nn->output_size, sizeof(int), 1, file);
+    for (int i = 0; i < nn->num_layers - 1; i++) {
+        int len = (int)strlen(nn->activation_functions[i]) + 1;
+        fwrite(&len, sizeof(int), 1, file);
+        fwrite(nn->activation_functions[i], 1, (size_t)len, file);
+    }
+    for (int i = 0; i < nn->num_layers - 1; i++) {
+        Layer* ly = &nn->layers[i];
+        fwrite(&ly->input_size, sizeof(int), 1, file);
+        fwrite(&ly->output_size, sizeof(int), 1, file);
+        fwrite(ly->weights, sizeof(float), (size_t)ly->input_size * ly->output_size, file);
+        fwrite(ly->biases, sizeof(float), (size_t)ly->output_size, file);
+    }
+}
+
+static void read_exact(void* dst, size_t sz, size_t n, FILE* f) {
+    if (fread(dst, sz, n, f) != n) die("checkpoint: unexpected end of file");
+}
+
+/* neural_network.cu:303-358; extra_floats lets load_policy keep log_std beside μ's parameters */
+NeuralNetwork* nn_load_ex(FILE* file, long extra_floats) {
+    int num_layers, output_size;
+    read_exact(&num_layers, sizeof(int), 1, file);
+    read_exact(&output_size, sizeof(int), 1, file);
+    if (num_layers < 2 || num_layers > 64) die("checkpoint: bad layer count");
+    const int L = num_layers - 1;
+    char** acts = (char**)xmalloc(sizeof(char*) * (size_t)L);
+    for (int i = 0; i < L; i++) {
+        int len;
+        read_exact(&len, sizeof(int), 1, file);
+        if (len <= 0 || len > 4096) die("checkpoint: bad activation name");
+        acts[i] = (char*)xmalloc((size_t)len);
+        read_exact(acts[i], 1, (size_t)len, file);
+        acts[i][len - 1] = 0;
+    }
+    long pos = ftell(file);
+    int* sizes = (int*)xmalloc(sizeof(int) * (size_t)num_layers);
+    /* first pass: sizes */
+    for (int i = 0; i < L; i++) {
+        int in, out;
+        read_exact(&in, sizeof(int), 1, file);
+        read_exact(&out, sizeof(int), 1, file);
+        sizes[i] = in;
+        sizes[i + 1] = out;
+        fseek(file, (long)sizeof(float) * ((long)in * out + out), SEEK_CUR);
+    }
+    fseek(file, pos, SEEK_SET);
+    NeuralNetwork* nn = nn_create_ex(sizes, acts, num_layers, extra_floats, 0);
+    for (int i = 0; i < L; i++) {
+        Layer* ly = &nn->layers[i];
+        int in, out;
+        read_exact(&in, sizeof(int), 1, file);
+        read_exact(&out, sizeof(int), 1, file);
+        read_exact(ly->weights, sizeof(float), (size_t)in * out, file);
+        read_exact(ly->biases, sizeof(float), (size_t)out, file);
+    }
+    nn_write_weights_to_device(nn);
+    for (int i = 0; i < L; i++) free(acts[i]);
+    free(acts);
+    free(sizes);
+    return nn;
+}
+
+NeuralNetwork* load_neural_network(FILE* file) { return nn_load_ex(file, 0); }

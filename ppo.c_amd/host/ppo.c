@@ -1,0 +1,426 @@
+/*
+ * ppo.c — PPO orchestration (reference /root/reference/src/ppo.cu).
+ *
+ * The update (GAE → value epochs → policy epochs) is issued entirely on
+ * libppo's HIP stream: no per-minibatch allocation, no device→host reads
+ * (the reference blocks on 1–2 scalar copies per minibatch), the
+ * losses accumulate on the device.  Per value minibatch:
+ *     gather → L × fused linear(+bias+ReLU) → MSE+grad → L × bwd_W(+bias grad)
+ *     → (L−1) × bwd_x(+ReLU′) → [RCCL all-reduce] → flat Adam
+ * and per policy minibatch the same with the fused Gaussian/clipped-surrogate
+ * head (csrc/kernels.hip) in place of the MSE.
+ */
+#include "internal.h"
+
+#include <math.h>
+
+void buffer_point_device(TrajectoryBuffer* b);
+
+/* ------------------------------------------------------------------ */
+/* device workspaces                                                   */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    int cap_B, S, A;
+    float *states, *actions, *old_lp, *adv, *tgt, *gv, *gmu;
+    float* stats;                 /* [0] Σ value loss, [1] Σ policy loss */
+    long n_v, n_p;
+    uint64_t key;                 /* device-shuffle epoch key */
+    unsigned long long seed;
+    int seeded;
+} PPODev;
+
+static float* g_v = NULL;         /* V(state), V(next_state) for compute_gae_cuda */
+static float* g_vn = NULL;
+static long g_v_cap = 0;
+static double* g_welford = NULL;  /* (n, mean, M2) */
+static double* g_welford_all = NULL;
+static int g_welford_world = 0;
+static float* g_adv_stats = NULL; /* (mean, std) as used for normalisation */
+
+static uint64_t splitmix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+static void ensure_gae_ws(long n) {
+    if (!g_welford) {
+        g_welford = (double*)phip_malloc(4 * sizeof(double));
+        g_adv_stats = (float*)phip_malloc(4 * sizeof(float));
+    }
+    const int world = phip_comm_world();
+    if (world > g_welford_world) {
+        phip_free(g_welford_all);
+        g_welford_all = (double*)phip_malloc(sizeof(double) * 3 * (size_t)world);
+        g_welford_world = world;
+    }
+    if (n > g_v_cap) {
+        phip_free(g_v);
+        phip_free(g_vn);
+        g_v = (float*)phip_malloc(sizeof(float) * (size_t)n);
+        g_vn = (float*)phip_malloc(sizeof(float) * (size_t)n);
+        g_v_cap = n;
+    }
+}
+
+static PPODev* dev_ws(PPO* ppo, int B) {
+    PPODev* d = (PPODev*)ppo->dev;
+    const int S = ppo->buffer->state_size, A = ppo->buffer->action_size;
+    if (!d) {
+        d = (PPODev*)xcalloc(1, sizeof(PPODev));
+        d->stats = (float*)phip_malloc(4 * sizeof(float));
+        ppo->dev = d;
+    }
+    if (B > d->cap_B) {
+        phip_free(d->states); phip_free(d->actions); phip_free(d->old_lp); phip_free(d->adv);
+        phip_free(d->tgt); phip_free(d->gv); phip_free(d->gmu);
+        d->states = (float*)phip_malloc(sizeof(float) * (size_t)B * S);
+        d->actions = (float*)phip_malloc(sizeof(float) * (size_t)B * A);
+        d->old_lp = (float*)phip_malloc(sizeof(float) * (size_t)B);
+        d->adv = (float*)phip_malloc(sizeof(float) * (size_t)B);
+        d->tgt = (float*)phip_malloc(sizeof(float) * (size_t)B);
+        d->gv = (float*)phip_malloc(sizeof(float) * (size_t)B);
+        d->gmu = (float*)phip_malloc(sizeof(float) * (size_t)B * A);
+        d->cap_B = B;
+    }
+    d->S = S;
+    d->A = A;
+    return d;
+}
+
+static void free_dev_ws(PPO* ppo) {
+    PPODev* d = (PPODev*)ppo->dev;
+    if (!d) return;
+    phip_free(d->states); phip_free(d->actions); phip_free(d->old_lp); phip_free(d->adv);
+    phip_free(d->tgt); phip_free(d->gv); phip_free(d->gmu); phip_free(d->stats);
+    free(d);
+    ppo->dev = NULL;
+}
+
+/* ------------------------------------------------------------------ */
+/* construction (ppo.cu:6-51)                                          */
+/* ------------------------------------------------------------------ */
+PPO* create_ppo(char** activation_functions, int* layer_sizes, int num_layers, int buffer_size, float lr_policy,
+                float lr_v, float lambda, float epsilon, float ent_coeff, float init_std, bool use_cuda) {
+    PPO* ppo = (PPO*)xcalloc(1, sizeof(PPO));
+    ppo->buffer = create_trajectory_buffer(buffer_size, layer_sizes[0], layer_sizes[num_layers - 1]);
+    ppo->policy = create_gaussian_policy(layer_sizes, activation_functions, num_layers, init_std);
+    int* sizes_v = (int*)xmalloc(sizeof(int) * (size_t)num_layers);
+    memcpy(sizes_v, layer_sizes, sizeof(int) * (size_t)(num_layers - 1));
+    sizes_v[num_layers - 1] = 1;                                         /* ppo.cu:12-16 */
+    ppo->V = create_neural_network(sizes_v, activation_functions, num_layers);
+    free(sizes_v);
+    ppo->adam_policy = create_adam_from_nn_cuda(ppo->policy->mu, 0.9f, 0.999f);
+    ppo->adam_V = create_adam_from_nn_cuda(ppo->V, 0.9f, 0.999f);
+    ppo->adam_entropy = create_adam_cuda(&ppo->policy->d_log_std, &ppo->policy->d_log_std_grad,
+                                         &ppo->policy->action_size, 1, ppo->policy->action_size, 0.9f, 0.999f);
+    ppo->lambda = lambda;
+    ppo->epsilon = epsilon;
+    ppo->ent_coeff = ent_coeff;
+    ppo->lr_policy = lr_policy;
+    ppo->lr_V = lr_v;
+    ppo->use_cuda = use_cuda;
+    ppo->dev = NULL;
+    return ppo;
+}
+
+void free_ppo(PPO* ppo) {
+    if (!ppo) return;
+    free_adam_cuda(ppo->adam_policy);
+    free_adam_cuda(ppo->adam_V);
+    free_adam_cuda(ppo->adam_entropy);
+    free_trajectory_buffer(ppo->buffer, ppo->use_cuda);
+    free_gaussian_policy(ppo->policy);
+    free_neural_network(ppo->V);
+    free_dev_ws(ppo);
+    free(ppo);
+}
+
+/* ------------------------------------------------------------------ */
+/* rollout (ppo.cu:54-79) — host loop over the Env ABI, out of scope of the accelerated path */
+/* ------------------------------------------------------------------ */
+void collect_trajectories(TrajectoryBuffer* buffer, Env* env, GaussianPolicy* policy, int steps) {
+    if (buffer->on_device) buffer_to_host(buffer);
+    env->reset_env(buffer->state(buffer, buffer->idx));
+    for (int i = 0; i < steps; i++) {
+        sample_action(policy, buffer->state(buffer, buffer->idx), buffer->action(buffer, buffer->idx),
+                      buffer->logprob(buffer, buffer->idx), 1);
+        env->step_env(buffer->action(buffer, buffer->idx), buffer->next_state(buffer, buffer->idx),
+                      buffer->reward(buffer, buffer->idx), buffer->terminated(buffer, buffer->idx),
+                      buffer->truncated(buffer, buffer->idx), buffer->action_size);
+        int new_idx = (buffer->idx + 1) % buffer->capacity;
+        if (i < steps - 1) {
+            if (*buffer->truncated(buffer, buffer->idx) || *buffer->terminated(buffer, buffer->idx))
+                env->reset_env(buffer->state(buffer, new_idx));
+            else
+                memcpy(buffer->state(buffer, new_idx), buffer->next_state(buffer, buffer->idx),
+                       sizeof(float) * (size_t)buffer->state_size);
+        } else if (!*buffer->terminated(buffer, buffer->idx)) {
+            *buffer->truncated(buffer, buffer->idx) = true;
+        }
+        buffer->idx = new_idx;
+        buffer->full = buffer->full || buffer->idx == 0;
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* GAE (ppo.cu:261-369)                                                */
+/* ------------------------------------------------------------------ */
+void ppo_gae_device(NeuralNetwork* V, TrajectoryBuffer* b, float gamma, float lambda) {
+    const int n = b->full ? b->capacity : b->idx;
+    ensure_gae_ws(n);
+    if (n > 0) {
+        nn_forward_dev(V, b->next_state_p, n);
+        phip_d2d(g_vn, V->d_output, sizeof(float) * (size_t)n);
+        nn_forward_dev(V, b->state_p, n);
+        phip_d2d(g_v, V->d_output, sizeof(float) * (size_t)n);
+    }
+    phip_gae_scan(g_v, g_vn, b->reward_p, (const uint8_t*)b->terminated_p, (const uint8_t*)b->truncated_p, n, gamma,
+                  lambda, b->advantage_p, b->adv_target_p, g_welford);
+    const int world = phip_comm_world();
+    if (world > 1) {       /* global advantage statistics across env shards */
+        phip_allgather_f64(g_welford, g_welford_all, 3);
+        phip_welford_combine(g_welford_all, world, g_welford);
+    }
+    phip_normalize(b->advantage_p, n, g_welford, g_adv_stats);
+}
+
+/* device buffer (after buffer_to_device); `horizon` is unused: the scan is exact (D7) */
+void compute_gae_cuda(NeuralNetwork* V, TrajectoryBuffer* buffer, float gamma, float lambda, int horizon) {
+    (void)horizon;
+    ppo_gae_device(V, buffer, gamma, lambda);
+}
+
+/* host buffer: staged through the device mirror */
+void compute_gae(NeuralNetwork* V, TrajectoryBuffer* buffer, float gamma, float lambda) {
+    const int was_device = buffer->on_device;
+    if (!was_device) buffer_to_device(buffer);
+    ppo_gae_device(V, buffer, gamma, lambda);
+    if (!was_device) buffer_to_host(buffer);
+}
+
+/* ------------------------------------------------------------------ */
+/* clipped surrogate (ppo.cu:82-169)                                   */
+/* ------------------------------------------------------------------ */
+float policy_loss_and_grad_cuda(float* grad_logprob, float* grad_entropy, float* adv, float* logprobs,
+                                float* old_logprobs, float entropy, float ent_coeff, float epsilon, int m) {
+    float* d = (float*)stage(ST_H, 16);
+    phip_h2d(d + 1, &entropy, sizeof(float));
+    phip_policy_loss(adv, logprobs, old_logprobs, grad_logprob, m, epsilon, ent_coeff, d + 1, d, NULL);
+    float loss = 0.f;
+    phip_d2h(&loss, d, sizeof(float));
+    *grad_entropy = -ent_coeff;
+    return loss;
+}
+
+float policy_loss_and_grad(float* grad_logprob, float* grad_entropy, float* adv, float* logprobs,
+                           float* old_logprobs, float entropy, float ent_coeff, float epsilon, int m) {
+    float* da = stage_up(ST_A, adv, (size_t)m);
+    float* dl = stage_up(ST_B, logprobs, (size_t)m);
+    float* dol = stage_up(ST_C, old_logprobs, (size_t)m);
+    float* dg = (float*)stage(ST_D, sizeof(float) * (size_t)(m > 0 ? m : 1));
+    float loss = policy_loss_and_grad_cuda(dg, grad_entropy, da, dl, dol, entropy, ent_coeff, epsilon, m);
+    phip_d2h(grad_logprob, dg, sizeof(float) * (size_t)m);
+    return loss;
+}
+
+/* ------------------------------------------------------------------ */
+/* the update                                                          */
+/* ------------------------------------------------------------------ */
+static const int* next_perm(PPO* ppo, PPODev* d, int shuffle_mode, uint64_t* key) {
+    if (shuffle_mode == PPO_SHUFFLE_DEVICE) {
+        *key = d->key++;
+        return NULL;
+    }
+    shuffle_buffer_cuda(ppo->buffer);                   /* reference: host rand() swap shuffle */
+    *key = 0;
+    return ppo->buffer->random_idx;
+}
+
+void ppo_update(void* vppo, float gamma, int batch_size, int n_epochs_policy, int n_epochs_value, int shuffle_mode,
+                unsigned long long seed) {
+    PPO* ppo = (PPO*)vppo;
+    TrajectoryBuffer* buf = ppo->buffer;
+    if (!buf->on_device) die("ppo_update: buffer must be device-resident (buffer_to_device / ppo_fill_synthetic)");
+    if (batch_size <= 0) die("ppo_update: batch_size must be positive");
+    PPODev* d = dev_ws(ppo, batch_size);
+    if (shuffle_mode == PPO_SHUFFLE_DEVICE && (!d->seeded || d->seed != seed)) {
+        d->seed = seed;
+        d->key = splitmix64(seed);
+        d->seeded = 1;
+    }
+    const int S = buf->state_size, A = buf->action_size, B = batch_size;
+    const int limit = buf->full ? buf->capacity : buf->idx;
+    const int num_batches = buf->capacity / B;                           /* D13 */
+    const int world = phip_comm_world();
+    const float gscale = 1.0f / (float)world;
+    ppo->adam_V->grad_scale = gscale;
+    ppo->adam_policy->grad_scale = gscale;
+    ppo->adam_entropy->grad_scale = gscale;
+    NeuralNetwork* V = ppo->V;
+    GaussianPolicy* pol = ppo->policy;
+    NeuralNetwork* mu = pol->mu;
+
+    ppo_gae_device(V, buf, gamma, ppo->lambda);
+
+    for (int j = 0; j < n_epochs_value; j++) {
+        uint64_t key;
+        const int* perm = next_perm(ppo, d, shuffle_mode, &key);
+        for (int k = 0; k < num_batches; k++) {
+            phip_gather(perm, key, k * B, limit, B, S, A, buf->state_p, buf->action_p, buf->logprob_p,
+                        buf->advantage_p, buf->adv_target_p, d->states, NULL, NULL, NULL, d->tgt);
+            nn_forward_dev(V, d->states, B);
+            phip_mse(V->d_output, d->tgt, B, d->gv, NULL, d->stats + 0);
+            nn_backward_dev(V, d->gv, B, 0);
+            phip_allreduce_sum_f32(V->d_grads, V->num_params);
+            adam_update_cuda(ppo->adam_V, ppo->lr_V);
+            d->n_v++;
+        }
+    }
+    for (int j = 0; j < n_epochs_policy; j++) {
+        uint64_t key;
+        const int* perm = next_perm(ppo, d, shuffle_mode, &key);
+        for (int k = 0; k < num_batches; k++) {
+            phip_gather(perm, key, k * B, limit, B, S, A, buf->state_p, buf->action_p, buf->logprob_p,
+                        buf->advantage_p, buf->adv_target_p, d->states, d->actions, d->old_lp, d->adv, NULL);
+            nn_forward_dev(mu, d->states, B);
+            phip_policy_head(mu->d_output, pol->d_log_std, d->actions, d->adv, d->old_lp, B, A, ppo->epsilon,
+                             ppo->ent_coeff, d->gmu, pol->d_log_std_grad, d->stats + 1);
+            nn_backward_dev(mu, d->gmu, B, 0);
+            phip_allreduce_sum_f32(mu->d_grads, mu->num_params + align4(A));   /* μ grads + log_std grad */
+            adam_update_cuda(ppo->adam_entropy, ppo->lr_policy);               /* ppo.cu:440-442 order */
+            adam_update_cuda(ppo->adam_policy, ppo->lr_policy);
+            d->n_p++;
+        }
+    }
+}
+
+void ppo_reset_stats(void* vppo) {
+    PPO* ppo = (PPO*)vppo;
+    PPODev* d = dev_ws(ppo, 1);
+    phip_memset(d->stats, 0, 4 * sizeof(float));
+    d->n_v = d->n_p = 0;
+}
+
+void ppo_read_stats(void* vppo, double* out, int n) {
+    PPO* ppo = (PPO*)vppo;
+    PPODev* d = dev_ws(ppo, 1);
+    float s[4] = {0, 0, 0, 0}, a[2] = {0, 0};
+    phip_d2h(s, d->stats, sizeof(s));
+    if (g_adv_stats) phip_d2h(a, g_adv_stats, sizeof(a));
+    double v[7] = {s[0], (double)d->n_v, s[1], (double)d->n_p, compute_entropy_cuda(ppo->policy), a[0], a[1]};
+    for (int i = 0; i < n && i < 7; i++) out[i] = v[i];
+}
+
+/* ppo.cu:451-558 */
+void train_ppo_epoch(PPO* ppo, Env* env, int steps_per_epoch, int batch_size, int n_epochs_policy,
+                     int n_epochs_value) {
+    for (int i = 0; i < steps_per_epoch / ppo->buffer->capacity; i++) {
+        collect_trajectories(ppo->buffer, env, ppo->policy, ppo->buffer->capacity);
+        buffer_to_device(ppo->buffer);
+        ppo_update(ppo, env->gamma, batch_size, n_epochs_policy, n_epochs_value, PPO_SHUFFLE_HOST_RAND, 0);
+        buffer_to_host(ppo->buffer);
+        policy_to_host(ppo->policy);
+        nn_write_weights_to_host(ppo->V);
+    }
+}
+
+/* ppo.cu:560-583: rollout `steps` and print the mean discounted return J and return R */
+void eval_ppo(PPO* ppo, Env* env, int steps) {
+    reset_buffer(ppo->buffer);
+    collect_trajectories(ppo->buffer, env, ppo->policy, steps);
+    TrajectoryBuffer* b = ppo->buffer;
+    float rewards = *b->reward(b, steps - 1);
+    float episode_J = *b->reward(b, steps - 1);
+    int n_episodes = 1;
+    float sum_J = 0;
+    for (int i = steps - 2; i >= 0; i--) {
+        rewards += *b->reward(b, i);
+        episode_J = *b->reward(b, i) + env->gamma * episode_J;
+        if (*b->terminated(b, i) || *b->truncated(b, i)) {
+            n_episodes++;
+            sum_J += episode_J;
+            episode_J = 0;
+        }
+    }
+    printf("J: %f R: %f Episodes: %d\n", sum_J / n_episodes, rewards / n_episodes, n_episodes);
+    reset_buffer(ppo->buffer);
+}
+
+/* ------------------------------------------------------------------ */
+/* batched sampling / synthetic rollouts (ppo_ext.h)                   */
+/* ------------------------------------------------------------------ */
+void ppo_sample_action_device(void* vpolicy, float* d_state, float* d_action, float* d_log_prob, int m,
+                              unsigned long long seed, unsigned long long offset) {
+    GaussianPolicy* p = (GaussianPolicy*)vpolicy;
+    nn_forward_dev(p->mu, d_state, m);
+    phip_sample(p->mu->d_output, p->d_log_std, d_action, d_log_prob, m, p->action_size, seed, offset);
+}
+
+void ppo_fill_synthetic(void* vppo, int n_envs, int horizon, unsigned long long seed, float p_terminate) {
+    PPO* ppo = (PPO*)vppo;
+    TrajectoryBuffer* b = ppo->buffer;
+    const long N = (long)n_envs * horizon;
+    if (N <= 0 || N > b->capacity) die("ppo_fill_synthetic: n_envs*horizon must be in [1, capacity]");
+    const int S = b->state_size, A = b->action_size;
+    const uint64_t s0 = splitmix64(seed);
+    phip_fill_uniform(b->d_state_p, N * S, s0 ^ 0x1, -1.f, 1.f);
+    phip_fill_rollout_flags((uint8_t*)b->d_terminated_p, (uint8_t*)b->d_truncated_p, n_envs, horizon, p_terminate,
+                            s0 ^ 0x2);
+    phip_link_next_state(b->d_next_state_p, b->d_state_p, (const uint8_t*)b->d_terminated_p, n_envs, horizon, S,
+                         s0 ^ 0x3);
+    phip_fill_normal(b->d_reward_p, N, s0 ^ 0x4, 0.1f);
+    ppo_sample_action_device(ppo->policy, b->d_state_p, b->d_action_p, b->d_logprob_p, (int)N, s0 ^ 0x5, 0);
+    phip_memset(b->d_advantage_p, 0, sizeof(float) * (size_t)N);
+    phip_memset(b->d_adv_target_p, 0, sizeof(float) * (size_t)N);
+    b->idx = (int)(N % b->capacity);
+    b->full = N == b->capacity;
+    buffer_point_device(b);
+    (void)A;
+}
+
+/* ------------------------------------------------------------------ */
+/* checkpoint (ppo.cu:585-648 byte layout)                             */
+/* ------------------------------------------------------------------ */
+void save_ppo(PPO* ppo, const char* filename) {
+    FILE* f = fopen(filename, "wb");
+    if (!f) die("save_ppo: cannot open file");
+    policy_to_host(ppo->policy);
+    nn_write_weights_to_host(ppo->V);
+    fwrite(&ppo->lambda, sizeof(float), 1, f);
+    fwrite(&ppo->epsilon, sizeof(float), 1, f);
+    fwrite(&ppo->ent_coeff, sizeof(float), 1, f);
+    fwrite(&ppo->lr_policy, sizeof(float), 1, f);
+    fwrite(&ppo->lr_V, sizeof(float), 1, f);
+    fwrite(&ppo->buffer->state_size, sizeof(int), 1, f);
+    fwrite(&ppo->buffer->action_size, sizeof(int), 1, f);
+    fwrite(&ppo->buffer->capacity, sizeof(int), 1, f);
+    save_policy(ppo->policy, f);
+    save_neural_network(ppo->V, f);
+    save_adam(ppo->adam_policy, f, true);
+    save_adam(ppo->adam_V, f, true);
+    save_adam(ppo->adam_entropy, f, true);
+    fclose(f);
+}
+
+PPO* load_ppo(const char* filename, bool use_cuda) {
+    FILE* f = fopen(filename, "rb");
+    if (!f) die("load_ppo: cannot open file");
+    PPO* ppo = (PPO*)xcalloc(1, sizeof(PPO));
+    ppo->use_cuda = use_cuda;
+    int S, A, cap;
+    if (fread(&ppo->lambda, sizeof(float), 1, f) != 1 || fread(&ppo->epsilon, sizeof(float), 1, f) != 1 ||
+        fread(&ppo->ent_coeff, sizeof(float), 1, f) != 1 || fread(&ppo->lr_policy, sizeof(float), 1, f) != 1 ||
+        fread(&ppo->lr_V, sizeof(float), 1, f) != 1 || fread(&S, sizeof(int), 1, f) != 1 ||
+        fread(&A, sizeof(int), 1, f) != 1 || fread(&cap, sizeof(int), 1, f) != 1)
+        die("load_ppo: unexpected end of file");
+    ppo->buffer = create_trajectory_buffer(cap, S, A);
+    ppo->policy = load_policy(f, S, A);
+    ppo->V = load_neural_network(f);
+    ppo->adam_policy = load_adam_from_nn(f, ppo->policy->mu, true);
+    ppo->adam_V = load_adam_from_nn(f, ppo->V, true);
+    ppo->adam_entropy = load_adam(f, &ppo->policy->d_log_std, &ppo->policy->d_log_std_grad, &A, true);
+    fclose(f);
+    return ppo;
+}

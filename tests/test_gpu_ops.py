@@ -1,0 +1,155 @@
+"""Op-level parity: libppo HIP kernels (through the C ABI) vs the oracle on identical seeded inputs.
+
+Shapes cover every layer of the BASELINE configs C1–C5 (fp32 path), ragged batches and edge cases.
+Tolerances are stated per op (see helpers.py and DESIGN.md §Parity).
+"""
+import numpy as np
+import pytest
+
+import ppo_ffi
+from helpers import F32, assert_gemm_close, assert_rel_close, dev, empty
+
+pytestmark = pytest.mark.gpu
+
+# (m, n, l): batch, in, out
+LINEAR_SHAPES = [
+    (64, 3, 64), (64, 64, 64), (64, 64, 1),            # C1/C2 Pendulum minibatch
+    (2048, 3, 64), (4096, 64, 1),                      # C2 GAE forwards
+    (1000, 17, 256), (1000, 256, 6),                   # C3, ragged batch
+    (8192, 256, 256),                                  # C3 minibatch N/32
+    (4096, 376, 512), (4096, 512, 512), (4096, 512, 17), (4096, 512, 1),   # C4 layers
+    (2048, 1024, 1024),                                # C5 hidden (fp32 path)
+    (1, 3, 64), (1, 376, 512), (33, 5, 7), (130, 129, 131),               # m = 1 rollout, odd sizes
+]
+
+
+def _rand(rng, shape, lo=-1.0, hi=1.0):
+    return rng.uniform(lo, hi, shape).astype(F32)
+
+
+@pytest.mark.parametrize("m,n,l", LINEAR_SHAPES)
+def test_mat_mul_cuda_forward(lib, oracle, m, n, l):
+    rng = np.random.default_rng(m * 7 + n * 3 + l)
+    x, W, b = _rand(rng, (m, n)), _rand(rng, (l, n), -0.2, 0.2), _rand(rng, l, -0.2, 0.2)
+    dx, dW, db, dy = dev(lib, x), dev(lib, W), dev(lib, b), empty(lib, m * l)
+    lib.mat_mul_cuda(None, dy.ptr, dx.ptr, dW.ptr, db.ptr, m, n, l)
+    got = dy.to_numpy(F32, m * l).reshape(m, l)
+    assert_gemm_close(got, oracle.mat_mul(x, W, b), n, "mat_mul_cuda")
+
+
+@pytest.mark.parametrize("m,n,l", LINEAR_SHAPES)
+def test_mat_mul_backwards_cuda(lib, oracle, m, n, l):
+    rng = np.random.default_rng(m * 5 + n + l * 11)
+    x, W, g = _rand(rng, (m, n)), _rand(rng, (l, n), -0.2, 0.2), _rand(rng, (m, l))
+    dx, dW, dg = dev(lib, x), dev(lib, W), dev(lib, g)
+    dgx, dgW = empty(lib, m * n), empty(lib, l * n)
+    lib.mat_mul_backwards_cuda(None, dgx.ptr, dgW.ptr, dg.ptr, dx.ptr, dW.ptr, m, n, l)
+    gx_ref, gW_ref = oracle.mat_mul_backwards(g, x, W)
+    assert_gemm_close(dgx.to_numpy(F32, m * n).reshape(m, n), gx_ref, l, "grad_x")
+    assert_gemm_close(dgW.to_numpy(F32, l * n).reshape(l, n), gW_ref, m, "grad_W")
+
+
+def test_mat_mul_host_pointer_api_accumulates(lib, oracle):
+    """mat_mul / mat_mul_backwards (host pointers) keep the CPU path's β=1 accumulation."""
+    rng = np.random.default_rng(3)
+    m, n, l = 70, 19, 23
+    x, W, b, g = _rand(rng, (m, n)), _rand(rng, (l, n)), _rand(rng, l), _rand(rng, (m, l))
+    out = np.empty((m, l), F32)
+    lib.mat_mul(out.ctypes.data, x.ctypes.data, W.ctypes.data, b.ctypes.data, m, n, l)
+    assert_gemm_close(out, oracle.mat_mul(x, W, b), n, "mat_mul host")
+    gx0, gW0 = _rand(rng, (m, n)), _rand(rng, (l, n))
+    gx, gW = gx0.copy(), gW0.copy()
+    lib.mat_mul_backwards(gx.ctypes.data, gW.ctypes.data, g.ctypes.data, x.ctypes.data, W.ctypes.data, m, n, l)
+    gx_ref, gW_ref = oracle.mat_mul_backwards(g, x, W, gx0, gW0)
+    assert_gemm_close(gx, gx_ref, l, "grad_x host")
+    assert_gemm_close(gW, gW_ref, m, "grad_W host")
+
+
+def test_relu_and_derivative(lib, oracle):
+    rng = np.random.default_rng(4)
+    x = _rand(rng, 100_003)
+    x[::97] = 0.0
+    g = _rand(rng, x.size)
+    d = dev(lib, x)
+    lib.ReLU_cuda(d.ptr, 1, x.size)
+    y = d.to_numpy(F32, x.size)
+    np.testing.assert_array_equal(y, oracle.relu(x))
+    dg = dev(lib, g)
+    lib.ReLU_derivative_cuda(d.ptr, dg.ptr, 1, x.size)
+    np.testing.assert_array_equal(dg.to_numpy(F32, x.size), oracle.relu_derivative(y, g))
+
+
+@pytest.mark.parametrize("m", [1, 64, 1000, 32768, 300_001])
+def test_mse_loss_and_grad(lib, oracle, m):
+    rng = np.random.default_rng(m)
+    y, t = _rand(rng, m, -3, 3), _rand(rng, m, -3, 3)
+    dy, dt, dg = dev(lib, y), dev(lib, t), empty(lib, m)
+    loss = lib.mean_squared_error_cuda(dy.ptr, dt.ptr, m, 1)
+    lib.mean_squared_error_derivative_cuda(dg.ptr, dy.ptr, dt.ptr, m, 1)
+    ref_loss, ref_g = oracle.mse(y, t)
+    assert abs(loss - ref_loss) <= 1e-5 * abs(ref_loss) + 1e-7        # reduction order differs
+    np.testing.assert_array_equal(dg.to_numpy(F32, m), ref_g)            # element-wise: bit-exact
+
+
+@pytest.mark.parametrize("m,A", [(64, 1), (1000, 6), (4096, 17), (7, 3)])
+def test_log_prob_forward_backward(lib, oracle, m, A):
+    """compute_log_prob_cuda / log_prob_backwards_cuda on a policy (correct for any A: D1/D2)."""
+    rng = np.random.default_rng(m + A)
+    S = 5
+    sizes = ppo_ffi.c_ints([S, 16, A])
+    pol = lib.create_gaussian_policy(sizes, ppo_ffi.c_strings(["relu", "none"]), 3, 1.0)
+    log_std = _rand(rng, A, -0.5, 0.5)
+    ppo_ffi.h2d(lib, pol.contents.d_log_std, log_std)
+    s, a, gin = _rand(rng, (m, S)), _rand(rng, (m, A), -2, 2), _rand(rng, m)
+    ds, da, dgin, dout = dev(lib, s), dev(lib, a), dev(lib, gin), empty(lib, m)
+    lib.compute_log_prob_cuda(pol, dout.ptr, ds.ptr, da.ptr, m)
+    mu = ppo_ffi.d2h(lib, pol.contents.mu.contents.d_output, F32, m * A).reshape(m, A)
+    assert_rel_close(dout.to_numpy(F32, m), oracle.log_prob(mu, log_std, a), 2e-6, 2e-6, "log_prob")
+    dgmu, dgls = empty(lib, m * A), empty(lib, A)
+    lib.log_prob_backwards_cuda(pol, dgin.ptr, dgmu.ptr, dgls.ptr, m)
+    gmu_ref, gls_ref = oracle.log_prob_backwards(mu, log_std, a, gin)
+    assert_rel_close(dgmu.to_numpy(F32, m * A).reshape(m, A), gmu_ref, 2e-6, 1e-7, "grad_mu")
+    assert_rel_close(dgls.to_numpy(F32, A), gls_ref, 1e-4, 1e-4 * np.abs(gls_ref).max(), "grad_log_std")
+    ent = lib.compute_entropy_cuda(pol)
+    assert abs(ent - oracle.entropy(log_std)) <= 1e-6
+    lib.free_gaussian_policy(pol)
+
+
+@pytest.mark.parametrize("m", [64, 4096, 32768])
+def test_policy_loss_and_grad_cuda(lib, oracle, m):
+    rng = np.random.default_rng(m + 1)
+    adv = rng.normal(size=m).astype(F32)
+    adv[::17] = 0.0                                  # A = 0 counts as "not positive"
+    old = rng.normal(size=m).astype(F32)
+    lp = (old + rng.normal(scale=0.3, size=m)).astype(F32)   # both clip branches
+    dadv, dlp, dold, dg = dev(lib, adv), dev(lib, lp), dev(lib, old), empty(lib, m)
+    import ctypes as C
+    ge = C.c_float(0)
+    ent, ec, eps = 1.4189385, 0.01, 0.2
+    loss = lib.policy_loss_and_grad_cuda(dg.ptr, C.byref(ge), dadv.ptr, dlp.ptr, dold.ptr, ent, ec, eps, m)
+    ref_loss, ref_g, ref_ge = oracle.policy_loss_and_grad(adv, lp, old, ent, ec, eps)
+    np.testing.assert_array_equal(dg.to_numpy(F32, m), ref_g)
+    assert abs(loss - ref_loss) <= 1e-5 * max(1.0, abs(ref_loss))
+    assert ge.value == ref_ge
+
+
+@pytest.mark.parametrize("n", [1, 2048, 4096, 262_144])
+def test_gae_scan_and_normalisation(lib, oracle, n):
+    """compute_gae_cuda's scan + Welford + normalisation vs the reference recursion (ppo.cu:326-369)."""
+    rng = np.random.default_rng(n)
+    v, vn, r = rng.normal(size=n).astype(F32), rng.normal(size=n).astype(F32), rng.normal(size=n).astype(F32)
+    term = (rng.uniform(size=n) < 1 / 200).astype(np.uint8)
+    trunc = np.zeros(n, np.uint8)
+    T = 1000
+    trunc[T - 1::T] = 1
+    trunc[-1] = 1
+    trunc &= 1 - term
+    adv_ref, tgt_ref, mean_ref, std_ref = oracle.gae(v, vn, r, term, trunc, 0.99, 0.95)
+    from gpu_internal import gae_device
+    adv, tgt = gae_device(lib, v, vn, r, term, trunc, 0.99, 0.95)
+    # targets = v + A (pre-normalisation): the parallel scan re-associates, so ~1e-6 relative
+    assert_rel_close(tgt, tgt_ref, 1e-5, 1e-5, "adv_target")
+    # normalised advantages (global mean / population σ): stated tolerance rtol 1e-4
+    assert_rel_close(adv, adv_ref, 1e-4, 1e-4, "normalised advantage")
+    raw = tgt.astype(np.float64) - v
+    assert abs(raw.mean() - mean_ref) <= 1e-4 * max(1.0, abs(mean_ref))
