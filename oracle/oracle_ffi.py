@@ -260,6 +260,62 @@ def adam_update(params, grads, m, v, t, lr, beta1=0.9, beta2=0.999):
     return ts.value
 
 
+def ppo_update(sizes, relu_flags, mu_params, log_std, v_params, buf, *, batch_size, n_epochs_policy=4,
+               n_epochs_value=10, gamma=0.99, lam=0.95, epsilon=0.2, ent_coeff=0.0, lr_policy=3e-4, lr_v=3e-4,
+               shuffle_mode=0, seed=0, max_value_steps=-1, max_policy_steps=-1, adam=None):
+    """One reference CPU update (ppo.cu:395-443 without the rollout) on copies of the inputs.
+
+    buf: dict of numpy arrays state, next_state, action, reward, logprob, terminated, truncated.
+    adam: optional dict with m/v/t for 'mu', 'v', 'ent' (fresh zeros otherwise).
+    Returns a dict with the updated parameters, Adam state, advantages and loss sums.
+    """
+    lib = load()
+    N = buf["reward"].size
+    cfg = RefUpdateCfg()
+    cfg.num_sizes = len(sizes)
+    for i, s in enumerate(sizes):
+        cfg.sizes_mu[i] = s
+    for i, r in enumerate(relu_flags):
+        cfg.relu[i] = r
+    cfg.N, cfg.batch_size = N, batch_size
+    cfg.n_epochs_policy, cfg.n_epochs_value = n_epochs_policy, n_epochs_value
+    cfg.gamma, cfg.lambda_, cfg.epsilon, cfg.ent_coeff = gamma, lam, epsilon, ent_coeff
+    cfg.lr_policy, cfg.lr_v = lr_policy, lr_v
+    cfg.shuffle_mode, cfg.seed = shuffle_mode, seed
+    cfg.max_value_steps, cfg.max_policy_steps = max_value_steps, max_policy_steps
+    out = {"mu": np.array(mu_params, _f32, copy=True), "log_std": np.array(log_std, _f32, copy=True),
+           "v": np.array(v_params, _f32, copy=True), "advantage": np.zeros(N, _f32),
+           "adv_target": np.zeros(N, _f32)}
+    A = sizes[-1]
+    ad = adam or {}
+    for k, n in (("mu", out["mu"].size), ("v", out["v"].size), ("ent", A)):
+        st = ad.get(k, {})
+        out["m_" + k] = np.array(st.get("m", np.zeros(n, _f32)), _f32, copy=True)
+        out["v_" + k] = np.array(st.get("v", np.zeros(n, _f32)), _f32, copy=True)
+    keep = {k: np.ascontiguousarray(buf[k], _f32) for k in ("state", "next_state", "action", "reward", "logprob")}
+    keep["terminated"] = np.ascontiguousarray(buf["terminated"], np.uint8)
+    keep["truncated"] = np.ascontiguousarray(buf["truncated"], np.uint8)
+
+    def fp(a):
+        return a.ctypes.data_as(C.POINTER(C.c_float))
+
+    st = RefUpdateState()
+    st.mu_params, st.log_std, st.v_params = fp(out["mu"]), fp(out["log_std"]), fp(out["v"])
+    st.m_mu, st.v_mu, st.t_mu = fp(out["m_mu"]), fp(out["v_mu"]), ad.get("mu", {}).get("t", 0)
+    st.m_v, st.v_v, st.t_v = fp(out["m_v"]), fp(out["v_v"]), ad.get("v", {}).get("t", 0)
+    st.m_ent, st.v_ent, st.t_ent = fp(out["m_ent"]), fp(out["v_ent"]), ad.get("ent", {}).get("t", 0)
+    st.state, st.next_state, st.action = fp(keep["state"]), fp(keep["next_state"]), fp(keep["action"])
+    st.reward, st.logprob = fp(keep["reward"]), fp(keep["logprob"])
+    st.terminated = keep["terminated"].ctypes.data_as(C.POINTER(C.c_uint8))
+    st.truncated = keep["truncated"].ctypes.data_as(C.POINTER(C.c_uint8))
+    st.advantage, st.adv_target = fp(out["advantage"]), fp(out["adv_target"])
+    lib.ref_ppo_update(C.byref(cfg), C.byref(st))
+    out.update(t_mu=st.t_mu, t_v=st.t_v, t_ent=st.t_ent, sum_v_loss=st.sum_v_loss,
+               sum_policy_loss=st.sum_policy_loss, n_v=st.n_v, n_p=st.n_p, adv_mean=st.adv_mean,
+               adv_std=st.adv_std, t_gae=st.t_gae, t_value=st.t_value, t_policy=st.t_policy)
+    return out
+
+
 def libc():
     return C.CDLL("libc.so.6")
 

@@ -87,7 +87,12 @@ def test_mse_loss_and_grad(lib, oracle, m):
     loss = lib.mean_squared_error_cuda(dy.ptr, dt.ptr, m, 1)
     lib.mean_squared_error_derivative_cuda(dg.ptr, dy.ptr, dt.ptr, m, 1)
     ref_loss, ref_g = oracle.mse(y, t)
-    assert abs(loss - ref_loss) <= 1e-5 * abs(ref_loss) + 1e-7        # reduction order differs
+    exact = float(np.mean((t.astype(np.float64) - y) ** 2))
+    # the reference accumulates Σ serially in fp32 (loss.cu:5-13): its own error grows with m.
+    # The device tree reduction must be within 1e-5 of the exact mean and no further from the
+    # oracle than the oracle is from the exact value (+1e-5).
+    assert abs(loss - exact) <= 1e-5 * exact + 1e-7
+    assert abs(loss - ref_loss) <= abs(ref_loss - exact) + 1e-5 * exact + 1e-7
     np.testing.assert_array_equal(dg.to_numpy(F32, m), ref_g)            # element-wise: bit-exact
 
 

@@ -1,0 +1,212 @@
+"""Update-level parity: the device-resident PPO update vs the oracle's CPU update on identical state.
+
+Checks, from the same seeded start:
+  * create_ppo's rand()-driven initialisation is bit-identical to the reference initialiser;
+  * GAE advantages / targets (normalised, global statistics);
+  * one value minibatch and one policy minibatch: every parameter gradient (stated GEMM
+    tolerance) and the Adam parameter delta (exact where |g| is not tiny, ≤ 2·lr elsewhere);
+  * both shuffles: the reference's host rand() swap shuffle and libppo's device Feistel shuffle;
+  * a whole C1-shaped update (10 value + 4 policy epochs): loss sums and parameter drift.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import ppo_ffi
+from gpu_internal import read_host_buffer, set_host_buffer
+from helpers import F32, assert_gemm_close, assert_rel_close, nn_grads_packed, nn_params_packed
+
+pytestmark = pytest.mark.gpu
+
+RELU = lambda sizes: [1] * (len(sizes) - 2) + [0]  # noqa: E731
+ACTS = lambda sizes: ["relu"] * (len(sizes) - 2) + ["none"]  # noqa: E731
+
+CONFIGS = {
+    "pendulum": dict(sizes=[3, 64, 64, 1], N=256),
+    "halfcheetah": dict(sizes=[17, 256, 256, 6], N=1024),
+    "humanoid": dict(sizes=[376, 512, 512, 512, 17], N=2048),
+}
+
+
+def make_ppo(lib, oracle, sizes, N, seed=1234, init_std=1.0, ent_coeff=0.0):
+    oracle.srand(seed)
+    ppo = lib.create_ppo(ppo_ffi.c_strings(ACTS(sizes)), ppo_ffi.c_ints(sizes), len(sizes), N, 3e-4, 3e-4, 0.95,
+                         0.2, ent_coeff, init_std, True)
+    return ppo
+
+
+def synthetic_buffer(oracle, sizes, mu_params, log_std, N, seed, n_envs=4):
+    rng = np.random.default_rng(seed)
+    S, A = sizes[0], sizes[-1]
+    state = rng.uniform(-1, 1, (N, S)).astype(F32)
+    next_state = np.roll(state, -1, axis=0).copy()
+    term = (rng.uniform(size=N) < 1 / 200).astype(np.uint8)
+    trunc = np.zeros(N, np.uint8)
+    T = N // n_envs
+    trunc[T - 1::T] = 1
+    trunc &= 1 - term
+    ends = (term | trunc).astype(bool)
+    next_state[ends] = rng.uniform(-1, 1, (int(ends.sum()), S)).astype(F32)
+    acts = oracle.mlp_forward(sizes, RELU(sizes), mu_params, state)
+    mu = oracle.mlp_layer_outputs(sizes, acts, N)[-1]
+    action = (mu + rng.normal(size=(N, A)).astype(F32) * np.exp(log_std)).astype(F32)
+    logprob = oracle.log_prob(mu, log_std, action)
+    reward = (0.1 * rng.normal(size=N)).astype(F32)
+    return dict(state=state, next_state=next_state, action=action, reward=reward, logprob=logprob,
+                terminated=term, truncated=trunc)
+
+
+def load_buffer(lib, ppo, buf):
+    b = ppo.contents.buffer
+    set_host_buffer(lib, b, state=buf["state"], next_state=buf["next_state"], action=buf["action"],
+                    reward=buf["reward"], logprob=buf["logprob"], term=buf["terminated"], trunc=buf["truncated"])
+    b.contents.idx = 0
+    b.contents.full = True
+    lib.buffer_to_device(b)
+
+
+def policy_state(lib, ppo):
+    pol = ppo.contents.policy.contents
+    mu = nn_params_packed(lib, ppo.contents.policy.contents.mu)
+    ls = ppo_ffi.d2h(lib, pol.d_log_std, F32, pol.action_size)
+    return mu, ls
+
+
+def assert_adam_delta(got, ref, g_ref, lr, what):
+    """Adam step from identical state: exact where |g| is not tiny; a sign flip (≤ 2·lr) allowed elsewhere."""
+    big = np.abs(g_ref) > 1e-3 * np.abs(g_ref).max()
+    err = np.abs(got - ref)
+    assert (err[big] <= 1e-6 * np.abs(ref[big]) + 1e-6 * lr).all(), \
+        f"{what}: Adam delta mismatch on large-|g| entries, worst {err[big].max():.3g}"
+    assert (err <= 2 * lr * 1.0001 + 1e-7).all(), f"{what}: delta beyond 2·lr, worst {err.max():.3g}"
+    return int((err > 1e-6 * lr + 1e-6 * np.abs(ref)).sum())
+
+
+def test_create_ppo_initialisation_bitexact(lib, oracle):
+    """neural_network.cu:40-51 / policy.cu:22-24 from srand(seed): μ net, then V net."""
+    sizes = [17, 256, 256, 6]
+    ppo = make_ppo(lib, oracle, sizes, 64, seed=42, init_std=0.5)
+    mu, ls = policy_state(lib, ppo)
+    v = nn_params_packed(lib, ppo.contents.V)
+    oracle.srand(42)
+    mu_ref = oracle.mlp_init(sizes)
+    v_ref = oracle.mlp_init(sizes[:-1] + [1])
+    np.testing.assert_array_equal(mu, mu_ref)
+    np.testing.assert_array_equal(v, v_ref)
+    np.testing.assert_array_equal(ls, np.full(6, np.log(np.float32(0.5)), F32))
+    lib.free_ppo(ppo)
+
+
+@pytest.mark.parametrize("cfg", sorted(CONFIGS))
+@pytest.mark.parametrize("shuffle_mode", [0, 1])
+def test_single_value_step(lib, oracle, cfg, shuffle_mode):
+    sizes, N = CONFIGS[cfg]["sizes"], CONFIGS[cfg]["N"]
+    ppo = make_ppo(lib, oracle, sizes, N)
+    mu0, ls0 = policy_state(lib, ppo)
+    v0 = nn_params_packed(lib, ppo.contents.V)
+    buf = synthetic_buffer(oracle, sizes, mu0, ls0, N, seed=7)
+    load_buffer(lib, ppo, buf)
+    oracle.srand(99)
+    lib.ppo_update(ppo, 0.99, N, 0, 1, shuffle_mode, 5)          # GAE + exactly one value minibatch
+    lib.ppo_synchronize()
+    b = ppo.contents.buffer.contents
+    adv = ppo_ffi.d2h(lib, b.d_advantage_p, F32, N)
+    tgt = ppo_ffi.d2h(lib, b.d_adv_target_p, F32, N)
+    gV = nn_grads_packed(lib, ppo.contents.V)
+    v1 = nn_params_packed(lib, ppo.contents.V)
+
+    oracle.srand(99)
+    ref = oracle.ppo_update(sizes, RELU(sizes), mu0, ls0, v0, buf, batch_size=N, n_epochs_policy=0,
+                            n_epochs_value=1, shuffle_mode=shuffle_mode, seed=5)
+    assert_rel_close(tgt, ref["adv_target"], 2e-4, 2e-4 * np.abs(ref["adv_target"]).max(), "adv_target")
+    assert_rel_close(adv, ref["advantage"], 2e-3, 2e-3, "advantage")
+    # value gradient of the minibatch (the whole buffer in permuted order) from the oracle
+    sv = sizes[:-1] + [1]
+    x = buf["state"]
+    acts = oracle.mlp_forward(sv, RELU(sv), v0, x)
+    y = oracle.mlp_layer_outputs(sv, acts, N)[-1].ravel()
+    _, g = oracle.mse(y, ref["adv_target"])
+    g_ref = oracle.mlp_backward(sv, RELU(sv), v0, x, acts, g)   # batch == buffer: order only permutes rows
+    assert_gemm_close(gV, g_ref, N, f"{cfg} value grads")
+    flips = assert_adam_delta(v1, ref["v"], g_ref, 3e-4, f"{cfg} value params")
+    assert flips <= max(2, v1.size // 1000)
+    assert ppo.contents.adam_V.contents.time_step == ref["t_v"] == 1
+    lib.free_ppo(ppo)
+
+
+@pytest.mark.parametrize("cfg", sorted(CONFIGS))
+@pytest.mark.parametrize("shuffle_mode", [0, 1])
+def test_single_policy_step(lib, oracle, cfg, shuffle_mode):
+    sizes, N = CONFIGS[cfg]["sizes"], CONFIGS[cfg]["N"]
+    A = sizes[-1]
+    ppo = make_ppo(lib, oracle, sizes, N, init_std=0.7, ent_coeff=0.01)
+    mu0, ls0 = policy_state(lib, ppo)
+    v0 = nn_params_packed(lib, ppo.contents.V)
+    buf = synthetic_buffer(oracle, sizes, mu0, ls0, N, seed=11)
+    # perturb the behaviour log-probs so ratios leave [1−ε, 1+ε] on both sides
+    buf["logprob"] = (buf["logprob"] + np.random.default_rng(3).normal(scale=0.4, size=N)).astype(F32)
+    load_buffer(lib, ppo, buf)
+    oracle.srand(17)
+    lib.ppo_update(ppo, 0.99, N, 1, 0, shuffle_mode, 9)          # GAE + exactly one policy minibatch
+    lib.ppo_synchronize()
+    pol = ppo.contents.policy.contents
+    gmu = nn_grads_packed(lib, ppo.contents.policy.contents.mu)
+    gls = ppo_ffi.d2h(lib, pol.d_log_std_grad, F32, A)
+    mu1, ls1 = policy_state(lib, ppo)
+    oracle.srand(17)
+    ref = oracle.ppo_update(sizes, RELU(sizes), mu0, ls0, v0, buf, batch_size=N, n_epochs_policy=1,
+                            n_epochs_value=0, ent_coeff=0.01, shuffle_mode=shuffle_mode, seed=9)
+    # oracle gradients on the same minibatch (the whole buffer; row order does not change sums)
+    x, a = buf["state"], buf["action"]
+    acts = oracle.mlp_forward(sizes, RELU(sizes), mu0, x)
+    mu = oracle.mlp_layer_outputs(sizes, acts, N)[-1]
+    lp = oracle.log_prob(mu, ls0, a)
+    _, glp, gent = oracle.policy_loss_and_grad(ref["advantage"], lp, buf["logprob"], oracle.entropy(ls0), 0.01,
+                                               0.2)
+    gmu_out, gls_ref = oracle.log_prob_backwards(mu, ls0, a, glp)
+    g_ref = oracle.mlp_backward(sizes, RELU(sizes), mu0, x, acts, gmu_out)
+    gls_ref = gls_ref + gent
+    assert_gemm_close(gmu, g_ref, N, f"{cfg} policy grads")
+    assert_rel_close(gls, gls_ref, 1e-3, 1e-4 * max(1.0, np.abs(gls_ref).max()), "log_std grad")
+    flips = assert_adam_delta(mu1, ref["mu"], g_ref, 3e-4, f"{cfg} policy params")
+    assert flips <= max(2, mu1.size // 1000)
+    assert_adam_delta(ls1, ref["log_std"], gls_ref, 3e-4, "log_std")
+    assert ppo.contents.adam_policy.contents.time_step == ppo.contents.adam_entropy.contents.time_step == 1
+    lib.free_ppo(ppo)
+
+
+@pytest.mark.parametrize("shuffle_mode", [0, 1])
+def test_full_update_c1(lib, oracle, shuffle_mode):
+    """C1: Pendulum shape, N = 2048, B = 64, 10 value + 4 policy epochs (448 minibatch steps).
+
+    Minibatch-level parity is exact up to fp32 re-association; over 448 Adam steps ReLU/clip
+    branch flips make trajectories drift, so the whole-update check is statistical: loss sums
+    within 2 % and parameter movement agreeing in direction (cosine > 0.95) and size (±10 %).
+    """
+    sizes, N, B = [3, 64, 64, 1], 2048, 64
+    ppo = make_ppo(lib, oracle, sizes, N)
+    mu0, ls0 = policy_state(lib, ppo)
+    v0 = nn_params_packed(lib, ppo.contents.V)
+    buf = synthetic_buffer(oracle, sizes, mu0, ls0, N, seed=21, n_envs=8)
+    load_buffer(lib, ppo, buf)
+    lib.ppo_reset_stats(ppo)
+    oracle.srand(5)
+    lib.ppo_update(ppo, 0.99, B, 4, 10, shuffle_mode, 77)
+    st = (C.c_double * 7)()
+    lib.ppo_read_stats(ppo, st, 7)
+    mu1, ls1 = policy_state(lib, ppo)
+    v1 = nn_params_packed(lib, ppo.contents.V)
+    oracle.srand(5)
+    ref = oracle.ppo_update(sizes, RELU(sizes), mu0, ls0, v0, buf, batch_size=B, shuffle_mode=shuffle_mode,
+                            seed=77)
+    assert st[1] == ref["n_v"] == 320 and st[3] == ref["n_p"] == 128
+    assert abs(st[0] - ref["sum_v_loss"]) <= 0.02 * abs(ref["sum_v_loss"])
+    assert abs(st[2] - ref["sum_policy_loss"]) <= 0.02 * abs(ref["sum_policy_loss"]) + 0.02
+    for got, start, want, what in ((v1, v0, ref["v"], "V"), (mu1, mu0, ref["mu"], "mu"),
+                                   (ls1, ls0, ref["log_std"], "log_std")):
+        d_got, d_ref = got - start, want - start
+        cos = float(d_got @ d_ref / (np.linalg.norm(d_got) * np.linalg.norm(d_ref) + 1e-30))
+        ratio = float(np.linalg.norm(d_got) / (np.linalg.norm(d_ref) + 1e-30))
+        assert cos > 0.95 and 0.9 < ratio < 1.1, f"{what}: cos {cos:.4f} norm ratio {ratio:.4f}"
+    lib.free_ppo(ppo)
