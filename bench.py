@@ -1,0 +1,242 @@
+#!/usr/bin/env python3
+"""bench.py — PPO-update throughput of libppo on MI355X (BASELINE.json metric).
+
+A "step" is ONE PPO update over a device-resident synthetic rollout: GAE (two value
+forwards over the whole buffer + exact scan + global normalisation), then 10 value
+epochs and 4 policy epochs of ⌊N/B⌋ minibatches each (reference defaults, main.c:39-40).
+Workload (config C4 of BASELINE.json): Humanoid-shaped 376 → 3×512 → 17 MLPs, 4096 steps ×
+256 envs per GPU, B = N/32 = 32768, fp32.  Data-parallel runs shard by whole environments:
+every rank owns its own 4096×256 rollout (weak scaling), gradients are all-reduced with RCCL
+inside libppo each minibatch, advantage statistics are global.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c3|c2|c5f32] [--batch B]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+Prints ONE JSON line (rank 0).  `value` = learner env-steps/s over all ranks = world·N / t_update.
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "ppo.c_amd"))
+
+# torch first: libppo then binds to the HIP runtime torch already loaded (same soname), so the
+# process holds ONE runtime.  Loading libppo first makes torch pull a second one, which aborts
+# at interpreter exit (measured on the MI355X box).
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import ppo_ffi  # noqa: E402
+
+LIB = ppo_ffi.load()
+
+CONFIGS = {
+    # name: (S, hidden, A, T, E, batch)   — BASELINE.json configs
+    "c2": (3, [64, 64], 1, 4096, 1, 64),
+    "c3": (17, [256, 256], 6, 4096, 64, 8192),
+    "c4": (376, [512, 512, 512], 17, 4096, 256, 32768),
+    "c5f32": (1024, [1024, 1024, 1024, 1024], 17, 8192, 64, 16384),
+}
+METRIC = "PPO updates/sec + env-steps/sec on 4096×256 synthetic rollout, 1/2/4/8 MI355X"
+PEAK_FP32_MFMA_TFLOPS = 157.3          # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 (spec; 155 measured)
+PEAK_HBM_GBPS = 8000.0
+
+
+def algorithmic_flops(S, H, A, N, B, n_v=10, n_p=4):
+    """F = 4·N·P_V + n_v·⌊N/B⌋·B·(6P_V − 2·S·H1) + n_p·⌊N/B⌋·B·(6P_μ − 2·S·H1)."""
+    def P(sizes):
+        return sum(a * b for a, b in zip(sizes[:-1], sizes[1:]))
+    P_mu, P_v = P([S] + H + [A]), P([S] + H + [1])
+    nb = (N // B) * B
+    return 4 * N * P_v + n_v * nb * (6 * P_v - 2 * S * H[0]) + n_p * nb * (6 * P_mu - 2 * S * H[0])
+
+
+def cpu_baseline(lib, ppo, S, H, A, N, B, sample_envs=16, steps=2):
+    """The oracle (plain-C restatement of the reference CPU path, OpenBLAS sgemm, 1 thread) on a bounded
+    sample of the same workload; extrapolated to one full update with the update formula."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_ffi
+
+    oracle_ffi.build()
+    olib = oracle_ffi.load(use_openblas=True)
+    blas = olib.ref_blas_name().decode()
+    T = N // 256 if N >= 256 else N
+    Ns = min(N, sample_envs * T)                          # whole envs → whole GAE segments
+    Bs = min(B, Ns)
+    b = ppo.contents.buffer.contents
+    buf = {
+        "state": ppo_ffi.d2h(lib, b.d_state_p, np.float32, Ns * S).reshape(Ns, S),
+        "next_state": ppo_ffi.d2h(lib, b.d_next_state_p, np.float32, Ns * S).reshape(Ns, S),
+        "action": ppo_ffi.d2h(lib, b.d_action_p, np.float32, Ns * A).reshape(Ns, A),
+        "reward": ppo_ffi.d2h(lib, b.d_reward_p, np.float32, Ns),
+        "logprob": ppo_ffi.d2h(lib, b.d_logprob_p, np.float32, Ns),
+        "terminated": ppo_ffi.d2h(lib, b.d_terminated_p, np.uint8, Ns),
+        "truncated": ppo_ffi.d2h(lib, b.d_truncated_p, np.uint8, Ns),
+    }
+    sizes = [S] + H + [A]
+
+    def packed(nn_ptr):
+        nn = nn_ptr.contents
+        out = []
+        for i in range(nn.num_layers - 1):
+            ly = nn.layers[i]
+            out.append(ppo_ffi.d2h(lib, ly.d_weights, np.float32, ly.input_size * ly.output_size))
+            out.append(ppo_ffi.d2h(lib, ly.d_biases, np.float32, ly.output_size))
+        return np.concatenate(out)
+
+    pol = ppo.contents.policy.contents
+    mu0 = packed(pol.mu)
+    ls0 = ppo_ffi.d2h(lib, pol.d_log_std, np.float32, A)
+    v0 = packed(ppo.contents.V)
+    r = oracle_ffi.ppo_update(sizes, [1] * len(H) + [0], mu0, ls0, v0, buf, batch_size=Bs, shuffle_mode=1,
+                              seed=1, max_value_steps=steps, max_policy_steps=steps)
+    nb = N // B
+    t_update = r["t_gae"] * (N / Ns) + 10 * nb * (r["t_value"] / max(1, r["n_v"])) * (B / Bs) \
+        + 4 * nb * (r["t_policy"] / max(1, r["n_p"])) * (B / Bs)
+    sample_s = r["t_gae"] + r["t_value"] + r["t_policy"]
+    return {
+        "value": N / t_update, "unit": "env-steps/s", "cores": 1, "kind": "port",
+        "sample": (f"oracle (C restatement of the reference CPU path, {blas}, 1 thread): GAE over {Ns} "
+                   f"transitions + {r['n_v']} value + {r['n_p']} policy minibatches at B={Bs}, "
+                   f"extrapolated to a full update (t={t_update:.1f}s); sample took {sample_s:.1f}s"),
+        "cpu": platform.processor() or platform.machine(),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=0)
+    ap.add_argument("--strong", action="store_true", help="split one 4096×256 rollout over the ranks")
+    ap.add_argument("--shuffle", type=int, default=1, help="1 = device Feistel shuffle, 0 = reference host rand()")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-events", action="store_true")
+    ap.add_argument("--seed", type=int, default=1234)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and not (world == 1 and args.gpus == 1):
+        if world == 1:
+            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one process per GPU)")
+    if LIB.ppo_set_device(local) != 0:
+        raise SystemExit(f"libppo: cannot select device {local}: {LIB.ppo_last_error().decode()}")
+    torch.cuda.set_device(local)
+
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)      # control plane only
+        uid = C.create_string_buffer(256)
+        n = LIB.ppo_comm_unique_id(uid, 256) if rank == 0 else 0
+        obj = [bytes(uid.raw[:n])] if rank == 0 else [None]
+        dist.broadcast_object_list(obj, src=0)
+        if LIB.ppo_comm_init(rank, world, obj[0]) != 0:                  # RCCL over xGMI for the data path
+            raise SystemExit(f"ppo_comm_init failed: {LIB.ppo_last_error().decode()}")
+
+    S, H, A, T, E, B = CONFIGS[args.config]
+    if args.strong and world > 1:
+        E = E // world
+        B = max(1, B // world)
+    if args.batch:
+        B = args.batch
+    N = T * E
+    sizes = [S] + H + [A]
+    acts = ["relu"] * len(H) + ["none"]
+
+    C.CDLL("libc.so.6").srand(args.seed)                                 # identical init on every rank
+    ppo = LIB.create_ppo(ppo_ffi.c_strings(acts), ppo_ffi.c_ints(sizes), len(sizes), N, 3e-4, 3e-4, 0.95, 0.2, 0.0,
+                         1.0, True)
+    LIB.ppo_fill_synthetic(ppo, E, T, args.seed * 1000 + rank, 1.0 / 500)
+    LIB.ppo_synchronize()
+
+    def barrier():
+        LIB.ppo_synchronize()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        LIB.ppo_update(ppo, 0.99, B, 4, 10, args.shuffle, args.seed)
+    barrier()
+    LIB.ppo_reset_stats(ppo)
+    LIB.ppo_prof_reset()
+    LIB.ppo_prof_enable(0 if args.no_kernel_events else 1)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        LIB.ppo_update(ppo, 0.99, B, 4, 10, args.shuffle, args.seed)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    LIB.ppo_prof_enable(0)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    ms = (C.c_double * 7)()
+    work = (C.c_double * 7)()
+    launches = (C.c_long * 7)()
+    LIB.ppo_prof_read(ms, work, launches)
+    stats = (C.c_double * 7)()
+    LIB.ppo_read_stats(ppo, stats, 7)
+
+    t_update = elapsed / args.steps
+    flops = algorithmic_flops(S, H, A, N, B)
+    gemm_ms, gemm_flops, gemm_n = ms[0], work[0], launches[0]
+    kernels = {k: {"ms_per_update": ms[i] / args.steps, "launches_per_update": launches[i] / args.steps}
+               for i, k in enumerate(["gemm", "gae", "adam", "gather", "head", "comm", "other"]) if launches[i]}
+    result = {
+        "metric": METRIC,
+        "value": world * N / t_update,
+        "unit": "env-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1000.0 * t_update,
+        "higher_is_better": True,
+        "scaling": "strong" if args.strong else "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (seeded device generator: obs U(-1,1), actions from the policy, rewards 0.1·N(0,1), "
+                "terminated Bernoulli(1/500), truncated at env-segment ends); random-init weights",
+        "config": {"workload": f"{args.config}: {S}->{'x'.join(map(str, H))}->{A} MLP (policy + value), "
+                               f"{T} steps x {E} envs per GPU, B={B}, 10 value + 4 policy epochs",
+                   "global_batch": B * world, "rollout_per_gpu": N, "parallelism": f"dp{world}",
+                   "shuffle": "device-feistel" if args.shuffle else "host-rand"},
+        "updates_per_sec": 1.0 / t_update,
+        "minibatch_steps_per_sec": 14 * (N // B) / t_update,
+        "algorithmic_tflop_per_update": flops / 1e12,
+        "mfma_frac_whole_update": flops / t_update / (PEAK_FP32_MFMA_TFLOPS * 1e12),
+        "kernels": kernels,
+        "loss": {"value_mean": stats[0] / max(1.0, stats[1]), "policy_mean": stats[2] / max(1.0, stats[3])},
+    }
+    if gemm_n and gemm_ms > 0:
+        achieved = gemm_flops / (gemm_ms * 1e-3) / 1e12
+        result["roofline"] = {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP32_MFMA_TFLOPS,
+                              "unit": "TFLOP/s", "frac": achieved / PEAK_FP32_MFMA_TFLOPS, "traffic": None,
+                              "kernel": "gemm_f32_kernel (all linear-layer launches: Σ 2MNK / Σ HIP-event time)",
+                              "launches": gemm_n, "avg_launch_us": 1000.0 * gemm_ms / gemm_n,
+                              "algorithmic_flop_per_launch": gemm_flops / gemm_n}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(LIB, ppo, S, H, A, N, B)
+        result["cpu_baseline"]["gpu_over_cpu"] = result["value"] / result["cpu_baseline"]["value"]
+    LIB.free_ppo(ppo)
+    if world > 1:
+        LIB.ppo_comm_finalize()
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+
+
+if __name__ == "__main__":
+    main()

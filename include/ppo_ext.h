@@ -77,6 +77,13 @@ void ppo_sample_action_device(void* policy, float* d_state, float* d_action, flo
  * terminated ~ Bernoulli(p_terminate), truncated at each segment end. */
 void ppo_fill_synthetic(void* ppo, int n_envs, int horizon, unsigned long long seed, float p_terminate);
 
+/* ---------------- GEMM tuning utilities ---------------- */
+/* force a tile configuration (−1 = automatic) and the split-K workgroup target of grad_W */
+void   ppo_gemm_tune(int force_cfg, int splitk_target);
+/* average device µs of one launch: op 0 = forward (bias+ReLU), 1 = grad_x, 2 = grad_W (+bias grad);
+ * m = batch, n = in, l = out; cfg −1 = automatic */
+double ppo_bench_gemm(int op, int m, int n, int l, int iters, int cfg);
+
 /* ---------------- kernel timing ---------------- */
 enum { PPO_K_GEMM = 0, PPO_K_GAE = 1, PPO_K_ADAM = 2, PPO_K_GATHER = 3, PPO_K_HEAD = 4,
        PPO_K_COMM = 5, PPO_K_OTHER = 6, PPO_K_COUNT = 7 };

@@ -27,8 +27,6 @@ namespace {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int BK = 32;
-constexpr int LDK = BK + 4;       // 36-float row pitch (144 B, 16-B aligned)
 constexpr int NT_ = 256;          // threads per workgroup
 
 enum Op { OP_NT = 0, OP_NN = 1, OP_TN = 2 };
@@ -47,11 +45,14 @@ struct Args {
 // ---------------------------------------------------------------------------
 // Loaders.  "kcont": element (row r, k) at P[r*ld + k]  (x, g in grad_x, W in forward)
 //           "mncont": element (row r, k) at P[k*ld + r] (W in grad_x, g and x in grad_W)
-// Both fill an LDS image [R][LDK] with zeros outside [0,Rmax) × [kbeg,kend).
+// Both fill an LDS image [R][BK+4] with zeros outside [0,Rmax) × [kbeg,kend).
 // ---------------------------------------------------------------------------
-template <int R>
+template <int R, int BK>
 struct Stage {
-    static constexpr int ITERS = R * BK / 4 / NT_;
+    static constexpr int LDK = BK + 4;
+    static constexpr int TOTAL = R * BK / 4;               // float4s per tile
+    static constexpr int ITERS = (TOTAL + NT_ - 1) / NT_;
+    static constexpr int KQ = BK / 4;                      // float4s per kcont row
     f32x4 v[ITERS];
 
     __device__ __forceinline__ void load_kcont(const float* __restrict__ P, int ld, int r0, int Rmax, int k0,
@@ -59,17 +60,19 @@ struct Stage {
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) {
             const int idx = tid + it * NT_;
-            const int kq = idx & 7, r = idx >> 3;
-            const int gr = r0 + r, gk = k0 + kq * 4;
             f32x4 x = {0.f, 0.f, 0.f, 0.f};
-            if (gr < Rmax) {
-                const float* p = P + (long)gr * ld + gk;
-                if (vec && gk + 3 < kend) {
-                    x = *reinterpret_cast<const f32x4*>(p);
-                } else {
+            if (TOTAL % NT_ == 0 || idx < TOTAL) {
+                const int kq = idx % KQ, r = idx / KQ;
+                const int gr = r0 + r, gk = k0 + kq * 4;
+                if (gr < Rmax) {
+                    const float* p = P + (long)gr * ld + gk;
+                    if (vec && gk + 3 < kend) {
+                        x = *reinterpret_cast<const f32x4*>(p);
+                    } else {
 #pragma unroll
-                    for (int e = 0; e < 4; ++e)
-                        if (gk + e < kend) x[e] = p[e];
+                        for (int e = 0; e < 4; ++e)
+                            if (gk + e < kend) x[e] = p[e];
+                    }
                 }
             }
             v[it] = x;
@@ -79,8 +82,10 @@ struct Stage {
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) {
             const int idx = tid + it * NT_;
-            const int kq = idx & 7, r = idx >> 3;
-            *reinterpret_cast<f32x4*>(lds + r * LDK + kq * 4) = v[it];
+            if (TOTAL % NT_ == 0 || idx < TOTAL) {
+                const int kq = idx % KQ, r = idx / KQ;
+                *reinterpret_cast<f32x4*>(lds + r * LDK + kq * 4) = v[it];
+            }
         }
     }
 
@@ -94,18 +99,21 @@ struct Stage {
                                                 int kend, bool vec, int tid) {
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) {
-            int kk, nq;
-            mn_coords(tid + it * NT_, kk, nq);
-            const int gk = k0 + kk, gr = r0 + nq * 4;
+            const int idx = tid + it * NT_;
             f32x4 x = {0.f, 0.f, 0.f, 0.f};
-            if (gk < kend) {
-                const float* p = P + (long)gk * ld + gr;
-                if (vec && gr + 3 < Rmax) {
-                    x = *reinterpret_cast<const f32x4*>(p);
-                } else {
+            if (TOTAL % NT_ == 0 || idx < TOTAL) {
+                int kk, nq;
+                mn_coords(idx, kk, nq);
+                const int gk = k0 + kk, gr = r0 + nq * 4;
+                if (gk < kend) {
+                    const float* p = P + (long)gk * ld + gr;
+                    if (vec && gr + 3 < Rmax) {
+                        x = *reinterpret_cast<const f32x4*>(p);
+                    } else {
 #pragma unroll
-                    for (int e = 0; e < 4; ++e)
-                        if (gr + e < Rmax) x[e] = p[e];
+                        for (int e = 0; e < 4; ++e)
+                            if (gr + e < Rmax) x[e] = p[e];
+                    }
                 }
             }
             v[it] = x;
@@ -114,20 +122,29 @@ struct Stage {
     __device__ __forceinline__ void store_mncont(float* lds, int tid) const {
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) {
-            int kk, nq;
-            mn_coords(tid + it * NT_, kk, nq);
+            const int idx = tid + it * NT_;
+            if (TOTAL % NT_ == 0 || idx < TOTAL) {
+                int kk, nq;
+                mn_coords(idx, kk, nq);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) lds[(nq * 4 + e) * LDK + kk] = v[it][e];
+                for (int e = 0; e < 4; ++e) lds[(nq * 4 + e) * LDK + kk] = v[it][e];
+            }
         }
     }
 };
 
-template <int OP, int BM, int BN, int WARPS_M>
-__global__ __launch_bounds__(NT_, 2) void gemm_f32_kernel(Args a) {
+// BK=16 tiles fit ≤128 VGPRs → 4 workgroups (16 waves) per CU; BK=32 needs 3, 256x128 needs 2
+constexpr int min_waves(int area, int bk) { return area >= 256 * 128 ? 2 : (bk >= 32 ? 3 : 4); }
+
+template <int OP, int BM, int BN, int WARPS_M, int BK>
+__global__ __launch_bounds__(NT_, min_waves(BM * BN, BK)) void gemm_f32_kernel(Args a) {
     constexpr int WARPS_N = 4 / WARPS_M;
     constexpr int WM = BM / WARPS_M, WN = BN / WARPS_N;
     constexpr int TM = WM / 32, TN = WN / 32;
+    constexpr int LDK = BK + 4;        // BK=16: 20, BK=32: 36 floats — ds_read_b128 conflict-free
+    constexpr int KH = BK / 2;         // k per lane-half per tile (k-permutation)
     static_assert(TM >= 1 && TN >= 1, "wave tile must be a multiple of 32x32");
+    static_assert(BK == 16 || BK == 32, "BK");
 
     __shared__ __attribute__((aligned(16))) float lds[(BM + BN) * LDK];
     float* As = lds;
@@ -159,12 +176,12 @@ __global__ __launch_bounds__(NT_, 2) void gemm_f32_kernel(Args a) {
 
     // bias-gradient row sums (OP_TN, tn == 0 workgroups only)
     constexpr int TPR = NT_ / BM > 0 ? NT_ / BM : 1;     // threads per A-row
-    constexpr int KPT = BK / TPR;                         // k per thread
-    const bool do_bsum = OP == OP_TN && a.gbias != nullptr && tn == 0 && (NT_ % BM == 0);
+    constexpr int KPT = BK / TPR > 0 ? BK / TPR : 1;      // k per thread
+    const bool do_bsum = OP == OP_TN && a.gbias != nullptr && tn == 0 && (NT_ % BM == 0) && BK >= TPR;
     float bsum = 0.f;
 
-    Stage<BM> sa;
-    Stage<BN> sb;
+    Stage<BM, BK> sa;
+    Stage<BN, BK> sb;
     const bool va = a.vec_a, vb = a.vec_b;
 
     auto load = [&](int k0) {
@@ -188,28 +205,21 @@ __global__ __launch_bounds__(NT_, 2) void gemm_f32_kernel(Args a) {
         }
 
 #pragma unroll
-        for (int half = 0; half < 2; ++half) {
-            f32x4 fa[TM][2], fb[TN][2];
+        for (int q4 = 0; q4 < KH / 4; ++q4) {
+            f32x4 fa[TM], fb[TN];
 #pragma unroll
-            for (int i = 0; i < TM; ++i) {
-                const float* p = As + (wm * WM + i * 32 + r) * LDK + h * 16 + half * 8;
-                fa[i][0] = *reinterpret_cast<const f32x4*>(p);
-                fa[i][1] = *reinterpret_cast<const f32x4*>(p + 4);
-            }
+            for (int i = 0; i < TM; ++i)
+                fa[i] = *reinterpret_cast<const f32x4*>(As + (wm * WM + i * 32 + r) * LDK + h * KH + q4 * 4);
 #pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                const float* p = Bs + (wn * WN + j * 32 + r) * LDK + h * 16 + half * 8;
-                fb[j][0] = *reinterpret_cast<const f32x4*>(p);
-                fb[j][1] = *reinterpret_cast<const f32x4*>(p + 4);
-            }
+            for (int j = 0; j < TN; ++j)
+                fb[j] = *reinterpret_cast<const f32x4*>(Bs + (wn * WN + j * 32 + r) * LDK + h * KH + q4 * 4);
 #pragma unroll
-            for (int s = 0; s < 8; ++s)
+            for (int s = 0; s < 4; ++s)
 #pragma unroll
                 for (int i = 0; i < TM; ++i)
 #pragma unroll
                     for (int j = 0; j < TN; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s >> 2][s & 3], fb[j][s >> 2][s & 3],
-                                                                         acc[i][j], 0, 0, 0);
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
         }
         __syncthreads();
     }
@@ -256,29 +266,112 @@ __global__ __launch_bounds__(NT_, 2) void gemm_f32_kernel(Args a) {
 
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
-template <int OP, int BM, int BN, int WARPS_M>
+template <int OP, int BM, int BN, int WARPS_M, int BK>
 void launch(Args a) {
     a.tiles_m = ppo_divup(a.M, BM);
     a.tiles_n = ppo_divup(a.N, BN);
     if (a.splits < 1) a.splits = 1;
     const long grid = (long)a.tiles_m * a.tiles_n * a.splits;
     PPO_REQUIRE(grid > 0 && grid < (1L << 31), "gemm: grid out of range");
-    hipLaunchKernelGGL((gemm_f32_kernel<OP, BM, BN, WARPS_M>), dim3((unsigned)grid), dim3(NT_), 0,
+    hipLaunchKernelGGL((gemm_f32_kernel<OP, BM, BN, WARPS_M, BK>), dim3((unsigned)grid), dim3(NT_), 0,
                        ppo::stream(), a);
     PPO_LAUNCH_CHECK();
 }
 
-// Tile selection: skinny-N (layer outputs 1 / A, Pendulum input 3), skinny-M, or 128x128.
+// Tile configurations: {BM, BN, WARPS_M, BK}
+struct TileCfg { int bm, bn, wm, bk; };
+constexpr TileCfg kCfgs[] = {
+    {128, 128, 2, 16},    // 0: main tile, 4 waves of 64x64, ≤128 VGPRs → 4 WG/CU
+    {128, 128, 2, 32},    // 1: main tile, deeper k-step
+    {128, 32, 4, 16},     // 2: skinny N (layer outputs 1 / A, tiny inputs)
+    {32, 128, 1, 16},     // 3: skinny M (grad_W of the output layer)
+    {64, 64, 2, 16},      // 4: small problems (Pendulum-sized layers)
+    {128, 64, 2, 16},     // 5: 4 waves of 64x32
+    {256, 128, 4, 16},    // 6: 4 waves of 64x128
+};
+constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
+int g_force_cfg = -1;          // tuning override (ppo_gemm_tune)
+int g_splitk_target = 1024;    // workgroups the split-K grad_W aims for
+
 template <int OP>
-void dispatch(Args& a) {
-    if (a.N <= 32 && a.M > 32)       launch<OP, 256, 32, 4>(a);
-    else if (a.M <= 32 && a.N > 32)  launch<OP, 32, 256, 1>(a);
-    else if (a.M <= 64 || a.N <= 64) launch<OP, 64, 64, 2>(a);
-    else                             launch<OP, 128, 128, 2>(a);
+void launch_cfg(int c, const Args& a) {
+    switch (c) {
+        case 0: launch<OP, 128, 128, 2, 16>(a); break;
+        case 1: launch<OP, 128, 128, 2, 32>(a); break;
+        case 2: launch<OP, 128, 32, 4, 16>(a); break;
+        case 3: launch<OP, 32, 128, 1, 16>(a); break;
+        case 4: launch<OP, 64, 64, 2, 16>(a); break;
+        case 5: launch<OP, 128, 64, 2, 16>(a); break;
+        default: launch<OP, 256, 128, 4, 16>(a); break;
+    }
 }
 
-int tile_m_for(int M, int N) { return (N <= 32 && M > 32) ? 256 : (M <= 32 && N > 32) ? 32 : (M <= 64 || N <= 64) ? 64 : 128; }
-int tile_n_for(int M, int N) { return (N <= 32 && M > 32) ? 32 : (M <= 32 && N > 32) ? 256 : (M <= 64 || N <= 64) ? 64 : 128; }
+// Measured on MI355X (tools/gemm_sweep.py): 128x128/BK16 at 4 WG/CU for large forward / grad_x
+// grids; 128x64 when a 128x128 grid would not give every CU two workgroups; 128x64 with a
+// ~1024-workgroup split-K for grad_W; skinny tiles for the 1- and A-wide output layers.
+int pick_cfg(int op, int M, int N) {
+    if (g_force_cfg >= 0 && g_force_cfg < kNumCfgs) return g_force_cfg;
+    if (N <= 32 && M > 32) return 2;
+    if (M <= 32 && N > 32) return 3;
+    if (M <= 64 || N <= 64) return 4;
+    if (op == OP_TN) return 5;
+    const long tiles = (long)ppo_divup(M, 128) * ppo_divup(N, 128);
+    return tiles < 512 ? 5 : 0;
+}
+
+void fwd(float* y, const float* x, const float* W, const float* b, int m, int n, int l, int relu, int cfg) {
+    Args a{};
+    a.A = x; a.lda = n; a.B = W; a.ldb = n; a.C = y; a.ldc = l;
+    a.M = m; a.N = l; a.K = n; a.kchunk = n; a.splits = 1;
+    a.bias = b; a.relu = relu;
+    a.vec_a = (n % 4 == 0) && aligned16(x);
+    a.vec_b = (n % 4 == 0) && aligned16(W);
+    launch_cfg<OP_NT>(cfg < 0 ? pick_cfg(OP_NT, m, l) : cfg, a);
+}
+
+void bwd_x(float* gx, const float* g, const float* W, const float* mask, int m, int n, int l, int cfg) {
+    Args a{};
+    a.A = g; a.lda = l; a.B = W; a.ldb = n; a.C = gx; a.ldc = n;
+    a.M = m; a.N = n; a.K = l; a.kchunk = l; a.splits = 1;
+    a.mask = mask; a.ldmask = n;
+    a.vec_a = (l % 4 == 0) && aligned16(g);
+    a.vec_b = (n % 4 == 0) && aligned16(W);
+    launch_cfg<OP_NN>(cfg < 0 ? pick_cfg(OP_NN, m, n) : cfg, a);
+}
+
+// grad_W reduces over the minibatch (K = m): split-K so the grid fills the chip; f32 atomics
+// into an output that is zero on entry (zeroed != 0) or zeroed here.
+void bwd_w(float* gW, float* gb, const float* g, const float* x, int m, int n, int l, int zeroed, int cfg) {
+    if (m <= 0) {
+        if (!zeroed) {
+            phip_memset(gW, 0, sizeof(float) * (size_t)l * n);
+            if (gb) phip_memset(gb, 0, sizeof(float) * (size_t)l);
+        }
+        return;
+    }
+    const int c = cfg < 0 ? pick_cfg(OP_TN, l, n) : cfg;
+    const TileCfg& tc = kCfgs[c];
+    Args a{};
+    a.A = g; a.lda = l; a.B = x; a.ldb = n; a.C = gW; a.ldc = n;
+    a.M = l; a.N = n; a.K = m;
+    a.gbias = gb;
+    a.vec_a = (l % 4 == 0) && aligned16(g);
+    a.vec_b = (n % 4 == 0) && aligned16(x);
+    const long tiles = (long)ppo_divup(l, tc.bm) * ppo_divup(n, tc.bn);
+    int splits = (int)((g_splitk_target + tiles - 1) / tiles);
+    const int max_splits = m / (8 * tc.bk) > 0 ? m / (8 * tc.bk) : 1;     // ≥ 8 k-tiles per split
+    if (splits > max_splits) splits = max_splits;
+    if (splits < 1) splits = 1;
+    int kchunk = ppo_divup(m, splits);
+    kchunk = ppo_divup(kchunk, tc.bk) * tc.bk;
+    splits = ppo_divup(m, kchunk);
+    a.kchunk = kchunk; a.splits = splits;
+    if (splits > 1 && !zeroed) {
+        phip_memset(gW, 0, sizeof(float) * (size_t)l * n);
+        if (gb) phip_memset(gb, 0, sizeof(float) * (size_t)l);
+    }
+    launch_cfg<OP_TN>(c, a);
+}
 
 }  // namespace
 
@@ -287,59 +380,66 @@ extern "C" {
 void phip_linear_fwd(float* y, const float* x, const float* W, const float* b, int m, int n, int l, int relu) {
     if (m <= 0 || l <= 0) return;
     PPO_REQUIRE(y && x && W && n > 0, "phip_linear_fwd: null operand");
-    Args a{};
-    a.A = x; a.lda = n; a.B = W; a.ldb = n; a.C = y; a.ldc = l;
-    a.M = m; a.N = l; a.K = n; a.kchunk = n; a.splits = 1;
-    a.bias = b; a.relu = relu;
-    a.vec_a = (n % 4 == 0) && aligned16(x);
-    a.vec_b = (n % 4 == 0) && aligned16(W);
     ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l);
-    dispatch<OP_NT>(a);
+    fwd(y, x, W, b, m, n, l, relu, -1);
 }
 
 void phip_linear_bwd_x(float* gx, const float* g, const float* W, const float* mask, int m, int n, int l) {
     if (m <= 0 || n <= 0) return;
     PPO_REQUIRE(gx && g && W && l > 0, "phip_linear_bwd_x: null operand");
-    Args a{};
-    a.A = g; a.lda = l; a.B = W; a.ldb = n; a.C = gx; a.ldc = n;
-    a.M = m; a.N = n; a.K = l; a.kchunk = l; a.splits = 1;
-    a.mask = mask; a.ldmask = n;
-    a.vec_a = (l % 4 == 0) && aligned16(g);
-    a.vec_b = (n % 4 == 0) && aligned16(W);
     ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l);
-    dispatch<OP_NN>(a);
+    bwd_x(gx, g, W, mask, m, n, l, -1);
+}
+
+void phip_linear_bwd_w_ex(float* gW, float* gb, const float* g, const float* x, int m, int n, int l, int zeroed) {
+    if (l <= 0 || n <= 0) return;
+    PPO_REQUIRE(gW && g && x, "phip_linear_bwd_w: null operand");
+    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l);
+    bwd_w(gW, gb, g, x, m, n, l, zeroed, -1);
 }
 
 void phip_linear_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, int n, int l) {
-    if (l <= 0 || n <= 0) return;
-    PPO_REQUIRE(gW && g && x, "phip_linear_bwd_w: null operand");
-    Args a{};
-    a.A = g; a.lda = l; a.B = x; a.ldb = n; a.C = gW; a.ldc = n;
-    a.M = l; a.N = n; a.K = m;
-    a.gbias = gb;
-    a.vec_a = (l % 4 == 0) && aligned16(g);
-    a.vec_b = (n % 4 == 0) && aligned16(x);
-    // split-K over the minibatch: aim for ~2 workgroups per CU, ≥ 8 k-tiles per split
-    const long tiles = (long)ppo_divup(l, tile_m_for(l, n)) * ppo_divup(n, tile_n_for(l, n));
-    int splits = (int)((512 + tiles - 1) / tiles);
-    const int max_splits = m / (8 * BK) > 0 ? m / (8 * BK) : 1;
-    if (splits > max_splits) splits = max_splits;
-    if (splits < 1) splits = 1;
-    int kchunk = ppo_divup(m, splits);
-    kchunk = ppo_divup(kchunk, BK) * BK;
-    splits = ppo_divup(m, kchunk);
-    a.kchunk = kchunk; a.splits = splits;
-    if (m <= 0) {   // empty batch: gradients are zero
-        phip_memset(gW, 0, sizeof(float) * (size_t)l * n);
-        if (gb) phip_memset(gb, 0, sizeof(float) * (size_t)l);
-        return;
-    }
-    if (splits > 1) {
-        phip_memset(gW, 0, sizeof(float) * (size_t)l * n);
-        if (gb) phip_memset(gb, 0, sizeof(float) * (size_t)l);
-    }
-    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l);
-    dispatch<OP_TN>(a);
+    phip_linear_bwd_w_ex(gW, gb, g, x, m, n, l, 0);
+}
+
+void ppo_gemm_tune(int force_cfg, int splitk_target) {
+    g_force_cfg = force_cfg;
+    if (splitk_target > 0) g_splitk_target = splitk_target;
+}
+
+// Tuning / roofline utility: average device time (µs) of one launch of `op` (0 fwd, 1 grad_x,
+// 2 grad_W) at the given shape, measured with HIP events on libppo's stream.
+double ppo_bench_gemm(int op, int m, int n, int l, int iters, int cfg) {
+    ppo::ensure_device();
+    const size_t sx = (size_t)m * n, sw = (size_t)l * n, sy = (size_t)m * l;
+    float* x = (float*)phip_malloc(sizeof(float) * sx);
+    float* W = (float*)phip_malloc(sizeof(float) * sw);
+    float* y = (float*)phip_malloc(sizeof(float) * (sy > sx ? sy : sx));
+    float* b = (float*)phip_malloc(sizeof(float) * (size_t)(l > n ? l : n));
+    float* gw = (float*)phip_malloc(sizeof(float) * sw);
+    phip_fill_uniform(x, (long)sx, 1, -1.f, 1.f);
+    phip_fill_uniform(W, (long)sw, 2, -0.1f, 0.1f);
+    phip_fill_uniform(y, (long)(sy > sx ? sy : sx), 3, -1.f, 1.f);
+    phip_fill_uniform(b, (long)(l > n ? l : n), 4, -0.1f, 0.1f);
+    auto run = [&]() {
+        if (op == 0) fwd(y, x, W, b, m, n, l, 1, cfg);
+        else if (op == 1) bwd_x(x, y, W, nullptr, m, n, l, cfg);
+        else bwd_w(gw, b, y, x, m, n, l, 0, cfg);
+    };
+    for (int i = 0; i < 3; ++i) run();
+    hipEvent_t e0, e1;
+    PPO_CHECK(hipEventCreate(&e0));
+    PPO_CHECK(hipEventCreate(&e1));
+    PPO_CHECK(hipEventRecord(e0, ppo::stream()));
+    for (int i = 0; i < iters; ++i) run();
+    PPO_CHECK(hipEventRecord(e1, ppo::stream()));
+    PPO_CHECK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    PPO_CHECK(hipEventElapsedTime(&ms, e0, e1));
+    PPO_CHECK(hipEventDestroy(e0));
+    PPO_CHECK(hipEventDestroy(e1));
+    phip_free(x); phip_free(W); phip_free(y); phip_free(b); phip_free(gw);
+    return 1000.0 * ms / (iters > 0 ? iters : 1);
 }
 
 }  // extern "C"

@@ -101,15 +101,18 @@ __global__ void log_prob_bwd_kernel(const float* __restrict__ mu, const float* _
     for (int j = threadIdx.x; j < A; j += TPB) sacc[j] = 0.f;
     __syncthreads();
     const int i = blockIdx.x * TPB + threadIdx.x;
-    if (i < m) {
-        const float g = grad_in[i];
-        for (int j = 0; j < A; ++j) {
+    const float g = i < m ? grad_in[i] : 0.f;
+    for (int j = 0; j < A; ++j) {          // column sums: wave shuffle, then one LDS add per wave
+        float c = 0.f;
+        if (i < m) {
             const long k = (long)i * A + j;
             const float d = action[k] - mu[k];
             const float e = expf(-2 * log_std[j]);
             grad_mu[k] = d * e * g;
-            atomicAdd(&sacc[j], (-1 + d * d * e) * g);
+            c = (-1 + d * d * e) * g;
         }
+        c = wave_sum(c);
+        if ((threadIdx.x & 63) == 0) atomicAdd(&sacc[j], c);
     }
     __syncthreads();
     for (int j = threadIdx.x; j < A; j += TPB) atomicAdd(grad_log_std + j, sacc[j]);
@@ -169,19 +172,23 @@ __global__ void policy_head_kernel(const float* __restrict__ mu, const float* __
         gls[j] = 0.f;
     }
     __syncthreads();
-    float s = 0.f;
+    float s = 0.f, g = 0.f;
     const int i = blockIdx.x * TPB + threadIdx.x;
+    const float* mr = mu + (long)i * A;
+    const float* ar = action + (long)i * A;
     if (i < m) {
-        const float* mr = mu + (long)i * A;
-        const float* ar = action + (long)i * A;
         const float lp = log_prob_row(mr, log_std, ar, A);
-        float g;
         s = surrogate(adv[i], lp, old_lp[i], eps, m, &g);
-        for (int j = 0; j < A; ++j) {
+    }
+    for (int j = 0; j < A; ++j) {          // column sums: wave shuffle, then one LDS add per wave
+        float c = 0.f;
+        if (i < m) {
             const float d = ar[j] - mr[j];
             grad_mu[(long)i * A + j] = d * e2[j] * g;
-            atomicAdd(&gls[j], (-1 + d * d * e2[j]) * g);
+            c = (-1 + d * d * e2[j]) * g;
         }
+        c = wave_sum(c);
+        if ((threadIdx.x & 63) == 0) atomicAdd(&gls[j], c);
     }
     s = block_sum(s, red);
     __syncthreads();

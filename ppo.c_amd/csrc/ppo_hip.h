@@ -34,6 +34,8 @@ void phip_linear_fwd(float* y, const float* x, const float* W, const float* b, i
 void phip_linear_bwd_x(float* gx, const float* g, const float* W, const float* mask, int m, int n, int l);
 /* gW[l,n] = g[m,l]ᵀ·x[m,n] and gb[l] = Σ_m g[m,l] (K4 + K7 fused); overwrites */
 void phip_linear_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, int n, int l);
+/* same, with gW/gb already zero on entry when `zeroed` (one memset per backward instead of two per layer) */
+void phip_linear_bwd_w_ex(float* gW, float* gb, const float* g, const float* x, int m, int n, int l, int zeroed);
 
 /* ---------------- element-wise / heads (kernels.hip) ---------------- */
 void phip_relu(float* x, long count);

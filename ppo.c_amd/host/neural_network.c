@@ -128,10 +128,13 @@ void nn_backward_dev(NeuralNetwork* nn, const float* d_grad_out, int m, int want
         phip_relu_bwd(nn->layers[L].d_input, top, (long)m * nn->output_size);
         g = top;
     }
+    /* one memset for every layer's gradient (split-K grad_W accumulates atomically);
+     * the trailing extra_floats (policy log_std grad) are owned by the caller and left alone */
+    phip_memset(nn->d_grads, 0, sizeof(float) * (size_t)nn->num_params);
     for (int i = L - 1; i >= 0; i--) {
         Layer* ly = &nn->layers[i];
         const float* x = i == 0 ? nn->d_x0 : ly->d_input;
-        phip_linear_bwd_w(ly->d_grad_weights, ly->d_grad_biases, g, x, m, ly->input_size, ly->output_size);
+        phip_linear_bwd_w_ex(ly->d_grad_weights, ly->d_grad_biases, g, x, m, ly->input_size, ly->output_size, 1);
         if (i > 0 || want_grad_x0) {
             const float* mask = (i > 0 && nn_is_relu(nn, i - 1)) ? ly->d_input : NULL;
             phip_linear_bwd_x(ly->d_grad_x, g, ly->d_weights, mask, m, ly->input_size, ly->output_size);

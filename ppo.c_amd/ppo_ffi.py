@@ -191,7 +191,11 @@ _lib = None
 
 
 def load(path=LIB_PATH):
-    """Load libppo.so (RTLD_GLOBAL so a later `import torch` reuses its HIP runtime)."""
+    """Load libppo.so.
+
+    In a process that also uses torch, `import torch` BEFORE calling load(): libppo then binds to the
+    HIP runtime torch already mapped (same soname, libamdhip64.so.7) and the process holds one runtime.
+    """
     global _lib
     if _lib is not None:
         return _lib

@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""GEMM tile/split sweep on the MI355X: device µs and TFLOP/s per (op, shape, tile config).
+
+    python ppo.c_amd/tools/gemm_sweep.py [--quick]
+op 0 = forward (bias+ReLU), 1 = grad_x, 2 = grad_W (+bias grad, split-K).
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import ppo_ffi  # noqa: E402
+
+CFG_NAMES = {0: "128x128/bk16", 1: "128x128/bk32", 2: "128x32/bk16", 3: "32x128/bk16", 4: "64x64/bk16",
+             5: "128x64/bk16", 6: "256x128/bk16"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--quick", action="store_true")
+    ap.add_argument("--out", default="")
+    args = ap.parse_args()
+    lib = ppo_ffi.load()
+    lib.ppo_bench_gemm.restype = C.c_double
+    lib.ppo_bench_gemm.argtypes = [C.c_int] * 5 + [C.c_int]
+    lib.ppo_gemm_tune.argtypes = [C.c_int, C.c_int]
+    lib.ppo_set_device(0)
+    B = 32768
+    shapes = [  # (m, n, l) = (batch, in, out) — C4 minibatch layers and the GAE forward
+        (B, 376, 512), (B, 512, 512), (B, 512, 17), (B, 512, 1), (1 << 20, 512, 512),
+        (8192, 256, 256), (8192, 17, 256),
+    ]
+    rows = []
+    for (m, n, l) in shapes:
+        for op in (0, 1, 2):
+            if op == 1 and n < 64:
+                continue
+            cfgs = [-1, 0, 1, 5, 6] if min(n, l) > 32 else [-1, 2, 3, 4]
+            if args.quick:
+                cfgs = [-1]
+            targets = [512] if op != 2 else [256, 512, 1024, 2048]
+            for cfg in cfgs:
+                for tgt in targets:
+                    lib.ppo_gemm_tune(-1, tgt)
+                    us = lib.ppo_bench_gemm(op, m, n, l, 10 if m < (1 << 20) else 3, cfg)
+                    tf = 2.0 * m * n * l / (us * 1e-6) / 1e12
+                    rows.append(dict(op=op, m=m, n=n, l=l, cfg=CFG_NAMES.get(cfg, "auto"), splitk=tgt, us=us,
+                                     tflops=tf))
+                    print(f"op{op} m={m:8d} n={n:4d} l={l:4d} {CFG_NAMES.get(cfg, 'auto'):14s} "
+                          f"split_target={tgt:5d} {us:9.1f} us {tf:7.1f} TF/s", flush=True)
+    lib.ppo_gemm_tune(-1, 1024)
+    if args.out:
+        json.dump(rows, open(args.out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
