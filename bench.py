@@ -57,6 +57,17 @@ def algorithmic_flops(S, H, A, N, B, n_v=10, n_p=4):
     return 4 * N * P_v + n_v * nb * (6 * P_v - 2 * S * H[0]) + n_p * nb * (6 * P_mu - 2 * S * H[0])
 
 
+def pmc_traffic():
+    """HBM bytes per GEMM launch from the newest committed PMC pass (profiles/rNN_pmc_gemm.json:
+    separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of this bench, (2·FETCH + WRITE)·1 KiB)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_gemm.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    return d.get("hbm_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
+
+
 def cpu_baseline(lib, ppo, S, H, A, N, B, sample_envs=16, steps=2):
     """The oracle (plain-C restatement of the reference CPU path, OpenBLAS sgemm, 1 thread) on a bounded
     sample of the same workload; extrapolated to one full update with the update formula."""
@@ -222,8 +233,10 @@ def main():
     }
     if gemm_n and gemm_ms > 0:
         achieved = gemm_flops / (gemm_ms * 1e-3) / 1e12
+        traffic, traffic_src = pmc_traffic()
         result["roofline"] = {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP32_MFMA_TFLOPS,
-                              "unit": "TFLOP/s", "frac": achieved / PEAK_FP32_MFMA_TFLOPS, "traffic": None,
+                              "unit": "TFLOP/s", "frac": achieved / PEAK_FP32_MFMA_TFLOPS, "traffic": traffic,
+                              "traffic_source": traffic_src,
                               "kernel": "gemm_f32_kernel (all linear-layer launches: Σ 2MNK / Σ HIP-event time)",
                               "launches": gemm_n, "avg_launch_us": 1000.0 * gemm_ms / gemm_n,
                               "algorithmic_flop_per_launch": gemm_flops / gemm_n}

@@ -1,0 +1,76 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 CSV output into the files committed under profiles/.
+
+    python ppo.c_amd/tools/summarize_profile.py --trace DIR/r1_kernel_trace.csv --stats DIR/r1_kernel_stats.csv \
+        [--fetch pmc/fetch_counter_collection.csv --write pmc/write_counter_collection.csv] --tag r01
+
+Writes profiles/<tag>_kernel_stats.csv (copy), profiles/<tag>_gemm_by_shape.txt (per tile/grid:
+launches, average µs) and, with PMC files, profiles/<tag>_pmc_gemm.json: average HBM bytes per GEMM
+launch = (2·FETCH_SIZE + WRITE_SIZE)·1024 (gfx950: FETCH_SIZE reports half of a wide coalesced read,
+MI355X_MICROARCH.md §HBM).
+"""
+import argparse
+import collections
+import csv
+import json
+import os
+import shutil
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..")
+
+
+def gemm_key(name, grid_threads):
+    tmpl = name.split("<", 1)[1].split(">", 1)[0] if "<" in name else name
+    return f"gemm<{tmpl}> grid={int(grid_threads) // 256}"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--trace", required=True)
+    ap.add_argument("--stats", required=True)
+    ap.add_argument("--fetch")
+    ap.add_argument("--write")
+    ap.add_argument("--tag", default="r01")
+    args = ap.parse_args()
+    out = os.path.join(ROOT, "profiles")
+    os.makedirs(out, exist_ok=True)
+    shutil.copy(args.stats, os.path.join(out, f"{args.tag}_kernel_stats.csv"))
+
+    by = collections.defaultdict(list)
+    total = 0
+    for r in csv.DictReader(open(args.trace)):
+        d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        total += d
+        if "gemm_f32_kernel" in r["Kernel_Name"]:
+            by[gemm_key(r["Kernel_Name"], r["Grid_Size_X"])].append(d)
+    g_tot = sum(sum(v) for v in by.values())
+    lines = [f"# rocprofv3 --kernel-trace: GEMM launches by tile config and grid ({args.tag})",
+             f"# all kernels: {total / 1e6:.1f} ms; gemm_f32_kernel: {g_tot / 1e6:.1f} ms "
+             f"({100 * g_tot / max(1, total):.1f} %), {sum(len(v) for v in by.values())} launches, "
+             f"avg {g_tot / max(1, sum(len(v) for v in by.values())) / 1e3:.1f} us"]
+    for k, v in sorted(by.items(), key=lambda kv: -sum(kv[1])):
+        lines.append(f"{k:48s} launches={len(v):6d} avg_us={sum(v) / len(v) / 1e3:9.1f} "
+                     f"share={100 * sum(v) / g_tot:5.1f}%")
+    open(os.path.join(out, f"{args.tag}_gemm_by_shape.txt"), "w").write("\n".join(lines) + "\n")
+    print("\n".join(lines))
+
+    if args.fetch and args.write:
+        def load(fn, ctr):
+            vals = []
+            for r in csv.DictReader(open(fn)):
+                if r["Counter_Name"] == ctr and "gemm_f32_kernel" in r["Kernel_Name"]:
+                    vals.append(float(r["Counter_Value"]))
+            return vals
+        f, w = load(args.fetch, "FETCH_SIZE"), load(args.write, "WRITE_SIZE")
+        n = len(f)
+        res = {"launches": n,
+               "fetch_size_kb_sum": sum(f), "write_size_kb_sum": sum(w),
+               "hbm_bytes_per_launch": (2 * sum(f) + sum(w)) * 1024 / max(1, n),
+               "note": "(2*FETCH_SIZE + WRITE_SIZE)*1024 per gemm_f32_kernel launch, averaged over one "
+                       "bench.py update (+ synthetic fill); separate --pmc passes for each counter"}
+        json.dump(res, open(os.path.join(out, f"{args.tag}_pmc_gemm.json"), "w"), indent=1)
+        print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
