@@ -78,8 +78,9 @@ void ppo_sample_action_device(void* policy, float* d_state, float* d_action, flo
 void ppo_fill_synthetic(void* ppo, int n_envs, int horizon, unsigned long long seed, float p_terminate);
 
 /* ---------------- GEMM tuning utilities ---------------- */
-/* force a tile configuration (−1 = automatic) and the split-K workgroup target of grad_W */
-void   ppo_gemm_tune(int force_cfg, int splitk_target);
+/* force a tile configuration (−1 = automatic) and the split-K workgroup target of grad_W
+ * (≤ 0 keeps the current one); returns the number of tile configurations */
+int    ppo_gemm_tune(int force_cfg, int splitk_target);
 /* average device µs of one launch: op 0 = forward (bias+ReLU), 1 = grad_x, 2 = grad_W (+bias grad);
  * m = batch, n = in, l = out; cfg −1 = automatic */
 double ppo_bench_gemm(int op, int m, int n, int l, int iters, int cfg);

@@ -46,6 +46,15 @@ struct Args {
 // Loaders.  "kcont": element (row r, k) at P[r*ld + k]  (x, g in grad_x, W in forward)
 //           "mncont": element (row r, k) at P[k*ld + r] (W in grad_x, g and x in grad_W)
 // Both fill an LDS image [R][BK+4] with zeros outside [0,Rmax) × [kbeg,kend).
+//
+// VEC: the contiguous extent (kend for kcont, Rmax for mncont) and the leading dimension are
+// multiples of 4 and the base is 16-B aligned, so every float4 lies wholly inside or wholly outside
+// the operand.  The load address is then clamped into the operand: the k-loop has no branches (the
+// guarded scalar form compiles to ~20 exec-mask branches per k-tile).  Rows past Rmax only feed
+// output rows/columns that are never stored, so they need no masking; k past kend must be zero and
+// is masked by a select at LDS-store time — never right after the load, where it would make the
+// wave wait for its prefetch before the current tile's MFMAs.  !VEC keeps the guarded scalar form
+// for odd shapes (S = 3, A = 17).
 // ---------------------------------------------------------------------------
 template <int R, int BK>
 struct Stage {
@@ -54,25 +63,33 @@ struct Stage {
     static constexpr int ITERS = (TOTAL + NT_ - 1) / NT_;
     static constexpr int KQ = BK / 4;                      // float4s per kcont row
     f32x4 v[ITERS];
+    bool kok[ITERS];                                       // VEC: element's k inside [k0, kend)
 
+    __device__ __forceinline__ f32x4 masked(int it) const {
+        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+        return kok[it] ? v[it] : z;
+    }
+
+    template <bool VEC>
     __device__ __forceinline__ void load_kcont(const float* __restrict__ P, int ld, int r0, int Rmax, int k0,
-                                               int kend, bool vec, int tid) {
+                                               int kend, int tid) {
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) {
             const int idx = tid + it * NT_;
             f32x4 x = {0.f, 0.f, 0.f, 0.f};
+            kok[it] = true;
             if (TOTAL % NT_ == 0 || idx < TOTAL) {
                 const int kq = idx % KQ, r = idx / KQ;
                 const int gr = r0 + r, gk = k0 + kq * 4;
-                if (gr < Rmax) {
+                if (VEC) {
+                    kok[it] = gk < kend;
+                    const float* p = P + (long)(gr < Rmax ? gr : Rmax - 1) * ld + (gk < kend ? gk : kend - 4);
+                    x = *reinterpret_cast<const f32x4*>(p);
+                } else if (gr < Rmax) {
                     const float* p = P + (long)gr * ld + gk;
-                    if (vec && gk + 3 < kend) {
-                        x = *reinterpret_cast<const f32x4*>(p);
-                    } else {
 #pragma unroll
-                        for (int e = 0; e < 4; ++e)
-                            if (gk + e < kend) x[e] = p[e];
-                    }
+                    for (int e = 0; e < 4; ++e)
+                        if (gk + e < kend) x[e] = p[e];
                 }
             }
             v[it] = x;
@@ -84,7 +101,7 @@ struct Stage {
             const int idx = tid + it * NT_;
             if (TOTAL % NT_ == 0 || idx < TOTAL) {
                 const int kq = idx % KQ, r = idx / KQ;
-                *reinterpret_cast<f32x4*>(lds + r * LDK + kq * 4) = v[it];
+                *reinterpret_cast<f32x4*>(lds + r * LDK + kq * 4) = masked(it);
             }
         }
     }
@@ -95,25 +112,27 @@ struct Stage {
         nq = rest % (R / 4);
         kk = (rest / (R / 4)) * 8 + kk_lo;
     }
+    template <bool VEC>
     __device__ __forceinline__ void load_mncont(const float* __restrict__ P, int ld, int r0, int Rmax, int k0,
-                                                int kend, bool vec, int tid) {
+                                                int kend, int tid) {
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) {
             const int idx = tid + it * NT_;
             f32x4 x = {0.f, 0.f, 0.f, 0.f};
+            kok[it] = true;
             if (TOTAL % NT_ == 0 || idx < TOTAL) {
                 int kk, nq;
                 mn_coords(idx, kk, nq);
                 const int gk = k0 + kk, gr = r0 + nq * 4;
-                if (gk < kend) {
+                if (VEC) {
+                    kok[it] = gk < kend;
+                    const float* p = P + (long)(gk < kend ? gk : kend - 1) * ld + (gr < Rmax ? gr : Rmax - 4);
+                    x = *reinterpret_cast<const f32x4*>(p);
+                } else if (gk < kend) {
                     const float* p = P + (long)gk * ld + gr;
-                    if (vec && gr + 3 < Rmax) {
-                        x = *reinterpret_cast<const f32x4*>(p);
-                    } else {
 #pragma unroll
-                        for (int e = 0; e < 4; ++e)
-                            if (gr + e < Rmax) x[e] = p[e];
-                    }
+                    for (int e = 0; e < 4; ++e)
+                        if (gr + e < Rmax) x[e] = p[e];
                 }
             }
             v[it] = x;
@@ -126,29 +145,32 @@ struct Stage {
             if (TOTAL % NT_ == 0 || idx < TOTAL) {
                 int kk, nq;
                 mn_coords(idx, kk, nq);
+                const f32x4 x = masked(it);
 #pragma unroll
-                for (int e = 0; e < 4; ++e) lds[(nq * 4 + e) * LDK + kk] = v[it][e];
+                for (int e = 0; e < 4; ++e) lds[(nq * 4 + e) * LDK + kk] = x[e];
             }
         }
     }
 };
 
-// BK=16 tiles fit ≤128 VGPRs → 4 workgroups (16 waves) per CU; BK=32 needs 3, 256x128 needs 2
+// Workgroups per CU the tile is built for: BK=16 128x128 fits ≤128 VGPRs → 4 (16 waves), BK=32
+// needs 3, 256x128 needs 2.  With DBUF the LDS image doubles (4 × 40 KiB = the whole 160 KiB).
 constexpr int min_waves(int area, int bk) { return area >= 256 * 128 ? 2 : (bk >= 32 ? 3 : 4); }
 
-template <int OP, int BM, int BN, int WARPS_M, int BK>
+// DBUF: two LDS images; the staged tile t+1 is written into the idle image behind tile t's MFMAs,
+// so each k-tile needs one barrier instead of two.
+template <int OP, int BM, int BN, int WARPS_M, int BK, bool VEC, bool DBUF>
 __global__ __launch_bounds__(NT_, min_waves(BM * BN, BK)) void gemm_f32_kernel(Args a) {
     constexpr int WARPS_N = 4 / WARPS_M;
     constexpr int WM = BM / WARPS_M, WN = BN / WARPS_N;
     constexpr int TM = WM / 32, TN = WN / 32;
     constexpr int LDK = BK + 4;        // BK=16: 20, BK=32: 36 floats — ds_read_b128 conflict-free
     constexpr int KH = BK / 2;         // k per lane-half per tile (k-permutation)
+    constexpr int IMG = (BM + BN) * LDK;
     static_assert(TM >= 1 && TN >= 1, "wave tile must be a multiple of 32x32");
     static_assert(BK == 16 || BK == 32, "BK");
 
-    __shared__ __attribute__((aligned(16))) float lds[(BM + BN) * LDK];
-    float* As = lds;
-    float* Bs = lds + BM * LDK;
+    __shared__ __attribute__((aligned(16))) float lds[(DBUF ? 2 : 1) * IMG];
 
     // XCD-aware bijective remap of the linear block id (guide §5 "XCD swizzle must be bijective")
     const int nwg = gridDim.x, b = blockIdx.x;
@@ -182,28 +204,25 @@ __global__ __launch_bounds__(NT_, min_waves(BM * BN, BK)) void gemm_f32_kernel(A
 
     Stage<BM, BK> sa;
     Stage<BN, BK> sb;
-    const bool va = a.vec_a, vb = a.vec_b;
 
     auto load = [&](int k0) {
-        if (OP == OP_TN) sa.load_mncont(a.A, a.lda, m0, a.M, k0, kend, va, tid);
-        else             sa.load_kcont(a.A, a.lda, m0, a.M, k0, kend, va, tid);
-        if (OP == OP_NT) sb.load_kcont(a.B, a.ldb, n0, a.N, k0, kend, vb, tid);
-        else             sb.load_mncont(a.B, a.ldb, n0, a.N, k0, kend, vb, tid);
+        if (OP == OP_TN) sa.template load_mncont<VEC>(a.A, a.lda, m0, a.M, k0, kend, tid);
+        else             sa.template load_kcont<VEC>(a.A, a.lda, m0, a.M, k0, kend, tid);
+        if (OP == OP_NT) sb.template load_kcont<VEC>(a.B, a.ldb, n0, a.N, k0, kend, tid);
+        else             sb.template load_mncont<VEC>(a.B, a.ldb, n0, a.N, k0, kend, tid);
     };
-
-    if (kbeg < kend) load(kbeg);
-    for (int k0 = kbeg; k0 < kend; k0 += BK) {
-        if (OP == OP_TN) sa.store_mncont(As, tid); else sa.store_kcont(As, tid);
-        if (OP == OP_NT) sb.store_kcont(Bs, tid);  else sb.store_mncont(Bs, tid);
-        __syncthreads();
-        if (k0 + BK < kend) load(k0 + BK);        // in flight during this tile's MFMAs
-
+    auto store = [&](float* img) {
+        if (OP == OP_TN) sa.store_mncont(img, tid); else sa.store_kcont(img, tid);
+        if (OP == OP_NT) sb.store_kcont(img + BM * LDK, tid); else sb.store_mncont(img + BM * LDK, tid);
+    };
+    auto compute = [&](const float* img) {
+        const float* As = img;
+        const float* Bs = img + BM * LDK;
         if (do_bsum) {
             const int row = tid / TPR, seg = tid % TPR;
 #pragma unroll
             for (int kk = 0; kk < KPT; ++kk) bsum += As[row * LDK + seg * KPT + kk];
         }
-
 #pragma unroll
         for (int q4 = 0; q4 < KH / 4; ++q4) {
             f32x4 fa[TM], fb[TN];
@@ -221,7 +240,32 @@ __global__ __launch_bounds__(NT_, min_waves(BM * BN, BK)) void gemm_f32_kernel(A
                     for (int j = 0; j < TN; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
         }
+    };
+
+    if (DBUF) {
+        int cur = 0;
+        if (kbeg < kend) {
+            load(kbeg);
+            store(lds);
+        }
         __syncthreads();
+        for (int k0 = kbeg; k0 < kend; k0 += BK) {
+            const bool more = k0 + BK < kend;
+            if (more) load(k0 + BK);               // in flight during this tile's MFMAs
+            compute(lds + cur * IMG);
+            if (more) store(lds + (cur ^ 1) * IMG);  // the idle image: its last readers passed the barrier
+            __syncthreads();
+            cur ^= 1;
+        }
+    } else {
+        if (kbeg < kend) load(kbeg);
+        for (int k0 = kbeg; k0 < kend; k0 += BK) {
+            store(lds);
+            __syncthreads();
+            if (k0 + BK < kend) load(k0 + BK);        // in flight during this tile's MFMAs
+            compute(lds);
+            __syncthreads();
+        }
     }
 
     if (do_bsum) {
@@ -266,28 +310,35 @@ __global__ __launch_bounds__(NT_, min_waves(BM * BN, BK)) void gemm_f32_kernel(A
 
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
-template <int OP, int BM, int BN, int WARPS_M, int BK>
+template <int OP, int BM, int BN, int WARPS_M, int BK, bool DBUF>
 void launch(Args a) {
     a.tiles_m = ppo_divup(a.M, BM);
     a.tiles_n = ppo_divup(a.N, BN);
     if (a.splits < 1) a.splits = 1;
     const long grid = (long)a.tiles_m * a.tiles_n * a.splits;
     PPO_REQUIRE(grid > 0 && grid < (1L << 31), "gemm: grid out of range");
-    hipLaunchKernelGGL((gemm_f32_kernel<OP, BM, BN, WARPS_M, BK>), dim3((unsigned)grid), dim3(NT_), 0,
-                       ppo::stream(), a);
+    if (a.vec_a && a.vec_b)
+        hipLaunchKernelGGL((gemm_f32_kernel<OP, BM, BN, WARPS_M, BK, true, DBUF>), dim3((unsigned)grid), dim3(NT_),
+                           0, ppo::stream(), a);
+    else
+        hipLaunchKernelGGL((gemm_f32_kernel<OP, BM, BN, WARPS_M, BK, false, DBUF>), dim3((unsigned)grid), dim3(NT_),
+                           0, ppo::stream(), a);
     PPO_LAUNCH_CHECK();
 }
 
-// Tile configurations: {BM, BN, WARPS_M, BK}
-struct TileCfg { int bm, bn, wm, bk; };
+// Tile configurations: {BM, BN, WARPS_M, BK, DBUF}
+struct TileCfg { int bm, bn, wm, bk, dbuf; };
 constexpr TileCfg kCfgs[] = {
-    {128, 128, 2, 16},    // 0: main tile, 4 waves of 64x64, ≤128 VGPRs → 4 WG/CU
-    {128, 128, 2, 32},    // 1: main tile, deeper k-step
-    {128, 32, 4, 16},     // 2: skinny N (layer outputs 1 / A, tiny inputs)
-    {32, 128, 1, 16},     // 3: skinny M (grad_W of the output layer)
-    {64, 64, 2, 16},      // 4: small problems (Pendulum-sized layers)
-    {128, 64, 2, 16},     // 5: 4 waves of 64x32
-    {256, 128, 4, 16},    // 6: 4 waves of 64x128
+    {128, 128, 2, 16, 0},    // 0: main tile, 4 waves of 64x64, ≤128 VGPRs → 4 WG/CU
+    {128, 128, 2, 32, 0},    // 1: main tile, deeper k-step
+    {128, 32, 4, 16, 0},     // 2: skinny N (layer outputs 1 / A, tiny inputs)
+    {32, 128, 1, 16, 0},     // 3: skinny M (grad_W of the output layer)
+    {64, 64, 2, 16, 0},      // 4: small problems (Pendulum-sized layers)
+    {128, 64, 2, 16, 0},     // 5: 4 waves of 64x32
+    {256, 128, 4, 16, 0},    // 6: 4 waves of 64x128
+    {128, 128, 2, 16, 1},    // 7: main tile, double-buffered LDS (one barrier per k-tile)
+    {128, 64, 2, 16, 1},     // 8: 128x64, double-buffered
+    {64, 64, 2, 32, 1},      // 9: 64x64 BK32 double-buffered (grad_W: small partial tiles)
 };
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 int g_force_cfg = -1;          // tuning override (ppo_gemm_tune)
@@ -296,13 +347,16 @@ int g_splitk_target = 1024;    // workgroups the split-K grad_W aims for
 template <int OP>
 void launch_cfg(int c, const Args& a) {
     switch (c) {
-        case 0: launch<OP, 128, 128, 2, 16>(a); break;
-        case 1: launch<OP, 128, 128, 2, 32>(a); break;
-        case 2: launch<OP, 128, 32, 4, 16>(a); break;
-        case 3: launch<OP, 32, 128, 1, 16>(a); break;
-        case 4: launch<OP, 64, 64, 2, 16>(a); break;
-        case 5: launch<OP, 128, 64, 2, 16>(a); break;
-        default: launch<OP, 256, 128, 4, 16>(a); break;
+        case 0: launch<OP, 128, 128, 2, 16, false>(a); break;
+        case 1: launch<OP, 128, 128, 2, 32, false>(a); break;
+        case 2: launch<OP, 128, 32, 4, 16, false>(a); break;
+        case 3: launch<OP, 32, 128, 1, 16, false>(a); break;
+        case 4: launch<OP, 64, 64, 2, 16, false>(a); break;
+        case 5: launch<OP, 128, 64, 2, 16, false>(a); break;
+        case 6: launch<OP, 256, 128, 4, 16, false>(a); break;
+        case 7: launch<OP, 128, 128, 2, 16, true>(a); break;
+        case 8: launch<OP, 128, 64, 2, 16, true>(a); break;
+        default: launch<OP, 64, 64, 2, 32, true>(a); break;
     }
 }
 
@@ -324,7 +378,7 @@ void fwd(float* y, const float* x, const float* W, const float* b, int m, int n,
     a.A = x; a.lda = n; a.B = W; a.ldb = n; a.C = y; a.ldc = l;
     a.M = m; a.N = l; a.K = n; a.kchunk = n; a.splits = 1;
     a.bias = b; a.relu = relu;
-    a.vec_a = (n % 4 == 0) && aligned16(x);
+    a.vec_a = (n % 4 == 0) && aligned16(x);             // kcont, extent K = n
     a.vec_b = (n % 4 == 0) && aligned16(W);
     launch_cfg<OP_NT>(cfg < 0 ? pick_cfg(OP_NT, m, l) : cfg, a);
 }
@@ -334,8 +388,8 @@ void bwd_x(float* gx, const float* g, const float* W, const float* mask, int m, 
     a.A = g; a.lda = l; a.B = W; a.ldb = n; a.C = gx; a.ldc = n;
     a.M = m; a.N = n; a.K = l; a.kchunk = l; a.splits = 1;
     a.mask = mask; a.ldmask = n;
-    a.vec_a = (l % 4 == 0) && aligned16(g);
-    a.vec_b = (n % 4 == 0) && aligned16(W);
+    a.vec_a = (l % 4 == 0) && aligned16(g);             // kcont, extent K = l
+    a.vec_b = (n % 4 == 0) && aligned16(W);             // mncont, extent N = n, ld = n
     launch_cfg<OP_NN>(cfg < 0 ? pick_cfg(OP_NN, m, n) : cfg, a);
 }
 
@@ -355,8 +409,8 @@ void bwd_w(float* gW, float* gb, const float* g, const float* x, int m, int n, i
     a.A = g; a.lda = l; a.B = x; a.ldb = n; a.C = gW; a.ldc = n;
     a.M = l; a.N = n; a.K = m;
     a.gbias = gb;
-    a.vec_a = (l % 4 == 0) && aligned16(g);
-    a.vec_b = (n % 4 == 0) && aligned16(x);
+    a.vec_a = (l % 4 == 0) && aligned16(g);             // mncont, extent M = l, ld = l
+    a.vec_b = (n % 4 == 0) && aligned16(x);             // mncont, extent N = n, ld = n
     const long tiles = (long)ppo_divup(l, tc.bm) * ppo_divup(n, tc.bn);
     int splits = (int)((g_splitk_target + tiles - 1) / tiles);
     const int max_splits = m / (8 * tc.bk) > 0 ? m / (8 * tc.bk) : 1;     // ≥ 8 k-tiles per split
@@ -402,9 +456,10 @@ void phip_linear_bwd_w(float* gW, float* gb, const float* g, const float* x, int
     phip_linear_bwd_w_ex(gW, gb, g, x, m, n, l, 0);
 }
 
-void ppo_gemm_tune(int force_cfg, int splitk_target) {
+int ppo_gemm_tune(int force_cfg, int splitk_target) {
     g_force_cfg = force_cfg;
     if (splitk_target > 0) g_splitk_target = splitk_target;
+    return kNumCfgs;
 }
 
 // Tuning / roofline utility: average device time (µs) of one launch of `op` (0 fwd, 1 grad_x,

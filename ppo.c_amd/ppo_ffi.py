@@ -98,6 +98,8 @@ _SIGS = {
     "ppo_set_device": (C.c_int, [C.c_int]),
     "ppo_last_error": (C.c_char_p, []),
     "ppo_synchronize": (None, []),
+    "ppo_gemm_tune": (C.c_int, [C.c_int, C.c_int]),
+    "ppo_bench_gemm": (C.c_double, [C.c_int] * 6),
     "ppo_build_info": (C.c_char_p, []),
     "ppo_struct_sizes": (C.c_int, [c_long_p, C.c_int]),
     "ppo_dev_alloc": (_P, [C.c_size_t]),

@@ -14,20 +14,41 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import ppo_ffi  # noqa: E402
 
 CFG_NAMES = {0: "128x128/bk16", 1: "128x128/bk32", 2: "128x32/bk16", 3: "32x128/bk16", 4: "64x64/bk16",
-             5: "128x64/bk16", 6: "256x128/bk16"}
+             5: "128x64/bk16", 6: "256x128/bk16", 7: "128x128/bk16/db", 8: "128x64/bk16/db", 9: "64x64/bk32/db"}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--out", default="")
+    ap.add_argument("--kscan", action="store_true", help="forward at fixed M,N over K (edge vs main-loop cost)")
+    ap.add_argument("--main", action="store_true", help="C4 minibatch shapes x the large-tile configs only")
     args = ap.parse_args()
     lib = ppo_ffi.load()
-    lib.ppo_bench_gemm.restype = C.c_double
-    lib.ppo_bench_gemm.argtypes = [C.c_int] * 5 + [C.c_int]
-    lib.ppo_gemm_tune.argtypes = [C.c_int, C.c_int]
     lib.ppo_set_device(0)
     B = 32768
+    if args.kscan:
+        for (m, l) in ((B, 512), (4096, 4096)):
+            for n in (64, 128, 256, 512, 1024, 2048, 4096, 8192):
+                us = lib.ppo_bench_gemm(0, m, n, l, 5, -1)
+                print(f"kscan fwd m={m} l={l} K={n:5d} {us:9.1f} us {2.0 * m * n * l / (us * 1e-6) / 1e12:7.1f} TF/s",
+                      flush=True)
+        return
+    if args.main:
+        for (m, n, l) in ((B, 376, 512), (B, 512, 512), (1 << 20, 512, 512)):
+            for op in (0, 1, 2):
+                if m > B and op:
+                    continue
+                cfgs = [0, 5, 7, 8] if op != 2 else [0, 5, 7, 8, 9]
+                for cfg in cfgs:
+                    for tgt in ([512, 1024, 2048] if op == 2 else [0]):
+                        lib.ppo_gemm_tune(-1, tgt)
+                        us = lib.ppo_bench_gemm(op, m, n, l, 10 if m <= B else 3, cfg)
+                        tf = 2.0 * m * n * l / (us * 1e-6) / 1e12
+                        print(f"op{op} m={m:8d} n={n:4d} l={l:4d} {CFG_NAMES[cfg]:16s} split_target={tgt:5d} "
+                              f"{us:9.1f} us {tf:7.1f} TF/s", flush=True)
+        lib.ppo_gemm_tune(-1, 1024)
+        return
     shapes = [  # (m, n, l) = (batch, in, out) — C4 minibatch layers and the GAE forward
         (B, 376, 512), (B, 512, 512), (B, 512, 17), (B, 512, 1), (1 << 20, 512, 512),
         (8192, 256, 256), (8192, 17, 256),

@@ -1,0 +1,79 @@
+"""Every GEMM tile configuration of csrc/gemm.hip, forced one at a time, against the oracle.
+
+The automatic tile picker only reaches some configurations at some shapes; tuning changes which
+one runs where.  Here each configuration runs (a) the three linear-layer GEMMs of the reference
+API (mat_mul_cuda, mat_mul_backwards_cuda; mat_mul.cu:132-217) on vector-path shapes (every
+contiguous extent a multiple of 4) and odd shapes (guarded scalar path), and (b) a whole MLP
+forward + backward through forward_propagation_cuda / backward_propagation_cuda
+(neural_network.cu:74-161), which adds the fused bias + ReLU epilogue, the ReLU′ mask of grad_x,
+the split-K grad_W with its bias-gradient row sums.  Tolerance: the stated fp32 GEMM bound
+(helpers.gemm_tol).
+"""
+import numpy as np
+import pytest
+
+import ppo_ffi
+from helpers import F32, assert_gemm_close, dev, empty, nn_grads_packed, nn_set_params_packed
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [(4096, 376, 512), (1000, 512, 256), (257, 64, 36), (513, 130, 67), (300, 17, 256)]
+
+
+@pytest.fixture(scope="module")
+def ncfg(lib):
+    n = lib.ppo_gemm_tune(-1, 0)
+    yield n
+    lib.ppo_gemm_tune(-1, 0)
+
+
+def _rand(rng, shape, lo=-1.0, hi=1.0):
+    return rng.uniform(lo, hi, shape).astype(F32)
+
+
+@pytest.mark.parametrize("m,n,l", SHAPES)
+def test_linear_every_cfg(lib, oracle, ncfg, m, n, l):
+    rng = np.random.default_rng(m + 3 * n + 7 * l)
+    x, W, b, g = _rand(rng, (m, n)), _rand(rng, (l, n), -0.2, 0.2), _rand(rng, l, -0.2, 0.2), _rand(rng, (m, l))
+    dx, dW, db, dg = dev(lib, x), dev(lib, W), dev(lib, b), dev(lib, g)
+    dy, dgx, dgW = empty(lib, m * l), empty(lib, m * n), empty(lib, l * n)
+    y_ref = oracle.mat_mul(x, W, b)
+    gx_ref, gW_ref = oracle.mat_mul_backwards(g, x, W)
+    try:
+        for c in range(ncfg):
+            lib.ppo_gemm_tune(c, 0)
+            lib.mat_mul_cuda(None, dy.ptr, dx.ptr, dW.ptr, db.ptr, m, n, l)
+            lib.mat_mul_backwards_cuda(None, dgx.ptr, dgW.ptr, dg.ptr, dx.ptr, dW.ptr, m, n, l)
+            assert_gemm_close(dy.to_numpy(F32, m * l).reshape(m, l), y_ref, n, f"cfg {c} forward")
+            assert_gemm_close(dgx.to_numpy(F32, m * n).reshape(m, n), gx_ref, l, f"cfg {c} grad_x")
+            assert_gemm_close(dgW.to_numpy(F32, l * n).reshape(l, n), gW_ref, m, f"cfg {c} grad_W")
+    finally:
+        lib.ppo_gemm_tune(-1, 0)
+
+
+@pytest.mark.parametrize("sizes,m", [([376, 512, 512, 17], 2048), ([17, 256, 256, 6], 1000), ([3, 64, 64, 1], 64)])
+def test_mlp_every_cfg(lib, oracle, ncfg, sizes, m):
+    rng = np.random.default_rng(len(sizes) * 1000 + m)
+    relu = [1] * (len(sizes) - 2) + [0]
+    acts_names = ["relu"] * (len(sizes) - 2) + ["none"]
+    nn = lib.create_neural_network(ppo_ffi.c_ints(sizes), ppo_ffi.c_strings(acts_names), len(sizes))
+    nparams = oracle.mlp_num_params(sizes)
+    params = (rng.uniform(-1, 1, nparams) * 0.1).astype(F32)
+    nn_set_params_packed(lib, nn, params)
+    x = _rand(rng, (m, sizes[0]))
+    gout = _rand(rng, (m, sizes[-1]))
+    acts = oracle.mlp_forward(sizes, relu, params, x)
+    y_ref = oracle.mlp_layer_outputs(sizes, acts, m)[-1]
+    g_ref = oracle.mlp_backward(sizes, relu, params, x, acts, gout)
+    dx, dgo = dev(lib, x), dev(lib, gout)
+    try:
+        for c in range(ncfg):
+            lib.ppo_gemm_tune(c, 0)
+            lib.forward_propagation_cuda(nn, dx.ptr, m)
+            y = ppo_ffi.d2h(lib, nn.contents.d_output, F32, m * sizes[-1]).reshape(m, sizes[-1])
+            assert_gemm_close(y, y_ref, max(sizes), f"cfg {c} MLP forward")
+            lib.backward_propagation_cuda(nn, dgo.ptr, m)
+            assert_gemm_close(nn_grads_packed(lib, nn), g_ref, m, f"cfg {c} MLP grads")
+    finally:
+        lib.ppo_gemm_tune(-1, 0)
+        lib.free_neural_network(nn)
