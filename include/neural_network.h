@@ -80,6 +80,8 @@ typedef struct {
     int    host_cap_m;      /* rows the host staging arrays can hold */
     long   extra_floats;    /* trailing floats in d_params/d_grads owned by the caller (policy log_std) */
     const float* d_x0;      /* input of layer 0 used by the last device forward */
+    unsigned* d_act_bits;   /* ReLU′ masks as bits, one [act_cap_m, ⌈size_i/32⌉] block per layer input */
+    int    bits_m;          /* rows of the forward that wrote d_act_bits (−1: none valid) */
 } NeuralNetwork;
 
 typedef struct {

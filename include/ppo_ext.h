@@ -79,7 +79,7 @@ void ppo_fill_synthetic(void* ppo, int n_envs, int horizon, unsigned long long s
 
 /* ---------------- GEMM tuning utilities ---------------- */
 /* force a tile configuration (−1 = automatic) and the split-K workgroup target of grad_W
- * (≤ 0 keeps the current one); returns the number of tile configurations */
+ * (0 = per-shape automatic, < 0 keeps the current setting); returns the number of tile configurations */
 int    ppo_gemm_tune(int force_cfg, int splitk_target);
 /* average device µs of one launch: op 0 = forward (bias+ReLU), 1 = grad_x, 2 = grad_W (+bias grad);
  * m = batch, n = in, l = out; cfg −1 = automatic */
@@ -88,11 +88,16 @@ double ppo_bench_gemm(int op, int m, int n, int l, int iters, int cfg);
 /* ---------------- kernel timing ---------------- */
 enum { PPO_K_GEMM = 0, PPO_K_GAE = 1, PPO_K_ADAM = 2, PPO_K_GATHER = 3, PPO_K_HEAD = 4,
        PPO_K_COMM = 5, PPO_K_OTHER = 6, PPO_K_COUNT = 7 };
-void ppo_prof_enable(int on);      /* record HIP events around every launch on libppo's stream */
+/* stride > 0: record HIP events around every stride-th launch of each class on libppo's stream
+ * (1 = every launch; an event pair costs a few µs of stream time, so throughput runs sample);
+ * 0 = off */
+void ppo_prof_enable(int stride);
 void ppo_prof_reset(void);
 /* per class: out_ms[k] = Σ kernel time (ms), out_work[k] = Σ algorithmic FLOPs (GEMM) or bytes,
  * out_launches[k] = launches.  Synchronises. */
 void ppo_prof_read(double* out_ms, double* out_work, long* out_launches);
+/* per class: launches issued while profiling was enabled (sampled or not) */
+void ppo_prof_counts(long* out_total);
 
 #ifdef __cplusplus
 }

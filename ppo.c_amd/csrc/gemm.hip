@@ -36,6 +36,9 @@ struct Args {
     int M, N, K, lda, ldb, ldc;
     const float* bias; int relu;          // OP_NT epilogue
     const float* mask; int ldmask;        // OP_NN epilogue (post-activation of the previous layer)
+    unsigned* bits_out;                   // OP_NT + relu: bit (row, col) = y > 0, rows of wpr words
+    const unsigned* bits_in;              // OP_NN: the ReLU′ mask as bits (replaces `mask`)
+    int wpr;                              // words per row of a bit mask = ⌈N/32⌉
     float* gbias;                         // OP_TN: Σ over k of A's rows
     int kchunk, splits;                   // OP_TN split-K
     int tiles_m, tiles_n;
@@ -43,9 +46,15 @@ struct Args {
 };
 
 // ---------------------------------------------------------------------------
-// Loaders.  "kcont": element (row r, k) at P[r*ld + k]  (x, g in grad_x, W in forward)
-//           "mncont": element (row r, k) at P[k*ld + r] (W in grad_x, g and x in grad_W)
-// Both fill an LDS image [R][BK+4] with zeros outside [0,Rmax) × [kbeg,kend).
+// Operand staging.  An operand tile covers R rows (of the output's M or N) × BK of k.
+//  "kcont"  (MN = false): element (row r, k) at P[r*ld + k]   (x and W in forward, g in grad_x).
+//           LDS image [R][BK+4]; each lane's fragments for one k-tile are KH = BK/2 consecutive k
+//           (lane half h owns k ∈ [h·KH, h·KH + KH)), read 4 at a time with ds_read_b128 —
+//           conflict-free because row·(BK+4)/4 mod 16 is a bijection over each 16-lane group.
+//  "mncont" (MN = true):  element (row r, k) at P[k*ld + r]   (W in grad_x, g and x in grad_W).
+//           LDS image [BK][R]: the loaded float4 (4 consecutive rows of one k) is stored as-is
+//           with ds_write_b128, and a fragment is one ds_read_b32 per k (32 consecutive rows per
+//           lane half: conflict-free).  No transpose through registers.
 //
 // VEC: the contiguous extent (kend for kcont, Rmax for mncont) and the leading dimension are
 // multiples of 4 and the base is 16-B aligned, so every float4 lies wholly inside or wholly outside
@@ -56,35 +65,47 @@ struct Args {
 // wave wait for its prefetch before the current tile's MFMAs.  !VEC keeps the guarded scalar form
 // for odd shapes (S = 3, A = 17).
 // ---------------------------------------------------------------------------
-template <int R, int BK>
+template <int R, int BK, bool MN>
 struct Stage {
-    static constexpr int LDK = BK + 4;
+    static constexpr int LDK = BK + 4;                     // kcont row pitch (floats)
+    static constexpr int IMG = MN ? BK * R : R * LDK;      // floats per LDS image
     static constexpr int TOTAL = R * BK / 4;               // float4s per tile
     static constexpr int ITERS = (TOTAL + NT_ - 1) / NT_;
     static constexpr int KQ = BK / 4;                      // float4s per kcont row
+    static constexpr int RQ = R / 4;                       // float4s per mncont k-row
+    static_assert(R % 4 == 0, "tile rows");
     f32x4 v[ITERS];
-    bool kok[ITERS];                                       // VEC: element's k inside [k0, kend)
+    bool kok[ITERS];                                       // element's k inside [k0, kend)
 
-    __device__ __forceinline__ f32x4 masked(int it) const {
-        const f32x4 z = {0.f, 0.f, 0.f, 0.f};
-        return kok[it] ? v[it] : z;
+    __device__ __forceinline__ static void coords(int idx, int& row, int& k) {
+        if (MN) { row = (idx % RQ) * 4; k = idx / RQ; }    // lanes sweep a k-row: full 128-B lines
+        else    { row = idx / KQ; k = (idx % KQ) * 4; }
     }
 
     template <bool VEC>
-    __device__ __forceinline__ void load_kcont(const float* __restrict__ P, int ld, int r0, int Rmax, int k0,
-                                               int kend, int tid) {
+    __device__ __forceinline__ void load(const float* __restrict__ P, int ld, int r0, int Rmax, int k0, int kend,
+                                         int tid) {
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) {
             const int idx = tid + it * NT_;
             f32x4 x = {0.f, 0.f, 0.f, 0.f};
             kok[it] = true;
             if (TOTAL % NT_ == 0 || idx < TOTAL) {
-                const int kq = idx % KQ, r = idx / KQ;
-                const int gr = r0 + r, gk = k0 + kq * 4;
+                int row, k;
+                coords(idx, row, k);
+                const int gr = r0 + row, gk = k0 + k;
                 if (VEC) {
                     kok[it] = gk < kend;
-                    const float* p = P + (long)(gr < Rmax ? gr : Rmax - 1) * ld + (gk < kend ? gk : kend - 4);
+                    const float* p = MN ? P + (long)(gk < kend ? gk : kend - 1) * ld + (gr < Rmax ? gr : Rmax - 4)
+                                        : P + (long)(gr < Rmax ? gr : Rmax - 1) * ld + (gk < kend ? gk : kend - 4);
                     x = *reinterpret_cast<const f32x4*>(p);
+                } else if (MN) {
+                    if (gk < kend) {
+                        const float* p = P + (long)gk * ld + gr;
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            if (gr + e < Rmax) x[e] = p[e];
+                    }
                 } else if (gr < Rmax) {
                     const float* p = P + (long)gr * ld + gk;
 #pragma unroll
@@ -95,61 +116,37 @@ struct Stage {
             v[it] = x;
         }
     }
-    __device__ __forceinline__ void store_kcont(float* lds, int tid) const {
+
+    __device__ __forceinline__ void store(float* img, int tid) const {
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) {
             const int idx = tid + it * NT_;
             if (TOTAL % NT_ == 0 || idx < TOTAL) {
-                const int kq = idx % KQ, r = idx / KQ;
-                *reinterpret_cast<f32x4*>(lds + r * LDK + kq * 4) = masked(it);
+                int row, k;
+                coords(idx, row, k);
+                const f32x4 z = {0.f, 0.f, 0.f, 0.f};
+                const f32x4 x = kok[it] ? v[it] : z;
+                *reinterpret_cast<f32x4*>(img + (MN ? k * R + row : row * LDK + k)) = x;
             }
         }
     }
 
-    // lanes: kk_lo = idx&7 (8 k-rows), then R/4 row-quads, then kk_hi → 8 full 128-B lines per wave
-    __device__ __forceinline__ static void mn_coords(int idx, int& kk, int& nq) {
-        const int kk_lo = idx & 7, rest = idx >> 3;
-        nq = rest % (R / 4);
-        kk = (rest / (R / 4)) * 8 + kk_lo;
-    }
-    template <bool VEC>
-    __device__ __forceinline__ void load_mncont(const float* __restrict__ P, int ld, int r0, int Rmax, int k0,
-                                                int kend, int tid) {
+    // fragments of k-group q4 (k = kb + s, s = 0..3, kb = h·KH + 4·q4) for image row `row`
+    __device__ __forceinline__ static f32x4 frag(const float* img, int row, int kb) {
+        if (MN) {
+            f32x4 f;
 #pragma unroll
-        for (int it = 0; it < ITERS; ++it) {
-            const int idx = tid + it * NT_;
-            f32x4 x = {0.f, 0.f, 0.f, 0.f};
-            kok[it] = true;
-            if (TOTAL % NT_ == 0 || idx < TOTAL) {
-                int kk, nq;
-                mn_coords(idx, kk, nq);
-                const int gk = k0 + kk, gr = r0 + nq * 4;
-                if (VEC) {
-                    kok[it] = gk < kend;
-                    const float* p = P + (long)(gk < kend ? gk : kend - 1) * ld + (gr < Rmax ? gr : Rmax - 4);
-                    x = *reinterpret_cast<const f32x4*>(p);
-                } else if (gk < kend) {
-                    const float* p = P + (long)gk * ld + gr;
-#pragma unroll
-                    for (int e = 0; e < 4; ++e)
-                        if (gr + e < Rmax) x[e] = p[e];
-                }
-            }
-            v[it] = x;
+            for (int s = 0; s < 4; ++s) f[s] = img[(kb + s) * R + row];
+            return f;
         }
+        return *reinterpret_cast<const f32x4*>(img + row * LDK + kb);
     }
-    __device__ __forceinline__ void store_mncont(float* lds, int tid) const {
-#pragma unroll
-        for (int it = 0; it < ITERS; ++it) {
-            const int idx = tid + it * NT_;
-            if (TOTAL % NT_ == 0 || idx < TOTAL) {
-                int kk, nq;
-                mn_coords(idx, kk, nq);
-                const f32x4 x = masked(it);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) lds[(nq * 4 + e) * LDK + kk] = x[e];
-            }
-        }
+
+    // Σ over the tile's k of image row `row`, k ∈ [k_lo, k_lo + n)
+    __device__ __forceinline__ static float rowsum(const float* img, int row, int k_lo, int n) {
+        float t = 0.f;
+        for (int kk = 0; kk < n; ++kk) t += MN ? img[(k_lo + kk) * R + row] : img[row * LDK + k_lo + kk];
+        return t;
     }
 };
 
@@ -164,9 +161,11 @@ __global__ __launch_bounds__(NT_, min_waves(BM * BN, BK)) void gemm_f32_kernel(A
     constexpr int WARPS_N = 4 / WARPS_M;
     constexpr int WM = BM / WARPS_M, WN = BN / WARPS_N;
     constexpr int TM = WM / 32, TN = WN / 32;
-    constexpr int LDK = BK + 4;        // BK=16: 20, BK=32: 36 floats — ds_read_b128 conflict-free
     constexpr int KH = BK / 2;         // k per lane-half per tile (k-permutation)
-    constexpr int IMG = (BM + BN) * LDK;
+    constexpr bool A_MN = OP == OP_TN, B_MN = OP != OP_NT;
+    using SA = Stage<BM, BK, A_MN>;
+    using SB = Stage<BN, BK, B_MN>;
+    constexpr int IMG = SA::IMG + SB::IMG;
     static_assert(TM >= 1 && TN >= 1, "wave tile must be a multiple of 32x32");
     static_assert(BK == 16 || BK == 32, "BK");
 
@@ -202,36 +201,29 @@ __global__ __launch_bounds__(NT_, min_waves(BM * BN, BK)) void gemm_f32_kernel(A
     const bool do_bsum = OP == OP_TN && a.gbias != nullptr && tn == 0 && (NT_ % BM == 0) && BK >= TPR;
     float bsum = 0.f;
 
-    Stage<BM, BK> sa;
-    Stage<BN, BK> sb;
+    SA sa;
+    SB sb;
 
     auto load = [&](int k0) {
-        if (OP == OP_TN) sa.template load_mncont<VEC>(a.A, a.lda, m0, a.M, k0, kend, tid);
-        else             sa.template load_kcont<VEC>(a.A, a.lda, m0, a.M, k0, kend, tid);
-        if (OP == OP_NT) sb.template load_kcont<VEC>(a.B, a.ldb, n0, a.N, k0, kend, tid);
-        else             sb.template load_mncont<VEC>(a.B, a.ldb, n0, a.N, k0, kend, tid);
+        sa.template load<VEC>(a.A, a.lda, m0, a.M, k0, kend, tid);
+        sb.template load<VEC>(a.B, a.ldb, n0, a.N, k0, kend, tid);
     };
     auto store = [&](float* img) {
-        if (OP == OP_TN) sa.store_mncont(img, tid); else sa.store_kcont(img, tid);
-        if (OP == OP_NT) sb.store_kcont(img + BM * LDK, tid); else sb.store_mncont(img + BM * LDK, tid);
+        sa.store(img, tid);
+        sb.store(img + SA::IMG, tid);
     };
     auto compute = [&](const float* img) {
         const float* As = img;
-        const float* Bs = img + BM * LDK;
-        if (do_bsum) {
-            const int row = tid / TPR, seg = tid % TPR;
-#pragma unroll
-            for (int kk = 0; kk < KPT; ++kk) bsum += As[row * LDK + seg * KPT + kk];
-        }
+        const float* Bs = img + SA::IMG;
+        if (do_bsum) bsum += SA::rowsum(As, tid / TPR, (tid % TPR) * KPT, KPT);
 #pragma unroll
         for (int q4 = 0; q4 < KH / 4; ++q4) {
             f32x4 fa[TM], fb[TN];
+            const int kb = h * KH + q4 * 4;
 #pragma unroll
-            for (int i = 0; i < TM; ++i)
-                fa[i] = *reinterpret_cast<const f32x4*>(As + (wm * WM + i * 32 + r) * LDK + h * KH + q4 * 4);
+            for (int i = 0; i < TM; ++i) fa[i] = SA::frag(As, wm * WM + i * 32 + r, kb);
 #pragma unroll
-            for (int j = 0; j < TN; ++j)
-                fb[j] = *reinterpret_cast<const f32x4*>(Bs + (wn * WN + j * 32 + r) * LDK + h * KH + q4 * 4);
+            for (int j = 0; j < TN; ++j) fb[j] = SB::frag(Bs, wn * WN + j * 32 + r, kb);
 #pragma unroll
             for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -278,32 +270,67 @@ __global__ __launch_bounds__(NT_, min_waves(BM * BN, BK)) void gemm_f32_kernel(A
         }
     }
 
-    // epilogue: 32x32 C/D map — col = lane&31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5)
+    // epilogue: 32x32 C/D map — col = lane&31, row = (reg&3) + 8*(reg>>2) + 4*(lane>>5).
+    // Every global load an output block needs (bias, ReLU′ mask) is issued as one batch before the
+    // block's first store: interleaved with the stores, the compiler cannot prove they do not alias
+    // and serialises one load→wait→store round trip per element.
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-            const int col = n0 + wn * WN + j * 32 + r;
-            if (col >= a.N) continue;
+            const int c0 = n0 + wn * WN + j * 32;            // 32-aligned: one bit-mask word per row
+            const int col = c0 + r;
+            const int r0 = m0 + wm * WM + i * 32 + 4 * h;
+            const bool col_ok = col < a.N;
+            const int colc = col_ok ? col : a.N - 1;
             float bcol = 0.f;
-            if (OP == OP_NT && a.bias) bcol = a.bias[col];
+            if (OP == OP_NT && a.bias) bcol = a.bias[colc];
+            bool keep[16];
+            if (OP == OP_NN) {                                // mode is wave-uniform: loads unconditional
+                if (a.bits_in) {
+                    unsigned wv[16];
+#pragma unroll
+                    for (int e = 0; e < 16; ++e)
+                        wv[e] = a.bits_in[(long)min(r0 + (e & 3) + 8 * (e >> 2), a.M - 1) * a.wpr + (c0 >> 5)];
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) keep[e] = (wv[e] >> r) & 1u;
+                } else if (a.mask) {
+                    float mv[16];
+#pragma unroll
+                    for (int e = 0; e < 16; ++e)
+                        mv[e] = a.mask[(long)min(r0 + (e & 3) + 8 * (e >> 2), a.M - 1) * a.ldmask + colc];
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) keep[e] = mv[e] > 0.f;
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) keep[e] = true;
+                }
+            }
+            unsigned word = 0;                                 // OP_NT bits: lane e (+32) keeps row e's word
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
-                const int row = m0 + wm * WM + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-                if (row >= a.M) continue;
+                const int row = r0 + (e & 3) + 8 * (e >> 2);
+                const bool ok = col_ok && row < a.M;
                 float v = acc[i][j][e];
                 float* dst = a.C + (long)row * a.ldc + col;
                 if (OP == OP_NT) {
                     v += bcol;
                     if (a.relu) v = v > 0.f ? v : 0.f;
-                    *dst = v;
+                    if (ok) *dst = v;
+                    if (a.bits_out) {                          // wave-uniform branch: ballot stays converged
+                        const unsigned long long b = __ballot(ok && v > 0.f);
+                        if (r == e) word = h ? (unsigned)(b >> 32) : (unsigned)b;
+                    }
                 } else if (OP == OP_NN) {
-                    if (a.mask && !(a.mask[(long)row * a.ldmask + col] > 0.f)) v = 0.f;
-                    *dst = v;
-                } else {
+                    if (ok) *dst = keep[e] ? v : 0.f;
+                } else if (ok) {
                     if (a.splits > 1) atomicAdd(dst, v);
                     else *dst = v;
                 }
+            }
+            if (OP == OP_NT && a.bits_out && r < 16) {
+                const int row = r0 + (r & 3) + 8 * (r >> 2);
+                if (row < a.M && c0 < a.N) a.bits_out[(long)row * a.wpr + (c0 >> 5)] = word;
             }
         }
 }
@@ -342,7 +369,7 @@ constexpr TileCfg kCfgs[] = {
 };
 constexpr int kNumCfgs = sizeof(kCfgs) / sizeof(kCfgs[0]);
 int g_force_cfg = -1;          // tuning override (ppo_gemm_tune)
-int g_splitk_target = 1024;    // workgroups the split-K grad_W aims for
+int g_splitk_override = 0;     // tuning override of the split-K workgroup target (0 = per shape)
 
 template <int OP>
 void launch_cfg(int c, const Args& a) {
@@ -360,34 +387,45 @@ void launch_cfg(int c, const Args& a) {
     }
 }
 
-// Measured on MI355X (tools/gemm_sweep.py): 128x128/BK16 at 4 WG/CU for large forward / grad_x
-// grids; 128x64 when a 128x128 grid would not give every CU two workgroups; 128x64 with a
-// ~1024-workgroup split-K for grad_W; skinny tiles for the 1- and A-wide output layers.
-int pick_cfg(int op, int M, int N) {
+// Measured on MI355X (tools/gemm_sweep.py, profiles/r01_gemm_sweep_*): 128x128/BK16 at 4 WG/CU
+// for large forward / grad_x grids; 128x64 when a 128x128 grid would not give every CU two
+// workgroups; skinny tiles for the 1- and A-wide output layers.  grad_W (split-K, f32 atomics):
+// 128x128 tiles at ~512 workgroups when the output has ≥ 16 such tiles and 128 | N, else 64x64
+// tiles at ~2048 workgroups (fewer atomic bytes per CU than wider tiles at the same occupancy).
+int pick_cfg(int op, int M, int N, int* splitk_target = nullptr) {
+    if (splitk_target) *splitk_target = 1024;
     if (g_force_cfg >= 0 && g_force_cfg < kNumCfgs) return g_force_cfg;
     if (N <= 32 && M > 32) return 2;
     if (M <= 32 && N > 32) return 3;
     if (M <= 64 || N <= 64) return 4;
-    if (op == OP_TN) return 5;
     const long tiles = (long)ppo_divup(M, 128) * ppo_divup(N, 128);
+    if (op == OP_TN) {
+        const bool big = tiles >= 16 && N % 128 == 0;
+        if (splitk_target) *splitk_target = big ? 512 : 2048;
+        return big ? 0 : 4;
+    }
     return tiles < 512 ? 5 : 0;
 }
 
-void fwd(float* y, const float* x, const float* W, const float* b, int m, int n, int l, int relu, int cfg) {
+void fwd(float* y, const float* x, const float* W, const float* b, int m, int n, int l, int relu, unsigned* bits,
+         int cfg) {
     Args a{};
     a.A = x; a.lda = n; a.B = W; a.ldb = n; a.C = y; a.ldc = l;
     a.M = m; a.N = l; a.K = n; a.kchunk = n; a.splits = 1;
     a.bias = b; a.relu = relu;
+    a.bits_out = bits; a.wpr = ppo_divup(l, 32);
     a.vec_a = (n % 4 == 0) && aligned16(x);             // kcont, extent K = n
     a.vec_b = (n % 4 == 0) && aligned16(W);
     launch_cfg<OP_NT>(cfg < 0 ? pick_cfg(OP_NT, m, l) : cfg, a);
 }
 
-void bwd_x(float* gx, const float* g, const float* W, const float* mask, int m, int n, int l, int cfg) {
+void bwd_x(float* gx, const float* g, const float* W, const float* mask, const unsigned* bits, int m, int n, int l,
+           int cfg) {
     Args a{};
     a.A = g; a.lda = l; a.B = W; a.ldb = n; a.C = gx; a.ldc = n;
     a.M = m; a.N = n; a.K = l; a.kchunk = l; a.splits = 1;
     a.mask = mask; a.ldmask = n;
+    a.bits_in = bits; a.wpr = ppo_divup(n, 32);
     a.vec_a = (l % 4 == 0) && aligned16(g);             // kcont, extent K = l
     a.vec_b = (n % 4 == 0) && aligned16(W);             // mncont, extent N = n, ld = n
     launch_cfg<OP_NN>(cfg < 0 ? pick_cfg(OP_NN, m, n) : cfg, a);
@@ -403,7 +441,9 @@ void bwd_w(float* gW, float* gb, const float* g, const float* x, int m, int n, i
         }
         return;
     }
-    const int c = cfg < 0 ? pick_cfg(OP_TN, l, n) : cfg;
+    int target = 1024;
+    const int c = cfg < 0 ? pick_cfg(OP_TN, l, n, &target) : cfg;
+    if (g_splitk_override > 0) target = g_splitk_override;
     const TileCfg& tc = kCfgs[c];
     Args a{};
     a.A = g; a.lda = l; a.B = x; a.ldb = n; a.C = gW; a.ldc = n;
@@ -412,7 +452,7 @@ void bwd_w(float* gW, float* gb, const float* g, const float* x, int m, int n, i
     a.vec_a = (l % 4 == 0) && aligned16(g);             // mncont, extent M = l, ld = l
     a.vec_b = (n % 4 == 0) && aligned16(x);             // mncont, extent N = n, ld = n
     const long tiles = (long)ppo_divup(l, tc.bm) * ppo_divup(n, tc.bn);
-    int splits = (int)((g_splitk_target + tiles - 1) / tiles);
+    int splits = (int)((target + tiles - 1) / tiles);
     const int max_splits = m / (8 * tc.bk) > 0 ? m / (8 * tc.bk) : 1;     // ≥ 8 k-tiles per split
     if (splits > max_splits) splits = max_splits;
     if (splits < 1) splits = 1;
@@ -431,18 +471,28 @@ void bwd_w(float* gW, float* gb, const float* g, const float* x, int m, int n, i
 
 extern "C" {
 
-void phip_linear_fwd(float* y, const float* x, const float* W, const float* b, int m, int n, int l, int relu) {
+void phip_linear_fwd_bits(float* y, const float* x, const float* W, const float* b, int m, int n, int l, int relu,
+                          unsigned* bits) {
     if (m <= 0 || l <= 0) return;
     PPO_REQUIRE(y && x && W && n > 0, "phip_linear_fwd: null operand");
     ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l);
-    fwd(y, x, W, b, m, n, l, relu, -1);
+    fwd(y, x, W, b, m, n, l, relu, relu ? bits : nullptr, -1);
 }
 
-void phip_linear_bwd_x(float* gx, const float* g, const float* W, const float* mask, int m, int n, int l) {
+void phip_linear_fwd(float* y, const float* x, const float* W, const float* b, int m, int n, int l, int relu) {
+    phip_linear_fwd_bits(y, x, W, b, m, n, l, relu, nullptr);
+}
+
+void phip_linear_bwd_x_bits(float* gx, const float* g, const float* W, const float* mask, const unsigned* bits, int m,
+                            int n, int l) {
     if (m <= 0 || n <= 0) return;
     PPO_REQUIRE(gx && g && W && l > 0, "phip_linear_bwd_x: null operand");
     ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l);
-    bwd_x(gx, g, W, mask, m, n, l, -1);
+    bwd_x(gx, g, W, mask, bits, m, n, l, -1);
+}
+
+void phip_linear_bwd_x(float* gx, const float* g, const float* W, const float* mask, int m, int n, int l) {
+    phip_linear_bwd_x_bits(gx, g, W, mask, nullptr, m, n, l);
 }
 
 void phip_linear_bwd_w_ex(float* gW, float* gb, const float* g, const float* x, int m, int n, int l, int zeroed) {
@@ -458,7 +508,7 @@ void phip_linear_bwd_w(float* gW, float* gb, const float* g, const float* x, int
 
 int ppo_gemm_tune(int force_cfg, int splitk_target) {
     g_force_cfg = force_cfg;
-    if (splitk_target > 0) g_splitk_target = splitk_target;
+    if (splitk_target >= 0) g_splitk_override = splitk_target;
     return kNumCfgs;
 }
 
@@ -477,8 +527,8 @@ double ppo_bench_gemm(int op, int m, int n, int l, int iters, int cfg) {
     phip_fill_uniform(y, (long)(sy > sx ? sy : sx), 3, -1.f, 1.f);
     phip_fill_uniform(b, (long)(l > n ? l : n), 4, -0.1f, 0.1f);
     auto run = [&]() {
-        if (op == 0) fwd(y, x, W, b, m, n, l, 1, cfg);
-        else if (op == 1) bwd_x(x, y, W, nullptr, m, n, l, cfg);
+        if (op == 0) fwd(y, x, W, b, m, n, l, 1, nullptr, cfg);
+        else if (op == 1) bwd_x(x, y, W, nullptr, nullptr, m, n, l, cfg);
         else bwd_w(gw, b, y, x, m, n, l, 0, cfg);
     };
     for (int i = 0; i < 3; ++i) run();

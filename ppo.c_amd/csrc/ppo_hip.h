@@ -30,8 +30,15 @@ void  phip_record_error(const char* msg);
 /* ---------------- dense layers (gemm.hip) ---------------- */
 /* y[m,l] = x[m,n]·W[l,n]ᵀ + b[l], optional ReLU (mat_mul.cu:132-163 + K1/K5 fused) */
 void phip_linear_fwd(float* y, const float* x, const float* W, const float* b, int m, int n, int l, int relu);
+/* same, and (relu) writes the ReLU′ mask as bits: word (row, c/32) bit c%32 = y[row, c] > 0,
+ * ⌈l/32⌉ words per row — 1/32 of the bytes the float mask costs the backward */
+void phip_linear_fwd_bits(float* y, const float* x, const float* W, const float* b, int m, int n, int l, int relu,
+                          unsigned* bits);
 /* gx[m,n] = g[m,l]·W[l,n]; if mask: gx = (mask > 0) ? gx : 0 (K3 + K6 fused) */
 void phip_linear_bwd_x(float* gx, const float* g, const float* W, const float* mask, int m, int n, int l);
+/* same with the mask given as bits (phip_linear_fwd_bits layout, ⌈n/32⌉ words per row) */
+void phip_linear_bwd_x_bits(float* gx, const float* g, const float* W, const float* mask, const unsigned* bits, int m,
+                            int n, int l);
 /* gW[l,n] = g[m,l]ᵀ·x[m,n] and gb[l] = Σ_m g[m,l] (K4 + K7 fused); overwrites */
 void phip_linear_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, int n, int l);
 /* same, with gW/gb already zero on entry when `zeroed` (one memset per backward instead of two per layer) */

@@ -64,6 +64,8 @@ hipStream_t stream() {
 // ---------------- per-launch event timing ----------------
 struct ProfSlot { hipEvent_t a, b; int k; double work; };
 static bool                  g_prof_on = false;
+static int                   g_prof_stride = 1;
+static long                  g_issued[PPO_K_COUNT];
 static std::vector<ProfSlot> g_slots;       // recorded, not yet harvested
 static std::vector<hipEvent_t> g_free_events;
 static double g_ms[PPO_K_COUNT], g_work[PPO_K_COUNT];
@@ -102,6 +104,7 @@ extern "C" {
 
 int phip_prof_begin(int cls, double work) {
     if (!g_prof_on) return -1;
+    if (g_issued[cls]++ % g_prof_stride != 0) return -1;
     if (g_slots.size() >= (1u << 16)) harvest();
     ProfSlot s{take_event(), take_event(), cls, work};
     PPO_CHECK(hipEventRecord(s.a, stream()));
@@ -192,14 +195,19 @@ void  ppo_d2d(void* dst, const void* src, size_t bytes) { phip_d2d(dst, src, byt
 void  ppo_dev_memset(void* dst, int value, size_t bytes) { phip_memset(dst, value, bytes); phip_sync(); }
 
 // ---------------- ppo_ext.h: kernel timing ----------------
-void ppo_prof_enable(int on) {
-    if (!on && g_prof_on) harvest();
-    g_prof_on = on != 0;
+void ppo_prof_enable(int stride) {
+    if (stride <= 0 && g_prof_on) harvest();
+    g_prof_on = stride > 0;
+    if (stride > 0) g_prof_stride = stride;
+}
+
+void ppo_prof_counts(long* out_total) {
+    for (int k = 0; k < PPO_K_COUNT; k++) out_total[k] = g_issued[k];
 }
 
 void ppo_prof_reset(void) {
     harvest();
-    for (int k = 0; k < PPO_K_COUNT; k++) { g_ms[k] = 0; g_work[k] = 0; g_launches[k] = 0; }
+    for (int k = 0; k < PPO_K_COUNT; k++) { g_ms[k] = 0; g_work[k] = 0; g_launches[k] = 0; g_issued[k] = 0; }
 }
 
 void ppo_prof_read(double* out_ms, double* out_work, long* out_launches) {

@@ -36,6 +36,7 @@ NeuralNetwork* nn_create_ex(int* layer_sizes, char** activation_functions, int n
     NeuralNetwork* nn = (NeuralNetwork*)xcalloc(1, sizeof(NeuralNetwork));
     nn->num_layers = num_layers;
     nn->layers = (Layer*)xcalloc((size_t)num_layers, sizeof(Layer));
+    nn->bits_m = -1;
     nn->activation_functions = (char**)xmalloc(sizeof(char*) * (size_t)L);
     nn->param_offset = (long*)xmalloc(sizeof(long) * (size_t)L);
     nn->bias_offset = (long*)xmalloc(sizeof(long) * (size_t)L);
@@ -85,12 +86,24 @@ NeuralNetwork* create_neural_network(int* layer_sizes, char** activation_functio
     return nn_create_ex(layer_sizes, activation_functions, num_layers, 0, 1);
 }
 
+static long bits_words(const NeuralNetwork* nn, int upto, int m) {   /* words before layer `upto`'s block */
+    long w = 0;
+    for (int i = 0; i < upto; i++) w += (long)m * ((nn->layers[i].input_size + 31) / 32);
+    return w;
+}
+
+/* ReLU′ bit mask of layers[i].d_input (written by the forward of layer i−1) */
+static unsigned* act_bits(NeuralNetwork* nn, int i) { return nn->d_act_bits + bits_words(nn, i, nn->act_cap_m); }
+
 void nn_ensure_act(NeuralNetwork* nn, int m) {
     if (m <= nn->act_cap_m) return;
     for (int i = 0; i < nn->num_layers; i++) {
         phip_free(nn->layers[i].d_input);
         nn->layers[i].d_input = (float*)phip_malloc(sizeof(float) * (size_t)m * nn->layers[i].input_size);
     }
+    phip_free(nn->d_act_bits);
+    nn->d_act_bits = (unsigned*)phip_malloc(sizeof(unsigned) * (size_t)bits_words(nn, nn->num_layers, m));
+    nn->bits_m = -1;
     nn->act_cap_m = m;
 }
 
@@ -111,9 +124,11 @@ void nn_forward_dev(NeuralNetwork* nn, const float* d_x, int m) {
     for (int i = 0; i < L; i++) {
         Layer* ly = &nn->layers[i];
         float* out = nn->layers[i + 1].d_input;
-        phip_linear_fwd(out, in, ly->d_weights, ly->d_biases, m, ly->input_size, ly->output_size, nn_is_relu(nn, i));
+        phip_linear_fwd_bits(out, in, ly->d_weights, ly->d_biases, m, ly->input_size, ly->output_size,
+                             nn_is_relu(nn, i), act_bits(nn, i + 1));
         in = out;
     }
+    nn->bits_m = m;
     nn->cache_m_forward = m;
     nn->d_output = nn->layers[L].d_input;
 }
@@ -136,8 +151,10 @@ void nn_backward_dev(NeuralNetwork* nn, const float* d_grad_out, int m, int want
         const float* x = i == 0 ? nn->d_x0 : ly->d_input;
         phip_linear_bwd_w_ex(ly->d_grad_weights, ly->d_grad_biases, g, x, m, ly->input_size, ly->output_size, 1);
         if (i > 0 || want_grad_x0) {
-            const float* mask = (i > 0 && nn_is_relu(nn, i - 1)) ? ly->d_input : NULL;
-            phip_linear_bwd_x(ly->d_grad_x, g, ly->d_weights, mask, m, ly->input_size, ly->output_size);
+            const int relu_in = i > 0 && nn_is_relu(nn, i - 1);
+            const float* mask = relu_in ? ly->d_input : NULL;
+            const unsigned* bits = relu_in && nn->bits_m == m ? act_bits(nn, i) : NULL;   /* this forward's bits */
+            phip_linear_bwd_x_bits(ly->d_grad_x, g, ly->d_weights, mask, bits, m, ly->input_size, ly->output_size);
         }
         g = ly->d_grad_x;
     }
@@ -219,6 +236,7 @@ void free_neural_network(NeuralNetwork* nn) {
         phip_free(nn->layers[i].d_input);
         phip_free(nn->layers[i].d_grad_x);
     }
+    phip_free(nn->d_act_bits);
     phip_free(nn->d_params);
     phip_free(nn->d_grads);
     free(nn->activation_functions);

@@ -39,7 +39,8 @@ class NeuralNetwork(C.Structure):
                 ("d_params", c_float_p), ("d_grads", c_float_p), ("num_params", C.c_long),
                 ("num_params_packed", C.c_long), ("param_offset", c_long_p), ("bias_offset", c_long_p),
                 ("act_cap_m", C.c_int), ("grad_cap_m", C.c_int), ("host_cap_m", C.c_int),
-                ("extra_floats", C.c_long), ("d_x0", c_float_p)]
+                ("extra_floats", C.c_long), ("d_x0", c_float_p), ("d_act_bits", C.POINTER(C.c_uint)),
+                ("bits_m", C.c_int)]
 
 
 class GaussianPolicy(C.Structure):
@@ -122,6 +123,7 @@ _SIGS = {
     "ppo_prof_enable": (None, [C.c_int]),
     "ppo_prof_reset": (None, []),
     "ppo_prof_read": (None, [C.POINTER(C.c_double), C.POINTER(C.c_double), c_long_p]),
+    "ppo_prof_counts": (None, [c_long_p]),
     # mat_mul.h
     "mat_mul": (None, [_P, _P, _P, _P, C.c_int, C.c_int, C.c_int]),
     "mat_mul_backwards": (None, [_P, _P, _P, _P, _P, C.c_int, C.c_int, C.c_int]),

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--kscan", action="store_true", help="forward at fixed M,N over K (edge vs main-loop cost)")
     ap.add_argument("--main", action="store_true", help="C4 minibatch shapes x the large-tile configs only")
+    ap.add_argument("--cfgs", default="", help="comma-separated configs for --main (default: a fixed set)")
     args = ap.parse_args()
     lib = ppo_ffi.load()
     lib.ppo_set_device(0)
@@ -39,7 +40,9 @@ def main():
             for op in (0, 1, 2):
                 if m > B and op:
                     continue
-                cfgs = [0, 5, 7, 8] if op != 2 else [0, 5, 7, 8, 9]
+                cfgs = [0, 5, 7] if op != 2 else [0, 4, 5, 7, 9]
+                if args.cfgs:
+                    cfgs = [int(c) for c in args.cfgs.split(",")]
                 for cfg in cfgs:
                     for tgt in ([512, 1024, 2048] if op == 2 else [0]):
                         lib.ppo_gemm_tune(-1, tgt)
@@ -47,7 +50,7 @@ def main():
                         tf = 2.0 * m * n * l / (us * 1e-6) / 1e12
                         print(f"op{op} m={m:8d} n={n:4d} l={l:4d} {CFG_NAMES[cfg]:16s} split_target={tgt:5d} "
                               f"{us:9.1f} us {tf:7.1f} TF/s", flush=True)
-        lib.ppo_gemm_tune(-1, 1024)
+        lib.ppo_gemm_tune(-1, 0)
         return
     shapes = [  # (m, n, l) = (batch, in, out) — C4 minibatch layers and the GAE forward
         (B, 376, 512), (B, 512, 512), (B, 512, 17), (B, 512, 1), (1 << 20, 512, 512),
@@ -71,7 +74,7 @@ def main():
                                      tflops=tf))
                     print(f"op{op} m={m:8d} n={n:4d} l={l:4d} {CFG_NAMES.get(cfg, 'auto'):14s} "
                           f"split_target={tgt:5d} {us:9.1f} us {tf:7.1f} TF/s", flush=True)
-    lib.ppo_gemm_tune(-1, 1024)
+    lib.ppo_gemm_tune(-1, 0)
     if args.out:
         json.dump(rows, open(args.out, "w"), indent=1)
 
