@@ -44,7 +44,7 @@ __global__ void gather_kernel(const int* __restrict__ perm, Feistel f, int offse
                               const float* __restrict__ logprob, const float* __restrict__ advantage,
                               const float* __restrict__ adv_target, float* __restrict__ states,
                               float* __restrict__ actions, float* __restrict__ logprobs, float* __restrict__ advs,
-                              float* __restrict__ adv_targets) {
+                              float* __restrict__ adv_targets, int* __restrict__ rows) {
     const int lane = threadIdx.x & 63;
     const int waves = gridDim.x * (TPB / 64);
     for (int i = blockIdx.x * (TPB / 64) + (threadIdx.x >> 6); i < batch; i += waves) {
@@ -61,10 +61,34 @@ __global__ void gather_kernel(const int* __restrict__ perm, Feistel f, int offse
             for (int c = lane; c < A; c += 64) dp[c] = sp[c];
         }
         if (lane == 0) {
+            if (rows) rows[i] = src;
             if (logprobs) logprobs[i] = logprob[src];
             if (advs) advs[i] = advantage[src];
             if (adv_targets) adv_targets[i] = adv_target[src];
         }
+    }
+}
+
+// No state rows to copy (layer 0 gathers them itself): one thread per minibatch slot writes the
+// slot's source row and its small per-row fields — one pass, every slot's loads in flight together.
+__global__ void gather_small_kernel(const int* __restrict__ perm, Feistel f, int offset, int limit, int batch, int A,
+                                    const float* __restrict__ action, const float* __restrict__ logprob,
+                                    const float* __restrict__ advantage, const float* __restrict__ adv_target,
+                                    float* __restrict__ actions, float* __restrict__ logprobs,
+                                    float* __restrict__ advs, float* __restrict__ adv_targets,
+                                    int* __restrict__ rows) {
+    const int i = blockIdx.x * TPB + threadIdx.x;
+    if (i >= batch) return;
+    const int list = (int)(((long)offset + i) % limit);
+    const int src = perm ? perm[list] : (int)feistel_index((uint32_t)list, f);
+    if (rows) rows[i] = src;
+    if (logprobs) logprobs[i] = logprob[src];
+    if (advs) advs[i] = advantage[src];
+    if (adv_targets) adv_targets[i] = adv_target[src];
+    if (actions) {
+        const float* sp = action + (long)src * A;
+        float* dp = actions + (long)i * A;
+        for (int c = 0; c < A; ++c) dp[c] = sp[c];
     }
 }
 
@@ -79,10 +103,10 @@ uint64_t splitmix64(uint64_t z) {
 
 extern "C" {
 
-void phip_gather(const int* perm, uint64_t key, int offset, int limit, int batch, int S, int A,
-                 const float* state, const float* action, const float* logprob, const float* advantage,
-                 const float* adv_target, float* states, float* actions, float* logprobs, float* advs,
-                 float* adv_targets) {
+void phip_gather_rows(const int* perm, uint64_t key, int offset, int limit, int batch, int S, int A,
+                      const float* state, const float* action, const float* logprob, const float* advantage,
+                      const float* adv_target, float* states, float* actions, float* logprobs, float* advs,
+                      float* adv_targets, int* rows) {
     if (batch <= 0) return;
     PPO_REQUIRE(limit > 0, "phip_gather: empty buffer");
     Feistel f{};
@@ -92,12 +116,28 @@ void phip_gather(const int* perm, uint64_t key, int offset, int limit, int batch
     f.mask = (1u << f.half) - 1u;
     f.n = (uint32_t)limit;
     for (int r = 0; r < 4; ++r) f.k[r] = (uint32_t)splitmix64(key + (uint64_t)r);
+    ppo::ProfScope ps(PPO_K_GATHER, 8.0 * batch * ((states ? S : 0) + (actions ? A : 0) + 3));
+    if (!states && (!actions || A <= 32)) {
+        hipLaunchKernelGGL(gather_small_kernel, dim3(ppo_divup(batch, TPB)), dim3(TPB), 0, ppo::stream(), perm, f,
+                           offset, limit, batch, A, action, logprob, advantage, adv_target, actions, logprobs, advs,
+                           adv_targets, rows);
+        PPO_LAUNCH_CHECK();
+        return;
+    }
     int grid = ppo_divup(batch, TPB / 64);
     if (grid > 8192) grid = 8192;
-    ppo::ProfScope ps(PPO_K_GATHER, 8.0 * batch * (S + A + 3));
     hipLaunchKernelGGL(gather_kernel, dim3(grid), dim3(TPB), 0, ppo::stream(), perm, f, offset, limit, batch, S, A,
-                       state, action, logprob, advantage, adv_target, states, actions, logprobs, advs, adv_targets);
+                       state, action, logprob, advantage, adv_target, states, actions, logprobs, advs, adv_targets,
+                       rows);
     PPO_LAUNCH_CHECK();
+}
+
+void phip_gather(const int* perm, uint64_t key, int offset, int limit, int batch, int S, int A,
+                 const float* state, const float* action, const float* logprob, const float* advantage,
+                 const float* adv_target, float* states, float* actions, float* logprobs, float* advs,
+                 float* adv_targets) {
+    phip_gather_rows(perm, key, offset, limit, batch, S, A, state, action, logprob, advantage, adv_target, states,
+                     actions, logprobs, advs, adv_targets, nullptr);
 }
 
 }  // extern "C"

@@ -36,6 +36,8 @@ struct Args {
     int M, N, K, lda, ldb, ldc;
     const float* bias; int relu;          // OP_NT epilogue
     const float* mask; int ldmask;        // OP_NN epilogue (post-activation of the previous layer)
+    const int* ridx;                      // OP_NT: A row r is memory row ridx[r] (fused gather)
+    float* acopy;                         // OP_NT: tn == 0 workgroups write the gathered A rows here
     unsigned* bits_out;                   // OP_NT + relu: bit (row, col) = y > 0, rows of wpr words
     const unsigned* bits_in;              // OP_NN: the ReLU′ mask as bits (replaces `mask`)
     int wpr;                              // words per row of a bit mask = ⌈N/32⌉
@@ -76,6 +78,19 @@ struct Stage {
     static_assert(R % 4 == 0, "tile rows");
     f32x4 v[ITERS];
     bool kok[ITERS];                                       // element's k inside [k0, kend)
+    int src[ITERS];                                        // kcont: memory row of tile row (gather)
+
+    // kcont rows are fixed for the whole k-loop: resolve them (clamp, optional row indirection
+    // `ridx` — the minibatch gather fused into layer 0) once, before it.
+    __device__ __forceinline__ void prep(const int* __restrict__ ridx, int r0, int Rmax, int tid) {
+#pragma unroll
+        for (int it = 0; it < ITERS; ++it) {
+            int row, k;
+            coords(tid + it * NT_, row, k);
+            const int gr = min(r0 + row, Rmax - 1);
+            src[it] = ridx ? ridx[gr] : gr;
+        }
+    }
 
     __device__ __forceinline__ static void coords(int idx, int& row, int& k) {
         if (MN) { row = (idx % RQ) * 4; k = idx / RQ; }    // lanes sweep a k-row: full 128-B lines
@@ -97,7 +112,7 @@ struct Stage {
                 if (VEC) {
                     kok[it] = gk < kend;
                     const float* p = MN ? P + (long)(gk < kend ? gk : kend - 1) * ld + (gr < Rmax ? gr : Rmax - 4)
-                                        : P + (long)(gr < Rmax ? gr : Rmax - 1) * ld + (gk < kend ? gk : kend - 4);
+                                        : P + (long)src[it] * ld + (gk < kend ? gk : kend - 4);
                     x = *reinterpret_cast<const f32x4*>(p);
                 } else if (MN) {
                     if (gk < kend) {
@@ -107,13 +122,37 @@ struct Stage {
                             if (gr + e < Rmax) x[e] = p[e];
                     }
                 } else if (gr < Rmax) {
-                    const float* p = P + (long)gr * ld + gk;
+                    const float* p = P + (long)src[it] * ld + gk;
 #pragma unroll
                     for (int e = 0; e < 4; ++e)
                         if (gk + e < kend) x[e] = p[e];
                 }
             }
             v[it] = x;
+        }
+    }
+
+    // kcont: write the staged tile (rows < Rmax, k < kend) to dst[row*ldd + k] — the gathered
+    // minibatch that layer 0's grad_W reads back.  Called at LDS-store time (data already waited for).
+    __device__ __forceinline__ void copy_out(float* __restrict__ dst, int ldd, int r0, int Rmax, int k0, int kend,
+                                             int tid) const {
+#pragma unroll
+        for (int it = 0; it < ITERS; ++it) {
+            const int idx = tid + it * NT_;
+            if (TOTAL % NT_ == 0 || idx < TOTAL) {
+                int row, k;
+                coords(idx, row, k);
+                const int gr = r0 + row, gk = k0 + k;
+                if (gr >= Rmax) continue;
+                float* q = dst + (long)gr * ldd + gk;
+                if (gk + 3 < kend && ((ldd & 3) == 0)) {
+                    *reinterpret_cast<f32x4*>(q) = v[it];
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (gk + e < kend) q[e] = v[it][e];
+                }
+            }
         }
     }
 
@@ -204,11 +243,16 @@ __global__ __launch_bounds__(NT_, min_waves(BM * BN, BK)) void gemm_f32_kernel(A
     SA sa;
     SB sb;
 
+    if (!A_MN) sa.prep(OP == OP_NT ? a.ridx : nullptr, m0, a.M, tid);
+    if (!B_MN) sb.prep(nullptr, n0, a.N, tid);
+    const bool do_copy = OP == OP_NT && a.acopy != nullptr && tn == 0;
+
     auto load = [&](int k0) {
         sa.template load<VEC>(a.A, a.lda, m0, a.M, k0, kend, tid);
         sb.template load<VEC>(a.B, a.ldb, n0, a.N, k0, kend, tid);
     };
-    auto store = [&](float* img) {
+    auto store = [&](float* img, int k0) {
+        if (do_copy) sa.copy_out(a.acopy, a.K, m0, a.M, k0, kend, tid);
         sa.store(img, tid);
         sb.store(img + SA::IMG, tid);
     };
@@ -238,21 +282,21 @@ __global__ __launch_bounds__(NT_, min_waves(BM * BN, BK)) void gemm_f32_kernel(A
         int cur = 0;
         if (kbeg < kend) {
             load(kbeg);
-            store(lds);
+            store(lds, kbeg);
         }
         __syncthreads();
         for (int k0 = kbeg; k0 < kend; k0 += BK) {
             const bool more = k0 + BK < kend;
             if (more) load(k0 + BK);               // in flight during this tile's MFMAs
             compute(lds + cur * IMG);
-            if (more) store(lds + (cur ^ 1) * IMG);  // the idle image: its last readers passed the barrier
+            if (more) store(lds + (cur ^ 1) * IMG, k0 + BK);  // idle image: its last readers passed the barrier
             __syncthreads();
             cur ^= 1;
         }
     } else {
         if (kbeg < kend) load(kbeg);
         for (int k0 = kbeg; k0 < kend; k0 += BK) {
-            store(lds);
+            store(lds, k0);
             __syncthreads();
             if (k0 + BK < kend) load(k0 + BK);        // in flight during this tile's MFMAs
             compute(lds);
@@ -408,8 +452,9 @@ int pick_cfg(int op, int M, int N, int* splitk_target = nullptr) {
 }
 
 void fwd(float* y, const float* x, const float* W, const float* b, int m, int n, int l, int relu, unsigned* bits,
-         int cfg) {
+         int cfg, const int* ridx = nullptr, float* acopy = nullptr) {
     Args a{};
+    a.ridx = ridx; a.acopy = acopy;
     a.A = x; a.lda = n; a.B = W; a.ldb = n; a.C = y; a.ldc = l;
     a.M = m; a.N = l; a.K = n; a.kchunk = n; a.splits = 1;
     a.bias = b; a.relu = relu;
@@ -481,6 +526,14 @@ void phip_linear_fwd_bits(float* y, const float* x, const float* W, const float*
 
 void phip_linear_fwd(float* y, const float* x, const float* W, const float* b, int m, int n, int l, int relu) {
     phip_linear_fwd_bits(y, x, W, b, m, n, l, relu, nullptr);
+}
+
+void phip_linear_fwd_gather(float* y, const float* x, const int* ridx, float* xcopy, const float* W, const float* b,
+                            int m, int n, int l, int relu, unsigned* bits) {
+    if (m <= 0 || l <= 0) return;
+    PPO_REQUIRE(y && x && ridx && W && n > 0, "phip_linear_fwd_gather: null operand");
+    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l);
+    fwd(y, x, W, b, m, n, l, relu, relu ? bits : nullptr, -1, ridx, xcopy);
 }
 
 void phip_linear_bwd_x_bits(float* gx, const float* g, const float* W, const float* mask, const unsigned* bits, int m,

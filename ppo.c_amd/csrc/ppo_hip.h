@@ -36,6 +36,10 @@ void phip_linear_fwd_bits(float* y, const float* x, const float* W, const float*
                           unsigned* bits);
 /* gx[m,n] = g[m,l]·W[l,n]; if mask: gx = (mask > 0) ? gx : 0 (K3 + K6 fused) */
 void phip_linear_bwd_x(float* gx, const float* g, const float* W, const float* mask, int m, int n, int l);
+/* forward whose input row r is x[ridx[r]] (the minibatch gather fused into layer 0); the gathered
+ * rows are also written to xcopy[m, n] (for the layer's grad_W) when xcopy != NULL */
+void phip_linear_fwd_gather(float* y, const float* x, const int* ridx, float* xcopy, const float* W, const float* b,
+                            int m, int n, int l, int relu, unsigned* bits);
 /* same with the mask given as bits (phip_linear_fwd_bits layout, ⌈n/32⌉ words per row) */
 void phip_linear_bwd_x_bits(float* gx, const float* g, const float* W, const float* mask, const unsigned* bits, int m,
                             int n, int l);
@@ -81,6 +85,12 @@ void phip_normalize(float* adv, int n, const double* d_welford, float* d_stats_o
 /* ---------------- buffer (buffer.hip) ---------------- */
 /* minibatch gather: row i ← perm[(offset+i) % limit] (perm != NULL) or
  * feistel((offset+i) % limit, limit, key) (perm == NULL).  Any dst may be NULL. */
+/* phip_gather that also (or, with states == NULL, instead of copying states) writes each slot's
+ * source row to rows[batch] — for layer 0's fused gather (phip_linear_fwd_gather) */
+void phip_gather_rows(const int* perm, uint64_t key, int offset, int limit, int batch, int S, int A,
+                      const float* state, const float* action, const float* logprob, const float* advantage,
+                      const float* adv_target, float* states, float* actions, float* logprobs, float* advs,
+                      float* adv_targets, int* rows);
 void phip_gather(const int* perm, uint64_t key, int offset, int limit, int batch, int S, int A,
                  const float* state, const float* action, const float* logprob,
                  const float* advantage, const float* adv_target,

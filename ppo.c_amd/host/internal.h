@@ -38,6 +38,7 @@ void nn_ensure_act(NeuralNetwork* nn, int m);
 void nn_ensure_grad(NeuralNetwork* nn, int m);
 /* device forward using d_x as layer-0 input (no copy) */
 void nn_forward_dev(NeuralNetwork* nn, const float* d_x, int m);
+void nn_forward_dev_rows(NeuralNetwork* nn, const float* d_x, const int* d_rows, float* d_xcopy, int m);
 /* device backward from d_grad_out (no copy unless the output activation needs masking) */
 void nn_backward_dev(NeuralNetwork* nn, const float* d_grad_out, int m, int want_grad_x0);
 

@@ -116,22 +116,31 @@ void nn_ensure_grad(NeuralNetwork* nn, int m) {
     nn->grad_cap_m = m;
 }
 
-void nn_forward_dev(NeuralNetwork* nn, const float* d_x, int m) {
+/* Forward over m rows.  With d_rows != NULL, input row r is d_x[d_rows[r]] (the minibatch gather
+ * fused into layer 0), and the gathered rows are written to d_xcopy, which backward then uses as
+ * layer 0's input. */
+void nn_forward_dev_rows(NeuralNetwork* nn, const float* d_x, const int* d_rows, float* d_xcopy, int m) {
     nn_ensure_act(nn, m);
     const int L = nn->num_layers - 1;
-    nn->d_x0 = d_x;
+    nn->d_x0 = d_rows ? d_xcopy : d_x;
     const float* in = d_x;
     for (int i = 0; i < L; i++) {
         Layer* ly = &nn->layers[i];
         float* out = nn->layers[i + 1].d_input;
-        phip_linear_fwd_bits(out, in, ly->d_weights, ly->d_biases, m, ly->input_size, ly->output_size,
-                             nn_is_relu(nn, i), act_bits(nn, i + 1));
+        if (i == 0 && d_rows)
+            phip_linear_fwd_gather(out, in, d_rows, d_xcopy, ly->d_weights, ly->d_biases, m, ly->input_size,
+                                   ly->output_size, nn_is_relu(nn, i), act_bits(nn, i + 1));
+        else
+            phip_linear_fwd_bits(out, in, ly->d_weights, ly->d_biases, m, ly->input_size, ly->output_size,
+                                 nn_is_relu(nn, i), act_bits(nn, i + 1));
         in = out;
     }
     nn->bits_m = m;
     nn->cache_m_forward = m;
     nn->d_output = nn->layers[L].d_input;
 }
+
+void nn_forward_dev(NeuralNetwork* nn, const float* d_x, int m) { nn_forward_dev_rows(nn, d_x, NULL, NULL, m); }
 
 void nn_backward_dev(NeuralNetwork* nn, const float* d_grad_out, int m, int want_grad_x0) {
     nn_ensure_grad(nn, m);

@@ -22,6 +22,7 @@ void buffer_point_device(TrajectoryBuffer* b);
 typedef struct {
     int cap_B, S, A;
     float *states, *actions, *old_lp, *adv, *tgt, *gv, *gmu;
+    int* rows;                    /* minibatch slot → buffer row (layer 0's fused gather) */
     float* stats;                 /* [0] Σ value loss, [1] Σ policy loss */
     long n_v, n_p;
     uint64_t key;                 /* device-shuffle epoch key */
@@ -74,7 +75,8 @@ static PPODev* dev_ws(PPO* ppo, int B) {
     }
     if (B > d->cap_B) {
         phip_free(d->states); phip_free(d->actions); phip_free(d->old_lp); phip_free(d->adv);
-        phip_free(d->tgt); phip_free(d->gv); phip_free(d->gmu);
+        phip_free(d->tgt); phip_free(d->gv); phip_free(d->gmu); phip_free(d->rows);
+        d->rows = (int*)phip_malloc(sizeof(int) * (size_t)B);
         d->states = (float*)phip_malloc(sizeof(float) * (size_t)B * S);
         d->actions = (float*)phip_malloc(sizeof(float) * (size_t)B * A);
         d->old_lp = (float*)phip_malloc(sizeof(float) * (size_t)B);
@@ -93,7 +95,7 @@ static void free_dev_ws(PPO* ppo) {
     PPODev* d = (PPODev*)ppo->dev;
     if (!d) return;
     phip_free(d->states); phip_free(d->actions); phip_free(d->old_lp); phip_free(d->adv);
-    phip_free(d->tgt); phip_free(d->gv); phip_free(d->gmu); phip_free(d->stats);
+    phip_free(d->tgt); phip_free(d->gv); phip_free(d->gmu); phip_free(d->stats); phip_free(d->rows);
     free(d);
     ppo->dev = NULL;
 }
@@ -268,9 +270,11 @@ void ppo_update(void* vppo, float gamma, int batch_size, int n_epochs_policy, in
         uint64_t key;
         const int* perm = next_perm(ppo, d, shuffle_mode, &key);
         for (int k = 0; k < num_batches; k++) {
-            phip_gather(perm, key, k * B, limit, B, S, A, buf->state_p, buf->action_p, buf->logprob_p,
-                        buf->advantage_p, buf->adv_target_p, d->states, NULL, NULL, NULL, d->tgt);
-            nn_forward_dev(V, d->states, B);
+            /* gather fused into layer 0: the kernel emits row indices (+ targets); the layer-0 GEMM
+             * reads the buffer rows through them and leaves the gathered copy for its grad_W */
+            phip_gather_rows(perm, key, k * B, limit, B, S, A, buf->state_p, buf->action_p, buf->logprob_p,
+                             buf->advantage_p, buf->adv_target_p, NULL, NULL, NULL, NULL, d->tgt, d->rows);
+            nn_forward_dev_rows(V, buf->state_p, d->rows, d->states, B);
             phip_mse(V->d_output, d->tgt, B, d->gv, NULL, d->stats + 0);
             nn_backward_dev(V, d->gv, B, 0);
             phip_allreduce_sum_f32(V->d_grads, V->num_params);
@@ -282,9 +286,10 @@ void ppo_update(void* vppo, float gamma, int batch_size, int n_epochs_policy, in
         uint64_t key;
         const int* perm = next_perm(ppo, d, shuffle_mode, &key);
         for (int k = 0; k < num_batches; k++) {
-            phip_gather(perm, key, k * B, limit, B, S, A, buf->state_p, buf->action_p, buf->logprob_p,
-                        buf->advantage_p, buf->adv_target_p, d->states, d->actions, d->old_lp, d->adv, NULL);
-            nn_forward_dev(mu, d->states, B);
+            phip_gather_rows(perm, key, k * B, limit, B, S, A, buf->state_p, buf->action_p, buf->logprob_p,
+                             buf->advantage_p, buf->adv_target_p, NULL, d->actions, d->old_lp, d->adv, NULL,
+                             d->rows);
+            nn_forward_dev_rows(mu, buf->state_p, d->rows, d->states, B);
             phip_policy_head(mu->d_output, pol->d_log_std, d->actions, d->adv, d->old_lp, B, A, ppo->epsilon,
                              ppo->ent_coeff, d->gmu, pol->d_log_std_grad, d->stats + 1);
             nn_backward_dev(mu, d->gmu, B, 0);
