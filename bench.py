@@ -9,7 +9,7 @@ Workload (config C4 of BASELINE.json): Humanoid-shaped 376 → 3×512 → 17 MLP
 every rank owns its own 4096×256 rollout (weak scaling), gradients are all-reduced with RCCL
 inside libppo each minibatch, advantage statistics are global.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c3|c2|c5f32] [--batch B]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c3|c2|c5|c5f32] [--batch B]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
 
 Prints ONE JSON line (rank 0).  `value` = learner env-steps/s over all ranks = world·N / t_update.
@@ -41,10 +41,13 @@ CONFIGS = {
     "c2": (3, [64, 64], 1, 4096, 1, 64),
     "c3": (17, [256, 256], 6, 4096, 64, 8192),
     "c4": (376, [512, 512, 512], 17, 4096, 256, 32768),
+    "c5": (1024, [1024, 1024, 1024, 1024], 17, 8192, 64, 16384),        # bf16 MFMA (8-GPU shard of 8192×512)
     "c5f32": (1024, [1024, 1024, 1024, 1024], 17, 8192, 64, 16384),
 }
 METRIC = "PPO updates/sec + env-steps/sec on 4096×256 synthetic rollout, 1/2/4/8 MI355X"
 PEAK_FP32_MFMA_TFLOPS = 157.3          # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 (spec; 155 measured)
+PEAK_BF16_MFMA_TFLOPS = 2500.0         # MI355X_MICROARCH.md: dense bf16 MFMA (spec, no sparsity)
+DTYPE = {"c5": "bf16"}                 # compute precision per config (default fp32)
 PEAK_HBM_GBPS = 8000.0
 
 
@@ -170,6 +173,10 @@ def main():
     C.CDLL("libc.so.6").srand(args.seed)                                 # identical init on every rank
     ppo = LIB.create_ppo(ppo_ffi.c_strings(acts), ppo_ffi.c_ints(sizes), len(sizes), N, 3e-4, 3e-4, 0.95, 0.2, 0.0,
                          1.0, True)
+    dtype = DTYPE.get(args.config, "fp32")
+    peak = PEAK_BF16_MFMA_TFLOPS if dtype == "bf16" else PEAK_FP32_MFMA_TFLOPS
+    if LIB.ppo_set_compute_dtype(ppo, 1 if dtype == "bf16" else 0) != 0:
+        raise SystemExit("ppo_set_compute_dtype failed")
     LIB.ppo_fill_synthetic(ppo, E, T, args.seed * 1000 + rank, 1.0 / 500)
     LIB.ppo_synchronize()
 
@@ -225,7 +232,7 @@ def main():
         "higher_is_better": True,
         "scaling": "strong" if args.strong else "weak",
         "vs_baseline": None,
-        "dtype": "fp32",
+        "dtype": dtype,
         "data": "synthetic (seeded device generator: obs U(-1,1), actions from the policy, rewards 0.1·N(0,1), "
                 "terminated Bernoulli(1/500), truncated at env-segment ends); random-init weights",
         "config": {"workload": f"{args.config}: {S}->{'x'.join(map(str, H))}->{A} MLP (policy + value), "
@@ -235,17 +242,19 @@ def main():
         "updates_per_sec": 1.0 / t_update,
         "minibatch_steps_per_sec": 14 * (N // B) / t_update,
         "algorithmic_tflop_per_update": flops / 1e12,
-        "mfma_frac_whole_update": flops / t_update / (PEAK_FP32_MFMA_TFLOPS * 1e12),
+        "mfma_frac_whole_update": flops / t_update / (peak * 1e12),
         "kernels": kernels,
         "loss": {"value_mean": stats[0] / max(1.0, stats[1]), "policy_mean": stats[2] / max(1.0, stats[3])},
     }
     if gemm_n and gemm_ms > 0:
         achieved = gemm_flops / (gemm_ms * 1e-3) / 1e12
-        traffic, traffic_src = pmc_traffic()
-        result["roofline"] = {"bound": "mfma", "achieved": achieved, "peak": PEAK_FP32_MFMA_TFLOPS,
-                              "unit": "TFLOP/s", "frac": achieved / PEAK_FP32_MFMA_TFLOPS, "traffic": traffic,
+        traffic, traffic_src = pmc_traffic() if args.config == "c4" else (None, None)   # PMC pass is of c4
+        result["roofline"] = {"bound": "mfma", "achieved": achieved, "peak": peak,
+                              "unit": "TFLOP/s", "frac": achieved / peak, "traffic": traffic,
                               "traffic_source": traffic_src,
-                              "kernel": "gemm_f32_kernel (linear-layer launches, every event_stride-th sampled over the timed region: Σ 2MNK / Σ HIP-event time)",
+                              "kernel": ("gemm_bf16_kernel" if dtype == "bf16" else "gemm_f32_kernel") +
+                                        " (linear-layer launches, every event_stride-th sampled over the timed "
+                                        "region: Σ 2MNK / Σ HIP-event time)",
                               "launches": gemm_n, "event_stride": args.event_stride,
                               "avg_launch_us": 1000.0 * gemm_ms / gemm_n,
                               "algorithmic_flop_per_launch": gemm_flops / gemm_n}

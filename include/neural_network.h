@@ -82,6 +82,9 @@ typedef struct {
     const float* d_x0;      /* input of layer 0 used by the last device forward */
     unsigned* d_act_bits;   /* ReLU′ masks as bits, one [act_cap_m, ⌈size_i/32⌉] block per layer input */
     int    bits_m;          /* rows of the forward that wrote d_act_bits (−1: none valid) */
+    int    dtype;           /* compute mode: 0 = fp32 (default), 1 = bf16 MFMA (C5) — see ppo_ext.h */
+    int    x0_dtype;        /* storage of d_x0: 0 = fp32, 1 = bf16 (the gathered copy in bf16 mode) */
+    unsigned short* d_w16;  /* bf16 mode: bf16 shadow of d_params (same offsets), refreshed after updates */
 } NeuralNetwork;
 
 typedef struct {

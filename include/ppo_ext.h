@@ -77,6 +77,13 @@ void ppo_sample_action_device(void* policy, float* d_state, float* d_action, flo
  * terminated ~ Bernoulli(p_terminate), truncated at each segment end. */
 void ppo_fill_synthetic(void* ppo, int n_envs, int horizon, unsigned long long seed, float p_terminate);
 
+/* ---------------- compute precision ---------------- */
+/* 0 = fp32 (default: exact fp32 MFMA GEMMs), 1 = bf16 MFMA GEMMs with fp32 accumulation, fp32
+ * master parameters / Adam / heads / GAE, bf16 storage of hidden activations and their gradients
+ * (BASELINE config C5).  Returns 0, or −1 for an invalid dtype. */
+int ppo_set_compute_dtype(void* ppo, int dtype);
+int nn_set_compute_dtype(void* nn, int dtype);          /* NeuralNetwork* */
+
 /* ---------------- GEMM tuning utilities ---------------- */
 /* force a tile configuration (−1 = automatic) and the split-K workgroup target of grad_W
  * (0 = per-shape automatic, < 0 keeps the current setting); returns the number of tile configurations */
@@ -84,6 +91,8 @@ int    ppo_gemm_tune(int force_cfg, int splitk_target);
 /* average device µs of one launch: op 0 = forward (bias+ReLU), 1 = grad_x, 2 = grad_W (+bias grad);
  * m = batch, n = in, l = out; cfg −1 = automatic */
 double ppo_bench_gemm(int op, int m, int n, int l, int iters, int cfg);
+/* bf16 GEMMs: force a tile configuration (−1 = automatic); returns the number of configurations */
+int    ppo_gemm16_tune(int force_cfg);
 
 /* ---------------- kernel timing ---------------- */
 enum { PPO_K_GEMM = 0, PPO_K_GAE = 1, PPO_K_ADAM = 2, PPO_K_GATHER = 3, PPO_K_HEAD = 4,

@@ -1,0 +1,493 @@
+// gemm16.hip — bf16-MFMA GEMMs for the bf16 compute mode (BASELINE config C5: "4×1024 MLP bf16").
+//
+// The same three linear-layer products as gemm.hip (reference mat_mul.cu:122-217, the fused
+// bias/ReLU of activation_function.cu and the bias-gradient sum of neural_network.cu:108-118), on
+// v_mfma_f32_32x32x16_bf16: bf16 operands, fp32 accumulation, 16× the fp32-MFMA rate.
+//   forward   y = x·Wᵀ + b (+ReLU, +ReLU′ bits)     NT
+//   grad_x    gx = (g·W) ⊙ 1[y_prev > 0]              NN
+//   grad_W    gW += gᵀ·x, gb += Σ g   (split-K, f32 atomics)  TN
+// Operands may be stored fp32 (network input, the heads' output gradient) or bf16 (hidden
+// activations and their gradients, the bf16 weight shadow); they are rounded to bf16 on the way
+// into LDS.  Outputs are fp32 or bf16 (hidden activations / gradients), accumulation always fp32.
+//
+// Design (gfx950):
+//  * 256-thread workgroups (4 waves), block tile BM×BN, BK = 32 (two MFMA k-steps per tile).
+//  * k-contiguous operands ("kcont": x, g in grad_x, W in forward) are staged as [row][BK+8] bf16:
+//    a lane's fragment (A[r][8h..8h+7]) is one conflict-free ds_read_b128 (80-B pitch: row·20 mod
+//    64 dwords spreads every 16-lane group over distinct banks).
+//  * row-contiguous operands ("mncont": W in grad_x, g and x in grad_W) are staged as
+//    [BK][R (+32)] bf16 exactly as loaded, and a fragment is two ds_read_b64_tr_b16 hardware
+//    transposes (4 k × 16 rows per 16-lane group); the pitch ≡ 16 or 48 dwords (mod 64) keeps the
+//    4 rows × 2 groups of each 32-lane half on disjoint banks.
+//  * Branch-free clamped loads, the k-mask applied at LDS-store time, register prefetch of the next
+//    k-tile behind this tile's MFMAs, XCD-aware block remap — as in gemm.hip.
+#include "dev.h"
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int NT_ = 256;
+constexpr int BK = 32;
+
+enum Op { OP_NT = 0, OP_NN = 1, OP_TN = 2 };
+
+struct Args {
+    const void* A; const void* B; void* C;
+    int M, N, K, lda, ldb, ldc;
+    const float* bias; int relu;
+    const int* ridx; void* acopy;         // OP_NT: fused gather of A's rows + the gathered copy (bf16)
+    unsigned* bits_out; const unsigned* bits_in; int wpr;
+    float* gbias;
+    int kchunk, splits, tiles_m, tiles_n;
+    int vec;
+};
+
+// fp32 → bf16, round to nearest even (NaN stays NaN: v_cvt_pk_bf16_f32)
+__device__ __forceinline__ unsigned pack2(float lo, float hi) {
+    typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+    bf16x2 p = {(__bf16)lo, (__bf16)hi};
+    return __builtin_bit_cast(unsigned, p);
+}
+__device__ __forceinline__ float bf_lo(unsigned u) { return __builtin_bit_cast(float, u << 16); }
+
+// ---------------------------------------------------------------------------
+// Staging of one operand tile (R rows × BK k) into a bf16 LDS image.  T = float or unsigned short
+// (bf16 bits).  One 16-B global load per slot: 4 fp32 or 8 bf16 elements.
+// ---------------------------------------------------------------------------
+template <int R, bool MN, typename T>
+struct Stage16 {
+    static constexpr bool F32 = sizeof(T) == 4;
+    static constexpr int EPL = F32 ? 4 : 8;                 // elements per 16-B load
+    static constexpr int PK = BK + 8;                       // kcont pitch (elements) = 80 B
+    static constexpr int PR = ((R / 2) % 64 == 16 || (R / 2) % 64 == 48) ? R : R + 32;   // mncont pitch
+    static constexpr int IMG = MN ? BK * PR : R * PK;       // bf16 elements
+    static constexpr int PER_ROW = MN ? R / EPL : BK / EPL; // loads along the contiguous dimension
+    static constexpr int TOTAL = MN ? BK * PER_ROW : R * PER_ROW;
+    static constexpr int ITERS = (TOTAL + NT_ - 1) / NT_;
+    static_assert(R % EPL == 0 && R >= 32, "tile rows");
+    u32x4 v[ITERS];
+    bool kok[ITERS];
+    int src[ITERS];
+
+    __device__ __forceinline__ static void coords(int idx, int& row, int& k) {
+        if (MN) { row = (idx % PER_ROW) * EPL; k = idx / PER_ROW; }
+        else    { row = idx / PER_ROW; k = (idx % PER_ROW) * EPL; }
+    }
+
+    __device__ __forceinline__ void prep(const int* __restrict__ ridx, int r0, int Rmax, int tid) {
+#pragma unroll
+        for (int it = 0; it < ITERS; ++it) {
+            int row, k;
+            coords(tid + it * NT_, row, k);
+            const int gr = min(r0 + row, Rmax - 1);
+            src[it] = ridx ? ridx[gr] : gr;
+        }
+    }
+
+    // vec: every contiguous extent and ld are multiples of EPL and the base is 16-B aligned
+    __device__ __forceinline__ void load(const T* __restrict__ P, int ld, int r0, int Rmax, int k0, int kend,
+                                         bool vec, int tid) {
+#pragma unroll
+        for (int it = 0; it < ITERS; ++it) {
+            const int idx = tid + it * NT_;
+            u32x4 x = {0u, 0u, 0u, 0u};
+            kok[it] = true;
+            if (TOTAL % NT_ == 0 || idx < TOTAL) {
+                int row, k;
+                coords(idx, row, k);
+                const int gr = r0 + row, gk = k0 + k;
+                if (vec) {
+                    kok[it] = gk < kend;
+                    const T* p = MN ? P + (long)(gk < kend ? gk : kend - 1) * ld + (gr < Rmax ? gr : Rmax - EPL)
+                                    : P + (long)src[it] * ld + (gk < kend ? gk : kend - EPL);
+                    x = *reinterpret_cast<const u32x4*>(p);
+                } else {
+                    T e[EPL];
+#pragma unroll
+                    for (int q = 0; q < EPL; ++q) e[q] = T(0);
+                    if (MN) {
+                        if (gk < kend) {
+                            const T* p = P + (long)gk * ld + gr;
+#pragma unroll
+                            for (int q = 0; q < EPL; ++q)
+                                if (gr + q < Rmax) e[q] = p[q];
+                        }
+                    } else if (gr < Rmax) {
+                        const T* p = P + (long)src[it] * ld + gk;
+#pragma unroll
+                        for (int q = 0; q < EPL; ++q)
+                            if (gk + q < kend) e[q] = p[q];
+                    }
+                    x = __builtin_bit_cast(u32x4, e);
+                }
+            }
+            v[it] = x;
+        }
+    }
+
+    __device__ __forceinline__ void store(unsigned short* img, int tid) const {
+#pragma unroll
+        for (int it = 0; it < ITERS; ++it) {
+            const int idx = tid + it * NT_;
+            if (TOTAL % NT_ == 0 || idx < TOTAL) {
+                int row, k;
+                coords(idx, row, k);
+                unsigned short* d = img + (MN ? k * PR + row : row * PK + k);
+                const u32x4 z = {0u, 0u, 0u, 0u};
+                const u32x4 x = kok[it] ? v[it] : z;
+                if (F32) {
+                    const f32x4 f = __builtin_bit_cast(f32x4, x);
+                    const u32x2 p = {pack2(f[0], f[1]), pack2(f[2], f[3])};
+                    *reinterpret_cast<u32x2*>(d) = p;
+                } else {
+                    *reinterpret_cast<u32x4*>(d) = x;
+                }
+            }
+        }
+    }
+
+    // A-side fused gather: write the staged rows (rows < Rmax, k < kend) as bf16 to dst[row*ldd + k]
+    __device__ __forceinline__ void copy_out(unsigned short* __restrict__ dst, int ldd, int r0, int Rmax, int k0,
+                                             int kend, int tid) const {
+#pragma unroll
+        for (int it = 0; it < ITERS; ++it) {
+            const int idx = tid + it * NT_;
+            if (TOTAL % NT_ == 0 || idx < TOTAL) {
+                int row, k;
+                coords(idx, row, k);
+                const int gr = r0 + row, gk = k0 + k;
+                if (gr >= Rmax) continue;
+                unsigned short* q = dst + (long)gr * ldd + gk;
+                if (F32) {
+                    const f32x4 f = __builtin_bit_cast(f32x4, v[it]);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (gk + e < kend) q[e] = (unsigned short)(pack2(f[e], 0.f) & 0xffffu);
+                } else {
+                    const unsigned short* s = reinterpret_cast<const unsigned short*>(&v[it]);
+#pragma unroll
+                    for (int e = 0; e < 8; ++e)
+                        if (gk + e < kend) q[e] = s[e];
+                }
+            }
+        }
+    }
+
+    // MFMA fragment of k-step ks for image row `row`: elements k = 16·ks + 8h + j, j = 0..7
+    __device__ __forceinline__ static bf16x8 frag(const unsigned short* img, int row, int ks, int lane) {
+        const int h = lane >> 5;
+        if (!MN) return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(img + row * PK + 16 * ks + 8 * h));
+        // hardware transpose: in each 16-lane group, lane 4q+p addresses k-row q, rows 4p..4p+3 of the
+        // group's 16; lane i receives row i of the 4 k-rows.  Two reads give k = 8h+0..3 and 8h+4..7.
+        const int gi = lane & 15, q = gi >> 2, p = gi & 3;
+        const int rbase = row - gi;                       // first row of this lane's 16-row group
+        typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+        const unsigned short* a0 = img + (16 * ks + 8 * h + q) * PR + rbase + 4 * p;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 4 * PR));
+        typedef short s16x8 __attribute__((ext_vector_type(8)));
+        const s16x8 f = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        return __builtin_bit_cast(bf16x8, f);
+    }
+
+    // Σ over this tile's k of image row `row` (fp32), k ∈ [k_lo, k_lo + n)
+    __device__ __forceinline__ static float rowsum(const unsigned short* img, int row, int k_lo, int n) {
+        float t = 0.f;
+        for (int kk = 0; kk < n; ++kk) {
+            const unsigned short b = MN ? img[(k_lo + kk) * PR + row] : img[row * PK + k_lo + kk];
+            t += __builtin_bit_cast(float, (unsigned)b << 16);
+        }
+        return t;
+    }
+};
+
+template <typename T> struct Bits;
+template <> struct Bits<float> { static constexpr int code = 0; };
+template <> struct Bits<unsigned short> { static constexpr int code = 1; };
+
+template <int OP, int BM, int BN, int WARPS_M, typename TA, typename TB, typename TC>
+__global__ __launch_bounds__(NT_, 2) void gemm_bf16_kernel(Args a) {
+    constexpr int WARPS_N = 4 / WARPS_M;
+    constexpr int WM = BM / WARPS_M, WN = BN / WARPS_N;
+    constexpr int TM = WM / 32, TN = WN / 32;
+    constexpr bool A_MN = OP == OP_TN, B_MN = OP != OP_NT;
+    using SA = Stage16<BM, A_MN, TA>;
+    using SB = Stage16<BN, B_MN, TB>;
+    static_assert(TM >= 1 && TN >= 1, "wave tile must be a multiple of 32x32");
+    static_assert(!(OP == OP_TN) || sizeof(TC) == 4, "grad_W accumulates in fp32");
+
+    __shared__ __attribute__((aligned(16))) unsigned short lds[SA::IMG + SB::IMG];
+
+    const int nwg = gridDim.x, b = blockIdx.x;
+    const int xcd = b & 7, qq = nwg >> 3, rr = nwg & 7;
+    const int t = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (b >> 3);
+    const int tn = t % a.tiles_n;
+    const int rest = t / a.tiles_n;
+    const int tm = rest % a.tiles_m;
+    const int split = rest / a.tiles_m;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int kbeg = split * a.kchunk;
+    const int kend = min(a.K, kbeg + a.kchunk);
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = w / WARPS_N, wn = w % WARPS_N;
+    const int r = lane & 31, h = lane >> 5;
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+    constexpr int TPR = NT_ / BM > 0 ? NT_ / BM : 1;
+    constexpr int KPT = BK / TPR > 0 ? BK / TPR : 1;
+    const bool do_bsum = OP == OP_TN && a.gbias != nullptr && tn == 0 && (NT_ % BM == 0);
+    float bsum = 0.f;
+
+    SA sa;
+    SB sb;
+    if (!A_MN) sa.prep(OP == OP_NT ? a.ridx : nullptr, m0, a.M, tid);
+    if (!B_MN) sb.prep(nullptr, n0, a.N, tid);
+    const bool do_copy = OP == OP_NT && a.acopy != nullptr && tn == 0;
+    const bool vec = a.vec != 0;
+    const TA* __restrict__ PA = static_cast<const TA*>(a.A);
+    const TB* __restrict__ PB = static_cast<const TB*>(a.B);
+
+    auto load = [&](int k0) {
+        sa.load(PA, a.lda, m0, a.M, k0, kend, vec, tid);
+        sb.load(PB, a.ldb, n0, a.N, k0, kend, vec, tid);
+    };
+
+    if (kbeg < kend) load(kbeg);
+    for (int k0 = kbeg; k0 < kend; k0 += BK) {
+        if (do_copy) sa.copy_out(static_cast<unsigned short*>(a.acopy), a.K, m0, a.M, k0, kend, tid);
+        sa.store(lds, tid);
+        sb.store(lds + SA::IMG, tid);
+        __syncthreads();
+        if (k0 + BK < kend) load(k0 + BK);            // in flight during this tile's MFMAs
+        const unsigned short* As = lds;
+        const unsigned short* Bs = lds + SA::IMG;
+        if (do_bsum) bsum += SA::rowsum(As, tid / TPR, (tid % TPR) * KPT, KPT);
+#pragma unroll
+        for (int ks = 0; ks < BK / 16; ++ks) {
+            bf16x8 fa[TM], fb[TN];
+#pragma unroll
+            for (int i = 0; i < TM; ++i) fa[i] = SA::frag(As, wm * WM + i * 32 + r, ks, lane);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) fb[j] = SB::frag(Bs, wn * WN + j * 32 + r, ks, lane);
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+
+    if (do_bsum) {
+#pragma unroll
+        for (int o = TPR / 2; o > 0; o >>= 1) bsum += __shfl_xor(bsum, o, 64);
+        const int row = tid / TPR, seg = tid % TPR;
+        if (seg == 0 && m0 + row < a.M) {
+            if (a.splits > 1) atomicAdd(a.gbias + m0 + row, bsum);
+            else a.gbias[m0 + row] = bsum;
+        }
+    }
+
+    // epilogue (C/D map as gemm.hip); every load a block needs is issued before its stores
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int c0 = n0 + wn * WN + j * 32;
+            const int col = c0 + r;
+            const int r0 = m0 + wm * WM + i * 32 + 4 * h;
+            const bool col_ok = col < a.N;
+            float bcol = 0.f;
+            if (OP == OP_NT && a.bias) bcol = a.bias[col_ok ? col : a.N - 1];
+            bool keep[16];
+            if (OP == OP_NN) {
+                if (a.bits_in) {
+                    unsigned wv[16];
+#pragma unroll
+                    for (int e = 0; e < 16; ++e)
+                        wv[e] = a.bits_in[(long)min(r0 + (e & 3) + 8 * (e >> 2), a.M - 1) * a.wpr + (c0 >> 5)];
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) keep[e] = (wv[e] >> r) & 1u;
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) keep[e] = true;
+                }
+            }
+            unsigned word = 0;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int row = r0 + (e & 3) + 8 * (e >> 2);
+                const bool ok = col_ok && row < a.M;
+                float v = acc[i][j][e];
+                const long off = (long)row * a.ldc + col;
+                if (OP == OP_NT) {
+                    v += bcol;
+                    if (a.relu) v = v > 0.f ? v : 0.f;
+                    if (Bits<TC>::code == 1) {
+                        const unsigned short hv = (unsigned short)(pack2(v, 0.f) & 0xffffu);
+                        v = bf_lo(hv);                  // bits describe the stored (rounded) value
+                        if (ok) static_cast<unsigned short*>(a.C)[off] = hv;
+                    } else if (ok) {
+                        static_cast<float*>(a.C)[off] = v;
+                    }
+                    if (a.bits_out) {
+                        const unsigned long long bb = __ballot(ok && v > 0.f);
+                        if (r == e) word = h ? (unsigned)(bb >> 32) : (unsigned)bb;
+                    }
+                } else if (OP == OP_NN) {
+                    if (ok) {
+                        v = keep[e] ? v : 0.f;
+                        if (Bits<TC>::code == 1) static_cast<unsigned short*>(a.C)[off] =
+                            (unsigned short)(pack2(v, 0.f) & 0xffffu);
+                        else static_cast<float*>(a.C)[off] = v;
+                    }
+                } else if (ok) {
+                    float* dst = static_cast<float*>(a.C) + off;
+                    if (a.splits > 1) atomicAdd(dst, v);
+                    else *dst = v;
+                }
+            }
+            if (OP == OP_NT && a.bits_out && r < 16) {
+                const int row = r0 + (r & 3) + 8 * (r >> 2);
+                if (row < a.M && c0 < a.N) a.bits_out[(long)row * a.wpr + (c0 >> 5)] = word;
+            }
+        }
+}
+
+using f32 = float;
+using b16 = unsigned short;
+
+template <int OP, int BM, int BN, int WM_, typename TA, typename TB, typename TC>
+void launch(Args a) {
+    a.tiles_m = ppo_divup(a.M, BM);
+    a.tiles_n = ppo_divup(a.N, BN);
+    if (a.splits < 1) a.splits = 1;
+    const long grid = (long)a.tiles_m * a.tiles_n * a.splits;
+    PPO_REQUIRE(grid > 0 && grid < (1L << 31), "gemm16: grid out of range");
+    hipLaunchKernelGGL((gemm_bf16_kernel<OP, BM, BN, WM_, TA, TB, TC>), dim3((unsigned)grid), dim3(NT_), 0,
+                       ppo::stream(), a);
+    PPO_LAUNCH_CHECK();
+}
+
+// tile configurations: 0 = 128x128 (4 waves of 64x64), 1 = 128x32 (skinny N), 2 = 32x128
+// (skinny M), 3 = 64x64
+struct Cfg { int bm, bn; };
+constexpr Cfg kCfgs[] = {{128, 128}, {128, 32}, {32, 128}, {64, 64}};
+int g_force16 = -1;
+
+template <int OP, typename TA, typename TB, typename TC>
+void launch_cfg(int c, const Args& a) {
+    switch (c) {
+        case 0: launch<OP, 128, 128, 2, TA, TB, TC>(a); break;
+        case 1: launch<OP, 128, 32, 4, TA, TB, TC>(a); break;
+        case 2: launch<OP, 32, 128, 1, TA, TB, TC>(a); break;
+        default: launch<OP, 64, 64, 2, TA, TB, TC>(a); break;
+    }
+}
+
+int pick16(int M, int N) {
+    if (g_force16 >= 0) return g_force16;
+    if (N <= 32 && M > 32) return 1;
+    if (M <= 32 && N > 32) return 2;
+    if (M <= 64 || N <= 64) return 3;
+    return 0;
+}
+
+inline bool al16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+inline int epl(int t) { return t ? 8 : 4; }
+
+}  // namespace
+
+extern "C" {
+
+// dtype codes: 0 = fp32, 1 = bf16 (storage).  W16 is the bf16 shadow of W [l, n].
+void phip_linear16_fwd(void* y, int ty, const void* x, int tx, const int* ridx, void* xcopy16, const void* W16,
+                       const float* b, int m, int n, int l, int relu, unsigned* bits) {
+    if (m <= 0 || l <= 0) return;
+    PPO_REQUIRE(y && x && W16 && n > 0, "phip_linear16_fwd: null operand");
+    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l);
+    Args a{};
+    a.A = x; a.lda = n; a.B = W16; a.ldb = n; a.C = y; a.ldc = l;
+    a.M = m; a.N = l; a.K = n; a.kchunk = n; a.splits = 1;
+    a.bias = b; a.relu = relu; a.ridx = ridx; a.acopy = xcopy16;
+    a.bits_out = relu ? bits : nullptr; a.wpr = ppo_divup(l, 32);
+    a.vec = n % 8 == 0 && al16(x) && al16(W16);
+    const int c = pick16(m, l);
+    if (tx == 0 && ty == 0) launch_cfg<OP_NT, f32, b16, f32>(c, a);
+    else if (tx == 0) launch_cfg<OP_NT, f32, b16, b16>(c, a);
+    else if (ty == 0) launch_cfg<OP_NT, b16, b16, f32>(c, a);
+    else launch_cfg<OP_NT, b16, b16, b16>(c, a);
+}
+
+void phip_linear16_bwd_x(void* gx, int tgx, const void* g, int tg, const void* W16, const unsigned* bits, int m,
+                         int n, int l) {
+    if (m <= 0 || n <= 0) return;
+    PPO_REQUIRE(gx && g && W16 && l > 0, "phip_linear16_bwd_x: null operand");
+    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l);
+    Args a{};
+    a.A = g; a.lda = l; a.B = W16; a.ldb = n; a.C = gx; a.ldc = n;
+    a.M = m; a.N = n; a.K = l; a.kchunk = l; a.splits = 1;
+    a.bits_in = bits; a.wpr = ppo_divup(n, 32);
+    a.vec = l % epl(tg) == 0 && n % 8 == 0 && al16(g) && al16(W16);
+    const int c = pick16(m, n);
+    if (tg == 0 && tgx == 0) launch_cfg<OP_NN, f32, b16, f32>(c, a);
+    else if (tg == 0) launch_cfg<OP_NN, f32, b16, b16>(c, a);
+    else if (tgx == 0) launch_cfg<OP_NN, b16, b16, f32>(c, a);
+    else launch_cfg<OP_NN, b16, b16, b16>(c, a);
+}
+
+void phip_linear16_bwd_w(float* gW, float* gb, const void* g, int tg, const void* x, int tx, int m, int n, int l,
+                         int zeroed) {
+    if (l <= 0 || n <= 0) return;
+    PPO_REQUIRE(gW && g && x, "phip_linear16_bwd_w: null operand");
+    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l);
+    if (m <= 0) {
+        if (!zeroed) {
+            phip_memset(gW, 0, sizeof(float) * (size_t)l * n);
+            if (gb) phip_memset(gb, 0, sizeof(float) * (size_t)l);
+        }
+        return;
+    }
+    const int c = pick16(l, n);
+    const long tiles = (long)ppo_divup(l, kCfgs[c].bm) * ppo_divup(n, kCfgs[c].bn);
+    int splits = (int)((1024 + tiles - 1) / tiles);
+    const int max_splits = m / (4 * BK) > 0 ? m / (4 * BK) : 1;          // ≥ 4 k-tiles per split
+    if (splits > max_splits) splits = max_splits;
+    if (splits < 1) splits = 1;
+    int kchunk = ppo_divup(ppo_divup(m, splits), BK) * BK;
+    splits = ppo_divup(m, kchunk);
+    Args a{};
+    a.A = g; a.lda = l; a.B = x; a.ldb = n; a.C = gW; a.ldc = n;
+    a.M = l; a.N = n; a.K = m; a.kchunk = kchunk; a.splits = splits;
+    a.gbias = gb;
+    a.vec = l % epl(tg) == 0 && n % epl(tx) == 0 && al16(g) && al16(x);
+    if (splits > 1 && !zeroed) {
+        phip_memset(gW, 0, sizeof(float) * (size_t)l * n);
+        if (gb) phip_memset(gb, 0, sizeof(float) * (size_t)l);
+    }
+    if (tg == 0 && tx == 0) launch_cfg<OP_TN, f32, f32, f32>(c, a);
+    else if (tg == 0) launch_cfg<OP_TN, f32, b16, f32>(c, a);
+    else if (tx == 0) launch_cfg<OP_TN, b16, f32, f32>(c, a);
+    else launch_cfg<OP_TN, b16, b16, f32>(c, a);
+}
+
+int ppo_gemm16_tune(int force_cfg) {
+    g_force16 = force_cfg;
+    return (int)(sizeof(kCfgs) / sizeof(kCfgs[0]));
+}
+
+}  // extern "C"

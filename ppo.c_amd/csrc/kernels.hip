@@ -54,6 +54,11 @@ __global__ void relu_bwd_kernel(const float* __restrict__ y, float* __restrict__
         if (!(y[i] > 0.f)) g[i] = 0.f;
 }
 
+// fp32 → bf16 (round to nearest even, NaN preserved: the plain cast lowers to v_cvt_pk_bf16_f32)
+__global__ void f32_to_bf16_kernel(__bf16* __restrict__ dst, const float* __restrict__ src, long n) {
+    for (long i = blockIdx.x * (long)TPB + threadIdx.x; i < n; i += (long)gridDim.x * TPB) dst[i] = (__bf16)src[i];
+}
+
 __global__ void axpy_kernel(float* __restrict__ y, const float* __restrict__ x, long n) {
     for (long i = blockIdx.x * (long)TPB + threadIdx.x; i < n; i += (long)gridDim.x * TPB) y[i] += x[i];
 }
@@ -223,6 +228,14 @@ void phip_relu_bwd(const float* y, float* g, long count) {
     if (count <= 0) return;
     ppo::ProfScope ps(PPO_K_OTHER, 12.0 * count);
     hipLaunchKernelGGL(relu_bwd_kernel, dim3(grid_for(count, 4)), dim3(TPB), 0, ppo::stream(), y, g, count);
+    PPO_LAUNCH_CHECK();
+}
+
+void phip_f32_to_bf16(unsigned short* dst, const float* src, long count) {
+    if (count <= 0) return;
+    ppo::ProfScope ps(PPO_K_OTHER, 6.0 * count);
+    hipLaunchKernelGGL(f32_to_bf16_kernel, dim3(grid_for(count, 4)), dim3(TPB), 0, ppo::stream(),
+                       reinterpret_cast<__bf16*>(dst), src, count);
     PPO_LAUNCH_CHECK();
 }
 

@@ -48,6 +48,19 @@ void phip_linear_bwd_w(float* gW, float* gb, const float* g, const float* x, int
 /* same, with gW/gb already zero on entry when `zeroed` (one memset per backward instead of two per layer) */
 void phip_linear_bwd_w_ex(float* gW, float* gb, const float* g, const float* x, int m, int n, int l, int zeroed);
 
+/* ---------------- bf16-MFMA dense layers (gemm16.hip) ---------------- */
+/* dtype codes t*: 0 = fp32 storage, 1 = bf16 storage; W16 = bf16 shadow of W [l, n]; fp32 accumulation.
+ * forward (optional fused gather: ridx / bf16 copy of the gathered rows in xcopy16) */
+void phip_linear16_fwd(void* y, int ty, const void* x, int tx, const int* ridx, void* xcopy16, const void* W16,
+                       const float* b, int m, int n, int l, int relu, unsigned* bits);
+/* gx = (g·W) ⊙ bits (bits may be NULL: no mask) */
+void phip_linear16_bwd_x(void* gx, int tgx, const void* g, int tg, const void* W16, const unsigned* bits, int m,
+                         int n, int l);
+/* gW[l,n] (+)= gᵀ·x, gb (+)= Σ g in fp32 (zeroed != 0: outputs already zero) */
+void phip_linear16_bwd_w(float* gW, float* gb, const void* g, int tg, const void* x, int tx, int m, int n, int l,
+                         int zeroed);
+void phip_f32_to_bf16(unsigned short* dst, const float* src, long count);
+
 /* ---------------- element-wise / heads (kernels.hip) ---------------- */
 void phip_relu(float* x, long count);
 void phip_relu_bwd(const float* y, float* g, long count);

@@ -43,6 +43,7 @@ void nn_forward_dev_rows(NeuralNetwork* nn, const float* d_x, const int* d_rows,
 void nn_backward_dev(NeuralNetwork* nn, const float* d_grad_out, int m, int want_grad_x0);
 
 NeuralNetwork* nn_load_ex(FILE* file, long extra_floats);
+void nn_sync_w16(NeuralNetwork* nn);       /* bf16 mode: refresh the bf16 weight shadow */
 
 /* trajectory_buffer.c */
 void buffer_point_device(TrajectoryBuffer* b);

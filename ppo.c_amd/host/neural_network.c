@@ -119,10 +119,36 @@ void nn_ensure_grad(NeuralNetwork* nn, int m) {
 /* Forward over m rows.  With d_rows != NULL, input row r is d_x[d_rows[r]] (the minibatch gather
  * fused into layer 0), and the gathered rows are written to d_xcopy, which backward then uses as
  * layer 0's input. */
+static void nn_forward_dev_bf16(NeuralNetwork* nn, const float* d_x, const int* d_rows, float* d_xcopy, int m) {
+    const int L = nn->num_layers - 1;
+    nn->d_x0 = d_rows ? d_xcopy : d_x;
+    nn->x0_dtype = d_rows ? 1 : 0;                 /* the gathered copy is written as bf16 */
+    const void* in = d_x;
+    int tin = 0;
+    for (int i = 0; i < L; i++) {
+        Layer* ly = &nn->layers[i];
+        float* out = nn->layers[i + 1].d_input;    /* hidden: bf16 storage; network output: fp32 */
+        const int tout = i == L - 1 ? 0 : 1;
+        phip_linear16_fwd(out, tout, in, tin, i == 0 ? d_rows : NULL, i == 0 ? (void*)d_xcopy : NULL,
+                          nn->d_w16 + nn->param_offset[i], ly->d_biases, m, ly->input_size, ly->output_size,
+                          nn_is_relu(nn, i), act_bits(nn, i + 1));
+        in = out;
+        tin = tout;
+    }
+}
+
 void nn_forward_dev_rows(NeuralNetwork* nn, const float* d_x, const int* d_rows, float* d_xcopy, int m) {
     nn_ensure_act(nn, m);
     const int L = nn->num_layers - 1;
+    if (nn->dtype == 1) {
+        nn_forward_dev_bf16(nn, d_x, d_rows, d_xcopy, m);
+        nn->bits_m = m;
+        nn->cache_m_forward = m;
+        nn->d_output = nn->layers[L].d_input;
+        return;
+    }
     nn->d_x0 = d_rows ? d_xcopy : d_x;
+    nn->x0_dtype = 0;
     const float* in = d_x;
     for (int i = 0; i < L; i++) {
         Layer* ly = &nn->layers[i];
@@ -155,6 +181,27 @@ void nn_backward_dev(NeuralNetwork* nn, const float* d_grad_out, int m, int want
     /* one memset for every layer's gradient (split-K grad_W accumulates atomically);
      * the trailing extra_floats (policy log_std grad) are owned by the caller and left alone */
     phip_memset(nn->d_grads, 0, sizeof(float) * (size_t)nn->num_params);
+    if (nn->dtype == 1) {      /* bf16 mode: hidden gradients stored bf16, the top one (heads) fp32 */
+        if (nn->bits_m != m) die("nn_backward_dev (bf16): backward must follow a forward over the same rows");
+        int tg = 0;
+        for (int i = L - 1; i >= 0; i--) {
+            Layer* ly = &nn->layers[i];
+            const void* x = i == 0 ? (const void*)nn->d_x0 : (const void*)ly->d_input;
+            phip_linear16_bwd_w(ly->d_grad_weights, ly->d_grad_biases, g, tg, x, i == 0 ? nn->x0_dtype : 1, m,
+                                ly->input_size, ly->output_size, 1);
+            int tgx = tg;
+            if (i > 0 || want_grad_x0) {
+                const int relu_in = i > 0 && nn_is_relu(nn, i - 1);
+                tgx = i > 0 ? 1 : 0;
+                phip_linear16_bwd_x(ly->d_grad_x, tgx, g, tg, nn->d_w16 + nn->param_offset[i],
+                                    relu_in ? act_bits(nn, i) : NULL, m, ly->input_size, ly->output_size);
+            }
+            g = ly->d_grad_x;
+            tg = tgx;
+        }
+        nn->cache_m_backward = m;
+        return;
+    }
     for (int i = L - 1; i >= 0; i--) {
         Layer* ly = &nn->layers[i];
         const float* x = i == 0 ? nn->d_x0 : ly->d_input;
@@ -211,12 +258,30 @@ void backward_propagation(NeuralNetwork* nn, float* grad_in, int m) {
     }
 }
 
+void nn_sync_w16(NeuralNetwork* nn);
+
 void nn_write_weights_to_device(NeuralNetwork* nn) {
     for (int i = 0; i < nn->num_layers - 1; i++) {
         Layer* ly = &nn->layers[i];
         phip_h2d(ly->d_weights, ly->weights, sizeof(float) * (size_t)ly->input_size * ly->output_size);
         phip_h2d(ly->d_biases, ly->biases, sizeof(float) * (size_t)ly->output_size);
     }
+    nn_sync_w16(nn);
+}
+
+/* bf16 mode: refresh the bf16 shadow of the parameters (after every parameter update) */
+void nn_sync_w16(NeuralNetwork* nn) {
+    if (nn && nn->dtype == 1) phip_f32_to_bf16(nn->d_w16, nn->d_params, nn->num_params);
+}
+
+int nn_set_compute_dtype(void* vnn, int dtype) {
+    NeuralNetwork* nn = (NeuralNetwork*)vnn;
+    if (!nn || (dtype != 0 && dtype != 1)) return -1;
+    if (dtype == 1 && !nn->d_w16) nn->d_w16 = (unsigned short*)phip_malloc(sizeof(unsigned short) * (size_t)nn->num_params);
+    nn->dtype = dtype;
+    nn->bits_m = -1;
+    nn_sync_w16(nn);
+    return 0;
 }
 
 void nn_write_weights_to_host(NeuralNetwork* nn) {
@@ -246,6 +311,7 @@ void free_neural_network(NeuralNetwork* nn) {
         phip_free(nn->layers[i].d_grad_x);
     }
     phip_free(nn->d_act_bits);
+    phip_free(nn->d_w16);
     phip_free(nn->d_params);
     phip_free(nn->d_grads);
     free(nn->activation_functions);

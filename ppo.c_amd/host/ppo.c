@@ -279,6 +279,7 @@ void ppo_update(void* vppo, float gamma, int batch_size, int n_epochs_policy, in
             nn_backward_dev(V, d->gv, B, 0);
             phip_allreduce_sum_f32(V->d_grads, V->num_params);
             adam_update_cuda(ppo->adam_V, ppo->lr_V);
+            nn_sync_w16(V);
             d->n_v++;
         }
     }
@@ -296,6 +297,7 @@ void ppo_update(void* vppo, float gamma, int batch_size, int n_epochs_policy, in
             phip_allreduce_sum_f32(mu->d_grads, mu->num_params + align4(A));   /* μ grads + log_std grad */
             adam_update_cuda(ppo->adam_entropy, ppo->lr_policy);               /* ppo.cu:440-442 order */
             adam_update_cuda(ppo->adam_policy, ppo->lr_policy);
+            nn_sync_w16(mu);
             d->n_p++;
         }
     }
@@ -428,4 +430,12 @@ PPO* load_ppo(const char* filename, bool use_cuda) {
     ppo->adam_entropy = load_adam(f, &ppo->policy->d_log_std, &ppo->policy->d_log_std_grad, &A, true);
     fclose(f);
     return ppo;
+}
+
+/* ppo_ext.h: compute precision of both networks (bf16 MFMA for config C5) */
+int ppo_set_compute_dtype(void* vppo, int dtype) {
+    PPO* ppo = (PPO*)vppo;
+    if (!ppo) return -1;
+    if (nn_set_compute_dtype(ppo->V, dtype) != 0) return -1;
+    return nn_set_compute_dtype(ppo->policy->mu, dtype);
 }

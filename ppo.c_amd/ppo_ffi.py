@@ -40,7 +40,7 @@ class NeuralNetwork(C.Structure):
                 ("num_params_packed", C.c_long), ("param_offset", c_long_p), ("bias_offset", c_long_p),
                 ("act_cap_m", C.c_int), ("grad_cap_m", C.c_int), ("host_cap_m", C.c_int),
                 ("extra_floats", C.c_long), ("d_x0", c_float_p), ("d_act_bits", C.POINTER(C.c_uint)),
-                ("bits_m", C.c_int)]
+                ("bits_m", C.c_int), ("dtype", C.c_int), ("x0_dtype", C.c_int), ("d_w16", C.c_void_p)]
 
 
 class GaussianPolicy(C.Structure):
@@ -100,6 +100,9 @@ _SIGS = {
     "ppo_last_error": (C.c_char_p, []),
     "ppo_synchronize": (None, []),
     "ppo_gemm_tune": (C.c_int, [C.c_int, C.c_int]),
+    "ppo_gemm16_tune": (C.c_int, [C.c_int]),
+    "ppo_set_compute_dtype": (C.c_int, [_P, C.c_int]),
+    "nn_set_compute_dtype": (C.c_int, [_P, C.c_int]),
     "ppo_bench_gemm": (C.c_double, [C.c_int] * 6),
     "ppo_build_info": (C.c_char_p, []),
     "ppo_struct_sizes": (C.c_int, [c_long_p, C.c_int]),

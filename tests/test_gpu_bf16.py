@@ -1,0 +1,139 @@
+"""bf16 compute mode (BASELINE config C5: "4×1024 MLP bf16") — csrc/gemm16.hip through the C ABI.
+
+Two references:
+  * a bf16-emulated one (numpy, float64 accumulation) that rounds exactly what the kernels round:
+    layer inputs and the weight shadow to bf16 on the way into the MFMA, hidden activations and
+    hidden gradients stored as bf16, the network output and the heads' gradient fp32, bias
+    gradients summed from the bf16-rounded gradient.  Tolerance 2e-3·max|ref| (fp32 accumulation
+    order only) — this pins the kernels;
+  * the oracle (fp32 restatement of the reference CPU path): bf16 agrees within 3e-2·max|ref|
+    (SURVEY §8c's bf16 bound) — this pins that bf16 mode still computes the reference's layers.
+Every bf16 tile configuration is forced once.
+"""
+import numpy as np
+import pytest
+
+import ppo_ffi
+from helpers import F32, dev, nn_grads_packed, nn_set_params_packed
+
+pytestmark = pytest.mark.gpu
+
+
+def bf16(a):
+    """round-to-nearest-even to bf16, returned as float32 (NaN-free inputs)"""
+    u = np.ascontiguousarray(a, F32).view(np.uint32).astype(np.uint64)
+    u = (u + 0x7FFF + ((u >> 16) & 1)) & 0xFFFF0000
+    return u.astype(np.uint32).view(F32)
+
+
+def unpack(sizes, params):
+    out, off = [], 0
+    for i in range(len(sizes) - 1):
+        nw = sizes[i] * sizes[i + 1]
+        W = params[off:off + nw].reshape(sizes[i + 1], sizes[i])
+        off += nw
+        b = params[off:off + sizes[i + 1]]
+        off += sizes[i + 1]
+        out.append((W, b))
+    return out
+
+
+def emulate(sizes, params, x, gout):
+    """bf16-mode forward + backward as the kernels compute it (float64 accumulation)."""
+    layers = unpack(sizes, params)
+    L = len(layers)
+    hs = [bf16(x)]                                  # layer inputs as the MFMA sees them
+    for i, (W, b) in enumerate(layers):
+        z = hs[-1].astype(np.float64) @ bf16(W).astype(np.float64).T + b
+        if i < L - 1:
+            hs.append(bf16(np.maximum(z, 0.0).astype(F32)))
+        else:
+            y = z.astype(F32)
+    grads = [None] * L
+    g = gout.astype(F32)                            # fp32 from the heads, rounded in the loader
+    for i in range(L - 1, -1, -1):
+        W, _ = layers[i]
+        gb16 = bf16(g).astype(np.float64)
+        gW = gb16.T @ hs[i].astype(np.float64)
+        gbias = gb16.sum(axis=0)
+        grads[i] = (gW.astype(F32).ravel(), gbias.astype(F32))
+        if i > 0:
+            gx = gb16 @ bf16(W).astype(np.float64)
+            gx = np.where(hs[i] > 0, gx, 0.0)
+            g = bf16(gx.astype(F32))                # hidden gradients stored bf16
+    packed = np.concatenate([np.concatenate([gw, gb]) for gw, gb in grads])
+    return y, packed
+
+
+def close(got, ref, rel, what):
+    err = float(np.abs(got - ref).max())
+    tol = rel * float(np.abs(ref).max()) + 1e-6
+    assert err <= tol, f"{what}: max |err| {err:.3g} > {tol:.3g}"
+
+
+@pytest.fixture(scope="module")
+def ncfg16(lib):
+    n = lib.ppo_gemm16_tune(-1)
+    yield n
+    lib.ppo_gemm16_tune(-1)
+
+
+@pytest.mark.parametrize("sizes,m", [([1024, 1024, 1024, 17], 1024), ([376, 512, 512, 17], 2048),
+                                     ([17, 256, 256, 6], 1000), ([3, 64, 64, 1], 64)])
+def test_bf16_mlp_every_cfg(lib, oracle, ncfg16, sizes, m):
+    rng = np.random.default_rng(sum(sizes) + m)
+    relu = [1] * (len(sizes) - 2) + [0]
+    names = ["relu"] * (len(sizes) - 2) + ["none"]
+    nn = lib.create_neural_network(ppo_ffi.c_ints(sizes), ppo_ffi.c_strings(names), len(sizes))
+    params = (rng.uniform(-1, 1, oracle.mlp_num_params(sizes)) * (1.0 / np.sqrt(max(sizes)))).astype(F32)
+    nn_set_params_packed(lib, nn, params)
+    assert lib.nn_set_compute_dtype(nn, 1) == 0
+    x = rng.uniform(-1, 1, (m, sizes[0])).astype(F32)
+    gout = rng.uniform(-1, 1, (m, sizes[-1])).astype(F32)
+    y_emu, g_emu = emulate(sizes, params, x, gout)
+    acts = oracle.mlp_forward(sizes, relu, params, x)
+    y_ref = oracle.mlp_layer_outputs(sizes, acts, m)[-1]
+    g_ref = oracle.mlp_backward(sizes, relu, params, x, acts, gout)
+    dx, dgo = dev(lib, x), dev(lib, gout)
+    try:
+        for c in range(ncfg16):
+            lib.ppo_gemm16_tune(c)
+            lib.forward_propagation_cuda(nn, dx.ptr, m)
+            y = ppo_ffi.d2h(lib, nn.contents.d_output, F32, m * sizes[-1]).reshape(m, sizes[-1])
+            close(y, y_emu, 2e-3, f"cfg {c} forward vs bf16 emulation")
+            close(y, y_ref, 3e-2, f"cfg {c} forward vs fp32 oracle")
+            lib.backward_propagation_cuda(nn, dgo.ptr, m)
+            g = nn_grads_packed(lib, nn)
+            close(g, g_emu, 2e-3, f"cfg {c} grads vs bf16 emulation")
+            close(g, g_ref, 3e-2, f"cfg {c} grads vs fp32 oracle")
+    finally:
+        lib.ppo_gemm16_tune(-1)
+        lib.free_neural_network(nn)
+
+
+def test_bf16_update_tracks_fp32(lib):
+    """A whole C5-shaped PPO update in bf16 mode from the same state as fp32: value / policy losses agree
+    within bf16 tolerance and the parameters move the same way."""
+    sizes, T, E, B = [1024, 1024, 1024, 17], 512, 8, 1024
+    N = T * E
+    out = {}
+    for dtype in (0, 1):
+        ppo_ffi.C.CDLL("libc.so.6").srand(77)
+        ppo = lib.create_ppo(ppo_ffi.c_strings(["relu", "relu", "none"]), ppo_ffi.c_ints(sizes), 4, N, 3e-4, 3e-4,
+                             0.95, 0.2, 0.0, 1.0, True)
+        assert lib.ppo_set_compute_dtype(ppo, dtype) == 0
+        lib.ppo_fill_synthetic(ppo, E, T, 99, 1.0 / 500)
+        p0 = ppo_ffi.d2h(lib, ppo.contents.V.contents.d_params, F32, ppo.contents.V.contents.num_params)
+        lib.ppo_reset_stats(ppo)
+        lib.ppo_update(ppo, 0.99, B, 1, 2, 1, 5)
+        stats = (ppo_ffi.C.c_double * 7)()
+        lib.ppo_read_stats(ppo, stats, 7)
+        p1 = ppo_ffi.d2h(lib, ppo.contents.V.contents.d_params, F32, ppo.contents.V.contents.num_params)
+        out[dtype] = (np.array(stats[:4]), p1 - p0)
+        lib.free_ppo(ppo)
+    (s32, d32), (s16, d16) = out[0], out[1]
+    assert s32[1] == s16[1] and s32[3] == s16[3]
+    assert abs(s16[0] - s32[0]) <= 0.03 * abs(s32[0]) + 1e-4, (s16, s32)
+    assert abs(s16[2] - s32[2]) <= 0.05 * abs(s32[2]) + 1e-3, (s16, s32)
+    cos = float(d16 @ d32 / (np.linalg.norm(d16) * np.linalg.norm(d32) + 1e-30))
+    assert cos > 0.9, cos
