@@ -93,6 +93,8 @@ int    ppo_gemm_tune(int force_cfg, int splitk_target);
 double ppo_bench_gemm(int op, int m, int n, int l, int iters, int cfg);
 /* bf16 GEMMs: force a tile configuration (−1 = automatic); returns the number of configurations */
 int    ppo_gemm16_tune(int force_cfg);
+/* average device µs of one bf16 launch (op as ppo_bench_gemm; bf16 operands); splitk_target 0 = automatic */
+double ppo_bench_gemm16(int op, int m, int n, int l, int iters, int cfg, int splitk_target);
 
 /* ---------------- kernel timing ---------------- */
 enum { PPO_K_GEMM = 0, PPO_K_GAE = 1, PPO_K_ADAM = 2, PPO_K_GATHER = 3, PPO_K_HEAD = 4,

@@ -33,7 +33,6 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int NT_ = 256;
-constexpr int BK = 32;
 
 enum Op { OP_NT = 0, OP_NN = 1, OP_TN = 2 };
 
@@ -60,7 +59,7 @@ __device__ __forceinline__ float bf_lo(unsigned u) { return __builtin_bit_cast(f
 // Staging of one operand tile (R rows × BK k) into a bf16 LDS image.  T = float or unsigned short
 // (bf16 bits).  One 16-B global load per slot: 4 fp32 or 8 bf16 elements.
 // ---------------------------------------------------------------------------
-template <int R, bool MN, typename T>
+template <int R, int BK, bool MN, typename T>
 struct Stage16 {
     static constexpr bool F32 = sizeof(T) == 4;
     static constexpr int EPL = F32 ? 4 : 8;                 // elements per 16-B load
@@ -166,9 +165,16 @@ struct Stage16 {
                 unsigned short* q = dst + (long)gr * ldd + gk;
                 if (F32) {
                     const f32x4 f = __builtin_bit_cast(f32x4, v[it]);
+                    if (gk + 3 < kend && (ldd & 3) == 0) {             // one 8-B store of 4 bf16
+                        const u32x2 p = {pack2(f[0], f[1]), pack2(f[2], f[3])};
+                        *reinterpret_cast<u32x2*>(q) = p;
+                    } else {
 #pragma unroll
-                    for (int e = 0; e < 4; ++e)
-                        if (gk + e < kend) q[e] = (unsigned short)(pack2(f[e], 0.f) & 0xffffu);
+                        for (int e = 0; e < 4; ++e)
+                            if (gk + e < kend) q[e] = (unsigned short)(pack2(f[e], 0.f) & 0xffffu);
+                    }
+                } else if (gk + 7 < kend && (ldd & 7) == 0) {
+                    *reinterpret_cast<u32x4*>(q) = v[it];
                 } else {
                     const unsigned short* s = reinterpret_cast<const unsigned short*>(&v[it]);
 #pragma unroll
@@ -211,14 +217,14 @@ template <typename T> struct Bits;
 template <> struct Bits<float> { static constexpr int code = 0; };
 template <> struct Bits<unsigned short> { static constexpr int code = 1; };
 
-template <int OP, int BM, int BN, int WARPS_M, typename TA, typename TB, typename TC>
+template <int OP, int BM, int BN, int WARPS_M, int BK, typename TA, typename TB, typename TC>
 __global__ __launch_bounds__(NT_, 2) void gemm_bf16_kernel(Args a) {
     constexpr int WARPS_N = 4 / WARPS_M;
     constexpr int WM = BM / WARPS_M, WN = BN / WARPS_N;
     constexpr int TM = WM / 32, TN = WN / 32;
     constexpr bool A_MN = OP == OP_TN, B_MN = OP != OP_NT;
-    using SA = Stage16<BM, A_MN, TA>;
-    using SB = Stage16<BN, B_MN, TB>;
+    using SA = Stage16<BM, BK, A_MN, TA>;
+    using SB = Stage16<BN, BK, B_MN, TB>;
     static_assert(TM >= 1 && TN >= 1, "wave tile must be a multiple of 32x32");
     static_assert(!(OP == OP_TN) || sizeof(TC) == 4, "grad_W accumulates in fp32");
 
@@ -371,40 +377,44 @@ __global__ __launch_bounds__(NT_, 2) void gemm_bf16_kernel(Args a) {
 using f32 = float;
 using b16 = unsigned short;
 
-template <int OP, int BM, int BN, int WM_, typename TA, typename TB, typename TC>
+template <int OP, int BM, int BN, int WM_, int BK, typename TA, typename TB, typename TC>
 void launch(Args a) {
     a.tiles_m = ppo_divup(a.M, BM);
     a.tiles_n = ppo_divup(a.N, BN);
     if (a.splits < 1) a.splits = 1;
     const long grid = (long)a.tiles_m * a.tiles_n * a.splits;
     PPO_REQUIRE(grid > 0 && grid < (1L << 31), "gemm16: grid out of range");
-    hipLaunchKernelGGL((gemm_bf16_kernel<OP, BM, BN, WM_, TA, TB, TC>), dim3((unsigned)grid), dim3(NT_), 0,
+    hipLaunchKernelGGL((gemm_bf16_kernel<OP, BM, BN, WM_, BK, TA, TB, TC>), dim3((unsigned)grid), dim3(NT_), 0,
                        ppo::stream(), a);
     PPO_LAUNCH_CHECK();
 }
 
-// tile configurations: 0 = 128x128 (4 waves of 64x64), 1 = 128x32 (skinny N), 2 = 32x128
-// (skinny M), 3 = 64x64
-struct Cfg { int bm, bn; };
-constexpr Cfg kCfgs[] = {{128, 128}, {128, 32}, {32, 128}, {64, 64}};
+// tile configurations {BM, BN, BK}: 0 = 128x128 (4 waves of 64x64), 1 = 128x32 (skinny N),
+// 2 = 32x128 (skinny M), 3 = 64x64, 4 = 128x128 with BK = 64
+struct Cfg { int bm, bn, bk; };
+constexpr Cfg kCfgs[] = {{128, 128, 32}, {128, 32, 32}, {32, 128, 32}, {64, 64, 32}, {128, 128, 64}};
 int g_force16 = -1;
+int g_split16 = 0;          // split-K workgroup target override for grad_W (0 = automatic)
 
 template <int OP, typename TA, typename TB, typename TC>
 void launch_cfg(int c, const Args& a) {
     switch (c) {
-        case 0: launch<OP, 128, 128, 2, TA, TB, TC>(a); break;
-        case 1: launch<OP, 128, 32, 4, TA, TB, TC>(a); break;
-        case 2: launch<OP, 32, 128, 1, TA, TB, TC>(a); break;
-        default: launch<OP, 64, 64, 2, TA, TB, TC>(a); break;
+        case 0: launch<OP, 128, 128, 2, 32, TA, TB, TC>(a); break;
+        case 1: launch<OP, 128, 32, 4, 32, TA, TB, TC>(a); break;
+        case 2: launch<OP, 32, 128, 1, 32, TA, TB, TC>(a); break;
+        case 3: launch<OP, 64, 64, 2, 32, TA, TB, TC>(a); break;
+        default: launch<OP, 128, 128, 2, 64, TA, TB, TC>(a); break;
     }
 }
 
-int pick16(int M, int N) {
+// measured (tools/gemm16_sweep.py, profiles/r01_gemm16_sweep.txt): 128x128/BK32 for forward and
+// grad_W (split-K ~512 workgroups), BK64 for grad_x
+int pick16(int M, int N, int op = OP_NT) {
     if (g_force16 >= 0) return g_force16;
     if (N <= 32 && M > 32) return 1;
     if (M <= 32 && N > 32) return 2;
     if (M <= 64 || N <= 64) return 3;
-    return 0;
+    return op == OP_NN ? 4 : 0;
 }
 
 inline bool al16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
@@ -443,7 +453,7 @@ void phip_linear16_bwd_x(void* gx, int tgx, const void* g, int tg, const void* W
     a.M = m; a.N = n; a.K = l; a.kchunk = l; a.splits = 1;
     a.bits_in = bits; a.wpr = ppo_divup(n, 32);
     a.vec = l % epl(tg) == 0 && n % 8 == 0 && al16(g) && al16(W16);
-    const int c = pick16(m, n);
+    const int c = pick16(m, n, OP_NN);
     if (tg == 0 && tgx == 0) launch_cfg<OP_NN, f32, b16, f32>(c, a);
     else if (tg == 0) launch_cfg<OP_NN, f32, b16, b16>(c, a);
     else if (tgx == 0) launch_cfg<OP_NN, b16, b16, f32>(c, a);
@@ -463,8 +473,10 @@ void phip_linear16_bwd_w(float* gW, float* gb, const void* g, int tg, const void
         return;
     }
     const int c = pick16(l, n);
+    const int BK = kCfgs[c].bk;
     const long tiles = (long)ppo_divup(l, kCfgs[c].bm) * ppo_divup(n, kCfgs[c].bn);
-    int splits = (int)((1024 + tiles - 1) / tiles);
+    const int target = g_split16 > 0 ? g_split16 : 512;
+    int splits = (int)((target + tiles - 1) / tiles);
     const int max_splits = m / (4 * BK) > 0 ? m / (4 * BK) : 1;          // ≥ 4 k-tiles per split
     if (splits > max_splits) splits = max_splits;
     if (splits < 1) splits = 1;
@@ -488,6 +500,50 @@ void phip_linear16_bwd_w(float* gW, float* gb, const void* g, int tg, const void
 int ppo_gemm16_tune(int force_cfg) {
     g_force16 = force_cfg;
     return (int)(sizeof(kCfgs) / sizeof(kCfgs[0]));
+}
+
+// Tuning utility: average device µs of one bf16 launch — op 0 forward (bf16 in/out, +ReLU/bits),
+// 1 grad_x (bf16), 2 grad_W (bf16 operands, fp32 out) — at m = batch, n = in, l = out.
+double ppo_bench_gemm16(int op, int m, int n, int l, int iters, int cfg, int splitk_target) {
+    ppo::ensure_device();
+    const size_t sx = (size_t)m * n, sw = (size_t)l * n, sy = (size_t)m * l;
+    unsigned short* x = (unsigned short*)phip_malloc(2 * sx);
+    unsigned short* W = (unsigned short*)phip_malloc(2 * sw);
+    unsigned short* y = (unsigned short*)phip_malloc(2 * (sy > sx ? sy : sx));
+    float* tmp = (float*)phip_malloc(4 * (sx > sw ? (sx > sy ? sx : sy) : (sw > sy ? sw : sy)));
+    float* b = (float*)phip_malloc(4 * (size_t)(l > n ? l : n));
+    float* gw = (float*)phip_malloc(4 * sw);
+    unsigned* bits = (unsigned*)phip_malloc(4 * (size_t)m * ppo_divup(l > n ? l : n, 32));
+    phip_fill_uniform(tmp, (long)sx, 1, -1.f, 1.f);
+    phip_f32_to_bf16(x, tmp, (long)sx);
+    phip_fill_uniform(tmp, (long)sw, 2, -0.05f, 0.05f);
+    phip_f32_to_bf16(W, tmp, (long)sw);
+    phip_fill_uniform(tmp, (long)(sy > sx ? sy : sx), 3, -1.f, 1.f);
+    phip_f32_to_bf16(y, tmp, (long)(sy > sx ? sy : sx));
+    const int saved = g_force16, saved_split = g_split16;
+    g_force16 = cfg;
+    g_split16 = splitk_target;
+    auto run = [&]() {
+        if (op == 0) phip_linear16_fwd(y, 1, x, 1, nullptr, nullptr, W, b, m, n, l, 1, bits);
+        else if (op == 1) phip_linear16_bwd_x(x, 1, y, 1, W, bits, m, n, l);
+        else phip_linear16_bwd_w(gw, b, y, 1, x, 1, m, n, l, 0);
+    };
+    for (int i = 0; i < 3; ++i) run();
+    hipEvent_t e0, e1;
+    PPO_CHECK(hipEventCreate(&e0));
+    PPO_CHECK(hipEventCreate(&e1));
+    PPO_CHECK(hipEventRecord(e0, ppo::stream()));
+    for (int i = 0; i < iters; ++i) run();
+    PPO_CHECK(hipEventRecord(e1, ppo::stream()));
+    PPO_CHECK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    PPO_CHECK(hipEventElapsedTime(&ms, e0, e1));
+    PPO_CHECK(hipEventDestroy(e0));
+    PPO_CHECK(hipEventDestroy(e1));
+    g_force16 = saved;
+    g_split16 = saved_split;
+    phip_free(x); phip_free(W); phip_free(y); phip_free(tmp); phip_free(b); phip_free(gw); phip_free(bits);
+    return 1000.0 * ms / (iters > 0 ? iters : 1);
 }
 
 }  // extern "C"
