@@ -134,6 +134,7 @@ def main():
     ap.add_argument("--shuffle", type=int, default=1, help="1 = device Feistel shuffle, 0 = reference host rand()")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-events", action="store_true")
+    ap.add_argument("--no-rollout", action="store_true", help="skip the rollout env-steps/s measurement")
     ap.add_argument("--event-stride", type=int, default=7,
                     help="HIP events around every k-th launch of each kernel class (1 = all; each event pair "
                          "costs a few µs of stream time, so the throughput run samples)")
@@ -204,6 +205,22 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    # batched device rollout of the same E x T (SURVEY §8d "rollout env-steps/s", reported beside
+    # the learner throughput; not part of `value`): one warm call, then one timed call
+    env_kind = 0 if (S, A) == (3, 1) else 1
+    t_rollout = None
+    if not args.no_rollout:
+        LIB.ppo_rollout_device(ppo, E, T, env_kind, args.seed + rank)
+        barrier()
+        r0 = time.perf_counter()
+        LIB.ppo_rollout_device(ppo, E, T, env_kind, args.seed + rank)
+        barrier()
+        t_rollout = time.perf_counter() - r0
+        if world > 1:
+            tr = torch.tensor([t_rollout], dtype=torch.float64)
+            dist.all_reduce(tr, op=dist.ReduceOp.MAX)
+            t_rollout = float(tr.item())
+
     ms = (C.c_double * 7)()
     work = (C.c_double * 7)()
     launches = (C.c_long * 7)()
@@ -240,6 +257,10 @@ def main():
                    "global_batch": B * world, "rollout_per_gpu": N, "parallelism": f"dp{world}",
                    "shuffle": "device-feistel" if args.shuffle else "host-rand"},
         "updates_per_sec": 1.0 / t_update,
+        "rollout_env_steps_per_sec": (world * N / t_rollout) if t_rollout else None,
+        "iteration_env_steps_per_sec": (world * N / (t_rollout + t_update)) if t_rollout else None,
+        "rollout": {"env": "pendulum-v1" if env_kind == 0 else "synthetic", "envs_per_gpu": E, "horizon": T,
+                    "ms": 1000.0 * t_rollout if t_rollout else None},
         "minibatch_steps_per_sec": 14 * (N // B) / t_update,
         "algorithmic_tflop_per_update": flops / 1e12,
         "mfma_frac_whole_update": flops / t_update / (peak * 1e12),

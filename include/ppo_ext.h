@@ -77,6 +77,14 @@ void ppo_sample_action_device(void* policy, float* d_state, float* d_action, flo
  * terminated ~ Bernoulli(p_terminate), truncated at each segment end. */
 void ppo_fill_synthetic(void* ppo, int n_envs, int horizon, unsigned long long seed, float p_terminate);
 
+/* Batched on-device rollout: `horizon` steps of all `n_envs` environments — μ forward
+ * over the E current observations, Gaussian sampling (Philox), one environment step — written
+ * env-major into the device buffer (transition (e, t) at row e·horizon + t; each segment ends
+ * truncated), ready for ppo_update.  env_kind 0 = Pendulum-v1 (S = 3, A = 1; gymnasium dynamics),
+ * 1 = synthetic (any S, A).  Episodes continue across calls; the first call (or a change of
+ * n_envs / env_kind) resets every environment from `seed`. */
+void ppo_rollout_device(void* ppo, int n_envs, int horizon, int env_kind, unsigned long long seed);
+
 /* ---------------- compute precision ---------------- */
 /* 0 = fp32 (default: exact fp32 MFMA GEMMs), 1 = bf16 MFMA GEMMs with fp32 accumulation, fp32
  * master parameters / Adam / heads / GAE, bf16 storage of hidden activations and their gradients

@@ -379,6 +379,97 @@ __global__ __launch_bounds__(NT_, min_waves(BM * BN, BK)) void gemm_f32_kernel(A
         }
 }
 
+// ---------------------------------------------------------------------------
+// Small-M forward (rollout steps over E environments, Pendulum-sized minibatches): y = x·Wᵀ + b
+// for M ≤ a few hundred rows.  The 128-row tiles of gemm_f32_kernel would put a 256 × 512 layer on
+// 16 workgroups that each walk the whole K serially (25 µs).  Here a 512-thread workgroup owns a
+// 32 × 32 output block and splits K over its 8 waves; each wave streams its K-slice straight from
+// global memory into MFMA operands (lane half h takes 32 consecutive k of each 64-deep chunk: 8
+// float4 loads per operand, no LDS staging), and the 8 partial 32×32 accumulators are summed
+// through LDS before the fused bias / ReLU / ReLU′-bit epilogue.  Same fp32 MFMA numerics.
+// ---------------------------------------------------------------------------
+constexpr int SM_WAVES = 8;
+
+template <bool VEC>
+__global__ __launch_bounds__(64 * SM_WAVES) void gemm_smallm_kernel(Args a) {
+    __shared__ float red[SM_WAVES][32 * 33];
+    const int tiles_n = a.tiles_n;
+    const int tm = blockIdx.x / tiles_n, tn = blockIdx.x % tiles_n;
+    const int m0 = tm * 32, n0 = tn * 32;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int K = a.K;
+    const int kslice = ((K + SM_WAVES - 1) / SM_WAVES + 63) / 64 * 64;   // per-wave K range, 64-aligned
+    const int kb = w * kslice, ke = min(K, kb + kslice);
+    const float* __restrict__ X = static_cast<const float*>(a.A);
+    const float* __restrict__ W = static_cast<const float*>(a.B);
+    const int arow = min(m0 + r, a.M - 1);
+    const long abase = (long)(a.ridx ? a.ridx[arow] : arow) * a.lda;
+    const long bbase = (long)min(n0 + r, a.N - 1) * a.ldb;
+
+    f32x16 acc;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+    for (int k0 = kb; k0 < ke; k0 += 64) {
+        const int kl = k0 + 32 * h;                      // this lane's 32 k values
+        float av[32], bv[32];
+        if (VEC) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int kq = kl + 4 * q;
+                const bool ok = kq < ke;
+                const int kc = ok ? kq : 0;
+                const f32x4 ta = *reinterpret_cast<const f32x4*>(X + abase + kc);
+                const f32x4 tb = *reinterpret_cast<const f32x4*>(W + bbase + kc);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    av[4 * q + e] = ok ? ta[e] : 0.f;
+                    bv[4 * q + e] = ok ? tb[e] : 0.f;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 32; ++q) {
+                const bool ok = kl + q < ke;
+                av[q] = ok ? X[abase + kl + q] : 0.f;
+                bv[q] = ok ? W[bbase + kl + q] : 0.f;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 32; ++q) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[q], bv[q], acc, 0, 0, 0);
+    }
+    // C/D map: col = r, row = (e&3) + 8(e>>2) + 4h
+#pragma unroll
+    for (int e = 0; e < 16; ++e) red[w][((e & 3) + 8 * (e >> 2) + 4 * h) * 33 + r] = acc[e];
+    __syncthreads();
+    if (w == 0) {
+        const int col = n0 + r;
+        const bool col_ok = col < a.N;
+        const float bcol = (a.bias && col_ok) ? a.bias[col] : 0.f;
+        unsigned word = 0;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const int rr = (e & 3) + 8 * (e >> 2) + 4 * h;
+            float v = 0.f;
+#pragma unroll
+            for (int q = 0; q < SM_WAVES; ++q) v += red[q][rr * 33 + r];
+            v += bcol;
+            if (a.relu) v = v > 0.f ? v : 0.f;
+            const int row = m0 + rr;
+            const bool ok = col_ok && row < a.M;
+            if (ok) static_cast<float*>(a.C)[(long)row * a.ldc + col] = v;
+            if (a.bits_out) {
+                const unsigned long long bb = __ballot(ok && v > 0.f);
+                if (r == e) word = h ? (unsigned)(bb >> 32) : (unsigned)bb;
+            }
+        }
+        if (a.bits_out && r < 16) {
+            const int row = m0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (row < a.M && n0 < a.N) a.bits_out[(long)row * a.wpr + (n0 >> 5)] = word;
+        }
+    }
+}
+
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 template <int OP, int BM, int BN, int WARPS_M, int BK, bool DBUF>
@@ -451,6 +542,12 @@ int pick_cfg(int op, int M, int N, int* splitk_target = nullptr) {
     return tiles < 512 ? 5 : 0;
 }
 
+// the tiled kernel leaves most CUs idle when its grid is small and each workgroup walks all of K
+bool use_smallm(int m, int n, int l) {
+    const long tiled_wgs = (long)ppo_divup(m, 128) * ppo_divup(l, 64);
+    return m <= 1024 && tiled_wgs < 64;
+}
+
 void fwd(float* y, const float* x, const float* W, const float* b, int m, int n, int l, int relu, unsigned* bits,
          int cfg, const int* ridx = nullptr, float* acopy = nullptr) {
     Args a{};
@@ -461,6 +558,18 @@ void fwd(float* y, const float* x, const float* W, const float* b, int m, int n,
     a.bits_out = bits; a.wpr = ppo_divup(l, 32);
     a.vec_a = (n % 4 == 0) && aligned16(x);             // kcont, extent K = n
     a.vec_b = (n % 4 == 0) && aligned16(W);
+    // small M (rollout over E envs, Pendulum-sized minibatches): split-K inside a workgroup —
+    // only when no gathered copy is wanted (that path keeps the tiled kernel's copy-out)
+    if (cfg < 0 && g_force_cfg < 0 && !acopy && use_smallm(m, n, l)) {
+        a.tiles_n = ppo_divup(l, 32);
+        const int grid = ppo_divup(m, 32) * a.tiles_n;
+        if (a.vec_a && a.vec_b)
+            hipLaunchKernelGGL(gemm_smallm_kernel<true>, dim3(grid), dim3(64 * SM_WAVES), 0, ppo::stream(), a);
+        else
+            hipLaunchKernelGGL(gemm_smallm_kernel<false>, dim3(grid), dim3(64 * SM_WAVES), 0, ppo::stream(), a);
+        PPO_LAUNCH_CHECK();
+        return;
+    }
     launch_cfg<OP_NT>(cfg < 0 ? pick_cfg(OP_NT, m, l) : cfg, a);
 }
 

@@ -61,6 +61,16 @@ void phip_linear16_bwd_w(float* gW, float* gb, const void* g, int tg, const void
                          int zeroed);
 void phip_f32_to_bf16(unsigned short* dst, const float* src, long count);
 
+/* ---------------- batched device rollout (rollout.hip) ---------------- */
+/* env kinds: 0 = Pendulum-v1 (S = 3, A = 1), 1 = synthetic (any S, A) */
+void phip_rollout_rows(int* rows, int E, int T);             /* rows[t·E + e] = e·T + t */
+void phip_env_reset(int kind, float* env_state, float* state, int E, int T, int S, uint64_t seed);
+void phip_env_first_obs(int kind, const float* env_state, float* state, int E, int T, int S);
+void phip_sample_rows(const float* mu, const float* log_std, const int* rows, float* action, float* logprob, int E,
+                      int A, uint64_t seed, uint64_t step);
+void phip_env_step(int kind, float* env_state, float* state, const float* action, float* next_state, float* reward,
+                   uint8_t* term, uint8_t* trunc, int E, int T, int t, int S, int A, uint64_t seed);
+
 /* ---------------- element-wise / heads (kernels.hip) ---------------- */
 void phip_relu(float* x, long count);
 void phip_relu_bwd(const float* y, float* g, long count);

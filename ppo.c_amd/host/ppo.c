@@ -23,6 +23,10 @@ typedef struct {
     int cap_B, S, A;
     float *states, *actions, *old_lp, *adv, *tgt, *gv, *gmu;
     int* rows;                    /* minibatch slot → buffer row (layer 0's fused gather) */
+    int* ro_rows;                 /* rollout: rows[t·E + e] = e·T + t */
+    float* env_state;             /* rollout: per-environment state */
+    int ro_E, ro_T, ro_kind, ro_S;
+    unsigned long long ro_step;   /* rollout step counter (Philox stream offset) */
     float* stats;                 /* [0] Σ value loss, [1] Σ policy loss */
     long n_v, n_p;
     uint64_t key;                 /* device-shuffle epoch key */
@@ -96,6 +100,7 @@ static void free_dev_ws(PPO* ppo) {
     if (!d) return;
     phip_free(d->states); phip_free(d->actions); phip_free(d->old_lp); phip_free(d->adv);
     phip_free(d->tgt); phip_free(d->gv); phip_free(d->gmu); phip_free(d->stats); phip_free(d->rows);
+    phip_free(d->ro_rows); phip_free(d->env_state);
     free(d);
     ppo->dev = NULL;
 }
@@ -363,6 +368,48 @@ void ppo_sample_action_device(void* vpolicy, float* d_state, float* d_action, fl
     GaussianPolicy* p = (GaussianPolicy*)vpolicy;
     nn_forward_dev(p->mu, d_state, m);
     phip_sample(p->mu->d_output, p->d_log_std, d_action, d_log_prob, m, p->action_size, seed, offset);
+}
+
+void ppo_rollout_device(void* vppo, int n_envs, int horizon, int env_kind, unsigned long long seed) {
+    PPO* ppo = (PPO*)vppo;
+    TrajectoryBuffer* b = ppo->buffer;
+    const int E = n_envs, T = horizon;
+    const long N = (long)E * T;
+    if (E <= 0 || T <= 0 || N > b->capacity) die("ppo_rollout_device: n_envs*horizon must be in [1, capacity]");
+    if (env_kind != 0 && env_kind != 1) die("ppo_rollout_device: env_kind must be 0 (Pendulum-v1) or 1 (synthetic)");
+    const int S = b->state_size, A = b->action_size;
+    if (env_kind == 0 && (S != 3 || A != 1)) die("ppo_rollout_device: Pendulum-v1 needs state_size 3, action_size 1");
+    PPODev* d = dev_ws(ppo, 1);
+    if (d->ro_E != E || d->ro_T != T) {
+        phip_free(d->ro_rows);
+        d->ro_rows = (int*)phip_malloc(sizeof(int) * (size_t)N);
+        phip_rollout_rows(d->ro_rows, E, T);
+        d->ro_T = T;
+    }
+    if (d->ro_E != E || d->ro_kind != env_kind || d->ro_S != S || !d->env_state) {
+        phip_free(d->env_state);
+        d->env_state = (float*)phip_malloc(sizeof(float) * (size_t)E * (S > 3 ? S : 3));
+        phip_env_reset(env_kind, d->env_state, b->d_state_p, E, T, S, splitmix64(seed));
+        d->ro_E = E;
+        d->ro_kind = env_kind;
+        d->ro_S = S;
+    }
+    const uint64_t key = splitmix64(seed ^ 0x524F4C4CULL);
+    GaussianPolicy* pol = ppo->policy;
+    phip_env_first_obs(env_kind, d->env_state, b->d_state_p, E, T, S);
+    for (int t = 0; t < T; t++) {
+        const int* rows = d->ro_rows + (long)t * E;
+        nn_forward_dev_rows(pol->mu, b->d_state_p, rows, NULL, E);
+        phip_sample_rows(pol->mu->d_output, pol->d_log_std, rows, b->d_action_p, b->d_logprob_p, E, A, key,
+                         d->ro_step++);
+        phip_env_step(env_kind, d->env_state, b->d_state_p, b->d_action_p, b->d_next_state_p, b->d_reward_p,
+                      (uint8_t*)b->d_terminated_p, (uint8_t*)b->d_truncated_p, E, T, t, S, A, key);
+    }
+    phip_memset(b->d_advantage_p, 0, sizeof(float) * (size_t)N);
+    phip_memset(b->d_adv_target_p, 0, sizeof(float) * (size_t)N);
+    b->idx = (int)(N % b->capacity);
+    b->full = N == b->capacity;
+    buffer_point_device(b);
 }
 
 void ppo_fill_synthetic(void* vppo, int n_envs, int horizon, unsigned long long seed, float p_terminate) {

@@ -103,6 +103,7 @@ _SIGS = {
     "ppo_gemm16_tune": (C.c_int, [C.c_int]),
     "ppo_bench_gemm16": (C.c_double, [C.c_int] * 7),
     "ppo_set_compute_dtype": (C.c_int, [_P, C.c_int]),
+    "ppo_rollout_device": (None, [_P, C.c_int, C.c_int, C.c_int, C.c_ulonglong]),
     "nn_set_compute_dtype": (C.c_int, [_P, C.c_int]),
     "ppo_bench_gemm": (C.c_double, [C.c_int] * 6),
     "ppo_build_info": (C.c_char_p, []),
