@@ -41,7 +41,7 @@ def main():
     for r in csv.DictReader(open(args.trace)):
         d = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
         total += d
-        if "gemm_f32_kernel" in r["Kernel_Name"]:
+        if "gemm_" in r["Kernel_Name"] and "_kernel" in r["Kernel_Name"]:
             by[gemm_key(r["Kernel_Name"], r["Grid_Size_X"])].append(d)
     g_tot = sum(sum(v) for v in by.values())
     lines = [f"# rocprofv3 --kernel-trace: GEMM launches by tile config and grid ({args.tag})",
