@@ -45,6 +45,7 @@ struct Args {
     int kchunk, splits;                   // OP_TN split-K
     int tiles_m, tiles_n;
     int vec_a, vec_b;
+    int flags;                            // experiment bits (ppo_gemm_flags): 1 = s_setprio around MFMAs
 };
 
 // ---------------------------------------------------------------------------
@@ -260,6 +261,12 @@ __global__ __launch_bounds__(NT_, min_waves(BM * BN, BK)) void gemm_f32_kernel(A
         const float* As = img;
         const float* Bs = img + SA::IMG;
         if (do_bsum) bsum += SA::rowsum(As, tid / TPR, (tid % TPR) * KPT, KPT);
+        // s_setprio 1 around the MFMA block: +1.5–4 % on forward, grad_x and the 64×64 grad_W tiles,
+        // −1…3 % on 128×128 grad_W tiles (tools/gemm_sweep.py --flags 0,1, profiles/r01_gemm_sweep_prio.txt);
+        // flag bit 0 inverts the default for experiments
+        constexpr bool PRIO = !(OP == OP_TN && BM * BN >= 128 * 128);
+        const bool prio = PRIO != ((a.flags & 1) != 0);
+        if (prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int q4 = 0; q4 < KH / 4; ++q4) {
             f32x4 fa[TM], fb[TN];
@@ -276,6 +283,7 @@ __global__ __launch_bounds__(NT_, min_waves(BM * BN, BK)) void gemm_f32_kernel(A
                     for (int j = 0; j < TN; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
         }
+        if (prio) __builtin_amdgcn_s_setprio(0);
     };
 
     if (DBUF) {
@@ -472,11 +480,14 @@ __global__ __launch_bounds__(64 * SM_WAVES) void gemm_smallm_kernel(Args a) {
 
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
+int g_flags = 0;               // experiment bits passed to every tiled launch (ppo_gemm_flags)
+
 template <int OP, int BM, int BN, int WARPS_M, int BK, bool DBUF>
 void launch(Args a) {
     a.tiles_m = ppo_divup(a.M, BM);
     a.tiles_n = ppo_divup(a.N, BN);
     if (a.splits < 1) a.splits = 1;
+    a.flags = g_flags;
     const long grid = (long)a.tiles_m * a.tiles_n * a.splits;
     PPO_REQUIRE(grid > 0 && grid < (1L << 31), "gemm: grid out of range");
     if (a.vec_a && a.vec_b)
@@ -666,6 +677,12 @@ void phip_linear_bwd_w_ex(float* gW, float* gb, const float* g, const float* x, 
 
 void phip_linear_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, int n, int l) {
     phip_linear_bwd_w_ex(gW, gb, g, x, m, n, l, 0);
+}
+
+int ppo_gemm_flags(int flags) {
+    const int old = g_flags;
+    if (flags >= 0) g_flags = flags;
+    return old;
 }
 
 int ppo_gemm_tune(int force_cfg, int splitk_target) {

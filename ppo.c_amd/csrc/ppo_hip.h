@@ -24,7 +24,13 @@ void  phip_h2d(void* dst, const void* src, size_t bytes);   /* completes before 
 void  phip_d2h(void* dst, const void* src, size_t bytes);   /* completes before return */
 void  phip_d2d(void* dst, const void* src, size_t bytes);   /* async */
 void  phip_memset(void* dst, int value, size_t bytes);      /* async */
-void  phip_sync(void);
+void  phip_sync(void);                     /* both queues */
+/* a second queue for independent work: fork = the side queue waits for everything issued so far on
+ * the main queue; use(1) routes launches to the side queue until use(0); join = the main queue
+ * waits for everything issued so far on the side queue */
+void  phip_side_fork(void);
+void  phip_side_use(int on);
+void  phip_side_join(void);
 void  phip_record_error(const char* msg);
 
 /* ---------------- dense layers (gemm.hip) ---------------- */

@@ -17,6 +17,9 @@ namespace ppo {
 
 static int          g_device = -1;
 static hipStream_t  g_stream = nullptr;
+static hipStream_t  g_side = nullptr;        // second queue for independent work (grad_W beside grad_x)
+static int          g_use_side = 0;
+static hipEvent_t   g_fork_ev = nullptr, g_join_ev = nullptr;
 static char         g_err[512] = "";
 static std::once_flag g_init_once;
 
@@ -52,13 +55,16 @@ static void init_impl() {
         fail(buf, __FILE__, __LINE__);
     }
     PPO_CHECK(hipStreamCreateWithFlags(&g_stream, hipStreamNonBlocking));
+    PPO_CHECK(hipStreamCreateWithFlags(&g_side, hipStreamNonBlocking));
+    PPO_CHECK(hipEventCreateWithFlags(&g_fork_ev, hipEventDisableTiming));
+    PPO_CHECK(hipEventCreateWithFlags(&g_join_ev, hipEventDisableTiming));
 }
 
 void ensure_device() { std::call_once(g_init_once, init_impl); }
 
 hipStream_t stream() {
     ensure_device();
-    return g_stream;
+    return g_use_side ? g_side : g_stream;
 }
 
 // ---------------- per-launch event timing ----------------
@@ -81,6 +87,7 @@ static hipEvent_t take_event() {
 static void harvest() {
     if (g_slots.empty()) return;
     PPO_CHECK(hipStreamSynchronize(g_stream));
+    PPO_CHECK(hipStreamSynchronize(g_side));
     for (auto& s : g_slots) {
         float ms = 0.f;
         PPO_CHECK(hipEventElapsedTime(&ms, s.a, s.b));
@@ -130,7 +137,7 @@ void* phip_malloc(size_t bytes) {
 
 void phip_free(void* p) {
     if (!p) return;
-    PPO_CHECK(hipStreamSynchronize(stream()));
+    phip_sync();
     PPO_CHECK(hipFree(p));
 }
 
@@ -156,7 +163,25 @@ void phip_memset(void* dst, int value, size_t bytes) {
     PPO_CHECK(hipMemsetAsync(dst, value, bytes, stream()));
 }
 
-void phip_sync(void) { PPO_CHECK(hipStreamSynchronize(stream())); }
+void phip_sync(void) {
+    ensure_device();
+    PPO_CHECK(hipStreamSynchronize(g_side));
+    PPO_CHECK(hipStreamSynchronize(g_stream));
+}
+
+void phip_side_fork(void) {
+    ensure_device();
+    PPO_CHECK(hipEventRecord(g_fork_ev, g_stream));
+    PPO_CHECK(hipStreamWaitEvent(g_side, g_fork_ev, 0));
+}
+
+void phip_side_use(int on) { g_use_side = on != 0; }
+
+void phip_side_join(void) {
+    ensure_device();
+    PPO_CHECK(hipEventRecord(g_join_ev, g_side));
+    PPO_CHECK(hipStreamWaitEvent(g_stream, g_join_ev, 0));
+}
 
 void phip_record_error(const char* msg) {
     if (!g_err[0]) snprintf(g_err, sizeof(g_err), "%s", msg);

@@ -202,6 +202,8 @@ void nn_backward_dev(NeuralNetwork* nn, const float* d_grad_out, int m, int want
         nn->cache_m_backward = m;
         return;
     }
+    /* (measured: running grad_W on a second queue beside grad_x of the same layer made the pair
+     * slower than back to back — both kernels fill the chip and thrash each other's L2) */
     for (int i = L - 1; i >= 0; i--) {
         Layer* ly = &nn->layers[i];
         const float* x = i == 0 ? nn->d_x0 : ly->d_input;

@@ -101,6 +101,7 @@ _SIGS = {
     "ppo_synchronize": (None, []),
     "ppo_gemm_tune": (C.c_int, [C.c_int, C.c_int]),
     "ppo_gemm16_tune": (C.c_int, [C.c_int]),
+    "ppo_gemm_flags": (C.c_int, [C.c_int]),
     "ppo_bench_gemm16": (C.c_double, [C.c_int] * 7),
     "ppo_set_compute_dtype": (C.c_int, [_P, C.c_int]),
     "ppo_rollout_device": (None, [_P, C.c_int, C.c_int, C.c_int, C.c_ulonglong]),

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--kscan", action="store_true", help="forward at fixed M,N over K (edge vs main-loop cost)")
     ap.add_argument("--main", action="store_true", help="C4 minibatch shapes x the large-tile configs only")
     ap.add_argument("--cfgs", default="", help="comma-separated configs for --main (default: a fixed set)")
+    ap.add_argument("--flags", default="0", help="comma-separated ppo_gemm_flags values to compare (--main)")
     args = ap.parse_args()
     lib = ppo_ffi.load()
     lib.ppo_set_device(0)
@@ -45,11 +46,14 @@ def main():
                     cfgs = [int(c) for c in args.cfgs.split(",")]
                 for cfg in cfgs:
                     for tgt in ([512, 1024, 2048] if op == 2 else [0]):
-                        lib.ppo_gemm_tune(-1, tgt)
-                        us = lib.ppo_bench_gemm(op, m, n, l, 10 if m <= B else 3, cfg)
-                        tf = 2.0 * m * n * l / (us * 1e-6) / 1e12
-                        print(f"op{op} m={m:8d} n={n:4d} l={l:4d} {CFG_NAMES[cfg]:16s} split_target={tgt:5d} "
-                              f"{us:9.1f} us {tf:7.1f} TF/s", flush=True)
+                        for fl in (int(f) for f in args.flags.split(",")):
+                            lib.ppo_gemm_tune(-1, tgt)
+                            lib.ppo_gemm_flags(fl)
+                            us = lib.ppo_bench_gemm(op, m, n, l, 10 if m <= B else 3, cfg)
+                            tf = 2.0 * m * n * l / (us * 1e-6) / 1e12
+                            print(f"op{op} m={m:8d} n={n:4d} l={l:4d} {CFG_NAMES[cfg]:16s} split_target={tgt:5d} "
+                                  f"flags={fl} {us:9.1f} us {tf:7.1f} TF/s", flush=True)
+                lib.ppo_gemm_flags(0)
         lib.ppo_gemm_tune(-1, 0)
         return
     shapes = [  # (m, n, l) = (batch, in, out) — C4 minibatch layers and the GAE forward
