@@ -85,6 +85,8 @@ typedef struct {
     int    dtype;           /* compute mode: 0 = fp32 (default), 1 = bf16 MFMA (C5) — see ppo_ext.h */
     int    x0_dtype;        /* storage of d_x0: 0 = fp32, 1 = bf16 (the gathered copy in bf16 mode) */
     unsigned short* d_w16;  /* bf16 mode: bf16 shadow of d_params (same offsets), refreshed after updates */
+    float* d_tiny_wt;       /* small-network update path: transposed weights scratch */
+    long   tiny_wt_cap;
 } NeuralNetwork;
 
 typedef struct {

@@ -77,6 +77,31 @@ void phip_sample_rows(const float* mu, const float* log_std, const int* rows, fl
 void phip_env_step(int kind, float* env_state, float* state, const float* action, float* next_state, float* reward,
                    uint8_t* term, uint8_t* trunc, int E, int T, int t, int S, int A, uint64_t seed);
 
+/* ---------------- single-workgroup update phase for small networks (tiny.hip) ---------------- */
+typedef struct {
+    int L;                          /* linear layers (≤ 8) */
+    int sizes[9];                   /* widths (≤ 128; output ≤ 32) */
+    int relu[8];
+    long woff[8], boff[8];          /* offsets of W_l / b_l in params / grads */
+    float *params, *grads, *m, *v;  /* flat parameter / gradient buffers, the network's Adam moments */
+    long span;                      /* floats the network's Adam updates */
+    float *log_std, *log_std_grad, *m_ls, *v_ls;   /* policy: log σ and its Adam (entropy) state */
+    float* wt; long wt_cap;         /* scratch for the transposed weights (Σ in·out floats) */
+} PhipTinyNet;
+typedef struct {
+    int policy;                     /* 0 = value epochs (MSE), 1 = policy epochs (clipped surrogate) */
+    const float *state, *action, *logprob, *adv, *adv_target;   /* device buffer arrays */
+    int limit, B, num_batches, n_epochs;        /* n_epochs ≤ 16 */
+    const int* perms;               /* [n_epochs][limit] permutations, or NULL: device Feistel */
+    uint32_t feistel_k[64];         /* per epoch, 4 round keys (when perms == NULL) */
+    const float *steps, *steps_ls;  /* device [n_steps][2] = {lr/bc1, bc2} per Adam step */
+    float b1, b2, eps, ent_coeff;
+    float* stats;                   /* device [0] Σ value loss, [1] Σ policy loss */
+} PhipTinyPhase;
+/* runs every minibatch step of the phase in one workgroup; returns −1 (nothing launched) when the
+ * network or minibatch does not fit */
+int phip_tiny_update(const PhipTinyNet* net, const PhipTinyPhase* ph);
+
 /* ---------------- element-wise / heads (kernels.hip) ---------------- */
 void phip_relu(float* x, long count);
 void phip_relu_bwd(const float* y, float* g, long count);

@@ -1,0 +1,505 @@
+// tiny.hip — the whole minibatch loop of a PPO update in ONE workgroup, for small networks.
+//
+// Configs C1/C2 (Pendulum: 3 → 64 → 64 → 1, B = 64) do 896 minibatch steps per update, each a
+// chain of ~12 tiny launches (gather, 3 forward GEMMs, loss, 3 grad_W + 2 grad_x GEMMs, Adam):
+// launch- and latency-bound at ≈65 µs per step, slower than one CPU core.  Here one 1024-thread
+// workgroup runs all minibatch steps of a phase (the value epochs, or the policy epochs) back to
+// back: the minibatch's activations and gradients stay in LDS, the parameters, gradients and Adam
+// moments (a few hundred KB at most) stay in L2, and the only synchronisation is __syncthreads().
+//
+// Per step, exactly the reference's arithmetic (ppo.cu:391-447 / :479-539):
+//   rows = perm[(k·B + i) mod limit]               (trajectory_buffer.cu:168-200; host rand()
+//                                                   permutations or libppo's device Feistel)
+//   forward  y = act(x·Wᵀ + b) per layer           (neural_network.cu:74-105)
+//   value:   L = Σ(t−y)²/B, g = 2(y−t)/B           (loss.cu:5-23)
+//   policy:  log π, ratio, clipped surrogate, ∂/∂μ, ∂/∂logσ (−c_ent)   (ppo.cu:82-107,
+//            policy.cu:67-111, ppo.cu:436-438)
+//   backward gW = gᵀ·x, gb = Σ g, gx = (g·W) ⊙ 1[x > 0]   (neural_network.cu:121-161)
+//   Adam     (adam.cu:138-169; the entropy Adam before the policy Adam, ppo.cu:440-442), with the
+//            bias corrections the host computes for every step (same powf as the multi-launch path)
+// GEMMs are v_mfma_f32_16x16x4_f32 (exact fp32; 16×16 tiles keep all 16 waves busy on 64-wide
+// layers), one output tile per wave, operands read straight from LDS.  When they fit (C2: 3→64→64→1
+// at B = 64 uses 158 KB), the parameters, gradients, Adam moments and a transposed weight copy (so
+// the forward's B operand is read along rows) live in LDS for the whole phase; otherwise in L2.
+// One CU's fp32 MFMA rate (256 FLOP/clk) bounds a 64-wide step at ≈4 µs; measured ≈26 µs per step
+// (PPO_TINY_STAMPS=1 prints the per-phase split), against ≈65 µs for the multi-launch loop.
+#include "dev.h"
+
+#include <cmath>
+#include <cstdlib>
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int TPB = 1024;
+constexpr int NWAVES = TPB / 64;
+constexpr int MAXL = 8;            // linear layers
+
+struct Feistel { uint32_t k[4]; uint32_t half, mask, n; };
+
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+    return x;
+}
+
+// identical to buffer.hip's feistel_index (restated in oracle/ref_cpu.c: ref_feistel_index)
+__device__ __forceinline__ uint32_t feistel_index(uint32_t i, const Feistel& f) {
+    uint32_t x = i;
+    do {
+        uint32_t L = x >> f.half, R = x & f.mask;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t nl = R;
+            R = L ^ (mix32(R ^ f.k[r]) & f.mask);
+            L = nl;
+        }
+        x = (L << f.half) | R;
+    } while (x >= f.n);
+    return x;
+}
+
+struct TinyArgs {
+    int L;                          // linear layers
+    int sizes[MAXL + 1];            // widths, sizes[0] = S, sizes[L] = output width
+    int relu[MAXL];                 // activation after layer l
+    long woff[MAXL], boff[MAXL];    // offsets of W_l / b_l in the flat parameter / gradient buffers
+    float* params; float* grads; float* m; float* v; long span;       // network + its Adam state
+    float* wt; long wtoff[MAXL];    // transposed weights Wᵀ[k][j] (kept current by the Adam loop):
+                                    // the forward's B operand then loads 16 consecutive floats per row
+    // policy only: log_std and its gradient / Adam state
+    float* log_std; float* log_std_grad; float* m_ls; float* v_ls; int A;
+    int policy;                     // 0: value phase (MSE), 1: policy phase (clipped surrogate)
+    // buffer
+    const float* state; const float* action; const float* logprob; const float* adv; const float* adv_target;
+    int limit, B, num_batches, n_epochs;
+    const int* perms;               // [n_epochs][limit] host rand() permutations, or nullptr → Feistel
+    Feistel fk[16];                 // per-epoch Feistel keys (device shuffle)
+    const float* steps;             // per step: {lr/bc1, bc2} of the network's Adam (value / policy)
+    const float* steps_ls;          // per step: {lr/bc1, bc2} of the entropy Adam (policy)
+    float b1, b2, eps, ent_coeff;
+    float* stats;                   // [0] Σ value loss, [1] Σ policy loss
+    int ld[MAXL + 1];               // LDS row pitch (floats) of each activation
+    int act_off[MAXL + 1];          // LDS offset of each activation [B][ld]
+    int g_off[2];                   // LDS offsets of the two gradient buffers [B][gld]
+    int gld;
+    int misc_off;                   // LDS: rows[B] (int), targets / adv / old_lp [B], actions [B][A]
+    unsigned long long* stamps;     // diagnostics (PPO_TINY_STAMPS): s_memrealtime at phase boundaries
+    int res_off;                    // RESIDENT: LDS offset of [params | grads | m | v | Wᵀ]
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// C[M×N] = A(M×K)·B(K×N) on 16×16 tiles, one tile per wave per round; A(i, k) = A[i·a_si + k·a_sk],
+// B(k, j) = B[k·b_sk + j·b_sj] (LDS or global).  Operand lane maps: A lane l holds
+// A[i0 + (l&15)][k0 + (l>>4)], B lane l holds B[k0 + (l>>4)][j0 + (l&15)]; C/D: col = l&15,
+// row = 4·(l>>4) + reg.  Loads are unconditional (indices clamped, out-of-range values zeroed by a
+// select) and issued 8 MFMAs' worth at a time, so no exec-mask branches or per-MFMA waits.
+// EPI 0: C[i][j] = act(v + bias[j]) (forward, LDS); 1: C[i][j] = v (grad_W, global);
+// EPI 2: C[i][j] = (X[i][j] > 0 or !mask) ? v : 0 (grad_x with the ReLU′ mask, LDS).
+template <int EPI>
+__device__ __forceinline__ void tile_gemm(int M, int N, int K, const float* __restrict__ A, int a_si, int a_sk,
+                                          const float* __restrict__ B, int b_sk, int b_sj, float* __restrict__ C,
+                                          int c_si, const float* __restrict__ bias, int flag,
+                                          const float* __restrict__ X, int x_si) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int tm = (M + 15) / 16, tn = (N + 15) / 16;
+    const int c = lane & 15, q = lane >> 4;
+    for (int t = w; t < tm * tn; t += NWAVES) {
+        const int i0 = (t / tn) * 16, j0 = (t % tn) * 16;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        const int ia = i0 + c, jb = j0 + c;
+        const bool iok = ia < M, jok = jb < N;
+        const float* Ar = A + (long)min(ia, M - 1) * a_si;
+        const float* Bc = B + (long)min(jb, N - 1) * b_sj;
+        for (int k0 = 0; k0 < K; k0 += 32) {
+            float av[8], bv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int k = k0 + 4 * u + q;
+                const int kc = min(k, K - 1);
+                const float x = Ar[(long)kc * a_sk], y = Bc[(long)kc * b_sk];
+                av[u] = (iok && k < K) ? x : 0.f;
+                bv[u] = (jok && k < K) ? y : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], acc, 0, 0, 0);
+        }
+        const int j = j0 + c;
+        if (j < N) {
+            const float bj = EPI == 0 ? bias[j] : 0.f;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const int i = i0 + 4 * q + e;
+                if (i >= M) continue;
+                float v = acc[e];
+                if (EPI == 0) {
+                    v += bj;
+                    if (flag) v = v > 0.f ? v : 0.f;
+                } else if (EPI == 2) {
+                    if (flag && !(X[(long)i * x_si + j] > 0.f)) v = 0.f;
+                }
+                C[(long)i * c_si + j] = v;
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ float log_prob_row(const float* mu, const float* log_std, const float* a, int A) {
+    const float cst = (float)(-0.5 * A * (double)logf((float)(2 * M_PI)));
+    float lp = cst;
+    for (int j = 0; j < A; ++j) {
+        const float z = (a[j] - mu[j]) / expf(log_std[j]);
+        lp = (float)((double)lp - ((double)log_std[j] + 0.5 * (double)(z * z)));
+    }
+    return lp;
+}
+
+__device__ __forceinline__ float surrogate(float adv, float lp, float old_lp, float eps, int m, float* grad) {
+    const float ratio = (float)exp((double)(lp - old_lp));
+    const int adv_pos = adv > 0;
+    const int ratio_pos = ratio > 1 + eps;
+    const int ratio_neg = ratio < 1 - eps;
+    *grad = -(adv_pos * !ratio_pos + !adv_pos * !ratio_neg) * adv * ratio / m;
+    return adv * (adv_pos * (ratio_pos * (1 + eps) + !ratio_pos * ratio) +
+                  !adv_pos * (ratio_neg * (1 - eps) + !ratio_neg * ratio));
+}
+
+__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, float step, float b1, float b2,
+                                          float bc2) {
+    m = b1 * m + (1 - b1) * g;
+    v = b2 * v + (1 - b2) * (g * g);
+    const float denom = (float)((double)sqrtf(v / bc2) + 1e-8);
+    p -= step * m / denom;
+}
+
+#define TINY_STAMP(slot)                                                                         \
+    do {                                                                                         \
+        if (a.stamps && tid == 0 && step < 64) {                                                 \
+            a.stamps[step * 8 + (slot)] = wall_clock64();                                        \
+            if ((slot) == 0) a.stamps[step * 8 + 6] = __builtin_amdgcn_s_memtime();              \
+        }                                                                                        \
+    } while (0)
+
+// RESIDENT: parameters, gradients, Adam moments and Wᵀ live in LDS for the whole phase (loaded at
+// the start, written back at the end) — every minibatch step then touches global memory only for
+// its gather.  Otherwise they stay in L2 (wider networks).
+template <bool RESIDENT>
+__global__ __launch_bounds__(TPB) void tiny_update_kernel(TinyArgs a) {
+    extern __shared__ float lds[];
+    float* P = RESIDENT ? lds + a.res_off : a.params;
+    const long sp = (a.span + 3) & ~3L;                      // LDS regions stay 16-B aligned
+    float* Gd = RESIDENT ? P + sp : a.grads;
+    float* Mv = RESIDENT ? Gd + sp : a.m;
+    float* Vv = RESIDENT ? Mv + sp : a.v;
+    float* WT = RESIDENT ? Vv + sp : a.wt;
+    if (RESIDENT) {
+        for (long e = threadIdx.x; e < a.span; e += TPB) {
+            P[e] = a.params[e];
+            Gd[e] = 0.f;
+            Mv[e] = a.m[e];
+            Vv[e] = a.v[e];
+        }
+        __syncthreads();
+    }
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int B = a.B, L = a.L, S = a.sizes[0];
+    int* rows = reinterpret_cast<int*>(lds + a.misc_off);
+    float* tgt = lds + a.misc_off + B;            // value: target; policy: advantage
+    float* olp = tgt + B;                         // policy: old log-prob
+    float* act = olp + B;                         // policy: actions [B][A]
+    __shared__ float red[NWAVES];
+    __shared__ float gls_acc[32];
+
+    int step = 0;
+    for (int l = 0; l < L; ++l) {                             // Wᵀ from the current parameters
+        const int n = a.sizes[l], o = a.sizes[l + 1];
+        for (int e = tid; e < n * o; e += TPB) {
+            const int j = e / n, k = e % n;
+            WT[a.wtoff[l] + (long)k * o + j] = P[a.woff[l] + e];
+        }
+    }
+    __threadfence_block();
+    __syncthreads();
+    for (int ep = 0; ep < a.n_epochs; ++ep) {
+        for (int kb = 0; kb < a.num_batches; ++kb, ++step) {
+            TINY_STAMP(0);
+            // ---- gather (trajectory_buffer.cu:168-200) ----
+            for (int i = tid; i < B; i += TPB) {
+                const int list = (int)(((long)kb * B + i) % a.limit);
+                const int src = a.perms ? a.perms[(long)ep * a.limit + list]
+                                        : (int)feistel_index((uint32_t)list, a.fk[ep & 15]);
+                rows[i] = src;
+                if (a.policy) {
+                    tgt[i] = a.adv[src];
+                    olp[i] = a.logprob[src];
+                } else {
+                    tgt[i] = a.adv_target[src];
+                }
+            }
+            __syncthreads();
+            {
+                float* x0 = lds + a.act_off[0];
+                const int ld0 = a.ld[0];
+                for (int e = tid; e < B * S; e += TPB) {
+                    const int i = e / S, j = e % S;
+                    x0[i * ld0 + j] = a.state[(long)rows[i] * S + j];
+                }
+                if (a.policy)
+                    for (int e = tid; e < B * a.A; e += TPB) {
+                        const int i = e / a.A, j = e % a.A;
+                        act[i * a.A + j] = a.action[(long)rows[i] * a.A + j];
+                    }
+            }
+            __syncthreads();
+            TINY_STAMP(1);
+            // ---- forward ----
+            for (int l = 0; l < L; ++l) {
+                const float* X = lds + a.act_off[l];
+                float* Y = lds + a.act_off[l + 1];
+                const int ldx = a.ld[l], ldy = a.ld[l + 1], n = a.sizes[l], o = a.sizes[l + 1];
+                // y[b][j] = Σ_k x[b][k]·W[j][k]:  A = x (LDS), B(k, j) = Wᵀ[k·o + j] (L2, coalesced)
+                tile_gemm<0>(B, o, n, X, ldx, 1, WT + a.wtoff[l], o, 1, Y, ldy, P + a.boff[l],
+                             a.relu[l], nullptr, 0);
+                __syncthreads();
+                if (a.stamps && tid == 0 && step < 64 && l < 3) a.stamps[64 * 8 + step * 4 + l] = wall_clock64();
+            }
+            TINY_STAMP(2);
+            // ---- head: output gradient into g buffer 0 ----
+            const float* Yo = lds + a.act_off[L];
+            const int ldo = a.ld[L];
+            float* G = lds + a.g_off[0];
+            const int gld = a.gld;
+            float part = 0.f;
+            if (!a.policy) {                                   // loss.cu:5-23
+                for (int i = tid; i < B; i += TPB) {
+                    const float y = Yo[i * ldo], t = tgt[i];
+                    const float d = t - y;
+                    part += d * d;
+                    G[i * gld] = 2 * (y - t) / (float)B;
+                }
+            } else {                                           // ppo.cu:82-107, policy.cu:67-111
+                if (tid < a.A) gls_acc[tid] = 0.f;
+                __syncthreads();
+                for (int i = tid; i < B; i += TPB) {
+                    float g;
+                    const float lp = log_prob_row(Yo + i * ldo, a.log_std, act + i * a.A, a.A);
+                    part += surrogate(tgt[i], lp, olp[i], a.eps, B, &g);
+                    for (int j = 0; j < a.A; ++j) {
+                        const float e2 = expf(-2 * a.log_std[j]);
+                        const float d = act[i * a.A + j] - Yo[i * ldo + j];
+                        G[i * gld + j] = d * e2 * g;
+                        atomicAdd(&gls_acc[j], (-1 + d * d * e2) * g);
+                    }
+                }
+            }
+            part = wave_sum(part);
+            if (lane == 0) red[w] = part;
+            __syncthreads();
+            if (tid == 0) {
+                float s = 0.f;
+                for (int q = 0; q < NWAVES; ++q) s += red[q];
+                if (!a.policy) {
+                    atomicAdd(a.stats + 0, s * (1.0f / (float)B));
+                } else {
+                    float ent = (float)(a.A * 0.5 * (1 + log(2 * M_PI)));
+                    for (int j = 0; j < a.A; ++j) ent += a.log_std[j];
+                    atomicAdd(a.stats + 1, -s / B - a.ent_coeff * ent);
+                }
+            }
+            if (a.policy && tid < a.A) a.log_std_grad[tid] = gls_acc[tid] + -a.ent_coeff;   // ppo.cu:436-438
+            __syncthreads();
+            TINY_STAMP(3);
+            // ---- backward ----
+            int gi = 0;
+            for (int l = L - 1; l >= 0; --l) {
+                const float* X = lds + a.act_off[l];
+                const int ldx = a.ld[l], n = a.sizes[l], o = a.sizes[l + 1];
+                const float* Gc = lds + a.g_off[gi];
+                float* gb = Gd + a.boff[l];
+                // gW[j][k] = Σ_b g[b][j]·x[b][k]:  A(j, b) = g (LDS), B(b, k) = x (LDS)
+                tile_gemm<1>(o, n, B, Gc, 1, gld, X, ldx, 1, Gd + a.woff[l], n, nullptr, 0, nullptr, 0);
+                for (int j = w; j < o; j += NWAVES) {          // bias gradient: Σ over the batch
+                    float s = 0.f;
+                    for (int b = lane; b < B; b += 64) s += Gc[b * gld + j];
+                    s = wave_sum(s);
+                    if (lane == 0) gb[j] = s;
+                }
+                if (l > 0) {
+                    // gx[b][k] = Σ_j g[b][j]·W[j][k], masked by x > 0:  A = g (LDS), B(j, k) = W[j·n + k]
+                    tile_gemm<2>(B, n, o, Gc, gld, 1, P + a.woff[l], n, 1, lds + a.g_off[gi ^ 1], gld,
+                                 nullptr, a.relu[l - 1], X, ldx);
+                }
+                __syncthreads();
+                gi ^= 1;
+            }
+            TINY_STAMP(4);
+            // make this step's gradient stores visible to every wave's Adam reads
+            __threadfence_block();
+            __syncthreads();
+            // ---- Adam: entropy (log σ) first, then the network (ppo.cu:440-442) ----
+            if (a.policy && tid < a.A) {
+                float p = a.log_std[tid], mm = a.m_ls[tid], vv = a.v_ls[tid];
+                adam_elem(p, a.log_std_grad[tid], mm, vv, a.steps_ls[2 * step], a.b1, a.b2, a.steps_ls[2 * step + 1]);
+                a.log_std[tid] = p; a.m_ls[tid] = mm; a.v_ls[tid] = vv;
+            }
+            const float st = a.steps[2 * step], bc2 = a.steps[2 * step + 1];
+            const long span4 = a.span & ~3L;
+            for (long e = span4 + tid; e < a.span; e += TPB) {
+                float p = P[e], mm = Mv[e], vv = Vv[e];
+                adam_elem(p, Gd[e], mm, vv, st, a.b1, a.b2, bc2);
+                P[e] = p; Mv[e] = mm; Vv[e] = vv;
+            }
+            for (long e = 4 * (long)tid; e < span4; e += 4 * (long)TPB) {
+                f32x4 p = *reinterpret_cast<const f32x4*>(P + e);
+                const f32x4 g = *reinterpret_cast<const f32x4*>(Gd + e);
+                f32x4 mm = *reinterpret_cast<const f32x4*>(Mv + e);
+                f32x4 vv = *reinterpret_cast<const f32x4*>(Vv + e);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    float pu = p[u], mu = mm[u], vu = vv[u];
+                    adam_elem(pu, g[u], mu, vu, st, a.b1, a.b2, bc2);
+                    p[u] = pu; mm[u] = mu; vv[u] = vu;
+                }
+                *reinterpret_cast<f32x4*>(P + e) = p;
+                *reinterpret_cast<f32x4*>(Mv + e) = mm;
+                *reinterpret_cast<f32x4*>(Vv + e) = vv;
+            }
+            __syncthreads();
+            for (int l = 0; l < L; ++l) {                         // refresh Wᵀ from the new weights
+                const int n = a.sizes[l], o = a.sizes[l + 1];
+                const float* Wl = P + a.woff[l];
+                float* Tl = WT + a.wtoff[l];
+                for (int e = tid; e < n * o; e += TPB) {
+                    const int j = e / n, k = e - j * n;
+                    Tl[k * o + j] = Wl[e];
+                }
+            }
+            __threadfence_block();
+            __syncthreads();
+            TINY_STAMP(5);
+        }
+    }
+    if (RESIDENT) {
+        for (long e = threadIdx.x; e < a.span; e += TPB) {
+            a.params[e] = P[e];
+            a.grads[e] = Gd[e];
+            a.m[e] = Mv[e];
+            a.v[e] = Vv[e];
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+// Returns 0 when launched; −1 if the network does not fit the single-workgroup path (caller falls
+// back to the multi-launch loop).
+int phip_tiny_update(const PhipTinyNet* net, const PhipTinyPhase* ph) {
+    TinyArgs a{};
+    if (net->L < 1 || net->L > MAXL || ph->B <= 0 || ph->n_epochs > 16) return -1;
+    if (((uintptr_t)net->params | (uintptr_t)net->grads | (uintptr_t)net->m | (uintptr_t)net->v) & 15) return -1;
+    a.L = net->L;
+    int maxw = 0;
+    for (int l = 0; l <= net->L; ++l) {
+        a.sizes[l] = net->sizes[l];
+        if (net->sizes[l] > 128 || net->sizes[l] <= 0) return -1;
+        if (l > 0 && net->sizes[l] > maxw) maxw = net->sizes[l];
+    }
+    if (net->sizes[net->L] > 32) return -1;
+    for (int l = 0; l < net->L; ++l) {
+        a.relu[l] = net->relu[l];
+        a.woff[l] = net->woff[l];
+        a.boff[l] = net->boff[l];
+    }
+    a.params = net->params; a.grads = net->grads; a.m = net->m; a.v = net->v; a.span = net->span;
+    a.wt = net->wt;
+    {
+        long off = 0;
+        for (int l = 0; l < net->L; ++l) {
+            a.wtoff[l] = off;
+            off += (long)net->sizes[l] * net->sizes[l + 1];
+        }
+        if (!net->wt || off > net->wt_cap) return -1;
+    }
+    a.log_std = net->log_std; a.log_std_grad = net->log_std_grad; a.m_ls = net->m_ls; a.v_ls = net->v_ls;
+    a.A = net->sizes[net->L];
+    a.policy = ph->policy;
+    a.state = ph->state; a.action = ph->action; a.logprob = ph->logprob; a.adv = ph->adv;
+    a.adv_target = ph->adv_target;
+    a.limit = ph->limit; a.B = ph->B; a.num_batches = ph->num_batches; a.n_epochs = ph->n_epochs;
+    a.perms = ph->perms;
+    for (int e = 0; e < ph->n_epochs && !ph->perms; ++e) {
+        Feistel& f = a.fk[e];
+        int bits = 2;
+        while ((1ULL << bits) < (unsigned long long)ph->limit) bits++;
+        f.half = (uint32_t)((bits + 1) / 2);
+        f.mask = (1u << f.half) - 1u;
+        f.n = (uint32_t)ph->limit;
+        for (int r = 0; r < 4; ++r) f.k[r] = ph->feistel_k[4 * e + r];
+    }
+    a.steps = ph->steps; a.steps_ls = ph->steps_ls;
+    a.b1 = ph->b1; a.b2 = ph->b2; a.eps = ph->eps; a.ent_coeff = ph->ent_coeff;
+    a.stats = ph->stats;
+    // LDS: activations [B][w+1] (odd pitch: conflict-free column reads), two gradient buffers, misc
+    int off = 0;
+    for (int l = 0; l <= net->L; ++l) {
+        a.ld[l] = net->sizes[l] | 1;
+        a.act_off[l] = off;
+        off += ph->B * a.ld[l];
+    }
+    a.gld = maxw | 1;
+    a.g_off[0] = off; off += ph->B * a.gld;
+    a.g_off[1] = off; off += ph->B * a.gld;
+    a.misc_off = off;
+    off += 3 * ph->B + ph->B * a.A;
+    off = (off + 3) & ~3;                                    // 16-B alignment for the float4 Adam loop
+    long nw = 0;
+    for (int l = 0; l < net->L; ++l) nw += (long)net->sizes[l] * net->sizes[l + 1];
+    const long res = 4 * ((net->span + 3) & ~3L) + nw;
+    const size_t kMaxLds = 160 * 1024 - 1024;              // the CU's 160 KiB less the static arrays
+    const bool resident = (size_t)(off + res) * sizeof(float) <= kMaxLds && !getenv("PPO_TINY_NO_RESIDENT");
+    a.res_off = off;
+    const size_t bytes = sizeof(float) * (size_t)(resident ? off + res : off);
+    if (bytes > kMaxLds) return -1;
+    if (ph->n_epochs <= 0 || ph->num_batches <= 0) return 0;     // fit check only
+    const void* kfn = resident ? (const void*)tiny_update_kernel<true> : (const void*)tiny_update_kernel<false>;
+    PPO_CHECK(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    static unsigned long long* stamps = nullptr;
+    if (getenv("PPO_TINY_STAMPS")) {
+        if (!stamps) stamps = (unsigned long long*)phip_malloc(sizeof(unsigned long long) * 64 * 12);
+        a.stamps = stamps;
+    }
+    ppo::ProfScope ps(PPO_K_OTHER, 0.0);
+    if (resident) hipLaunchKernelGGL(tiny_update_kernel<true>, dim3(1), dim3(TPB), bytes, ppo::stream(), a);
+    else hipLaunchKernelGGL(tiny_update_kernel<false>, dim3(1), dim3(TPB), bytes, ppo::stream(), a);
+    PPO_LAUNCH_CHECK();
+    if (a.stamps) {                      // diagnostics: mean µs per phase over steps 1..63
+        unsigned long long h[64 * 12];
+        phip_d2h(h, a.stamps, sizeof(h));
+        double acc[5] = {0, 0, 0, 0, 0};
+        int n = 0;
+        for (int st = 1; st < 64 && st < ph->n_epochs * ph->num_batches; ++st, ++n)
+            for (int k = 0; k < 5; ++k) acc[k] += (double)(h[st * 8 + k + 1] - h[st * 8 + k]) / 100.0;
+        const double clk = (double)(h[63 * 8 + 6] - h[1 * 8 + 6]) / ((double)(h[63 * 8] - h[1 * 8]) / 100.0);
+        if (n) fprintf(stderr, "tiny: shader clock %.0f MHz\n", clk);
+        double fl[3] = {0, 0, 0};
+        for (int st = 1; st < 64 && st < ph->n_epochs * ph->num_batches; ++st) {
+            fl[0] += (double)(h[512 + st * 4 + 0] - h[st * 8 + 1]) / 100.0;
+            fl[1] += (double)(h[512 + st * 4 + 1] - h[512 + st * 4 + 0]) / 100.0;
+            fl[2] += (double)(h[512 + st * 4 + 2] - h[512 + st * 4 + 1]) / 100.0;
+        }
+        if (n) fprintf(stderr, "tiny: forward layers (us): %.2f %.2f %.2f\n", fl[0] / n, fl[1] / n, fl[2] / n);
+        if (n)
+            fprintf(stderr, "tiny %s step phases (us): gather %.2f fwd %.2f head %.2f bwd %.2f adam %.2f\n",
+                    ph->policy ? "policy" : "value", acc[0] / n, acc[1] / n, acc[2] / n, acc[3] / n, acc[4] / n);
+    }
+    return 0;
+}
+
+}  // extern "C"

@@ -87,6 +87,14 @@ static void bias_corrections(Adam* a, float* bc1, float* bc2) {
     *bc2 = 1 - powf(a->beta2, a->time_step);
 }
 
+/* the next step's bias-corrected step size and second-moment correction, as adam_update_cuda
+ * computes them (advances time_step) — for kernels that run many Adam steps in one launch */
+void adam_next_step(Adam* a, float lr, float* step, float* bc2) {
+    float bc1;
+    bias_corrections(a, &bc1, bc2);
+    *step = lr / bc1;
+}
+
 /* host tensors: staged into HBM, updated by the multi-tensor kernel, copied back */
 void adam_update(Adam* adam, float lr) {
     if (adam->on_device) { adam_update_cuda(adam, lr); return; }

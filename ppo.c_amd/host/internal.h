@@ -45,6 +45,9 @@ void nn_backward_dev(NeuralNetwork* nn, const float* d_grad_out, int m, int want
 NeuralNetwork* nn_load_ex(FILE* file, long extra_floats);
 void nn_sync_w16(NeuralNetwork* nn);       /* bf16 mode: refresh the bf16 weight shadow */
 
+/* adam.c */
+void adam_next_step(Adam* a, float lr, float* step, float* bc2);
+
 /* trajectory_buffer.c */
 void buffer_point_device(TrajectoryBuffer* b);
 

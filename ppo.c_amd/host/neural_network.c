@@ -314,6 +314,7 @@ void free_neural_network(NeuralNetwork* nn) {
     }
     phip_free(nn->d_act_bits);
     phip_free(nn->d_w16);
+    phip_free(nn->d_tiny_wt);
     phip_free(nn->d_params);
     phip_free(nn->d_grads);
     free(nn->activation_functions);

@@ -24,6 +24,10 @@ typedef struct {
     float *states, *actions, *old_lp, *adv, *tgt, *gv, *gmu;
     int* rows;                    /* minibatch slot → buffer row (layer 0's fused gather) */
     int* ro_rows;                 /* rollout: rows[t·E + e] = e·T + t */
+    float* tiny_steps[3];         /* small-network path: per-step Adam step sizes (value, entropy, policy) */
+    int tiny_cap[3];
+    int* tiny_perm;               /* small-network path: one permutation per epoch (host rand() shuffle) */
+    long tiny_perm_cap;
     float* env_state;             /* rollout: per-environment state */
     int ro_E, ro_T, ro_kind, ro_S;
     unsigned long long ro_step;   /* rollout step counter (Philox stream offset) */
@@ -100,7 +104,8 @@ static void free_dev_ws(PPO* ppo) {
     if (!d) return;
     phip_free(d->states); phip_free(d->actions); phip_free(d->old_lp); phip_free(d->adv);
     phip_free(d->tgt); phip_free(d->gv); phip_free(d->gmu); phip_free(d->stats); phip_free(d->rows);
-    phip_free(d->ro_rows); phip_free(d->env_state);
+    phip_free(d->ro_rows); phip_free(d->env_state); phip_free(d->tiny_perm);
+    for (int i = 0; i < 3; i++) phip_free(d->tiny_steps[i]);
     free(d);
     ppo->dev = NULL;
 }
@@ -245,6 +250,131 @@ static const int* next_perm(PPO* ppo, PPODev* d, int shuffle_mode, uint64_t* key
     return ppo->buffer->random_idx;
 }
 
+/* ------------------------------------------------------------------ */
+/* small networks: every minibatch step of a phase in one workgroup    */
+/* (csrc/tiny.hip); same arithmetic, rand() order and Adam step counts  */
+/* ------------------------------------------------------------------ */
+static int tiny_net(NeuralNetwork* nn, Adam* adam, PhipTinyNet* t) {
+    const int L = nn->num_layers - 1;
+    if (nn->dtype != 0 || L < 1 || L > 8 || !adam->flat || adam->weights[0] != nn->d_params) return -1;
+    long nw = 0;
+    for (int i = 0; i < L; i++) nw += (long)nn->layers[i].input_size * nn->layers[i].output_size;
+    if (nw > nn->tiny_wt_cap) {
+        phip_free(nn->d_tiny_wt);
+        nn->d_tiny_wt = (float*)phip_malloc(sizeof(float) * (size_t)nw);
+        nn->tiny_wt_cap = nw;
+    }
+    memset(t, 0, sizeof(*t));
+    t->L = L;
+    for (int i = 0; i <= L; i++) t->sizes[i] = nn->layers[i].input_size;
+    for (int i = 0; i < L; i++) {
+        t->relu[i] = nn_is_relu(nn, i);
+        t->woff[i] = nn->param_offset[i];
+        t->boff[i] = nn->bias_offset[i];
+        if (nn->layers[i].input_size > 128 || nn->layers[i].output_size > 128) return -1;
+    }
+    if (t->sizes[L] > 32) return -1;
+    t->params = nn->d_params;
+    t->grads = nn->d_grads;
+    t->wt = (float*)nn->d_tiny_wt;
+    t->wt_cap = nn->tiny_wt_cap;
+    t->m = adam->m;
+    t->v = adam->v;
+    t->span = adam->span;
+    return 0;
+}
+
+static float* tiny_steps(PPODev* d, int slot, Adam* adam, float lr, int n) {
+    float* h = (float*)xmalloc(sizeof(float) * 2 * (size_t)n);
+    for (int i = 0; i < n; i++) adam_next_step(adam, lr, &h[2 * i], &h[2 * i + 1]);
+    if (n > d->tiny_cap[slot]) {
+        phip_free(d->tiny_steps[slot]);
+        d->tiny_steps[slot] = (float*)phip_malloc(sizeof(float) * 2 * (size_t)n);
+        d->tiny_cap[slot] = n;
+    }
+    phip_h2d(d->tiny_steps[slot], h, sizeof(float) * 2 * (size_t)n);
+    free(h);
+    return d->tiny_steps[slot];
+}
+
+/* permutations for n_epochs epochs, consumed in the reference's order (one shuffle per epoch) */
+static const int* tiny_perms(PPO* ppo, PPODev* d, int shuffle_mode, int n_epochs, int limit, PhipTinyPhase* ph) {
+    if (shuffle_mode == PPO_SHUFFLE_DEVICE) {
+        for (int e = 0; e < n_epochs; e++) {
+            const uint64_t key = d->key++;
+            for (int r = 0; r < 4; r++) ph->feistel_k[4 * e + r] = (uint32_t)splitmix64(key + (uint64_t)r);
+        }
+        return NULL;
+    }
+    const long need = (long)n_epochs * limit;
+    if (need > d->tiny_perm_cap) {
+        phip_free(d->tiny_perm);
+        d->tiny_perm = (int*)phip_malloc(sizeof(int) * (size_t)need);
+        d->tiny_perm_cap = need;
+    }
+    for (int e = 0; e < n_epochs; e++) {
+        shuffle_buffer_cuda(ppo->buffer);
+        phip_d2d(d->tiny_perm + (long)e * limit, ppo->buffer->random_idx, sizeof(int) * (size_t)limit);
+    }
+    return d->tiny_perm;
+}
+
+static int ppo_update_tiny(PPO* ppo, PPODev* d, int B, int n_epochs_policy, int n_epochs_value, int shuffle_mode) {
+    TrajectoryBuffer* buf = ppo->buffer;
+    const int limit = buf->full ? buf->capacity : buf->idx;
+    const int num_batches = buf->capacity / B;
+    if (getenv("PPO_NO_TINY") || phip_comm_world() > 1 || n_epochs_value > 16 || n_epochs_policy > 16) return -1;
+    PhipTinyNet nv, np;
+    if (tiny_net(ppo->V, ppo->adam_V, &nv) || tiny_net(ppo->policy->mu, ppo->adam_policy, &np)) return -1;
+    if (!ppo->adam_entropy->flat) return -1;
+    GaussianPolicy* pol = ppo->policy;
+    np.log_std = pol->d_log_std;
+    np.log_std_grad = pol->d_log_std_grad;
+    np.m_ls = ppo->adam_entropy->m;
+    np.v_ls = ppo->adam_entropy->v;
+    PhipTinyPhase ph;
+    memset(&ph, 0, sizeof(ph));
+    ph.state = buf->state_p; ph.action = buf->action_p; ph.logprob = buf->logprob_p;
+    ph.adv = buf->advantage_p; ph.adv_target = buf->adv_target_p;
+    ph.limit = limit; ph.B = B; ph.num_batches = num_batches;
+    ph.b1 = 0.9f; ph.b2 = 0.999f; ph.eps = ppo->epsilon; ph.ent_coeff = ppo->ent_coeff;
+    ph.stats = d->stats;
+    /* fit check before any state (rand() stream, Adam steps, keys) is consumed: a dry phase */
+    {
+        PhipTinyNet probe = nv;
+        PhipTinyPhase pp = ph;
+        pp.n_epochs = 0;
+        if (phip_tiny_update(&probe, &pp) != 0) return -1;
+        probe = np;
+        pp.policy = 1;
+        if (phip_tiny_update(&probe, &pp) != 0) return -1;
+    }
+    if (n_epochs_value > 0 && num_batches > 0) {
+        ph.policy = 0;
+        ph.n_epochs = n_epochs_value;
+        ph.perms = tiny_perms(ppo, d, shuffle_mode, n_epochs_value, limit, &ph);
+        ph.steps = tiny_steps(d, 0, ppo->adam_V, ppo->lr_V, n_epochs_value * num_batches);
+        if (phip_tiny_update(&nv, &ph) != 0) die("ppo_update: tiny value phase failed to launch");
+        d->n_v += (long)n_epochs_value * num_batches;
+    } else if (n_epochs_value > 0) {
+        for (int j = 0; j < n_epochs_value; j++) { uint64_t key; next_perm(ppo, d, shuffle_mode, &key); }
+    }
+    if (n_epochs_policy > 0 && num_batches > 0) {
+        ph.policy = 1;
+        ph.n_epochs = n_epochs_policy;
+        ph.perms = tiny_perms(ppo, d, shuffle_mode, n_epochs_policy, limit, &ph);
+        /* per step the entropy Adam steps before the policy Adam (ppo.cu:440-442); their step
+         * counters are independent, so the two sequences can be generated one after the other */
+        ph.steps_ls = tiny_steps(d, 1, ppo->adam_entropy, ppo->lr_policy, n_epochs_policy * num_batches);
+        ph.steps = tiny_steps(d, 2, ppo->adam_policy, ppo->lr_policy, n_epochs_policy * num_batches);
+        if (phip_tiny_update(&np, &ph) != 0) die("ppo_update: tiny policy phase failed to launch");
+        d->n_p += (long)n_epochs_policy * num_batches;
+    } else if (n_epochs_policy > 0) {
+        for (int j = 0; j < n_epochs_policy; j++) { uint64_t key; next_perm(ppo, d, shuffle_mode, &key); }
+    }
+    return 0;
+}
+
 void ppo_update(void* vppo, float gamma, int batch_size, int n_epochs_policy, int n_epochs_value, int shuffle_mode,
                 unsigned long long seed) {
     PPO* ppo = (PPO*)vppo;
@@ -270,6 +400,8 @@ void ppo_update(void* vppo, float gamma, int batch_size, int n_epochs_policy, in
     NeuralNetwork* mu = pol->mu;
 
     ppo_gae_device(V, buf, gamma, ppo->lambda);
+
+    if (ppo_update_tiny(ppo, d, B, n_epochs_policy, n_epochs_value, shuffle_mode) == 0) return;
 
     for (int j = 0; j < n_epochs_value; j++) {
         uint64_t key;

@@ -40,7 +40,8 @@ class NeuralNetwork(C.Structure):
                 ("num_params_packed", C.c_long), ("param_offset", c_long_p), ("bias_offset", c_long_p),
                 ("act_cap_m", C.c_int), ("grad_cap_m", C.c_int), ("host_cap_m", C.c_int),
                 ("extra_floats", C.c_long), ("d_x0", c_float_p), ("d_act_bits", C.POINTER(C.c_uint)),
-                ("bits_m", C.c_int), ("dtype", C.c_int), ("x0_dtype", C.c_int), ("d_w16", C.c_void_p)]
+                ("bits_m", C.c_int), ("dtype", C.c_int), ("x0_dtype", C.c_int), ("d_w16", C.c_void_p),
+                ("d_tiny_wt", c_float_p), ("tiny_wt_cap", C.c_long)]
 
 
 class GaussianPolicy(C.Structure):
