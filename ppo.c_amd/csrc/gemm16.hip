@@ -392,7 +392,8 @@ void launch(Args a) {
 // tile configurations {BM, BN, BK}: 0 = 128x128 (4 waves of 64x64), 1 = 128x32 (skinny N),
 // 2 = 32x128 (skinny M), 3 = 64x64, 4 = 128x128 with BK = 64
 struct Cfg { int bm, bn, bk; };
-constexpr Cfg kCfgs[] = {{128, 128, 32}, {128, 32, 32}, {32, 128, 32}, {64, 64, 32}, {128, 128, 64}};
+constexpr Cfg kCfgs[] = {{128, 128, 32}, {128, 32, 32}, {32, 128, 32}, {64, 64, 32}, {128, 128, 64},
+                         {256, 128, 64}, {128, 256, 64}, {256, 128, 32}};
 int g_force16 = -1;
 int g_split16 = 0;          // split-K workgroup target override for grad_W (0 = automatic)
 
@@ -403,17 +404,22 @@ void launch_cfg(int c, const Args& a) {
         case 1: launch<OP, 128, 32, 4, 32, TA, TB, TC>(a); break;
         case 2: launch<OP, 32, 128, 1, 32, TA, TB, TC>(a); break;
         case 3: launch<OP, 64, 64, 2, 32, TA, TB, TC>(a); break;
-        default: launch<OP, 128, 128, 2, 64, TA, TB, TC>(a); break;
+        case 4: launch<OP, 128, 128, 2, 64, TA, TB, TC>(a); break;
+        case 5: launch<OP, 256, 128, 2, 64, TA, TB, TC>(a); break;       // waves of 128x64
+        case 6: launch<OP, 128, 256, 2, 64, TA, TB, TC>(a); break;       // waves of 64x128
+        default: launch<OP, 256, 128, 2, 32, TA, TB, TC>(a); break;
     }
 }
 
-// measured (tools/gemm16_sweep.py, profiles/r01_gemm16_sweep.txt): 128x128/BK32 for forward and
-// grad_W (split-K ~512 workgroups), BK64 for grad_x
+// measured (tools/gemm16_sweep.py, profiles/r01_gemm16_sweep*.txt): 128x256/BK64 (waves of 64x128)
+// for all three products at the C5 shapes (grad_W with split-K at ~256 workgroups); 128x128/BK32
+// where N is not a multiple of 256
 int pick16(int M, int N, int op = OP_NT) {
     if (g_force16 >= 0) return g_force16;
     if (N <= 32 && M > 32) return 1;
     if (M <= 32 && N > 32) return 2;
     if (M <= 64 || N <= 64) return 3;
+    if (N % 256 == 0 && M >= 256) return 6;
     return op == OP_NN ? 4 : 0;
 }
 
@@ -475,7 +481,7 @@ void phip_linear16_bwd_w(float* gW, float* gb, const void* g, int tg, const void
     const int c = pick16(l, n);
     const int BK = kCfgs[c].bk;
     const long tiles = (long)ppo_divup(l, kCfgs[c].bm) * ppo_divup(n, kCfgs[c].bn);
-    const int target = g_split16 > 0 ? g_split16 : 512;
+    const int target = g_split16 > 0 ? g_split16 : (c == 6 ? 256 : 512);
     int splits = (int)((target + tiles - 1) / tiles);
     const int max_splits = m / (4 * BK) > 0 ? m / (4 * BK) : 1;          // ≥ 4 k-tiles per split
     if (splits > max_splits) splits = max_splits;

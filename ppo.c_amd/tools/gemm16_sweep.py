@@ -11,7 +11,8 @@ import sys
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 import ppo_ffi  # noqa: E402
 
-NAMES = {0: "128x128/bk32", 1: "128x32/bk32", 2: "32x128/bk32", 3: "64x64/bk32", 4: "128x128/bk64"}
+NAMES = {0: "128x128/bk32", 1: "128x32/bk32", 2: "32x128/bk32", 3: "64x64/bk32", 4: "128x128/bk64",
+         5: "256x128/bk64", 6: "128x256/bk64", 7: "256x128/bk32"}
 
 
 def main():
