@@ -99,7 +99,8 @@ int    ppo_gemm_tune(int force_cfg, int splitk_target);
 /* experiment switches of the fp32 tiled GEMM (bit 0: invert the s_setprio default around the MFMA block); flags < 0
  * only queries; returns the previous value */
 int    ppo_gemm_flags(int flags);
-/* average device µs of one launch: op 0 = forward (bias+ReLU), 1 = grad_x, 2 = grad_W (+bias grad);
+/* average device µs of one launch: op 0 = forward (bias+ReLU), 1 = grad_x, 2 = grad_W (+bias grad),
+ * 3 = forward without activation (output layer);
  * m = batch, n = in, l = out; cfg −1 = automatic */
 double ppo_bench_gemm(int op, int m, int n, int l, int iters, int cfg);
 /* bf16 GEMMs: force a tile configuration (−1 = automatic); returns the number of configurations */

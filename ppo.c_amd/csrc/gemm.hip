@@ -707,6 +707,7 @@ double ppo_bench_gemm(int op, int m, int n, int l, int iters, int cfg) {
     phip_fill_uniform(b, (long)(l > n ? l : n), 4, -0.1f, 0.1f);
     auto run = [&]() {
         if (op == 0) fwd(y, x, W, b, m, n, l, 1, nullptr, cfg);
+        else if (op == 3) fwd(y, x, W, b, m, n, l, 0, nullptr, cfg);        // output layer: no activation
         else if (op == 1) bwd_x(x, y, W, nullptr, nullptr, m, n, l, cfg);
         else bwd_w(gw, b, y, x, m, n, l, 0, cfg);
     };
