@@ -65,6 +65,8 @@ void phip_linear16_bwd_x(void* gx, int tgx, const void* g, int tg, const void* W
 /* gW[l,n] (+)= gᵀ·x, gb (+)= Σ g in fp32 (zeroed != 0: outputs already zero) */
 void phip_linear16_bwd_w(float* gW, float* gb, const void* g, int tg, const void* x, int tx, int m, int n, int l,
                          int zeroed);
+/* dst[i, :] = bf16(src[rows[i], :]) for i < m (S % 4 == 0): layer 0's gather in bf16 mode */
+void phip_gather_rows_bf16(unsigned short* dst, const float* src, const int* rows, int m, int S);
 void phip_f32_to_bf16(unsigned short* dst, const float* src, long count);
 
 /* ---------------- batched device rollout (rollout.hip) ---------------- */
@@ -153,6 +155,10 @@ void phip_gather(const int* perm, uint64_t key, int offset, int limit, int batch
 /* ---------------- Adam (adam.hip) ---------------- */
 void phip_adam_flat(float* p, const float* g, float* m, float* v, long n, float lr, float beta1,
                     float beta2, float bias_correction1, float bias_correction2, float grad_scale);
+/* the same, also writing bf16(p) into w16[0, n16) (bf16 mode's parameter shadow) */
+void phip_adam_flat_w16(float* p, const float* g, float* m, float* v, long n, float lr, float beta1, float beta2,
+                        float bias_correction1, float bias_correction2, float grad_scale, unsigned short* w16,
+                        long n16);
 /* multi-tensor: ptrs/lengths are HOST arrays describing device tensors; m/v are flat */
 void phip_adam_multi(float* const* params, float* const* grads, const int* lengths, int num_tensors,
                      float* m, float* v, float lr, float beta1, float beta2,

@@ -27,6 +27,9 @@ void fail(const char* msg, const char* file, int line) {
     if (!g_err[0]) snprintf(g_err, sizeof(g_err), "%s (%s:%d)", msg, file, line);
     fprintf(stderr, "libppo: FATAL: %s (%s:%d)\n", msg, file, line);
     fflush(stderr);
+    // drain work already queued so the process never dies with kernels in flight
+    if (g_stream) (void)hipStreamSynchronize(g_stream);
+    if (g_side) (void)hipStreamSynchronize(g_side);
     abort();
 }
 

@@ -47,6 +47,8 @@ void nn_sync_w16(NeuralNetwork* nn);       /* bf16 mode: refresh the bf16 weight
 
 /* adam.c */
 void adam_next_step(Adam* a, float lr, float* step, float* bc2);
+/* device Adam that also writes the bf16 shadow w16[0, n16) in the same pass; returns 1 when it did */
+int adam_update_cuda_w16(Adam* adam, float lr, unsigned short* w16, long n16);
 
 /* trajectory_buffer.c */
 void buffer_point_device(TrajectoryBuffer* b);

@@ -125,6 +125,14 @@ static void nn_forward_dev_bf16(NeuralNetwork* nn, const float* d_x, const int* 
     nn->x0_dtype = d_rows ? 1 : 0;                 /* the gathered copy is written as bf16 */
     const void* in = d_x;
     int tin = 0;
+    const int S = nn->layers[0].input_size;
+    if (d_rows && d_xcopy && S % 4 == 0) {                    /* gather + round once, then a plain bf16 GEMM */
+        phip_gather_rows_bf16((unsigned short*)d_xcopy, d_x, d_rows, m, S);
+        in = d_xcopy;
+        tin = 1;
+        d_rows = NULL;
+        d_xcopy = NULL;
+    }
     for (int i = 0; i < L; i++) {
         Layer* ly = &nn->layers[i];
         float* out = nn->layers[i + 1].d_input;    /* hidden: bf16 storage; network output: fp32 */

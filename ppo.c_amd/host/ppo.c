@@ -284,6 +284,14 @@ static int tiny_net(NeuralNetwork* nn, Adam* adam, PhipTinyNet* t) {
     return 0;
 }
 
+/* Adam step of a network's flat span; in bf16 mode the same pass refreshes the bf16 parameter
+ * shadow when the span starts at the network's parameters, else a separate conversion does */
+static void adam_update_net(Adam* adam, float lr, NeuralNetwork* nn) {
+    const int fused = nn->dtype == 1 && adam->flat && adam->weights[0] == nn->d_params;
+    if (!adam_update_cuda_w16(adam, lr, fused ? nn->d_w16 : NULL, nn->num_params) && nn->dtype == 1)
+        nn_sync_w16(nn);
+}
+
 static float* tiny_steps(PPODev* d, int slot, Adam* adam, float lr, int n) {
     float* h = (float*)xmalloc(sizeof(float) * 2 * (size_t)n);
     for (int i = 0; i < n; i++) adam_next_step(adam, lr, &h[2 * i], &h[2 * i + 1]);
@@ -415,8 +423,7 @@ void ppo_update(void* vppo, float gamma, int batch_size, int n_epochs_policy, in
             phip_mse(V->d_output, d->tgt, B, d->gv, NULL, d->stats + 0);
             nn_backward_dev(V, d->gv, B, 0);
             phip_allreduce_sum_f32(V->d_grads, V->num_params);
-            adam_update_cuda(ppo->adam_V, ppo->lr_V);
-            nn_sync_w16(V);
+            adam_update_net(ppo->adam_V, ppo->lr_V, V);
             d->n_v++;
         }
     }
@@ -433,8 +440,7 @@ void ppo_update(void* vppo, float gamma, int batch_size, int n_epochs_policy, in
             nn_backward_dev(mu, d->gmu, B, 0);
             phip_allreduce_sum_f32(mu->d_grads, mu->num_params + align4(A));   /* μ grads + log_std grad */
             adam_update_cuda(ppo->adam_entropy, ppo->lr_policy);               /* ppo.cu:440-442 order */
-            adam_update_cuda(ppo->adam_policy, ppo->lr_policy);
-            nn_sync_w16(mu);
+            adam_update_net(ppo->adam_policy, ppo->lr_policy, mu);
             d->n_p++;
         }
     }
