@@ -199,6 +199,39 @@ void ensure_ws(int nb) {
     g_wpart = (double*)phip_malloc(sizeof(double) * 3 * g_cap_blocks);
 }
 
+// V(next_state) reuse.  In a rollout buffer next_state[t] is state[t+1] unless the episode ended at
+// t (or t is the last row), so V(next_state[t]) = V(state[t+1]) — already computed by the state
+// forward.  One wave per transition compares the two rows bit for bit; equal rows take v[t+1],
+// the others are listed for their own forward (≈ N/500 + E rows at C4).  A buffer filled any other
+// way is handled exactly: every row that differs is evaluated.
+__global__ void next_value_map_kernel(const uint32_t* __restrict__ ns, const uint32_t* __restrict__ st,
+                                      const float* __restrict__ v, float* __restrict__ vn, int* __restrict__ own,
+                                      int* __restrict__ count, long n, int S) {
+    const int lane = threadIdx.x & 63;
+    const long waves = (long)gridDim.x * (TPB / 64);
+    for (long t = blockIdx.x * (long)(TPB / 64) + (threadIdx.x >> 6); t < n; t += waves) {
+        bool diff = t + 1 >= n;
+        if (!diff) {
+            const uint32_t* a = ns + t * S;
+            const uint32_t* b = st + (t + 1) * S;
+            for (int c = lane; c < S; c += 64) diff |= a[c] != b[c];
+        }
+        const bool any = __ballot(diff) != 0;
+        if (lane == 0) {
+            if (!any) vn[t] = v[t + 1];
+            else own[atomicAdd(count, 1)] = (int)t;
+        }
+    }
+}
+
+__global__ void scatter_values_kernel(float* __restrict__ vn, const int* __restrict__ own,
+                                      const float* __restrict__ vals, int m) {
+    const int i = blockIdx.x * TPB + threadIdx.x;
+    if (i < m) vn[own[i]] = vals[i];
+}
+
+int* g_count = nullptr;
+
 }  // namespace
 
 extern "C" {
@@ -242,6 +275,31 @@ void phip_normalize(float* adv, int n, const double* d_welford, float* d_stats_o
     ppo::ProfScope ps(PPO_K_GAE, 8.0 * n);
     hipLaunchKernelGGL(normalize_kernel, dim3(g), dim3(TPB), 0, ppo::stream(), adv, (long)n, d_welford,
                        d_stats_out);
+    PPO_LAUNCH_CHECK();
+}
+
+int phip_next_value_map(const float* next_state, const float* state, const float* v, float* vn, int* own, int n,
+                        int S) {
+    if (n <= 0) return 0;
+    if (!g_count) g_count = (int*)phip_malloc(sizeof(int));
+    phip_memset(g_count, 0, sizeof(int));
+    long g = ((long)n + TPB / 64 - 1) / (TPB / 64);
+    if (g > 8192) g = 8192;
+    {
+        ppo::ProfScope ps(PPO_K_GAE, 8.0 * n * S);
+        hipLaunchKernelGGL(next_value_map_kernel, dim3((int)g), dim3(TPB), 0, ppo::stream(),
+                           reinterpret_cast<const uint32_t*>(next_state), reinterpret_cast<const uint32_t*>(state), v,
+                           vn, own, g_count, (long)n, S);
+        PPO_LAUNCH_CHECK();
+    }
+    int count = 0;
+    phip_d2h(&count, g_count, sizeof(int));
+    return count;
+}
+
+void phip_scatter_values(float* vn, const int* own, const float* vals, int m) {
+    if (m <= 0) return;
+    hipLaunchKernelGGL(scatter_values_kernel, dim3(ppo_divup(m, TPB)), dim3(TPB), 0, ppo::stream(), vn, own, vals, m);
     PPO_LAUNCH_CHECK();
 }
 

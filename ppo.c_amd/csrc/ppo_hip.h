@@ -133,6 +133,12 @@ void phip_policy_head(const float* mu, const float* log_std, const float* action
 void phip_gae_scan(const float* v, const float* v_next, const float* reward, const uint8_t* term,
                    const uint8_t* trunc, int n, float gamma, float lambda, float* adv, float* adv_target,
                    double* d_welford);
+/* vn[t] = v[t+1] wherever next_state[t] == state[t+1] bit for bit; every other t is written to
+ * own[0, count) (any order).  Returns count (synchronises). */
+int phip_next_value_map(const float* next_state, const float* state, const float* v, float* vn, int* own, int n,
+                        int S);
+/* vn[own[i]] = vals[i] */
+void phip_scatter_values(float* vn, const int* own, const float* vals, int m);
 /* d_welford_all holds `world` triples; combine them into d_welford (3 doubles) */
 void phip_welford_combine(const double* d_welford_all, int world, double* d_welford);
 /* adv = (adv − mean)/(σ_pop + 1e-8); d_stats_out (optional) = {mean, std} as float */

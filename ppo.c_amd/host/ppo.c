@@ -40,6 +40,7 @@ typedef struct {
 
 static float* g_v = NULL;         /* V(state), V(next_state) for compute_gae_cuda */
 static float* g_vn = NULL;
+static int* g_own = NULL;         /* transitions whose V(next_state) needs its own forward */
 static long g_v_cap = 0;
 static double* g_welford = NULL;  /* (n, mean, M2) */
 static double* g_welford_all = NULL;
@@ -67,8 +68,10 @@ static void ensure_gae_ws(long n) {
     if (n > g_v_cap) {
         phip_free(g_v);
         phip_free(g_vn);
+        phip_free(g_own);
         g_v = (float*)phip_malloc(sizeof(float) * (size_t)n);
         g_vn = (float*)phip_malloc(sizeof(float) * (size_t)n);
+        g_own = (int*)phip_malloc(sizeof(int) * (size_t)n);
         g_v_cap = n;
     }
 }
@@ -179,14 +182,30 @@ void collect_trajectories(TrajectoryBuffer* buffer, Env* env, GaussianPolicy* po
 /* ------------------------------------------------------------------ */
 /* GAE (ppo.cu:261-369)                                                */
 /* ------------------------------------------------------------------ */
+/* PPO_GAE_FULL=1: evaluate V over every next_state row as the reference does (A/B checks) */
+static int gae_full_forwards(void) {
+    const char* e = getenv("PPO_GAE_FULL");
+    return e && *e && *e != '0';
+}
+
 void ppo_gae_device(NeuralNetwork* V, TrajectoryBuffer* b, float gamma, float lambda) {
     const int n = b->full ? b->capacity : b->idx;
     ensure_gae_ws(n);
-    if (n > 0) {
+    if (n > 0 && gae_full_forwards()) {     /* the reference's two full forwards (ppo.cu:333-336) */
         nn_forward_dev(V, b->next_state_p, n);
         phip_d2d(g_vn, V->d_output, sizeof(float) * (size_t)n);
         nn_forward_dev(V, b->state_p, n);
         phip_d2d(g_v, V->d_output, sizeof(float) * (size_t)n);
+    } else if (n > 0) {
+        /* V(state) once; V(next_state[t]) = V(state[t+1]) wherever the rows are bitwise equal
+         * (every transition that did not end an episode); the rest get their own forward */
+        nn_forward_dev(V, b->state_p, n);
+        phip_d2d(g_v, V->d_output, sizeof(float) * (size_t)n);
+        const int own = phip_next_value_map(b->next_state_p, b->state_p, g_v, g_vn, g_own, n, V->layers[0].input_size);
+        if (own > 0) {
+            nn_forward_dev_rows(V, b->next_state_p, g_own, NULL, own);
+            phip_scatter_values(g_vn, g_own, V->d_output, own);
+        }
     }
     phip_gae_scan(g_v, g_vn, b->reward_p, (const uint8_t*)b->terminated_p, (const uint8_t*)b->truncated_p, n, gamma,
                   lambda, b->advantage_p, b->adv_target_p, g_welford);

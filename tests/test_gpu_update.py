@@ -210,3 +210,44 @@ def test_full_update_c1(lib, oracle, shuffle_mode):
         ratio = float(np.linalg.norm(d_got) / (np.linalg.norm(d_ref) + 1e-30))
         assert cos > 0.95 and 0.9 < ratio < 1.1, f"{what}: cos {cos:.4f} norm ratio {ratio:.4f}"
     lib.free_ppo(ppo)
+
+
+@pytest.mark.parametrize("layout", ["rollout", "random", "mixed"])
+def test_gae_next_value_reuse(lib, oracle, layout, monkeypatch):
+    """V(next_state[t]) is taken from V(state[t+1]) only where the rows are bitwise equal.
+
+    rollout: next_state = state shifted by one except at episode ends (the reuse path);
+    random: no row equal (every transition gets its own forward); mixed: half the rows equal,
+    including rows at episode ends.  Targets equal the oracle's (two full forwards, ppo.cu:333-336)
+    and the PPO_GAE_FULL=1 path's.
+    """
+    sizes, N = [17, 256, 256, 6], 4096
+    ppo = make_ppo(lib, oracle, sizes, N)
+    mu0, ls0 = policy_state(lib, ppo)
+    v0 = nn_params_packed(lib, ppo.contents.V)
+    buf = synthetic_buffer(oracle, sizes, mu0, ls0, N, seed=13, n_envs=8)
+    rng = np.random.default_rng(5)
+    if layout != "rollout":
+        fresh = rng.uniform(-1, 1, buf["next_state"].shape).astype(F32)
+        pick = np.ones(N, bool) if layout == "random" else rng.uniform(size=N) < 0.5
+        buf["next_state"][pick] = fresh[pick]
+        if layout == "mixed":
+            ends = np.nonzero(buf["terminated"] | buf["truncated"])[0]
+            ends = ends[ends + 1 < N]
+            buf["next_state"][ends] = buf["state"][ends + 1]
+    load_buffer(lib, ppo, buf)
+    b = ppo.contents.buffer.contents
+    out = {}
+    for mode in ("reuse", "full"):
+        if mode == "full":
+            monkeypatch.setenv("PPO_GAE_FULL", "1")
+        lib.ppo_update(ppo, 0.99, N, 0, 0, 1, 5)                 # GAE only
+        lib.ppo_synchronize()
+        out[mode] = ppo_ffi.d2h(lib, b.d_adv_target_p, F32, N)
+    monkeypatch.delenv("PPO_GAE_FULL")
+    ref = oracle.ppo_update(sizes, RELU(sizes), mu0, ls0, v0, buf, batch_size=N, n_epochs_policy=0,
+                            n_epochs_value=0, shuffle_mode=1, seed=5)
+    for mode, tgt in out.items():
+        assert_rel_close(tgt, ref["adv_target"], 2e-4, 2e-4 * np.abs(ref["adv_target"]).max(), f"{layout} {mode}")
+    assert_rel_close(out["reuse"], out["full"], 1e-4, 1e-4 * np.abs(out["full"]).max(), f"{layout} reuse vs full")
+    lib.free_ppo(ppo)
