@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--kscan", action="store_true", help="forward at fixed M,N over K (edge vs main-loop cost)")
     ap.add_argument("--main", action="store_true", help="C4 minibatch shapes x the large-tile configs only")
     ap.add_argument("--cfgs", default="", help="comma-separated configs for --main (default: a fixed set)")
+    ap.add_argument("--skinny", action="store_true", help="output-layer shapes (N = 17 / 1) x every config")
     ap.add_argument("--flags", default="0", help="comma-separated ppo_gemm_flags values to compare (--main)")
     args = ap.parse_args()
     lib = ppo_ffi.load()
@@ -35,6 +36,17 @@ def main():
                 us = lib.ppo_bench_gemm(0, m, n, l, 5, -1)
                 print(f"kscan fwd m={m} l={l} K={n:5d} {us:9.1f} us {2.0 * m * n * l / (us * 1e-6) / 1e12:7.1f} TF/s",
                       flush=True)
+        return
+    if args.skinny:
+        for (m, n, l) in ((B, 512, 17), (B, 512, 1), (B, 1024, 17)):
+            for op in (3, 1, 2):
+                for cfg in range(lib.ppo_gemm_tune(-1, -1)):
+                    for tgt in ([256, 512, 1024, 2048] if op == 2 else [0]):
+                        lib.ppo_gemm_tune(-1, tgt)
+                        us = lib.ppo_bench_gemm(op, m, n, l, 20, cfg)
+                        print(f"op{op} m={m:6d} n={n:4d} l={l:3d} {CFG_NAMES[cfg]:16s} split_target={tgt:5d} "
+                              f"{us:8.1f} us {(m * n + m * l) * 4 / (us * 1e-6) / 1e9:7.0f} GB/s", flush=True)
+        lib.ppo_gemm_tune(-1, 0)
         return
     if args.main:
         for (m, n, l) in ((B, 376, 512), (B, 512, 512), (1 << 20, 512, 512)):
