@@ -192,7 +192,9 @@ def main():
     barrier()
     LIB.ppo_reset_stats(ppo)
     LIB.ppo_prof_reset()
-    LIB.ppo_prof_enable(0 if args.no_kernel_events else max(1, args.event_stride))
+    # the timed region only counts launches and their algorithmic work (a stride this large records
+    # one event pair per class); kernel timing is the serialised pass below
+    LIB.ppo_prof_enable(1 << 30)
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -221,23 +223,46 @@ def main():
             dist.all_reduce(tr, op=dist.ReduceOp.MAX)
             t_rollout = float(tr.item())
 
-    ms = (C.c_double * 7)()
-    work = (C.c_double * 7)()
-    launches = (C.c_long * 7)()
-    LIB.ppo_prof_read(ms, work, launches)
-    issued = (C.c_long * 7)()
-    LIB.ppo_prof_counts(issued)
+    def prof_snapshot():
+        ms, work, launches = (C.c_double * 7)(), (C.c_double * 7)(), (C.c_long * 7)()
+        LIB.ppo_prof_read(ms, work, launches)
+        issued, issued_work = (C.c_long * 7)(), (C.c_double * 7)()
+        LIB.ppo_prof_counts(issued)
+        LIB.ppo_prof_issued_work(issued_work)
+        return list(ms), list(work), list(launches), list(issued), list(issued_work)
+
+    ms, work, launches, issued, issued_work = prof_snapshot()
     stats = (C.c_double * 7)()
     LIB.ppo_read_stats(ppo, stats, 7)
 
+    # Kernel pass for the roofline (not part of `value`): in the timed region the value and policy
+    # minibatch loops overlap on two streams, so a launch's event time there includes the share of
+    # the chip the other stream held.  One more update with the loops serialised (PPO_SERIAL=1)
+    # times every event_stride-th launch running alone.
+    serial = None
+    if not args.no_kernel_events:
+        os.environ["PPO_SERIAL"] = "1"
+        LIB.ppo_prof_reset()
+        LIB.ppo_prof_enable(max(1, args.event_stride))
+        barrier()
+        s0 = time.perf_counter()
+        LIB.ppo_update(ppo, 0.99, B, 4, 10, args.shuffle, args.seed)
+        barrier()
+        serial_s = time.perf_counter() - s0
+        LIB.ppo_prof_enable(0)
+        del os.environ["PPO_SERIAL"]
+        serial = list(prof_snapshot()) + [serial_s]
+
     t_update = elapsed / args.steps
     flops = algorithmic_flops(S, H, A, N, B)
-    gemm_ms, gemm_flops, gemm_n = ms[0], work[0], launches[0]
     # sampled launches: class time per update = mean sampled launch time × launches issued
-    kernels = {k: {"ms_per_update": ms[i] / launches[i] * issued[i] / args.steps,
-                   "launches_per_update": issued[i] / args.steps, "avg_launch_us": 1000.0 * ms[i] / launches[i],
-                   "sampled_launches": launches[i]}
-               for i, k in enumerate(["gemm", "gae", "adam", "gather", "head", "comm", "other"]) if launches[i]}
+    # per-class breakdown from the serialised kernel pass (one update) when it ran
+    k_ms, k_launches, k_issued, k_updates = (serial[0], serial[2], serial[3], 1) if serial else \
+        (ms, launches, issued, args.steps)
+    kernels = {k: {"ms_per_update": k_ms[i] / k_launches[i] * k_issued[i] / k_updates,
+                   "launches_per_update": k_issued[i] / k_updates, "avg_launch_us": 1000.0 * k_ms[i] / k_launches[i],
+                   "sampled_launches": k_launches[i]}
+               for i, k in enumerate(["gemm", "gae", "adam", "gather", "head", "comm", "other"]) if k_launches[i]}
     result = {
         "metric": METRIC,
         "value": world * N / t_update,
@@ -267,18 +292,24 @@ def main():
         "kernels": kernels,
         "loss": {"value_mean": stats[0] / max(1.0, stats[1]), "policy_mean": stats[2] / max(1.0, stats[3])},
     }
-    if gemm_n and gemm_ms > 0:
-        achieved = gemm_flops / (gemm_ms * 1e-3) / 1e12
+    if serial and serial[2][0] and serial[0][0] > 0:
+        s_ms, s_work, s_launches = serial[0][0], serial[1][0], serial[2][0]
+        achieved = s_work / (s_ms * 1e-3) / 1e12
         traffic, traffic_src = pmc_traffic() if args.config == "c4" else (None, None)   # PMC pass is of c4
+        # lower bound of the GEMM class rate in the timed (concurrent) region: every GEMM launch's
+        # algorithmic FLOPs over the whole wall time (non-GEMM time counted as GEMM-idle)
+        conc = issued_work[0] / elapsed / 1e12
         result["roofline"] = {"bound": "mfma", "achieved": achieved, "peak": peak,
                               "unit": "TFLOP/s", "frac": achieved / peak, "traffic": traffic,
                               "traffic_source": traffic_src,
                               "kernel": ("gemm_bf16_kernel" if dtype == "bf16" else "gemm_f32_kernel") +
-                                        " (linear-layer launches, every event_stride-th sampled over the timed "
-                                        "region: Σ 2MNK / Σ HIP-event time)",
-                              "launches": gemm_n, "event_stride": args.event_stride,
-                              "avg_launch_us": 1000.0 * gemm_ms / gemm_n,
-                              "algorithmic_flop_per_launch": gemm_flops / gemm_n}
+                                        " (linear-layer launches; Σ 2MNK / Σ HIP-event time over every "
+                                        "event_stride-th launch of one serialised update after the timed region)",
+                              "launches": s_launches, "event_stride": args.event_stride,
+                              "avg_launch_us": 1000.0 * s_ms / s_launches,
+                              "algorithmic_flop_per_launch": s_work / s_launches,
+                              "serial_update_ms": 1000.0 * serial[5],
+                              "concurrent_class_tflops": conc, "concurrent_class_frac": conc / peak}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(LIB, ppo, S, H, A, N, B)
         result["cpu_baseline"]["gpu_over_cpu"] = result["value"] / result["cpu_baseline"]["value"]

@@ -103,6 +103,9 @@ int    ppo_gemm_flags(int flags);
  * 3 = forward without activation (output layer);
  * m = batch, n = in, l = out; cfg −1 = automatic */
 double ppo_bench_gemm(int op, int m, int n, int l, int iters, int cfg);
+/* two independent C4-shaped minibatch GEMM chains (B rows, `out` outputs), `steps` steps each,
+ * interleaved on one stream (two = 0) or two streams (two = 1); total device µs */
+double ppo_bench_streams(int two, int steps, int B, int out);
 /* bf16 GEMMs: force a tile configuration (−1 = automatic); returns the number of configurations */
 int    ppo_gemm16_tune(int force_cfg);
 /* average device µs of one bf16 launch (op as ppo_bench_gemm; bf16 operands); splitk_target 0 = automatic */
@@ -121,6 +124,8 @@ void ppo_prof_reset(void);
 void ppo_prof_read(double* out_ms, double* out_work, long* out_launches);
 /* per class: launches issued while profiling was enabled (sampled or not) */
 void ppo_prof_counts(long* out_total);
+/* per class: Σ algorithmic work of every launch issued while profiling was enabled */
+void ppo_prof_issued_work(double* out_work);
 
 #ifdef __cplusplus
 }

@@ -727,4 +727,70 @@ double ppo_bench_gemm(int op, int m, int n, int l, int iters, int cfg) {
     return 1000.0 * ms / (iters > 0 ? iters : 1);
 }
 
+// Two independent C4-shaped minibatch chains (376 → 512 ×3 → out: forward with bits, then grad_W /
+// grad_x per layer), `steps` steps each, issued interleaved either on one stream (two = 0) or on
+// two streams (two = 1).  Returns total device µs.  Measures what running the value and policy
+// minibatch loops concurrently would gain.
+double ppo_bench_streams(int two, int steps, int B, int out) {
+    ppo::ensure_device();
+    const int S = 376, H = 512;
+    const int dims[5] = {S, H, H, H, out};
+    struct Chain { float *x, *act[5], *g[5], *W[4], *b[4], *gW[4], *gb[4]; unsigned* bits[4]; } c[2];
+    for (auto& ch : c) {
+        ch.x = (float*)phip_malloc(sizeof(float) * (size_t)B * S);
+        phip_fill_uniform(ch.x, (long)B * S, 1, -1.f, 1.f);
+        ch.act[0] = ch.x;
+        for (int i = 0; i < 4; ++i) {
+            const size_t wn = (size_t)dims[i] * dims[i + 1];
+            ch.W[i] = (float*)phip_malloc(sizeof(float) * wn);
+            phip_fill_uniform(ch.W[i], (long)wn, 2 + i, -0.05f, 0.05f);
+            ch.b[i] = (float*)phip_malloc(sizeof(float) * dims[i + 1]);
+            phip_fill_uniform(ch.b[i], dims[i + 1], 9 + i, -0.05f, 0.05f);
+            ch.gW[i] = (float*)phip_malloc(sizeof(float) * wn);
+            ch.gb[i] = (float*)phip_malloc(sizeof(float) * dims[i + 1]);
+            ch.act[i + 1] = (float*)phip_malloc(sizeof(float) * (size_t)B * dims[i + 1]);
+            ch.g[i + 1] = (float*)phip_malloc(sizeof(float) * (size_t)B * dims[i + 1]);
+            ch.bits[i] = (unsigned*)phip_malloc(sizeof(unsigned) * (size_t)B * ppo_divup(dims[i + 1], 32));
+        }
+        phip_fill_uniform(ch.g[4], (long)B * out, 17, -1.f, 1.f);
+    }
+    auto step = [&](Chain& ch) {
+        for (int i = 0; i < 4; ++i)
+            fwd(ch.act[i + 1], ch.act[i], ch.W[i], ch.b[i], B, dims[i], dims[i + 1], i < 3, i < 3 ? ch.bits[i] : nullptr,
+                -1);
+        for (int i = 3; i >= 0; --i) {
+            bwd_w(ch.gW[i], ch.gb[i], ch.g[i + 1], ch.act[i], B, dims[i], dims[i + 1], 0, -1);
+            if (i > 0) bwd_x(ch.g[i], ch.g[i + 1], ch.W[i], nullptr, ch.bits[i - 1], B, dims[i], dims[i + 1], -1);
+        }
+    };
+    hipEvent_t e0, e1;
+    PPO_CHECK(hipEventCreate(&e0));
+    PPO_CHECK(hipEventCreate(&e1));
+    for (int rep = 0; rep < 2; ++rep) {              // rep 0 warms up
+        PPO_CHECK(hipEventRecord(e0, ppo::stream()));
+        if (two) phip_side_fork();
+        for (int k = 0; k < steps; ++k) {
+            step(c[0]);
+            if (two) phip_side_use(1);
+            step(c[1]);
+            if (two) phip_side_use(0);
+        }
+        if (two) phip_side_join();
+        PPO_CHECK(hipEventRecord(e1, ppo::stream()));
+        PPO_CHECK(hipEventSynchronize(e1));
+    }
+    float ms = 0.f;
+    PPO_CHECK(hipEventElapsedTime(&ms, e0, e1));
+    PPO_CHECK(hipEventDestroy(e0));
+    PPO_CHECK(hipEventDestroy(e1));
+    for (auto& ch : c) {
+        phip_free(ch.x);
+        for (int i = 0; i < 4; ++i) {
+            phip_free(ch.W[i]); phip_free(ch.b[i]); phip_free(ch.gW[i]); phip_free(ch.gb[i]);
+            phip_free(ch.act[i + 1]); phip_free(ch.g[i + 1]); phip_free(ch.bits[i]);
+        }
+    }
+    return 1000.0 * ms;
+}
+
 }  // extern "C"

@@ -75,6 +75,7 @@ struct ProfSlot { hipEvent_t a, b; int k; double work; };
 static bool                  g_prof_on = false;
 static int                   g_prof_stride = 1;
 static long                  g_issued[PPO_K_COUNT];
+static double                g_issued_work[PPO_K_COUNT];   // algorithmic work of every issued launch
 static std::vector<ProfSlot> g_slots;       // recorded, not yet harvested
 static std::vector<hipEvent_t> g_free_events;
 static double g_ms[PPO_K_COUNT], g_work[PPO_K_COUNT];
@@ -114,6 +115,7 @@ extern "C" {
 
 int phip_prof_begin(int cls, double work) {
     if (!g_prof_on) return -1;
+    g_issued_work[cls] += work;
     if (g_issued[cls]++ % g_prof_stride != 0) return -1;
     if (g_slots.size() >= (1u << 16)) harvest();
     ProfSlot s{take_event(), take_event(), cls, work};
@@ -134,7 +136,7 @@ void* phip_malloc(size_t bytes) {
     void* p = nullptr;
     if (bytes == 0) bytes = 256;
     PPO_CHECK(hipMalloc(&p, bytes));
-    PPO_CHECK(hipMemsetAsync(p, 0, bytes, g_stream));
+    PPO_CHECK(hipMemsetAsync(p, 0, bytes, stream()));   // ordered before this stream's first use
     return p;
 }
 
@@ -147,13 +149,13 @@ void phip_free(void* p) {
 void phip_h2d(void* dst, const void* src, size_t bytes) {
     if (!bytes) return;
     PPO_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, stream()));
-    PPO_CHECK(hipStreamSynchronize(g_stream));   // the host buffer may be reused right after
+    PPO_CHECK(hipStreamSynchronize(stream()));   // the host buffer may be reused right after
 }
 
 void phip_d2h(void* dst, const void* src, size_t bytes) {
     if (!bytes) return;
     PPO_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, stream()));
-    PPO_CHECK(hipStreamSynchronize(g_stream));
+    PPO_CHECK(hipStreamSynchronize(stream()));
 }
 
 void phip_d2d(void* dst, const void* src, size_t bytes) {
@@ -179,6 +181,8 @@ void phip_side_fork(void) {
 }
 
 void phip_side_use(int on) { g_use_side = on != 0; }
+
+int phip_side_active(void) { return g_use_side; }
 
 void phip_side_join(void) {
     ensure_device();
@@ -233,9 +237,13 @@ void ppo_prof_counts(long* out_total) {
     for (int k = 0; k < PPO_K_COUNT; k++) out_total[k] = g_issued[k];
 }
 
+void ppo_prof_issued_work(double* out_work) {
+    for (int k = 0; k < PPO_K_COUNT; k++) out_work[k] = g_issued_work[k];
+}
+
 void ppo_prof_reset(void) {
     harvest();
-    for (int k = 0; k < PPO_K_COUNT; k++) { g_ms[k] = 0; g_work[k] = 0; g_launches[k] = 0; g_issued[k] = 0; }
+    for (int k = 0; k < PPO_K_COUNT; k++) { g_ms[k] = 0; g_work[k] = 0; g_launches[k] = 0; g_issued[k] = 0; g_issued_work[k] = 0; }
 }
 
 void ppo_prof_read(double* out_ms, double* out_work, long* out_launches) {

@@ -23,11 +23,13 @@ typedef struct {
     int cap_B, S, A;
     float *states, *actions, *old_lp, *adv, *tgt, *gv, *gmu;
     int* rows;                    /* minibatch slot → buffer row (layer 0's fused gather) */
+    int* rows_p;                  /* the policy loop's own rows / gathered states (it runs on the */
+    float* states_p;              /* side stream beside the value loop) */
+    int* perm[2];                 /* host rand() shuffle: every epoch's permutation (value, policy) */
+    long perm_cap[2];
     int* ro_rows;                 /* rollout: rows[t·E + e] = e·T + t */
     float* tiny_steps[3];         /* small-network path: per-step Adam step sizes (value, entropy, policy) */
     int tiny_cap[3];
-    int* tiny_perm;               /* small-network path: one permutation per epoch (host rand() shuffle) */
-    long tiny_perm_cap;
     float* env_state;             /* rollout: per-environment state */
     int ro_E, ro_T, ro_kind, ro_S;
     unsigned long long ro_step;   /* rollout step counter (Philox stream offset) */
@@ -87,8 +89,11 @@ static PPODev* dev_ws(PPO* ppo, int B) {
     if (B > d->cap_B) {
         phip_free(d->states); phip_free(d->actions); phip_free(d->old_lp); phip_free(d->adv);
         phip_free(d->tgt); phip_free(d->gv); phip_free(d->gmu); phip_free(d->rows);
+        phip_free(d->rows_p); phip_free(d->states_p);
         d->rows = (int*)phip_malloc(sizeof(int) * (size_t)B);
+        d->rows_p = (int*)phip_malloc(sizeof(int) * (size_t)B);
         d->states = (float*)phip_malloc(sizeof(float) * (size_t)B * S);
+        d->states_p = (float*)phip_malloc(sizeof(float) * (size_t)B * S);
         d->actions = (float*)phip_malloc(sizeof(float) * (size_t)B * A);
         d->old_lp = (float*)phip_malloc(sizeof(float) * (size_t)B);
         d->adv = (float*)phip_malloc(sizeof(float) * (size_t)B);
@@ -107,7 +112,8 @@ static void free_dev_ws(PPO* ppo) {
     if (!d) return;
     phip_free(d->states); phip_free(d->actions); phip_free(d->old_lp); phip_free(d->adv);
     phip_free(d->tgt); phip_free(d->gv); phip_free(d->gmu); phip_free(d->stats); phip_free(d->rows);
-    phip_free(d->ro_rows); phip_free(d->env_state); phip_free(d->tiny_perm);
+    phip_free(d->ro_rows); phip_free(d->env_state); phip_free(d->perm[0]); phip_free(d->perm[1]);
+    phip_free(d->rows_p); phip_free(d->states_p);
     for (int i = 0; i < 3; i++) phip_free(d->tiny_steps[i]);
     free(d);
     ppo->dev = NULL;
@@ -324,26 +330,36 @@ static float* tiny_steps(PPODev* d, int slot, Adam* adam, float lr, int n) {
     return d->tiny_steps[slot];
 }
 
-/* permutations for n_epochs epochs, consumed in the reference's order (one shuffle per epoch) */
-static const int* tiny_perms(PPO* ppo, PPODev* d, int shuffle_mode, int n_epochs, int limit, PhipTinyPhase* ph) {
+/* every epoch's minibatch order for one phase (slot 0 value, 1 policy), drawn in the reference's
+ * order (one shuffle per epoch): device-shuffle keys into keys[], or host rand() permutations
+ * copied into HBM, epoch e at the returned pointer + e·limit */
+static const int* phase_perms(PPO* ppo, PPODev* d, int shuffle_mode, int n_epochs, int limit, int slot,
+                              uint64_t* keys) {
     if (shuffle_mode == PPO_SHUFFLE_DEVICE) {
-        for (int e = 0; e < n_epochs; e++) {
-            const uint64_t key = d->key++;
-            for (int r = 0; r < 4; r++) ph->feistel_k[4 * e + r] = (uint32_t)splitmix64(key + (uint64_t)r);
-        }
+        for (int e = 0; e < n_epochs; e++) keys[e] = d->key++;
         return NULL;
     }
     const long need = (long)n_epochs * limit;
-    if (need > d->tiny_perm_cap) {
-        phip_free(d->tiny_perm);
-        d->tiny_perm = (int*)phip_malloc(sizeof(int) * (size_t)need);
-        d->tiny_perm_cap = need;
+    if (need > d->perm_cap[slot]) {
+        phip_free(d->perm[slot]);
+        d->perm[slot] = (int*)phip_malloc(sizeof(int) * (size_t)need);
+        d->perm_cap[slot] = need;
     }
     for (int e = 0; e < n_epochs; e++) {
         shuffle_buffer_cuda(ppo->buffer);
-        phip_d2d(d->tiny_perm + (long)e * limit, ppo->buffer->random_idx, sizeof(int) * (size_t)limit);
+        phip_d2d(d->perm[slot] + (long)e * limit, ppo->buffer->random_idx, sizeof(int) * (size_t)limit);
+        keys[e] = 0;
     }
-    return d->tiny_perm;
+    return d->perm[slot];
+}
+
+static const int* tiny_perms(PPO* ppo, PPODev* d, int shuffle_mode, int n_epochs, int limit, PhipTinyPhase* ph) {
+    uint64_t keys[16];
+    const int* perms = phase_perms(ppo, d, shuffle_mode, n_epochs, limit, ph->policy, keys);
+    if (shuffle_mode == PPO_SHUFFLE_DEVICE)
+        for (int e = 0; e < n_epochs; e++)
+            for (int r = 0; r < 4; r++) ph->feistel_k[4 * e + r] = (uint32_t)splitmix64(keys[e] + (uint64_t)r);
+    return perms;
 }
 
 static int ppo_update_tiny(PPO* ppo, PPODev* d, int B, int n_epochs_policy, int n_epochs_value, int shuffle_mode) {
@@ -430,13 +446,30 @@ void ppo_update(void* vppo, float gamma, int batch_size, int n_epochs_policy, in
 
     if (ppo_update_tiny(ppo, d, B, n_epochs_policy, n_epochs_value, shuffle_mode) == 0) return;
 
-    for (int j = 0; j < n_epochs_value; j++) {
-        uint64_t key;
-        const int* perm = next_perm(ppo, d, shuffle_mode, &key);
-        for (int k = 0; k < num_batches; k++) {
+    /* The policy loop reads only the buffer and the advantages — nothing the value loop writes —
+     * so the two run concurrently: value steps on libppo's stream, policy steps on its side stream
+     * (own workspaces, own communicator), issued interleaved.  Every network sees exactly the
+     * reference's sequence of minibatches and Adam steps; epochs' shuffles are drawn up front in
+     * the reference's order (value epochs first).  PPO_SERIAL=1 runs them one after the other. */
+    const long nv = (long)n_epochs_value * num_batches, np = (long)n_epochs_policy * num_batches;
+    uint64_t* keys = (uint64_t*)xmalloc(sizeof(uint64_t) * (size_t)(n_epochs_value + n_epochs_policy + 1));
+    uint64_t* keys_v = keys;
+    uint64_t* keys_p = keys + n_epochs_value;
+    const int* perms_v = phase_perms(ppo, d, shuffle_mode, n_epochs_value, limit, 0, keys_v);
+    const int* perms_p = phase_perms(ppo, d, shuffle_mode, n_epochs_policy, limit, 1, keys_p);
+    const char* serial_env = getenv("PPO_SERIAL");
+    const int concurrent = nv > 0 && np > 0 && !(serial_env && *serial_env && *serial_env != '0');
+    if (concurrent) phip_side_fork();
+    long iv = 0, ip = 0;
+    while (iv < nv || ip < np) {
+        /* serial: every value step first (the reference's order); concurrent: issue in proportion */
+        const int take_v = iv < nv && (ip >= np || !concurrent || iv * np <= ip * nv);
+        if (take_v) {
+            const int j = (int)(iv / num_batches), k = (int)(iv % num_batches);
+            const int* perm = perms_v ? perms_v + (long)j * limit : NULL;
             /* gather fused into layer 0: the kernel emits row indices (+ targets); the layer-0 GEMM
              * reads the buffer rows through them and leaves the gathered copy for its grad_W */
-            phip_gather_rows(perm, key, k * B, limit, B, S, A, buf->state_p, buf->action_p, buf->logprob_p,
+            phip_gather_rows(perm, keys_v[j], k * B, limit, B, S, A, buf->state_p, buf->action_p, buf->logprob_p,
                              buf->advantage_p, buf->adv_target_p, NULL, NULL, NULL, NULL, d->tgt, d->rows);
             nn_forward_dev_rows(V, buf->state_p, d->rows, d->states, B);
             phip_mse(V->d_output, d->tgt, B, d->gv, NULL, d->stats + 0);
@@ -444,25 +477,28 @@ void ppo_update(void* vppo, float gamma, int batch_size, int n_epochs_policy, in
             phip_allreduce_sum_f32(V->d_grads, V->num_params);
             adam_update_net(ppo->adam_V, ppo->lr_V, V);
             d->n_v++;
-        }
-    }
-    for (int j = 0; j < n_epochs_policy; j++) {
-        uint64_t key;
-        const int* perm = next_perm(ppo, d, shuffle_mode, &key);
-        for (int k = 0; k < num_batches; k++) {
-            phip_gather_rows(perm, key, k * B, limit, B, S, A, buf->state_p, buf->action_p, buf->logprob_p,
+            iv++;
+        } else {
+            const int j = (int)(ip / num_batches), k = (int)(ip % num_batches);
+            const int* perm = perms_p ? perms_p + (long)j * limit : NULL;
+            if (concurrent) phip_side_use(1);
+            phip_gather_rows(perm, keys_p[j], k * B, limit, B, S, A, buf->state_p, buf->action_p, buf->logprob_p,
                              buf->advantage_p, buf->adv_target_p, NULL, d->actions, d->old_lp, d->adv, NULL,
-                             d->rows);
-            nn_forward_dev_rows(mu, buf->state_p, d->rows, d->states, B);
+                             d->rows_p);
+            nn_forward_dev_rows(mu, buf->state_p, d->rows_p, d->states_p, B);
             phip_policy_head(mu->d_output, pol->d_log_std, d->actions, d->adv, d->old_lp, B, A, ppo->epsilon,
                              ppo->ent_coeff, d->gmu, pol->d_log_std_grad, d->stats + 1);
             nn_backward_dev(mu, d->gmu, B, 0);
             phip_allreduce_sum_f32(mu->d_grads, mu->num_params + align4(A));   /* μ grads + log_std grad */
             adam_update_cuda(ppo->adam_entropy, ppo->lr_policy);               /* ppo.cu:440-442 order */
             adam_update_net(ppo->adam_policy, ppo->lr_policy, mu);
+            if (concurrent) phip_side_use(0);
             d->n_p++;
+            ip++;
         }
     }
+    if (concurrent) phip_side_join();
+    free(keys);
 }
 
 void ppo_reset_stats(void* vppo) {

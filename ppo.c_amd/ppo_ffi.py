@@ -108,6 +108,7 @@ _SIGS = {
     "ppo_rollout_device": (None, [_P, C.c_int, C.c_int, C.c_int, C.c_ulonglong]),
     "nn_set_compute_dtype": (C.c_int, [_P, C.c_int]),
     "ppo_bench_gemm": (C.c_double, [C.c_int] * 6),
+    "ppo_bench_streams": (C.c_double, [C.c_int] * 4),
     "ppo_build_info": (C.c_char_p, []),
     "ppo_struct_sizes": (C.c_int, [c_long_p, C.c_int]),
     "ppo_dev_alloc": (_P, [C.c_size_t]),
@@ -131,6 +132,7 @@ _SIGS = {
     "ppo_prof_reset": (None, []),
     "ppo_prof_read": (None, [C.POINTER(C.c_double), C.POINTER(C.c_double), c_long_p]),
     "ppo_prof_counts": (None, [c_long_p]),
+    "ppo_prof_issued_work": (None, [C.POINTER(C.c_double)]),
     # mat_mul.h
     "mat_mul": (None, [_P, _P, _P, _P, C.c_int, C.c_int, C.c_int]),
     "mat_mul_backwards": (None, [_P, _P, _P, _P, _P, C.c_int, C.c_int, C.c_int]),

@@ -10,10 +10,18 @@ import csv
 ap = argparse.ArgumentParser()
 ap.add_argument("trace")
 ap.add_argument("--top", type=int, default=30)
+ap.add_argument("--layers", type=int, default=4, help="value-network layers (C4: 4)")
 args = ap.parse_args()
 rows = sorted(csv.DictReader(open(args.trace)), key=lambda r: int(r["Start_Timestamp"]))
-starts = [i for i, r in enumerate(rows) if "gae_block" in r["Kernel_Name"]]
-last = rows[max(0, starts[-1] - 8):]                      # the 8 GAE-forward GEMMs precede the scan
+# the last update starts with V(state)'s forward GEMMs (one per layer) before next_value_map_kernel;
+# with PPO_GAE_FULL=1 both full forwards precede gae_block_kernel
+maps = [i for i, r in enumerate(rows) if "next_value_map" in r["Kernel_Name"]]
+layers = args.layers
+if maps:
+    last = rows[max(0, maps[-1] - layers):]
+else:
+    starts = [i for i, r in enumerate(rows) if "gae_block" in r["Kernel_Name"]]
+    last = rows[max(0, starts[-1] - 2 * layers):]
 t0, t1 = int(last[0]["Start_Timestamp"]), int(last[-1]["End_Timestamp"])
 busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in last)
 print(f"update span {(t1 - t0) / 1e6:.2f} ms, kernel busy {busy / 1e6:.2f} ms, {len(last)} launches")

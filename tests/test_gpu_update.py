@@ -251,3 +251,46 @@ def test_gae_next_value_reuse(lib, oracle, layout, monkeypatch):
         assert_rel_close(tgt, ref["adv_target"], 2e-4, 2e-4 * np.abs(ref["adv_target"]).max(), f"{layout} {mode}")
     assert_rel_close(out["reuse"], out["full"], 1e-4, 1e-4 * np.abs(out["full"]).max(), f"{layout} reuse vs full")
     lib.free_ppo(ppo)
+
+
+@pytest.mark.parametrize("shuffle_mode", [0, 1])
+def test_concurrent_value_policy_loops(lib, oracle, shuffle_mode, monkeypatch):
+    """The policy loop on the side stream beside the value loop == both loops one after the other.
+
+    Same minibatches, Adam step counts and host rand() consumption.  grad_W runs without split-K
+    here (forced), so the GEMMs are deterministic: the value network must match bit for bit; in
+    the policy only the head's log σ-gradient atomics can reorder.
+    """
+    sizes, N, B = [17, 256, 256, 6], 4096, 512
+    lib.ppo_gemm_tune(-1, 1)                                       # split-K target 1: no atomics
+    out = {}
+    for mode in ("serial", "concurrent"):
+        if mode == "serial":
+            monkeypatch.setenv("PPO_SERIAL", "1")
+        else:
+            monkeypatch.delenv("PPO_SERIAL", raising=False)
+        ppo = make_ppo(lib, oracle, sizes, N)
+        mu0, ls0 = policy_state(lib, ppo)
+        buf = synthetic_buffer(oracle, sizes, mu0, ls0, N, seed=3, n_envs=8)
+        load_buffer(lib, ppo, buf)
+        lib.ppo_reset_stats(ppo)
+        oracle.srand(41)
+        lib.ppo_update(ppo, 0.99, B, 2, 3, shuffle_mode, 8)
+        st = (C.c_double * 7)()
+        lib.ppo_read_stats(ppo, st, 7)
+        mu, ls = policy_state(lib, ppo)
+        out[mode] = dict(stats=np.array(st[:4]), v=nn_params_packed(lib, ppo.contents.V), mu=mu, ls=ls,
+                         next_rand=oracle.libc().rand(),
+                         t=(ppo.contents.adam_V.contents.time_step, ppo.contents.adam_policy.contents.time_step,
+                            ppo.contents.adam_entropy.contents.time_step))
+        lib.free_ppo(ppo)
+    lib.ppo_gemm_tune(-1, 0)
+    a, b = out["serial"], out["concurrent"]
+    assert a["t"] == b["t"] == (24, 16, 16)
+    assert a["next_rand"] == b["next_rand"]
+    np.testing.assert_allclose(a["stats"], b["stats"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_array_equal(a["v"], b["v"])                 # the value loop has no atomics left
+    for k in ("mu", "ls"):        # the log σ-gradient's atomics may flip an Adam step of a tiny gradient
+        err = np.abs(a[k] - b[k])
+        assert err.max() <= 2 * 3e-4, (k, err.max())
+        assert (err > 1e-6).mean() < 0.01, (k, (err > 1e-6).mean())
