@@ -13,10 +13,7 @@
 
 namespace {
 ncclComm_t g_comm = nullptr;
-ncclComm_t g_comm_side = nullptr;    // same ranks, for collectives issued on the side stream
 int g_rank = 0, g_world = 1;
-
-ncclComm_t active_comm() { return phip_side_active() ? g_comm_side : g_comm; }
 
 void nccl_check(ncclResult_t r, const char* what, int line) {
     if (r == ncclSuccess) return;
@@ -47,13 +44,6 @@ int ppo_comm_init(int rank, int world, const unsigned char* id) {
         phip_record_error(ncclGetErrorString(r));
         return -1;
     }
-    // the policy minibatch loop runs on libppo's side stream beside the value loop; collectives on
-    // two streams need two communicators (one communicator's kernels must not interleave)
-    r = ncclCommSplit(g_comm, 0, rank, &g_comm_side, nullptr);
-    if (r != ncclSuccess) {
-        phip_record_error(ncclGetErrorString(r));
-        return -1;
-    }
     g_rank = rank;
     g_world = world;
     return 0;
@@ -65,10 +55,8 @@ int ppo_comm_world(void) { return g_world; }
 void ppo_comm_finalize(void) {
     if (g_comm) {
         phip_sync();
-        if (g_comm_side) ncclCommDestroy(g_comm_side);
         ncclCommDestroy(g_comm);
         g_comm = nullptr;
-        g_comm_side = nullptr;
     }
     g_rank = 0;
     g_world = 1;
@@ -80,7 +68,7 @@ int phip_comm_rank(void) { return g_rank; }
 void phip_allreduce_sum_f32(float* d_buf, long n) {
     if (g_world <= 1 || n <= 0) return;
     ppo::ProfScope ps(PPO_K_COMM, 4.0 * n);
-    nccl_check(ncclAllReduce(d_buf, d_buf, (size_t)n, ncclFloat32, ncclSum, active_comm(), ppo::stream()),
+    nccl_check(ncclAllReduce(d_buf, d_buf, (size_t)n, ncclFloat32, ncclSum, g_comm, ppo::stream()),
                "ncclAllReduce", __LINE__);
 }
 
@@ -92,7 +80,7 @@ void phip_allgather_f64(const double* d_send, double* d_recv, long n_per_rank) {
         return;
     }
     ppo::ProfScope ps(PPO_K_COMM, 8.0 * n_per_rank * g_world);
-    nccl_check(ncclAllGather(d_send, d_recv, (size_t)n_per_rank, ncclFloat64, active_comm(), ppo::stream()),
+    nccl_check(ncclAllGather(d_send, d_recv, (size_t)n_per_rank, ncclFloat64, g_comm, ppo::stream()),
                "ncclAllGather", __LINE__);
 }
 

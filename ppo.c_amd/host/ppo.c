@@ -447,10 +447,12 @@ void ppo_update(void* vppo, float gamma, int batch_size, int n_epochs_policy, in
     if (ppo_update_tiny(ppo, d, B, n_epochs_policy, n_epochs_value, shuffle_mode) == 0) return;
 
     /* The policy loop reads only the buffer and the advantages — nothing the value loop writes —
-     * so the two run concurrently: value steps on libppo's stream, policy steps on its side stream
-     * (own workspaces, own communicator), issued interleaved.  Every network sees exactly the
-     * reference's sequence of minibatches and Adam steps; epochs' shuffles are drawn up front in
-     * the reference's order (value epochs first).  PPO_SERIAL=1 runs them one after the other. */
+     * so on one GPU the two run concurrently: value steps on libppo's stream, policy steps on its
+     * side stream (own workspaces), issued interleaved.  Every network sees exactly the reference's
+     * sequence of minibatches and Adam steps; epochs' shuffles are drawn up front in the
+     * reference's order (value epochs first).  PPO_SERIAL=1 runs them one after the other, and so
+     * does data parallelism (world > 1): RCCL collectives from two streams would need a second
+     * communicator and a cross-rank execution order that cannot be rehearsed on one GPU. */
     const long nv = (long)n_epochs_value * num_batches, np = (long)n_epochs_policy * num_batches;
     uint64_t* keys = (uint64_t*)xmalloc(sizeof(uint64_t) * (size_t)(n_epochs_value + n_epochs_policy + 1));
     uint64_t* keys_v = keys;
@@ -458,7 +460,7 @@ void ppo_update(void* vppo, float gamma, int batch_size, int n_epochs_policy, in
     const int* perms_v = phase_perms(ppo, d, shuffle_mode, n_epochs_value, limit, 0, keys_v);
     const int* perms_p = phase_perms(ppo, d, shuffle_mode, n_epochs_policy, limit, 1, keys_p);
     const char* serial_env = getenv("PPO_SERIAL");
-    const int concurrent = nv > 0 && np > 0 && !(serial_env && *serial_env && *serial_env != '0');
+    const int concurrent = nv > 0 && np > 0 && world == 1 && !(serial_env && *serial_env && *serial_env != '0');
     if (concurrent) phip_side_fork();
     long iv = 0, ip = 0;
     while (iv < nv || ip < np) {
