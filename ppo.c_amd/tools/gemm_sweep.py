@@ -24,10 +24,12 @@ def main():
     ap.add_argument("--kscan", action="store_true", help="forward at fixed M,N over K (edge vs main-loop cost)")
     ap.add_argument("--main", action="store_true", help="C4 minibatch shapes x the large-tile configs only")
     ap.add_argument("--cfgs", default="", help="comma-separated configs for --main (default: a fixed set)")
+    ap.add_argument("--lib", default="", help="load this libppo build instead of lib/libppo.so")
+    ap.add_argument("--ops", default="0,1,2", help="--main: ops to run")
     ap.add_argument("--skinny", action="store_true", help="output-layer shapes (N = 17 / 1) x every config")
     ap.add_argument("--flags", default="0", help="comma-separated ppo_gemm_flags values to compare (--main)")
     args = ap.parse_args()
-    lib = ppo_ffi.load()
+    lib = ppo_ffi.load(args.lib) if args.lib else ppo_ffi.load()
     lib.ppo_set_device(0)
     B = 32768
     if args.kscan:
@@ -50,7 +52,7 @@ def main():
         return
     if args.main:
         for (m, n, l) in ((B, 376, 512), (B, 512, 512), (1 << 20, 512, 512)):
-            for op in (0, 1, 2):
+            for op in (int(o) for o in args.ops.split(",")):
                 if m > B and op:
                     continue
                 cfgs = [0, 5, 7] if op != 2 else [0, 4, 5, 7, 9]
