@@ -134,6 +134,7 @@ def main():
     ap.add_argument("--shuffle", type=int, default=1, help="1 = device Feistel shuffle, 0 = reference host rand()")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-events", action="store_true")
+    ap.add_argument("--gemm-flags", type=int, default=0, help="ppo_gemm_flags experiment bits (A/B runs)")
     ap.add_argument("--no-rollout", action="store_true", help="skip the rollout env-steps/s measurement")
     ap.add_argument("--event-stride", type=int, default=7,
                     help="HIP events around every k-th launch of each kernel class (1 = all; each event pair "
@@ -171,6 +172,8 @@ def main():
     sizes = [S] + H + [A]
     acts = ["relu"] * len(H) + ["none"]
 
+    if args.gemm_flags:
+        LIB.ppo_gemm_flags(args.gemm_flags)
     C.CDLL("libc.so.6").srand(args.seed)                                 # identical init on every rank
     ppo = LIB.create_ppo(ppo_ffi.c_strings(acts), ppo_ffi.c_ints(sizes), len(sizes), N, 3e-4, 3e-4, 0.95, 0.2, 0.0,
                          1.0, True)

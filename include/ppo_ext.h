@@ -96,7 +96,7 @@ int nn_set_compute_dtype(void* nn, int dtype);          /* NeuralNetwork* */
 /* force a tile configuration (−1 = automatic) and the split-K workgroup target of grad_W
  * (0 = per-shape automatic, < 0 keeps the current setting); returns the number of tile configurations */
 int    ppo_gemm_tune(int force_cfg, int splitk_target);
-/* experiment switches of the fp32 tiled GEMM (bit 0: invert the s_setprio default around the MFMA block); flags < 0
+/* experiment switches of the fp32 tiled GEMM (bit 0: invert the s_setprio default around the MFMA block; bit 2 (value 4): grad_W and grad_x of a layer as two launches instead of one paired launch); flags < 0
  * only queries; returns the previous value */
 int    ppo_gemm_flags(int flags);
 /* average device µs of one launch: op 0 = forward (bias+ReLU), 1 = grad_x, 2 = grad_W (+bias grad),

@@ -196,8 +196,15 @@ constexpr int min_waves(int area, int bk) { return area >= 256 * 128 ? 2 : (bk >
 
 // DBUF: two LDS images; the staged tile t+1 is written into the idle image behind tile t's MFMAs,
 // so each k-tile needs one barrier instead of two.
+template <int OP, int BM, int BN, int BK, bool DBUF>
+constexpr int lds_floats() {
+    return (DBUF ? 2 : 1) * (Stage<BM, BK, OP == OP_TN>::IMG + Stage<BN, BK, OP != OP_NT>::IMG);
+}
+
+// One workgroup's output tile: block b of an nwg-block grid (the kernels below pass their own
+// block id, or an offset one when two GEMMs share a launch).
 template <int OP, int BM, int BN, int WARPS_M, int BK, bool VEC, bool DBUF>
-__global__ __launch_bounds__(NT_, min_waves(BM * BN, BK)) void gemm_f32_kernel(Args a) {
+__device__ __forceinline__ void gemm_tile(const Args& a, const int b, const int nwg, float* __restrict__ lds) {
     constexpr int WARPS_N = 4 / WARPS_M;
     constexpr int WM = BM / WARPS_M, WN = BN / WARPS_N;
     constexpr int TM = WM / 32, TN = WN / 32;
@@ -209,10 +216,7 @@ __global__ __launch_bounds__(NT_, min_waves(BM * BN, BK)) void gemm_f32_kernel(A
     static_assert(TM >= 1 && TN >= 1, "wave tile must be a multiple of 32x32");
     static_assert(BK == 16 || BK == 32, "BK");
 
-    __shared__ __attribute__((aligned(16))) float lds[(DBUF ? 2 : 1) * IMG];
-
     // XCD-aware bijective remap of the linear block id (guide §5 "XCD swizzle must be bijective")
-    const int nwg = gridDim.x, b = blockIdx.x;
     const int xcd = b & 7, q = nwg >> 3, rr = nwg & 7;
     const int t = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + (b >> 3);
     const int tn = t % a.tiles_n;
@@ -385,6 +389,23 @@ __global__ __launch_bounds__(NT_, min_waves(BM * BN, BK)) void gemm_f32_kernel(A
                 if (row < a.M && c0 < a.N) a.bits_out[(long)row * a.wpr + (c0 >> 5)] = word;
             }
         }
+}
+
+template <int OP, int BM, int BN, int WARPS_M, int BK, bool VEC, bool DBUF>
+__global__ __launch_bounds__(NT_, min_waves(BM * BN, BK)) void gemm_f32_kernel(Args a) {
+    __shared__ __attribute__((aligned(16))) float lds[lds_floats<OP, BM, BN, BK, DBUF>()];
+    gemm_tile<OP, BM, BN, WARPS_M, BK, VEC, DBUF>(a, blockIdx.x, gridDim.x, lds);
+}
+
+// grad_W and grad_x of one layer in one launch (both 128x128/BK16, vector loads): blocks
+// [0, g1) are grad_W tiles, the rest grad_x tiles.  The two products are independent, so grad_x
+// tiles fill the CUs that grad_W tiles leave while their split-K atomics drain — the lock-step
+// tail of two back-to-back one-round grids becomes one.
+__global__ __launch_bounds__(NT_, 4) void gemm_pair_kernel(Args aw, Args ax, int g1) {
+    constexpr int LW = lds_floats<OP_TN, 128, 128, 16, false>(), LX = lds_floats<OP_NN, 128, 128, 16, false>();
+    __shared__ __attribute__((aligned(16))) float lds[LW > LX ? LW : LX];
+    if ((int)blockIdx.x < g1) gemm_tile<OP_TN, 128, 128, 2, 16, true, false>(aw, blockIdx.x, g1, lds);
+    else gemm_tile<OP_NN, 128, 128, 2, 16, true, false>(ax, blockIdx.x - g1, gridDim.x - g1, lds);
 }
 
 // ---------------------------------------------------------------------------
@@ -584,8 +605,8 @@ void fwd(float* y, const float* x, const float* W, const float* b, int m, int n,
     launch_cfg<OP_NT>(cfg < 0 ? pick_cfg(OP_NT, m, l) : cfg, a);
 }
 
-void bwd_x(float* gx, const float* g, const float* W, const float* mask, const unsigned* bits, int m, int n, int l,
-           int cfg) {
+Args bwd_x_args(float* gx, const float* g, const float* W, const float* mask, const unsigned* bits, int m, int n,
+                int l) {
     Args a{};
     a.A = g; a.lda = l; a.B = W; a.ldb = n; a.C = gx; a.ldc = n;
     a.M = m; a.N = n; a.K = l; a.kchunk = l; a.splits = 1;
@@ -593,21 +614,22 @@ void bwd_x(float* gx, const float* g, const float* W, const float* mask, const u
     a.bits_in = bits; a.wpr = ppo_divup(n, 32);
     a.vec_a = (l % 4 == 0) && aligned16(g);             // kcont, extent K = l
     a.vec_b = (n % 4 == 0) && aligned16(W);             // mncont, extent N = n, ld = n
-    launch_cfg<OP_NN>(cfg < 0 ? pick_cfg(OP_NN, m, n) : cfg, a);
+    return a;
+}
+
+void bwd_x(float* gx, const float* g, const float* W, const float* mask, const unsigned* bits, int m, int n, int l,
+           int cfg) {
+    launch_cfg<OP_NN>(cfg < 0 ? pick_cfg(OP_NN, m, n) : cfg, bwd_x_args(gx, g, W, mask, bits, m, n, l));
 }
 
 // grad_W reduces over the minibatch (K = m): split-K so the grid fills the chip; f32 atomics
-// into an output that is zero on entry (zeroed != 0) or zeroed here.
-void bwd_w(float* gW, float* gb, const float* g, const float* x, int m, int n, int l, int zeroed, int cfg) {
-    if (m <= 0) {
-        if (!zeroed) {
-            phip_memset(gW, 0, sizeof(float) * (size_t)l * n);
-            if (gb) phip_memset(gb, 0, sizeof(float) * (size_t)l);
-        }
-        return;
-    }
+// into an output that is zero on entry (zeroed != 0) or zeroed here.  Returns the arguments and
+// tile configuration (m > 0).
+Args bwd_w_args(float* gW, float* gb, const float* g, const float* x, int m, int n, int l, int zeroed, int cfg,
+                int* c_out, int target_override = 0) {
     int target = 1024;
     const int c = cfg < 0 ? pick_cfg(OP_TN, l, n, &target) : cfg;
+    if (target_override > 0) target = target_override;
     if (g_splitk_override > 0) target = g_splitk_override;
     const TileCfg& tc = kCfgs[c];
     Args a{};
@@ -625,11 +647,63 @@ void bwd_w(float* gW, float* gb, const float* g, const float* x, int m, int n, i
     kchunk = ppo_divup(kchunk, tc.bk) * tc.bk;
     splits = ppo_divup(m, kchunk);
     a.kchunk = kchunk; a.splits = splits;
+    a.tiles_m = ppo_divup(a.M, tc.bm);
+    a.tiles_n = ppo_divup(a.N, tc.bn);
     if (splits > 1 && !zeroed) {
         phip_memset(gW, 0, sizeof(float) * (size_t)l * n);
         if (gb) phip_memset(gb, 0, sizeof(float) * (size_t)l);
     }
+    *c_out = c;
+    return a;
+}
+
+void bwd_w(float* gW, float* gb, const float* g, const float* x, int m, int n, int l, int zeroed, int cfg) {
+    if (m <= 0) {
+        if (!zeroed) {
+            phip_memset(gW, 0, sizeof(float) * (size_t)l * n);
+            if (gb) phip_memset(gb, 0, sizeof(float) * (size_t)l);
+        }
+        return;
+    }
+    int c = 0;
+    const Args a = bwd_w_args(gW, gb, g, x, m, n, l, zeroed, cfg, &c);
     launch_cfg<OP_TN>(c, a);
+}
+
+// grad_W and grad_x of one layer: one gemm_pair_kernel launch when both pick the 128x128/BK16
+// vector tile (hidden layers at C4/C5 minibatch sizes), else two launches.  Flag bit 4 (ppo_gemm_flags)
+// forces two launches (A/B runs, tests).  Measured at C4: update 544 → 539 ms (serialised loops:
+// 580 → 567 ms).
+void bwd_pair(float* gW, float* gb, float* gx, const float* g, const float* x, const float* W, const unsigned* bits,
+              int m, int n, int l, int zeroed) {
+    const bool pair = (g_flags & 4) == 0 && g_force_cfg < 0 && m > 0 && pick_cfg(OP_TN, l, n) == 0 &&
+                      pick_cfg(OP_NN, m, n) == 0;
+    if (pair) {
+        int c = 0;
+        // grad_W at a 1024-workgroup split target: with a 1024-tile grad_x the launch is two full
+        // rounds of 4 workgroups per CU (at the standalone 512 target it would be 1.5 rounds:
+        // measured 549 vs 539 ms per C4 update; 2048: 558 ms)
+        Args aw = bwd_w_args(gW, gb, g, x, m, n, l, zeroed, -1, &c, 1024);
+        Args ax = bwd_x_args(gx, g, W, nullptr, bits, m, n, l);
+        if (c == 0 && aw.vec_a && aw.vec_b && ax.vec_a && ax.vec_b) {
+            aw.flags = ax.flags = g_flags;
+            if (aw.splits < 1) aw.splits = 1;
+            ax.tiles_m = ppo_divup(ax.M, 128);
+            ax.tiles_n = ppo_divup(ax.N, 128);
+            const long g1 = (long)aw.tiles_m * aw.tiles_n * aw.splits;
+            const long g2 = (long)ax.tiles_m * ax.tiles_n;
+            PPO_REQUIRE(g1 > 0 && g2 > 0 && g1 + g2 < (1L << 31), "gemm pair: grid out of range");
+            hipLaunchKernelGGL(gemm_pair_kernel, dim3((unsigned)(g1 + g2)), dim3(NT_), 0, ppo::stream(), aw, ax,
+                               (int)g1);
+            PPO_LAUNCH_CHECK();
+            return;
+        }
+        launch_cfg<OP_TN>(c, aw);           // arguments built (and output zeroed) already
+        bwd_x(gx, g, W, nullptr, bits, m, n, l, -1);
+        return;
+    }
+    bwd_w(gW, gb, g, x, m, n, l, zeroed, -1);
+    bwd_x(gx, g, W, nullptr, bits, m, n, l, -1);
 }
 
 }  // namespace
@@ -677,6 +751,14 @@ void phip_linear_bwd_w_ex(float* gW, float* gb, const float* g, const float* x, 
 
 void phip_linear_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, int n, int l) {
     phip_linear_bwd_w_ex(gW, gb, g, x, m, n, l, 0);
+}
+
+void phip_linear_bwd_pair(float* gW, float* gb, float* gx, const float* g, const float* x, const float* W,
+                          const unsigned* bits, int m, int n, int l, int zeroed) {
+    if (l <= 0 || n <= 0) return;
+    PPO_REQUIRE(gW && gx && g && x && W, "phip_linear_bwd_pair: null operand");
+    ppo::ProfScope ps(PPO_K_GEMM, 4.0 * m * n * l);
+    bwd_pair(gW, gb, gx, g, x, W, bits, m, n, l, zeroed);
 }
 
 int ppo_gemm_flags(int flags) {

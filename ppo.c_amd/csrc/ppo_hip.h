@@ -53,6 +53,9 @@ void phip_linear_bwd_x_bits(float* gx, const float* g, const float* W, const flo
 /* gW[l,n] = g[m,l]ᵀ·x[m,n] and gb[l] = Σ_m g[m,l] (K4 + K7 fused); overwrites */
 void phip_linear_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, int n, int l);
 /* same, with gW/gb already zero on entry when `zeroed` (one memset per backward instead of two per layer) */
+/* grad_W (+ bias) and grad_x ⊙ ReLU′(bits) of one layer, one launch when the shapes allow */
+void phip_linear_bwd_pair(float* gW, float* gb, float* gx, const float* g, const float* x, const float* W,
+                          const unsigned* bits, int m, int n, int l, int zeroed);
 void phip_linear_bwd_w_ex(float* gW, float* gb, const float* g, const float* x, int m, int n, int l, int zeroed);
 
 /* ---------------- bf16-MFMA dense layers (gemm16.hip) ---------------- */

@@ -210,17 +210,23 @@ void nn_backward_dev(NeuralNetwork* nn, const float* d_grad_out, int m, int want
         nn->cache_m_backward = m;
         return;
     }
-    /* (measured: running grad_W on a second queue beside grad_x of the same layer made the pair
-     * slower than back to back — both kernels fill the chip and thrash each other's L2) */
+    /* grad_W and grad_x of a layer are independent: with the ReLU′ bits of this forward they go
+     * out as one launch (phip_linear_bwd_pair: grad_x tiles fill the CUs grad_W tiles leave).
+     * (measured: grad_W on a second queue beside grad_x was slower than back to back) */
     for (int i = L - 1; i >= 0; i--) {
         Layer* ly = &nn->layers[i];
         const float* x = i == 0 ? nn->d_x0 : ly->d_input;
-        phip_linear_bwd_w_ex(ly->d_grad_weights, ly->d_grad_biases, g, x, m, ly->input_size, ly->output_size, 1);
-        if (i > 0 || want_grad_x0) {
-            const int relu_in = i > 0 && nn_is_relu(nn, i - 1);
-            const float* mask = relu_in ? ly->d_input : NULL;
-            const unsigned* bits = relu_in && nn->bits_m == m ? act_bits(nn, i) : NULL;   /* this forward's bits */
-            phip_linear_bwd_x_bits(ly->d_grad_x, g, ly->d_weights, mask, bits, m, ly->input_size, ly->output_size);
+        const int want_gx = i > 0 || want_grad_x0;
+        const int relu_in = i > 0 && nn_is_relu(nn, i - 1);
+        const unsigned* bits = relu_in && nn->bits_m == m ? act_bits(nn, i) : NULL;   /* this forward's bits */
+        if (want_gx && (!relu_in || bits)) {
+            phip_linear_bwd_pair(ly->d_grad_weights, ly->d_grad_biases, ly->d_grad_x, g, x, ly->d_weights, bits, m,
+                                 ly->input_size, ly->output_size, 1);
+        } else {
+            phip_linear_bwd_w_ex(ly->d_grad_weights, ly->d_grad_biases, g, x, m, ly->input_size, ly->output_size, 1);
+            if (want_gx)
+                phip_linear_bwd_x_bits(ly->d_grad_x, g, ly->d_weights, relu_in ? ly->d_input : NULL, NULL, m,
+                                       ly->input_size, ly->output_size);
         }
         g = ly->d_grad_x;
     }

@@ -77,3 +77,58 @@ def test_mlp_every_cfg(lib, oracle, ncfg, sizes, m):
     finally:
         lib.ppo_gemm_tune(-1, 0)
         lib.free_neural_network(nn)
+
+
+def _mlp_grads_f64(sizes, params, x, gout):
+    """float64 numpy forward/backward of the packed MLP ([W0, b0, W1, b1, …], W as [out, in])."""
+    Ws, bs, off = [], [], 0
+    for i in range(len(sizes) - 1):
+        n_in, n_out = sizes[i], sizes[i + 1]
+        Ws.append(params[off:off + n_in * n_out].astype(np.float64).reshape(n_out, n_in))
+        off += n_in * n_out
+        bs.append(params[off:off + n_out].astype(np.float64))
+        off += n_out
+    hs = [x.astype(np.float64)]
+    for i in range(len(Ws)):
+        y = hs[-1] @ Ws[i].T + bs[i]
+        hs.append(np.maximum(y, 0) if i < len(Ws) - 1 else y)
+    g, grads = gout.astype(np.float64), []
+    for i in range(len(Ws) - 1, -1, -1):
+        grads = [(g.T @ hs[i]).ravel(), g.sum(0)] + grads
+        g = (g @ Ws[i]) * (hs[i] > 0) if i > 0 else g @ Ws[i]
+    return np.concatenate(grads)
+
+
+@pytest.mark.parametrize("sizes,m", [([376, 512, 512, 512, 17], 16384), ([64, 1024, 1024, 8], 8192)])
+def test_mlp_paired_backward(lib, sizes, m):
+    """grad_W + grad_x of a hidden layer as one launch (gemm_pair_kernel) vs two launches (flag 4):
+    grad_x identical bit for bit (same tiles, same k order), grad_W up to the split-K atomics'
+    order; both within the GEMM bound of a float64 reference (up to ReLU-mask flips)."""
+    rng = np.random.default_rng(m + len(sizes))
+    nn = lib.create_neural_network(ppo_ffi.c_ints(sizes), ppo_ffi.c_strings(["relu"] * (len(sizes) - 2) + ["none"]),
+                                   len(sizes))
+    nparams = sum(sizes[i] * sizes[i + 1] + sizes[i + 1] for i in range(len(sizes) - 1))
+    params = (rng.uniform(-1, 1, nparams) * 0.05).astype(F32)
+    nn_set_params_packed(lib, nn, params)
+    x, gout = _rand(rng, (m, sizes[0])), _rand(rng, (m, sizes[-1]))
+    g_ref = _mlp_grads_f64(sizes, params, x, gout)
+    dx, dgo = dev(lib, x), dev(lib, gout)
+    out = {}
+    try:
+        for flags in (0, 4):
+            lib.ppo_gemm_flags(flags)
+            lib.forward_propagation_cuda(nn, dx.ptr, m)
+            lib.backward_propagation_cuda(nn, dgo.ptr, m)
+            gx1 = ppo_ffi.d2h(lib, nn.contents.layers[1].d_grad_x, F32, m * sizes[1])
+            out[flags] = (nn_grads_packed(lib, nn), gx1)
+            # a pre-activation within fp32 rounding of 0 can take the other side of the ReLU than in
+            # float64 (a mask flip moves a few gradient entries by O(|g|·|h|)), so the bound must hold
+            # for all but a small fraction of entries here
+            err = np.abs(out[flags][0] - g_ref)
+            tol = 1e-4 * np.abs(g_ref).max() * max(1.0, np.sqrt(m / 1024))
+            assert (err > tol).mean() < 1e-3, f"flags {flags}: {(err > tol).sum()} entries beyond {tol:.3g}"
+    finally:
+        lib.ppo_gemm_flags(0)
+        lib.free_neural_network(nn)
+    np.testing.assert_array_equal(out[0][1], out[4][1])
+    np.testing.assert_allclose(out[0][0], out[4][0], rtol=1e-5, atol=1e-5 * np.abs(out[4][0]).max())
