@@ -401,11 +401,14 @@ __global__ __launch_bounds__(NT_, min_waves(BM * BN, BK)) void gemm_f32_kernel(A
 // [0, g1) are grad_W tiles, the rest grad_x tiles.  The two products are independent, so grad_x
 // tiles fill the CUs that grad_W tiles leave while their split-K atomics drain — the lock-step
 // tail of two back-to-back one-round grids becomes one.
+// Instantiated for the hidden layers (both 128x128, vector loads) and the output layer (grad_W on
+// 32x128 tiles, grad_x on 128x128; K = A is not a multiple of 4: guarded loads).
+template <int BMW, int BNW, int WMW, bool VW, int BMX, int BNX, int WMX, bool VX>
 __global__ __launch_bounds__(NT_, 4) void gemm_pair_kernel(Args aw, Args ax, int g1) {
-    constexpr int LW = lds_floats<OP_TN, 128, 128, 16, false>(), LX = lds_floats<OP_NN, 128, 128, 16, false>();
+    constexpr int LW = lds_floats<OP_TN, BMW, BNW, 16, false>(), LX = lds_floats<OP_NN, BMX, BNX, 16, false>();
     __shared__ __attribute__((aligned(16))) float lds[LW > LX ? LW : LX];
-    if ((int)blockIdx.x < g1) gemm_tile<OP_TN, 128, 128, 2, 16, true, false>(aw, blockIdx.x, g1, lds);
-    else gemm_tile<OP_NN, 128, 128, 2, 16, true, false>(ax, blockIdx.x - g1, gridDim.x - g1, lds);
+    if ((int)blockIdx.x < g1) gemm_tile<OP_TN, BMW, BNW, WMW, 16, VW, false>(aw, blockIdx.x, g1, lds);
+    else gemm_tile<OP_NN, BMX, BNX, WMX, 16, VX, false>(ax, blockIdx.x - g1, gridDim.x - g1, lds);
 }
 
 // ---------------------------------------------------------------------------
@@ -676,30 +679,37 @@ void bwd_w(float* gW, float* gb, const float* g, const float* x, int m, int n, i
 // 580 → 567 ms).
 void bwd_pair(float* gW, float* gb, float* gx, const float* g, const float* x, const float* W, const unsigned* bits,
               int m, int n, int l, int zeroed) {
-    const bool pair = (g_flags & 4) == 0 && g_force_cfg < 0 && m > 0 && pick_cfg(OP_TN, l, n) == 0 &&
-                      pick_cfg(OP_NN, m, n) == 0;
-    if (pair) {
+    const int cw = pick_cfg(OP_TN, l, n), cx = pick_cfg(OP_NN, m, n);
+    const bool hidden = cw == 0 && cx == 0;
+    const bool output = cw == 3 && cx == 0 && (g_flags & 32) == 0;
+    if ((g_flags & 4) == 0 && g_force_cfg < 0 && m > 0 && (hidden || output)) {
         int c = 0;
         // grad_W at a 1024-workgroup split target: with a 1024-tile grad_x the launch is two full
         // rounds of 4 workgroups per CU (at the standalone 512 target it would be 1.5 rounds:
         // measured 549 vs 539 ms per C4 update; 2048: 558 ms)
         Args aw = bwd_w_args(gW, gb, g, x, m, n, l, zeroed, -1, &c, 1024);
         Args ax = bwd_x_args(gx, g, W, nullptr, bits, m, n, l);
-        if (c == 0 && aw.vec_a && aw.vec_b && ax.vec_a && ax.vec_b) {
-            aw.flags = ax.flags = g_flags;
-            if (aw.splits < 1) aw.splits = 1;
-            ax.tiles_m = ppo_divup(ax.M, 128);
-            ax.tiles_n = ppo_divup(ax.N, 128);
-            const long g1 = (long)aw.tiles_m * aw.tiles_n * aw.splits;
-            const long g2 = (long)ax.tiles_m * ax.tiles_n;
-            PPO_REQUIRE(g1 > 0 && g2 > 0 && g1 + g2 < (1L << 31), "gemm pair: grid out of range");
-            hipLaunchKernelGGL(gemm_pair_kernel, dim3((unsigned)(g1 + g2)), dim3(NT_), 0, ppo::stream(), aw, ax,
-                               (int)g1);
-            PPO_LAUNCH_CHECK();
+        aw.flags = ax.flags = g_flags;
+        if (aw.splits < 1) aw.splits = 1;
+        ax.tiles_m = ppo_divup(ax.M, 128);
+        ax.tiles_n = ppo_divup(ax.N, 128);
+        const long g1 = (long)aw.tiles_m * aw.tiles_n * aw.splits;
+        const long g2 = (long)ax.tiles_m * ax.tiles_n;
+        PPO_REQUIRE(g1 > 0 && g2 > 0 && g1 + g2 < (1L << 31), "gemm pair: grid out of range");
+        const dim3 grid((unsigned)(g1 + g2));
+        const bool vw = aw.vec_a && aw.vec_b, vx = ax.vec_a && ax.vec_b;
+        if (hidden && vw && vx) {
+            hipLaunchKernelGGL((gemm_pair_kernel<128, 128, 2, true, 128, 128, 2, true>), grid, dim3(NT_), 0,
+                               ppo::stream(), aw, ax, (int)g1);
+        } else if (output && !vw && !vx) {
+            hipLaunchKernelGGL((gemm_pair_kernel<32, 128, 1, false, 128, 128, 2, false>), grid, dim3(NT_), 0,
+                               ppo::stream(), aw, ax, (int)g1);
+        } else {
+            launch_cfg<OP_TN>(c, aw);           // arguments built (and output zeroed) already
+            bwd_x(gx, g, W, nullptr, bits, m, n, l, -1);
             return;
         }
-        launch_cfg<OP_TN>(c, aw);           // arguments built (and output zeroed) already
-        bwd_x(gx, g, W, nullptr, bits, m, n, l, -1);
+        PPO_LAUNCH_CHECK();
         return;
     }
     bwd_w(gW, gb, g, x, m, n, l, zeroed, -1);

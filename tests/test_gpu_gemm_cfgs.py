@@ -101,7 +101,8 @@ def _mlp_grads_f64(sizes, params, x, gout):
 
 @pytest.mark.parametrize("sizes,m", [([376, 512, 512, 512, 17], 16384), ([64, 1024, 1024, 8], 8192)])
 def test_mlp_paired_backward(lib, sizes, m):
-    """grad_W + grad_x of a hidden layer as one launch (gemm_pair_kernel) vs two launches (flag 4):
+    """grad_W + grad_x of a layer as one launch (gemm_pair_kernel: hidden layers, and the 17-wide
+    output layer) vs two launches (flag 4):
     grad_x identical bit for bit (same tiles, same k order), grad_W up to the split-K atomics'
     order; both within the GEMM bound of a float64 reference (up to ReLU-mask flips)."""
     rng = np.random.default_rng(m + len(sizes))
@@ -119,8 +120,8 @@ def test_mlp_paired_backward(lib, sizes, m):
             lib.ppo_gemm_flags(flags)
             lib.forward_propagation_cuda(nn, dx.ptr, m)
             lib.backward_propagation_cuda(nn, dgo.ptr, m)
-            gx1 = ppo_ffi.d2h(lib, nn.contents.layers[1].d_grad_x, F32, m * sizes[1])
-            out[flags] = (nn_grads_packed(lib, nn), gx1)
+            gx = [ppo_ffi.d2h(lib, nn.contents.layers[i].d_grad_x, F32, m * sizes[i]) for i in range(1, len(sizes) - 1)]
+            out[flags] = (nn_grads_packed(lib, nn), gx)
             # a pre-activation within fp32 rounding of 0 can take the other side of the ReLU than in
             # float64 (a mask flip moves a few gradient entries by O(|g|·|h|)), so the bound must hold
             # for all but a small fraction of entries here
@@ -130,5 +131,6 @@ def test_mlp_paired_backward(lib, sizes, m):
     finally:
         lib.ppo_gemm_flags(0)
         lib.free_neural_network(nn)
-    np.testing.assert_array_equal(out[0][1], out[4][1])
+    for a, b in zip(out[0][1], out[4][1]):          # every hidden layer's grad_x, output layer's included
+        np.testing.assert_array_equal(a, b)
     np.testing.assert_allclose(out[0][0], out[4][0], rtol=1e-5, atol=1e-5 * np.abs(out[4][0]).max())
