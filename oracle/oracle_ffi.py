@@ -23,7 +23,7 @@ class RefUpdateCfg(C.Structure):
                 ("batch_size", C.c_int), ("n_epochs_policy", C.c_int), ("n_epochs_value", C.c_int),
                 ("gamma", C.c_float), ("lambda_", C.c_float), ("epsilon", C.c_float), ("ent_coeff", C.c_float),
                 ("lr_policy", C.c_float), ("lr_v", C.c_float), ("shuffle_mode", C.c_int), ("seed", C.c_uint64),
-                ("max_value_steps", C.c_int), ("max_policy_steps", C.c_int)]
+                ("max_value_steps", C.c_int), ("max_policy_steps", C.c_int), ("capacity", C.c_int)]
 
 
 _FP = C.POINTER(C.c_float)
@@ -262,10 +262,11 @@ def adam_update(params, grads, m, v, t, lr, beta1=0.9, beta2=0.999):
 
 def ppo_update(sizes, relu_flags, mu_params, log_std, v_params, buf, *, batch_size, n_epochs_policy=4,
                n_epochs_value=10, gamma=0.99, lam=0.95, epsilon=0.2, ent_coeff=0.0, lr_policy=3e-4, lr_v=3e-4,
-               shuffle_mode=0, seed=0, max_value_steps=-1, max_policy_steps=-1, adam=None):
+               shuffle_mode=0, seed=0, max_value_steps=-1, max_policy_steps=-1, adam=None, capacity=0):
     """One reference CPU update (ppo.cu:395-443 without the rollout) on copies of the inputs.
 
-    buf: dict of numpy arrays state, next_state, action, reward, logprob, terminated, truncated.
+    buf: dict of numpy arrays state, next_state, action, reward, logprob, terminated, truncated — the
+    `limit` filled rows of the buffer; capacity (> limit) gives a partly filled buffer's minibatch count.
     adam: optional dict with m/v/t for 'mu', 'v', 'ent' (fresh zeros otherwise).
     Returns a dict with the updated parameters, Adam state, advantages and loss sums.
     """
@@ -283,6 +284,7 @@ def ppo_update(sizes, relu_flags, mu_params, log_std, v_params, buf, *, batch_si
     cfg.lr_policy, cfg.lr_v = lr_policy, lr_v
     cfg.shuffle_mode, cfg.seed = shuffle_mode, seed
     cfg.max_value_steps, cfg.max_policy_steps = max_value_steps, max_policy_steps
+    cfg.capacity = capacity
     out = {"mu": np.array(mu_params, _f32, copy=True), "log_std": np.array(log_std, _f32, copy=True),
            "v": np.array(v_params, _f32, copy=True), "advantage": np.zeros(N, _f32),
            "adv_target": np.zeros(N, _f32)}

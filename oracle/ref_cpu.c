@@ -429,7 +429,9 @@ void ref_ppo_update(const RefUpdateCfg* c, RefUpdateState* st) {
     float* grads = (float*)malloc(sizeof(float) * (size_t)(np_mu > np_v ? np_mu : np_v));
     float* g_logstd = (float*)malloc(sizeof(float) * (size_t)A);
     int* perm = (int*)malloc(sizeof(int) * (size_t)N);
-    int num_batches = c->N / B;                       /* D13: ceilf(capacity / batch_size) */
+    /* D13: ceilf(capacity / batch_size) with integer division inside (ppo.cu:387-388); get_batch
+     * wraps the rows modulo limit = N (trajectory_buffer.cu:168-200) */
+    int num_batches = (c->capacity > 0 ? c->capacity : c->N) / B;
     uint64_t epoch_key = splitmix64(c->seed);
     int vsteps = 0, psteps = 0;
 

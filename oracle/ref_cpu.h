@@ -91,6 +91,8 @@ typedef struct {
     uint64_t seed;            /* Feistel key base when shuffle_mode == 1 */
     int max_value_steps;      /* <0: all; else stop after this many value minibatches (CPU-baseline sampling) */
     int max_policy_steps;
+    int capacity;             /* buffer capacity (0: N, a full buffer); minibatches per epoch = capacity / B
+                                 (D13) even when only N = idx < capacity rows are filled — rows wrap mod N */
 } RefUpdateCfg;
 
 typedef struct {

@@ -294,3 +294,47 @@ def test_concurrent_value_policy_loops(lib, oracle, shuffle_mode, monkeypatch):
         err = np.abs(a[k] - b[k])
         assert err.max() <= 2 * 3e-4, (k, err.max())
         assert (err > 1e-6).mean() < 0.01, (k, (err > 1e-6).mean())
+
+
+@pytest.mark.parametrize("cap,filled,B", [(4096, 3000, 512), (4096, 4096, 1000)])
+def test_partial_and_ragged_buffer(lib, oracle, cap, filled, B):
+    """A partly filled buffer (idx = filled < capacity, full = false) and a batch size that does not
+    divide the buffer: GAE over the filled rows only, ⌊capacity / B⌋ minibatches per epoch (D13)
+    whose rows wrap modulo the filled count (trajectory_buffer.cu:168-200).  One value and one policy
+    epoch (8 / 4 steps) from identical state: loss sums and parameter motion track the oracle."""
+    sizes = [17, 256, 256, 6]
+    ppo = make_ppo(lib, oracle, sizes, cap)
+    mu0, ls0 = policy_state(lib, ppo)
+    v0 = nn_params_packed(lib, ppo.contents.V)
+    buf = synthetic_buffer(oracle, sizes, mu0, ls0, filled, seed=17, n_envs=4)
+    pad = cap - filled
+    full_buf = {k: np.concatenate([v, np.full((pad,) + v.shape[1:], 7, v.dtype)]) for k, v in buf.items()}
+    b = ppo.contents.buffer
+    set_host_buffer(lib, b, state=full_buf["state"], next_state=full_buf["next_state"], action=full_buf["action"],
+                    reward=full_buf["reward"], logprob=full_buf["logprob"], term=full_buf["terminated"],
+                    trunc=full_buf["truncated"])
+    b.contents.idx = filled % cap
+    b.contents.full = filled == cap
+    lib.buffer_to_device(b)
+    lib.ppo_reset_stats(ppo)
+    oracle.srand(23)
+    lib.ppo_update(ppo, 0.99, B, 1, 1, 0, 3)
+    st = (C.c_double * 7)()
+    lib.ppo_read_stats(ppo, st, 7)
+    mu1, ls1 = policy_state(lib, ppo)
+    v1 = nn_params_packed(lib, ppo.contents.V)
+    tgt = ppo_ffi.d2h(lib, b.contents.d_adv_target_p, F32, filled)
+    oracle.srand(23)
+    ref = oracle.ppo_update(sizes, RELU(sizes), mu0, ls0, v0, buf, batch_size=B, n_epochs_policy=1,
+                            n_epochs_value=1, shuffle_mode=0, seed=3, capacity=cap)
+    nb = cap // B
+    assert st[1] == ref["n_v"] == nb and st[3] == ref["n_p"] == nb
+    assert_rel_close(tgt, ref["adv_target"], 2e-4, 2e-4 * np.abs(ref["adv_target"]).max(), "adv_target")
+    assert abs(st[0] - ref["sum_v_loss"]) <= 1e-3 * abs(ref["sum_v_loss"])
+    assert abs(st[2] - ref["sum_policy_loss"]) <= 1e-2 * abs(ref["sum_policy_loss"]) + 1e-4
+    for got, start, want, what in ((v1, v0, ref["v"], "V"), (mu1, mu0, ref["mu"], "mu"),
+                                   (ls1, ls0, ref["log_std"], "log_std")):
+        d_got, d_ref = got - start, want - start
+        cos = float(d_got @ d_ref / (np.linalg.norm(d_got) * np.linalg.norm(d_ref) + 1e-30))
+        assert cos > 0.99, f"{what}: cos {cos:.4f}"
+    lib.free_ppo(ppo)
