@@ -108,7 +108,7 @@ double ppo_bench_gemm(int op, int m, int n, int l, int iters, int cfg);
 double ppo_bench_streams(int two, int steps, int B, int out);
 /* bf16 GEMMs: force a tile configuration (−1 = automatic); returns the number of configurations */
 int    ppo_gemm16_tune(int force_cfg);
-/* average device µs of one bf16 launch (op as ppo_bench_gemm; bf16 operands); splitk_target 0 = automatic */
+/* average device µs of one bf16 launch (op as ppo_bench_gemm: 0 forward+ReLU, 1 grad_x, 2 grad_W, 3 forward to fp32 without activation; bf16 operands); splitk_target 0 = automatic */
 double ppo_bench_gemm16(int op, int m, int n, int l, int iters, int cfg, int splitk_target);
 
 /* ---------------- kernel timing ---------------- */

@@ -14,7 +14,8 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import ppo_ffi  # noqa: E402
 
 CFG_NAMES = {0: "128x128/bk16", 1: "128x128/bk32", 2: "128x32/bk16", 3: "32x128/bk16", 4: "64x64/bk16",
-             5: "128x64/bk16", 6: "256x128/bk16", 7: "128x128/bk16/db", 8: "128x64/bk16/db", 9: "64x64/bk32/db"}
+             5: "128x64/bk16", 6: "256x128/bk16", 7: "128x128/bk16/db", 8: "128x64/bk16/db", 9: "64x64/bk32/db",
+             10: "128x32/bk32"}
 
 
 def main():
@@ -42,7 +43,7 @@ def main():
     if args.skinny:
         for (m, n, l) in ((B, 512, 17), (B, 512, 1), (B, 1024, 17)):
             for op in (3, 1, 2):
-                for cfg in range(lib.ppo_gemm_tune(-1, -1)):
+                for cfg in (range(lib.ppo_gemm_tune(-1, -1)) if not args.cfgs else [int(c) for c in args.cfgs.split(",")]):
                     for tgt in ([256, 512, 1024, 2048] if op == 2 else [0]):
                         lib.ppo_gemm_tune(-1, tgt)
                         us = lib.ppo_bench_gemm(op, m, n, l, 20, cfg)
