@@ -45,10 +45,14 @@ def main():
             for op in (3, 1, 2):
                 for cfg in (range(lib.ppo_gemm_tune(-1, -1)) if not args.cfgs else [int(c) for c in args.cfgs.split(",")]):
                     for tgt in ([256, 512, 1024, 2048] if op == 2 else [0]):
-                        lib.ppo_gemm_tune(-1, tgt)
-                        us = lib.ppo_bench_gemm(op, m, n, l, 20, cfg)
-                        print(f"op{op} m={m:6d} n={n:4d} l={l:3d} {CFG_NAMES[cfg]:16s} split_target={tgt:5d} "
-                              f"{us:8.1f} us {(m * n + m * l) * 4 / (us * 1e-6) / 1e9:7.0f} GB/s", flush=True)
+                        for fl in (int(f) for f in args.flags.split(",")):
+                            lib.ppo_gemm_tune(-1, tgt)
+                            lib.ppo_gemm_flags(fl)
+                            us = lib.ppo_bench_gemm(op, m, n, l, 20, cfg)
+                            print(f"op{op} m={m:6d} n={n:4d} l={l:3d} {CFG_NAMES[cfg]:16s} split_target={tgt:5d} "
+                                  f"flags={fl} {us:8.1f} us {(m * n + m * l) * 4 / (us * 1e-6) / 1e9:7.0f} GB/s",
+                                  flush=True)
+        lib.ppo_gemm_flags(0)
         lib.ppo_gemm_tune(-1, 0)
         return
     if args.main:

@@ -45,7 +45,7 @@ def main():
             by[gemm_key(r["Kernel_Name"], r["Grid_Size_X"])].append(d)
     g_tot = sum(sum(v) for v in by.values())
     lines = [f"# rocprofv3 --kernel-trace: GEMM launches by tile config and grid ({args.tag})",
-             f"# all kernels: {total / 1e6:.1f} ms; gemm_f32_kernel: {g_tot / 1e6:.1f} ms "
+             f"# all kernels: {total / 1e6:.1f} ms; GEMM kernels: {g_tot / 1e6:.1f} ms "
              f"({100 * g_tot / max(1, total):.1f} %), {sum(len(v) for v in by.values())} launches, "
              f"avg {g_tot / max(1, sum(len(v) for v in by.values())) / 1e3:.1f} us"]
     for k, v in sorted(by.items(), key=lambda kv: -sum(kv[1])):
@@ -58,7 +58,7 @@ def main():
         def load(fn, ctr):
             vals = []
             for r in csv.DictReader(open(fn)):
-                if r["Counter_Name"] == ctr and "gemm_f32_kernel" in r["Kernel_Name"]:
+                if r["Counter_Name"] == ctr and "gemm_" in r["Kernel_Name"] and "_kernel" in r["Kernel_Name"]:
                     vals.append(float(r["Counter_Value"]))
             return vals
         f, w = load(args.fetch, "FETCH_SIZE"), load(args.write, "WRITE_SIZE")
@@ -66,7 +66,8 @@ def main():
         res = {"launches": n,
                "fetch_size_kb_sum": sum(f), "write_size_kb_sum": sum(w),
                "hbm_bytes_per_launch": (2 * sum(f) + sum(w)) * 1024 / max(1, n),
-               "note": "(2*FETCH_SIZE + WRITE_SIZE)*1024 per gemm_f32_kernel launch, averaged over one "
+               "note": "(2*FETCH_SIZE + WRITE_SIZE)*1024 per GEMM launch (gemm_f32_kernel / gemm_pair_kernel, a pair "
+                       "launch counting once as in bench.py's roofline), averaged over one "
                        "bench.py update (+ synthetic fill); separate --pmc passes for each counter"}
         json.dump(res, open(os.path.join(out, f"{args.tag}_pmc_gemm.json"), "w"), indent=1)
         print(json.dumps(res))
