@@ -443,6 +443,9 @@ void ppo_update(void* vppo, float gamma, int batch_size, int n_epochs_policy, in
     NeuralNetwork* mu = pol->mu;
 
     ppo_gae_device(V, buf, gamma, ppo->lambda);
+    /* D19: an empty buffer (idx = 0, not full) has nothing to train on; the reference would divide
+     * by zero (rand() % 0 in shuffle_buffer, % limit in get_batch) — here the update ends after GAE */
+    if (limit <= 0) return;
 
     if (ppo_update_tiny(ppo, d, B, n_epochs_policy, n_epochs_value, shuffle_mode) == 0) return;
 

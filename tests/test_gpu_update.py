@@ -338,3 +338,37 @@ def test_partial_and_ragged_buffer(lib, oracle, cap, filled, B):
         cos = float(d_got @ d_ref / (np.linalg.norm(d_got) * np.linalg.norm(d_ref) + 1e-30))
         assert cos > 0.99, f"{what}: cos {cos:.4f}"
     lib.free_ppo(ppo)
+
+
+def test_degenerate_updates(lib, oracle):
+    """Edge cases the loops must survive: B larger than the buffer (⌊N/B⌋ = 0 minibatches: GAE only),
+    zero epochs, and an empty buffer (D19: the update ends after GAE, no rand() consumed)."""
+    sizes, N = [17, 256, 256, 6], 1024
+    ppo = make_ppo(lib, oracle, sizes, N)
+    mu0, ls0 = policy_state(lib, ppo)
+    v0 = nn_params_packed(lib, ppo.contents.V)
+    buf = synthetic_buffer(oracle, sizes, mu0, ls0, N, seed=4)
+    load_buffer(lib, ppo, buf)
+    st = (C.c_double * 7)()
+    for B, n_pol, n_val in ((4096, 4, 10), (256, 0, 0)):
+        lib.ppo_reset_stats(ppo)
+        lib.ppo_update(ppo, 0.99, B, n_pol, n_val, 1, 2)
+        lib.ppo_read_stats(ppo, st, 7)
+        assert st[1] == 0 and st[3] == 0
+        np.testing.assert_array_equal(nn_params_packed(lib, ppo.contents.V), v0)
+        np.testing.assert_array_equal(policy_state(lib, ppo)[0], mu0)
+    assert ppo.contents.adam_V.contents.time_step == 0
+    tgt = ppo_ffi.d2h(lib, ppo.contents.buffer.contents.d_adv_target_p, F32, N)
+    assert np.isfinite(tgt).all() and np.abs(tgt).max() > 0          # GAE did run
+    b = ppo.contents.buffer.contents
+    b.idx, b.full = 0, False
+    oracle.srand(8)
+    lib.ppo_reset_stats(ppo)
+    lib.ppo_update(ppo, 0.99, 256, 4, 10, 0, 2)                       # host shuffle: must not consume rand()
+    lib.ppo_synchronize()
+    lib.ppo_read_stats(ppo, st, 7)
+    assert st[1] == 0 and st[3] == 0
+    r = oracle.libc().rand()
+    oracle.srand(8)
+    assert r == oracle.libc().rand()
+    lib.free_ppo(ppo)
