@@ -49,6 +49,9 @@ PEAK_FP32_MFMA_TFLOPS = 157.3          # MI355X_MICROARCH.md: v_mfma_f32_32x32x2
 PEAK_BF16_MFMA_TFLOPS = 2500.0         # MI355X_MICROARCH.md: dense bf16 MFMA (spec, no sparsity)
 DTYPE = {"c5": "bf16"}                 # compute precision per config (default fp32)
 PEAK_HBM_GBPS = 8000.0
+# x3 engine (fp32 mode's default GEMMs): six bf16-MFMA products per fp32 product, so the MFMA bound
+# of the fp32 algorithmic FLOPs is the dense bf16 peak / 6
+PEAK_X3_TFLOPS = PEAK_BF16_MFMA_TFLOPS / 6
 
 
 def algorithmic_flops(S, H, A, N, B, n_v=10, n_p=4):
@@ -178,7 +181,8 @@ def main():
     ppo = LIB.create_ppo(ppo_ffi.c_strings(acts), ppo_ffi.c_ints(sizes), len(sizes), N, 3e-4, 3e-4, 0.95, 0.2, 0.0,
                          1.0, True)
     dtype = DTYPE.get(args.config, "fp32")
-    peak = PEAK_BF16_MFMA_TFLOPS if dtype == "bf16" else PEAK_FP32_MFMA_TFLOPS
+    engine = "bf16" if dtype == "bf16" else ("x3" if LIB.ppo_gemm_f32_engine(-1) == 1 else "exact")
+    peak = {"bf16": PEAK_BF16_MFMA_TFLOPS, "x3": PEAK_X3_TFLOPS, "exact": PEAK_FP32_MFMA_TFLOPS}[engine]
     if LIB.ppo_set_compute_dtype(ppo, 1 if dtype == "bf16" else 0) != 0:
         raise SystemExit("ppo_set_compute_dtype failed")
     LIB.ppo_fill_synthetic(ppo, E, T, args.seed * 1000 + rank, 1.0 / 500)
@@ -305,9 +309,17 @@ def main():
         result["roofline"] = {"bound": "mfma", "achieved": achieved, "peak": peak,
                               "unit": "TFLOP/s", "frac": achieved / peak, "traffic": traffic,
                               "traffic_source": traffic_src,
-                              "kernel": ("gemm_bf16_kernel" if dtype == "bf16" else "gemm_f32_kernel") +
+                              "kernel": {"bf16": "gemm_bf16_kernel",
+                                         "x3": "gemm_bf16_kernel<P=3> (x3 engine: hidden and input layers) + "
+                                               "gemm_f32_kernel (1- and A-wide output layers)",
+                                         "exact": "gemm_f32_kernel"}[engine] +
                                         " (linear-layer launches; Σ 2MNK / Σ HIP-event time over every "
                                         "event_stride-th launch of one serialised update after the timed region)",
+                              "gemm_engine": engine,
+                              "peak_basis": {"bf16": "dense bf16 MFMA spec",
+                                             "x3": "dense bf16 MFMA spec / 6 (six bf16 products per fp32 product)",
+                                             "exact": "fp32 MFMA spec (v_mfma_f32_32x32x2_f32)"}[engine],
+                              "fp32_mfma_peak": PEAK_FP32_MFMA_TFLOPS,
                               "launches": s_launches, "event_stride": args.event_stride,
                               "avg_launch_us": 1000.0 * s_ms / s_launches,
                               "algorithmic_flop_per_launch": s_work / s_launches,

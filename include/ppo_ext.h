@@ -111,6 +111,17 @@ int    ppo_gemm16_tune(int force_cfg);
 /* average device µs of one bf16 launch (op as ppo_bench_gemm: 0 forward+ReLU, 1 grad_x, 2 grad_W, 3 forward to fp32 without activation; bf16 operands); splitk_target 0 = automatic */
 double ppo_bench_gemm16(int op, int m, int n, int l, int iters, int cfg, int splitk_target);
 
+/* fp32 GEMM engine of fp32 mode: 0 = exact fp32 MFMA (v_mfma_f32_32x32x2_f32), 1 = "x3": fp32
+ * operands split exactly into three bf16 planes, the six plane products with pa + pb <= 2 on the
+ * bf16 MFMA, fp32 accumulation (fp32-accurate, 6/16 of the fp32 MFMA cycles).  engine < 0 only
+ * queries; returns the previous engine.  Env PPO_F32_GEMM=exact|x3 sets the initial value. */
+int    ppo_gemm_f32_engine(int engine);
+/* x3 engine tuning: force a tile configuration (−1 = automatic) and the grad_W split-K workgroup
+ * target (0 = automatic, < 0 keeps); returns the number of configurations */
+int    ppo_gemm_x3_tune(int force_cfg, int splitk_target);
+/* average device µs of one x3 launch (fp32 operands; op as ppo_bench_gemm) */
+double ppo_bench_gemm_x3(int op, int m, int n, int l, int iters, int cfg, int splitk_target);
+
 /* ---------------- kernel timing ---------------- */
 enum { PPO_K_GEMM = 0, PPO_K_GAE = 1, PPO_K_ADAM = 2, PPO_K_GATHER = 3, PPO_K_HEAD = 4,
        PPO_K_COMM = 5, PPO_K_OTHER = 6, PPO_K_COUNT = 7 };

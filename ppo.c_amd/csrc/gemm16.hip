@@ -54,14 +54,16 @@ __device__ __forceinline__ unsigned pack2(float lo, float hi) {
     return __builtin_bit_cast(unsigned, p);
 }
 __device__ __forceinline__ float bf_lo(unsigned u) { return __builtin_bit_cast(float, u << 16); }
+__device__ __forceinline__ float bf_hi(unsigned u) { return __builtin_bit_cast(float, u & 0xffff0000u); }
 
 // ---------------------------------------------------------------------------
 // Staging of one operand tile (R rows × BK k) into a bf16 LDS image.  T = float or unsigned short
 // (bf16 bits).  One 16-B global load per slot: 4 fp32 or 8 bf16 elements.
 // ---------------------------------------------------------------------------
-template <int R, int BK, bool MN, typename T>
+template <int R, int BK, bool MN, typename T, int P = 1>
 struct Stage16 {
     static constexpr bool F32 = sizeof(T) == 4;
+    static_assert(P == 1 || (P == 3 && sizeof(T) == 4), "3-plane split needs fp32 operands");
     static constexpr int EPL = F32 ? 4 : 8;                 // elements per 16-B load
     static constexpr int PK = BK + 8;                       // kcont pitch (elements) = 80 B
     static constexpr int PR = ((R / 2) % 64 == 16 || (R / 2) % 64 == 48) ? R : R + 32;   // mncont pitch
@@ -90,7 +92,7 @@ struct Stage16 {
     }
 
     // vec: every contiguous extent and ld are multiples of EPL and the base is 16-B aligned
-    __device__ __forceinline__ void load(const T* __restrict__ P, int ld, int r0, int Rmax, int k0, int kend,
+    __device__ __forceinline__ void load(const T* __restrict__ src_p, int ld, int r0, int Rmax, int k0, int kend,
                                          bool vec, int tid) {
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) {
@@ -103,8 +105,8 @@ struct Stage16 {
                 const int gr = r0 + row, gk = k0 + k;
                 if (vec) {
                     kok[it] = gk < kend;
-                    const T* p = MN ? P + (long)(gk < kend ? gk : kend - 1) * ld + (gr < Rmax ? gr : Rmax - EPL)
-                                    : P + (long)src[it] * ld + (gk < kend ? gk : kend - EPL);
+                    const T* p = MN ? src_p + (long)(gk < kend ? gk : kend - 1) * ld + (gr < Rmax ? gr : Rmax - EPL)
+                                    : src_p + (long)src[it] * ld + (gk < kend ? gk : kend - EPL);
                     x = *reinterpret_cast<const u32x4*>(p);
                 } else {
                     T e[EPL];
@@ -112,13 +114,13 @@ struct Stage16 {
                     for (int q = 0; q < EPL; ++q) e[q] = T(0);
                     if (MN) {
                         if (gk < kend) {
-                            const T* p = P + (long)gk * ld + gr;
+                            const T* p = src_p + (long)gk * ld + gr;
 #pragma unroll
                             for (int q = 0; q < EPL; ++q)
                                 if (gr + q < Rmax) e[q] = p[q];
                         }
                     } else if (gr < Rmax) {
-                        const T* p = P + (long)src[it] * ld + gk;
+                        const T* p = src_p + (long)src[it] * ld + gk;
 #pragma unroll
                         for (int q = 0; q < EPL; ++q)
                             if (gk + q < kend) e[q] = p[q];
@@ -140,7 +142,21 @@ struct Stage16 {
                 unsigned short* d = img + (MN ? k * PR + row : row * PK + k);
                 const u32x4 z = {0u, 0u, 0u, 0u};
                 const u32x4 x = kok[it] ? v[it] : z;
-                if (F32) {
+                if (F32 && P == 3) {
+                    // exact 3-way split x = x0 + x1 + x2 (each bf16, round-to-nearest): x0 holds the
+                    // top 8 significant bits, the residual x − x0 has ≤ 16 and x1 takes 8 of them, so
+                    // x − x0 − x1 has ≤ 8 and is exactly a bf16 (fp32 subtractions are exact here)
+                    const f32x4 f = __builtin_bit_cast(f32x4, x);
+                    const unsigned a0 = pack2(f[0], f[1]), b0 = pack2(f[2], f[3]);
+                    const float r0 = f[0] - bf_lo(a0), r1 = f[1] - bf_hi(a0);
+                    const float r2 = f[2] - bf_lo(b0), r3 = f[3] - bf_hi(b0);
+                    const unsigned a1 = pack2(r0, r1), b1 = pack2(r2, r3);
+                    const unsigned a2 = pack2(r0 - bf_lo(a1), r1 - bf_hi(a1));
+                    const unsigned b2 = pack2(r2 - bf_lo(b1), r3 - bf_hi(b1));
+                    *reinterpret_cast<u32x2*>(d) = u32x2{a0, b0};
+                    *reinterpret_cast<u32x2*>(d + IMG) = u32x2{a1, b1};
+                    *reinterpret_cast<u32x2*>(d + 2 * IMG) = u32x2{a2, b2};
+                } else if (F32) {
                     const f32x4 f = __builtin_bit_cast(f32x4, x);
                     const u32x2 p = {pack2(f[0], f[1]), pack2(f[2], f[3])};
                     *reinterpret_cast<u32x2*>(d) = p;
@@ -151,9 +167,34 @@ struct Stage16 {
         }
     }
 
-    // A-side fused gather: write the staged rows (rows < Rmax, k < kend) as bf16 to dst[row*ldd + k]
-    __device__ __forceinline__ void copy_out(unsigned short* __restrict__ dst, int ldd, int r0, int Rmax, int k0,
+    // A-side fused gather: write the staged rows (rows < Rmax, k < kend) to dst[row*ldd + k] — as bf16,
+    // or (3-plane split mode) as the fp32 values themselves
+    __device__ __forceinline__ void copy_out(void* __restrict__ dstv, int ldd, int r0, int Rmax, int k0,
                                              int kend, int tid) const {
+        if (P == 3) {
+            float* __restrict__ dst = static_cast<float*>(dstv);
+#pragma unroll
+            for (int it = 0; it < ITERS; ++it) {
+                const int idx = tid + it * NT_;
+                if (TOTAL % NT_ == 0 || idx < TOTAL) {
+                    int row, k;
+                    coords(idx, row, k);
+                    const int gr = r0 + row, gk = k0 + k;
+                    if (gr >= Rmax) continue;
+                    float* q = dst + (long)gr * ldd + gk;
+                    const f32x4 f = __builtin_bit_cast(f32x4, v[it]);
+                    if (gk + 3 < kend && (ldd & 3) == 0) {
+                        *reinterpret_cast<f32x4*>(q) = f;
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            if (gk + e < kend) q[e] = f[e];
+                    }
+                }
+            }
+            return;
+        }
+        unsigned short* __restrict__ dst = static_cast<unsigned short*>(dstv);
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) {
             const int idx = tid + it * NT_;
@@ -202,12 +243,17 @@ struct Stage16 {
         return __builtin_bit_cast(bf16x8, f);
     }
 
-    // Σ over this tile's k of image row `row` (fp32), k ∈ [k_lo, k_lo + n)
+    // Σ over this tile's k of image row `row` (fp32), k ∈ [k_lo, k_lo + n); in 3-plane mode each
+    // element is recombined exactly (x0 + x1 + x2) before it is added
     __device__ __forceinline__ static float rowsum(const unsigned short* img, int row, int k_lo, int n) {
         float t = 0.f;
         for (int kk = 0; kk < n; ++kk) {
-            const unsigned short b = MN ? img[(k_lo + kk) * PR + row] : img[row * PK + k_lo + kk];
-            t += __builtin_bit_cast(float, (unsigned)b << 16);
+            const int o = MN ? (k_lo + kk) * PR + row : row * PK + k_lo + kk;
+            float e = __builtin_bit_cast(float, (unsigned)img[o] << 16);
+            if (P == 3)
+                e += __builtin_bit_cast(float, (unsigned)img[o + IMG] << 16) +
+                     __builtin_bit_cast(float, (unsigned)img[o + 2 * IMG] << 16);
+            t += e;
         }
         return t;
     }
@@ -217,18 +263,18 @@ template <typename T> struct Bits;
 template <> struct Bits<float> { static constexpr int code = 0; };
 template <> struct Bits<unsigned short> { static constexpr int code = 1; };
 
-template <int OP, int BM, int BN, int WARPS_M, int BK, typename TA, typename TB, typename TC>
+template <int OP, int BM, int BN, int WARPS_M, int BK, typename TA, typename TB, typename TC, int P>
 __global__ __launch_bounds__(NT_, 2) void gemm_bf16_kernel(Args a) {
     constexpr int WARPS_N = 4 / WARPS_M;
     constexpr int WM = BM / WARPS_M, WN = BN / WARPS_N;
     constexpr int TM = WM / 32, TN = WN / 32;
     constexpr bool A_MN = OP == OP_TN, B_MN = OP != OP_NT;
-    using SA = Stage16<BM, BK, A_MN, TA>;
-    using SB = Stage16<BN, BK, B_MN, TB>;
+    using SA = Stage16<BM, BK, A_MN, TA, P>;
+    using SB = Stage16<BN, BK, B_MN, TB, P>;
     static_assert(TM >= 1 && TN >= 1, "wave tile must be a multiple of 32x32");
     static_assert(!(OP == OP_TN) || sizeof(TC) == 4, "grad_W accumulates in fp32");
 
-    __shared__ __attribute__((aligned(16))) unsigned short lds[SA::IMG + SB::IMG];
+    __shared__ __attribute__((aligned(16))) unsigned short lds[(SA::IMG + SB::IMG) * P];
 
     const int nwg = gridDim.x, b = blockIdx.x;
     const int xcd = b & 7, qq = nwg >> 3, rr = nwg & 7;
@@ -274,26 +320,36 @@ __global__ __launch_bounds__(NT_, 2) void gemm_bf16_kernel(Args a) {
 
     if (kbeg < kend) load(kbeg);
     for (int k0 = kbeg; k0 < kend; k0 += BK) {
-        if (do_copy) sa.copy_out(static_cast<unsigned short*>(a.acopy), a.K, m0, a.M, k0, kend, tid);
+        if (do_copy) sa.copy_out(a.acopy, a.K, m0, a.M, k0, kend, tid);
         sa.store(lds, tid);
-        sb.store(lds + SA::IMG, tid);
+        sb.store(lds + P * SA::IMG, tid);
         __syncthreads();
         if (k0 + BK < kend) load(k0 + BK);            // in flight during this tile's MFMAs
         const unsigned short* As = lds;
-        const unsigned short* Bs = lds + SA::IMG;
+        const unsigned short* Bs = lds + P * SA::IMG;
         if (do_bsum) bsum += SA::rowsum(As, tid / TPR, (tid % TPR) * KPT, KPT);
 #pragma unroll
         for (int ks = 0; ks < BK / 16; ++ks) {
-            bf16x8 fa[TM], fb[TN];
+            bf16x8 fa[P][TM], fb[P][TN];
 #pragma unroll
-            for (int i = 0; i < TM; ++i) fa[i] = SA::frag(As, wm * WM + i * 32 + r, ks, lane);
+            for (int p = 0; p < P; ++p) {
 #pragma unroll
-            for (int j = 0; j < TN; ++j) fb[j] = SB::frag(Bs, wn * WN + j * 32 + r, ks, lane);
+                for (int i = 0; i < TM; ++i) fa[p][i] = SA::frag(As + p * SA::IMG, wm * WM + i * 32 + r, ks, lane);
 #pragma unroll
-            for (int i = 0; i < TM; ++i)
+                for (int j = 0; j < TN; ++j) fb[p][j] = SB::frag(Bs + p * SB::IMG, wn * WN + j * 32 + r, ks, lane);
+            }
+            // 3-plane mode: the six products whose planes sum to ≤ 2 (smallest first); the three
+            // dropped ones are below 2^-24 relative to the product
 #pragma unroll
-                for (int j = 0; j < TN; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+            for (int q = 0; q < (P == 3 ? 6 : 1); ++q) {
+                constexpr int pa_[6] = {2, 0, 1, 1, 0, 0}, pb_[6] = {0, 2, 1, 0, 1, 0};
+                const int pa = P == 3 ? pa_[q] : 0, pb = P == 3 ? pb_[q] : 0;
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[pa][i], fb[pb][j], acc[i][j], 0, 0, 0);
+            }
         }
         __syncthreads();
     }
@@ -377,14 +433,14 @@ __global__ __launch_bounds__(NT_, 2) void gemm_bf16_kernel(Args a) {
 using f32 = float;
 using b16 = unsigned short;
 
-template <int OP, int BM, int BN, int WM_, int BK, typename TA, typename TB, typename TC>
+template <int OP, int BM, int BN, int WM_, int BK, typename TA, typename TB, typename TC, int P = 1>
 void launch(Args a) {
     a.tiles_m = ppo_divup(a.M, BM);
     a.tiles_n = ppo_divup(a.N, BN);
     if (a.splits < 1) a.splits = 1;
     const long grid = (long)a.tiles_m * a.tiles_n * a.splits;
     PPO_REQUIRE(grid > 0 && grid < (1L << 31), "gemm16: grid out of range");
-    hipLaunchKernelGGL((gemm_bf16_kernel<OP, BM, BN, WM_, BK, TA, TB, TC>), dim3((unsigned)grid), dim3(NT_), 0,
+    hipLaunchKernelGGL((gemm_bf16_kernel<OP, BM, BN, WM_, BK, TA, TB, TC, P>), dim3((unsigned)grid), dim3(NT_), 0,
                        ppo::stream(), a);
     PPO_LAUNCH_CHECK();
 }
@@ -423,6 +479,37 @@ int pick16(int M, int N, int op = OP_NT) {
     if (M <= 64 || N <= 64) return 3;
     if (N % 256 == 0 && M >= 256) return 6;
     return op == OP_NN ? 4 : 0;
+}
+
+
+// ---------------------------------------------------------------------------
+// fp32 GEMMs on the bf16 MFMA ("x3" engine): fp32 operands are split exactly into three bf16
+// planes on the way into LDS and the six plane products with pa + pb ≤ 2 are accumulated in fp32.
+// The dropped products (1,2), (2,1), (2,2) are < 2^-25 of |a·b|, so each product is carried to
+// about fp32 rounding — same accuracy class as v_mfma_f32_32x32x2_f32 — at 6/16 of its MFMA cycles.
+// LDS: three bf16 images per operand (128x128/BK32: 60 KiB, 2 workgroups per CU).
+// tile configurations: 0 = 128x128, 1 = 128x32 (skinny N), 2 = 32x128 (skinny M), 3 = 64x64, all BK 32
+// ---------------------------------------------------------------------------
+int g_force3 = -1;
+int g_split3 = 0;
+
+template <int OP>
+void launch_cfg3(int c, const Args& a) {
+    switch (c) {
+        case 1: launch<OP, 128, 32, 4, 32, f32, f32, f32, 3>(a); break;
+        case 2: launch<OP, 32, 128, 1, 32, f32, f32, f32, 3>(a); break;
+        case 3: launch<OP, 64, 64, 2, 32, f32, f32, f32, 3>(a); break;
+        default: launch<OP, 128, 128, 2, 32, f32, f32, f32, 3>(a); break;
+    }
+}
+constexpr Cfg kCfgs3[] = {{128, 128, 32}, {128, 32, 32}, {32, 128, 32}, {64, 64, 32}};
+
+int pick3(int M, int N) {
+    if (g_force3 >= 0) return g_force3;
+    if (N <= 32 && M > 32) return 1;
+    if (M <= 32 && N > 32) return 2;
+    if (M <= 64 || N <= 64) return 3;
+    return 0;
 }
 
 inline bool al16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
@@ -503,6 +590,114 @@ void phip_linear16_bwd_w(float* gW, float* gb, const void* g, int tg, const void
     else if (tg == 0) launch_cfg<OP_TN, f32, b16, f32>(c, a);
     else if (tx == 0) launch_cfg<OP_TN, b16, f32, f32>(c, a);
     else launch_cfg<OP_TN, b16, b16, f32>(c, a);
+}
+
+// fp32 storage everywhere; fp32-accurate products on the bf16 MFMA (x3 engine, above)
+void phip_linear_x3_fwd(float* y, const float* x, const int* ridx, float* xcopy, const float* W, const float* b,
+                        int m, int n, int l, int relu, unsigned* bits) {
+    if (m <= 0 || l <= 0) return;
+    PPO_REQUIRE(y && x && W && n > 0, "phip_linear_x3_fwd: null operand");
+    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l);
+    Args a{};
+    a.A = x; a.lda = n; a.B = W; a.ldb = n; a.C = y; a.ldc = l;
+    a.M = m; a.N = l; a.K = n; a.kchunk = n; a.splits = 1;
+    a.bias = b; a.relu = relu; a.ridx = ridx; a.acopy = ridx ? xcopy : nullptr;
+    a.bits_out = relu ? bits : nullptr; a.wpr = ppo_divup(l, 32);
+    a.vec = n % 4 == 0 && al16(x) && al16(W);
+    launch_cfg3<OP_NT>(pick3(m, l), a);
+}
+
+void phip_linear_x3_bwd_x(float* gx, const float* g, const float* W, const unsigned* bits, int m, int n, int l) {
+    if (m <= 0 || n <= 0) return;
+    PPO_REQUIRE(gx && g && W && l > 0, "phip_linear_x3_bwd_x: null operand");
+    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l);
+    Args a{};
+    a.A = g; a.lda = l; a.B = W; a.ldb = n; a.C = gx; a.ldc = n;
+    a.M = m; a.N = n; a.K = l; a.kchunk = l; a.splits = 1;
+    a.bits_in = bits; a.wpr = ppo_divup(n, 32);
+    a.vec = l % 4 == 0 && n % 4 == 0 && al16(g) && al16(W);
+    launch_cfg3<OP_NN>(pick3(m, n), a);
+}
+
+void phip_linear_x3_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, int n, int l, int zeroed) {
+    if (l <= 0 || n <= 0) return;
+    PPO_REQUIRE(gW && g && x, "phip_linear_x3_bwd_w: null operand");
+    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l);
+    if (m <= 0) {
+        if (!zeroed) {
+            phip_memset(gW, 0, sizeof(float) * (size_t)l * n);
+            if (gb) phip_memset(gb, 0, sizeof(float) * (size_t)l);
+        }
+        return;
+    }
+    const int c = pick3(l, n);
+    const int BK = kCfgs3[c].bk;
+    const long tiles = (long)ppo_divup(l, kCfgs3[c].bm) * ppo_divup(n, kCfgs3[c].bn);
+    const int target = g_split3 > 0 ? g_split3 : 512;
+    int splits = (int)((target + tiles - 1) / tiles);
+    const int max_splits = m / (4 * BK) > 0 ? m / (4 * BK) : 1;          // ≥ 4 k-tiles per split
+    if (splits > max_splits) splits = max_splits;
+    if (splits < 1) splits = 1;
+    int kchunk = ppo_divup(ppo_divup(m, splits), BK) * BK;
+    splits = ppo_divup(m, kchunk);
+    Args a{};
+    a.A = g; a.lda = l; a.B = x; a.ldb = n; a.C = gW; a.ldc = n;
+    a.M = l; a.N = n; a.K = m; a.kchunk = kchunk; a.splits = splits;
+    a.gbias = gb;
+    a.vec = l % 4 == 0 && n % 4 == 0 && al16(g) && al16(x);
+    if (splits > 1 && !zeroed) {
+        phip_memset(gW, 0, sizeof(float) * (size_t)l * n);
+        if (gb) phip_memset(gb, 0, sizeof(float) * (size_t)l);
+    }
+    launch_cfg3<OP_TN>(c, a);
+}
+
+int ppo_gemm_x3_tune(int force_cfg, int splitk_target) {
+    g_force3 = force_cfg;
+    if (splitk_target >= 0) g_split3 = splitk_target;
+    return (int)(sizeof(kCfgs3) / sizeof(kCfgs3[0]));
+}
+
+// average device µs of one x3 launch (fp32 operands; op as ppo_bench_gemm)
+double ppo_bench_gemm_x3(int op, int m, int n, int l, int iters, int cfg, int splitk_target) {
+    ppo::ensure_device();
+    const size_t sx = (size_t)m * n, sw = (size_t)l * n, sy = (size_t)m * l;
+    float* x = (float*)phip_malloc(4 * sx);
+    float* W = (float*)phip_malloc(4 * sw);
+    float* y = (float*)phip_malloc(4 * (sy > sx ? sy : sx));
+    float* b = (float*)phip_malloc(4 * (size_t)(l > n ? l : n));
+    float* gw = (float*)phip_malloc(4 * sw);
+    unsigned* bits = (unsigned*)phip_malloc(4 * (size_t)m * ppo_divup(l > n ? l : n, 32));
+    phip_fill_uniform(x, (long)sx, 1, -1.f, 1.f);
+    phip_fill_uniform(W, (long)sw, 2, -0.1f, 0.1f);
+    phip_fill_uniform(y, (long)(sy > sx ? sy : sx), 3, -1.f, 1.f);
+    phip_fill_uniform(b, (long)(l > n ? l : n), 4, -0.1f, 0.1f);
+    phip_memset(bits, 0xff, 4 * (size_t)m * ppo_divup(l > n ? l : n, 32));
+    const int saved = g_force3, saved_split = g_split3;
+    g_force3 = cfg;
+    g_split3 = splitk_target;
+    auto run = [&]() {
+        if (op == 0) phip_linear_x3_fwd(y, x, nullptr, nullptr, W, b, m, n, l, 1, bits);
+        else if (op == 3) phip_linear_x3_fwd(y, x, nullptr, nullptr, W, b, m, n, l, 0, nullptr);
+        else if (op == 1) phip_linear_x3_bwd_x(x, y, W, bits, m, n, l);
+        else phip_linear_x3_bwd_w(gw, b, y, x, m, n, l, 0);
+    };
+    for (int i = 0; i < 3; ++i) run();
+    hipEvent_t e0, e1;
+    PPO_CHECK(hipEventCreate(&e0));
+    PPO_CHECK(hipEventCreate(&e1));
+    PPO_CHECK(hipEventRecord(e0, ppo::stream()));
+    for (int i = 0; i < iters; ++i) run();
+    PPO_CHECK(hipEventRecord(e1, ppo::stream()));
+    PPO_CHECK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    PPO_CHECK(hipEventElapsedTime(&ms, e0, e1));
+    PPO_CHECK(hipEventDestroy(e0));
+    PPO_CHECK(hipEventDestroy(e1));
+    g_force3 = saved;
+    g_split3 = saved_split;
+    phip_free(x); phip_free(W); phip_free(y); phip_free(b); phip_free(gw); phip_free(bits);
+    return 1000.0 * ms / (iters > 0 ? iters : 1);
 }
 
 int ppo_gemm16_tune(int force_cfg) {

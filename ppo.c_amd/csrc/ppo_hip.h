@@ -69,6 +69,13 @@ void phip_linear16_bwd_x(void* gx, int tgx, const void* g, int tg, const void* W
 /* gW[l,n] (+)= gᵀ·x, gb (+)= Σ g in fp32 (zeroed != 0: outputs already zero) */
 void phip_linear16_bwd_w(float* gW, float* gb, const void* g, int tg, const void* x, int tx, int m, int n, int l,
                          int zeroed);
+/* fp32 storage, fp32-accurate products on the bf16 MFMA (exact 3-plane bf16 split, 6 products):
+ * the "x3" engine of fp32 mode.  Forward with optional fused gather (ridx; xcopy = fp32 copy of the
+ * gathered rows) + bias/ReLU/ReLU' bits; grad_x with the bit mask; grad_W (+gb) split-K. */
+void phip_linear_x3_fwd(float* y, const float* x, const int* ridx, float* xcopy, const float* W, const float* b,
+                        int m, int n, int l, int relu, unsigned* bits);
+void phip_linear_x3_bwd_x(float* gx, const float* g, const float* W, const unsigned* bits, int m, int n, int l);
+void phip_linear_x3_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, int n, int l, int zeroed);
 /* dst[i, :] = bf16(src[rows[i], :]) for i < m (S % 4 == 0): layer 0's gather in bf16 mode */
 void phip_gather_rows_bf16(unsigned short* dst, const float* src, const int* rows, int m, int S);
 void phip_f32_to_bf16(unsigned short* dst, const float* src, long count);

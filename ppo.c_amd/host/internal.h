@@ -30,6 +30,13 @@ float* stage_up(int slot, const float* host, size_t count);   /* h2d into slot, 
 
 static inline long align4(long n) { return (n + 3) & ~3L; }
 
+/* fp32 GEMM engine used when PPO_F32_GEMM is unset (ppo_ext.h ppo_gemm_f32_engine): 1 = x3 */
+#define PPO_F32_ENGINE_DEFAULT 1
+/* linear-layer products of the reference API through the engine choice (neural_network.c) */
+void lin_fwd(float* y, const float* x, const float* W, const float* b, int m, int n, int l);
+void lin_bwd_x(float* gx, const float* g, const float* W, int m, int n, int l);
+void lin_bwd_w(float* gW, const float* g, const float* x, int m, int n, int l);
+
 /* neural_network.c internals used by policy.c / ppo.c */
 NeuralNetwork* nn_create_ex(int* layer_sizes, char** activation_functions, int num_layers, long extra_floats,
                             int init_from_rand);

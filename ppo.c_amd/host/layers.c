@@ -10,15 +10,15 @@
 /* ---------------- mat_mul.h ---------------- */
 void mat_mul_cuda(ppo_gpu_handle_t handle, float* out, float* x, float* weight, float* bias, int m, int n, int l) {
     (void)handle;
-    phip_linear_fwd(out, x, weight, bias, m, n, l, 0);
+    lin_fwd(out, x, weight, bias, m, n, l);
 }
 
 /* mat_mul.cu:165-217: both products overwrite (cuBLAS β = 0) */
 void mat_mul_backwards_cuda(ppo_gpu_handle_t handle, float* grad_x, float* grad_weight, float* grad_in, float* x,
                             float* weight, int m, int n, int l) {
     (void)handle;
-    if (grad_x) phip_linear_bwd_x(grad_x, grad_in, weight, NULL, m, n, l);
-    phip_linear_bwd_w(grad_weight, NULL, grad_in, x, m, n, l);
+    if (grad_x) lin_bwd_x(grad_x, grad_in, weight, m, n, l);
+    lin_bwd_w(grad_weight, grad_in, x, m, n, l);
 }
 
 void mat_mul(float* out, float* x, float* weight, float* bias, int m, int n, int l) {
@@ -26,7 +26,7 @@ void mat_mul(float* out, float* x, float* weight, float* bias, int m, int n, int
     float* dw = stage_up(ST_B, weight, (size_t)l * n);
     float* db = stage_up(ST_C, bias, (size_t)l);
     float* dy = (float*)stage(ST_D, sizeof(float) * (size_t)m * l);
-    phip_linear_fwd(dy, dx, dw, db, m, n, l, 0);
+    lin_fwd(dy, dx, dw, db, m, n, l);
     phip_d2h(out, dy, sizeof(float) * (size_t)m * l);
 }
 
@@ -39,12 +39,12 @@ void mat_mul_backwards(float* grad_x, float* grad_weight, float* grad_in, float*
     float* tmp = (float*)stage(ST_D, sizeof(float) * ((size_t)m * n > (size_t)l * n ? (size_t)m * n : (size_t)l * n));
     if (grad_x) {
         float* acc = stage_up(ST_E, grad_x, (size_t)m * n);
-        phip_linear_bwd_x(tmp, dg, dw, NULL, m, n, l);
+        lin_bwd_x(tmp, dg, dw, m, n, l);
         phip_axpy(acc, tmp, (long)m * n);
         phip_d2h(grad_x, acc, sizeof(float) * (size_t)m * n);
     }
     float* accw = stage_up(ST_F, grad_weight, (size_t)l * n);
-    phip_linear_bwd_w(tmp, NULL, dg, dx, m, n, l);
+    lin_bwd_w(tmp, dg, dx, m, n, l);
     phip_axpy(accw, tmp, (long)l * n);
     phip_d2h(grad_weight, accw, sizeof(float) * (size_t)l * n);
 }

@@ -13,6 +13,8 @@
 #include "internal.h"
 
 #include <math.h>
+#include <stdlib.h>
+#include <string.h>
 
 int nn_is_relu(const NeuralNetwork* nn, int layer) {
     const ActivationFunction* a = nn->layers[layer].d_activation_function;
@@ -145,6 +147,40 @@ static void nn_forward_dev_bf16(NeuralNetwork* nn, const float* d_x, const int* 
     }
 }
 
+/* fp32 GEMM engine (ppo_ext.h ppo_gemm_f32_engine): -1 = not yet read from PPO_F32_GEMM */
+static int g_f32_engine = -1;
+
+int ppo_gemm_f32_engine(int engine) {
+    if (g_f32_engine < 0) {
+        const char* e = getenv("PPO_F32_GEMM");
+        g_f32_engine = (e && strcmp(e, "exact") == 0) ? 0 : (e && strcmp(e, "x3") == 0) ? 1 : PPO_F32_ENGINE_DEFAULT;
+    }
+    const int old = g_f32_engine;
+    if (engine == 0 || engine == 1) g_f32_engine = engine;
+    return old;
+}
+
+/* the x3 engine serves the minibatch- and buffer-sized products; small-m forwards (rollout steps
+ * over E environments) keep the exact kernel family's small-M path */
+static int use_x3(int m) { return m > 1024 && ppo_gemm_f32_engine(-1) == 1; }
+/* per layer: the 1- and A-wide output layers are latency-bound skinny products where the exact
+ * kernels (and their paired backward launch) measure faster (profiles/r01_x3_sweep.txt) */
+static int use_x3_layer(int m, int n, int l) { return use_x3(m) && n > 32 && l > 32; }
+
+/* the reference-API products (mat_mul*_cuda, layers.c) through the same engine choice */
+void lin_fwd(float* y, const float* x, const float* W, const float* b, int m, int n, int l) {
+    if (use_x3(m)) phip_linear_x3_fwd(y, x, NULL, NULL, W, b, m, n, l, 0, NULL);
+    else phip_linear_fwd(y, x, W, b, m, n, l, 0);
+}
+void lin_bwd_x(float* gx, const float* g, const float* W, int m, int n, int l) {
+    if (use_x3(m)) phip_linear_x3_bwd_x(gx, g, W, NULL, m, n, l);
+    else phip_linear_bwd_x(gx, g, W, NULL, m, n, l);
+}
+void lin_bwd_w(float* gW, const float* g, const float* x, int m, int n, int l) {
+    if (use_x3(m)) phip_linear_x3_bwd_w(gW, NULL, g, x, m, n, l, 0);
+    else phip_linear_bwd_w(gW, NULL, g, x, m, n, l);
+}
+
 void nn_forward_dev_rows(NeuralNetwork* nn, const float* d_x, const int* d_rows, float* d_xcopy, int m) {
     nn_ensure_act(nn, m);
     const int L = nn->num_layers - 1;
@@ -161,7 +197,11 @@ void nn_forward_dev_rows(NeuralNetwork* nn, const float* d_x, const int* d_rows,
     for (int i = 0; i < L; i++) {
         Layer* ly = &nn->layers[i];
         float* out = nn->layers[i + 1].d_input;
-        if (i == 0 && d_rows)
+        if (use_x3_layer(m, ly->input_size, ly->output_size))
+            phip_linear_x3_fwd(out, in, i == 0 ? d_rows : NULL, i == 0 ? d_xcopy : NULL, ly->d_weights,
+                               ly->d_biases, m, ly->input_size, ly->output_size, nn_is_relu(nn, i),
+                               act_bits(nn, i + 1));
+        else if (i == 0 && d_rows)
             phip_linear_fwd_gather(out, in, d_rows, d_xcopy, ly->d_weights, ly->d_biases, m, ly->input_size,
                                    ly->output_size, nn_is_relu(nn, i), act_bits(nn, i + 1));
         else
@@ -219,7 +259,14 @@ void nn_backward_dev(NeuralNetwork* nn, const float* d_grad_out, int m, int want
         const int want_gx = i > 0 || want_grad_x0;
         const int relu_in = i > 0 && nn_is_relu(nn, i - 1);
         const unsigned* bits = relu_in && nn->bits_m == m ? act_bits(nn, i) : NULL;   /* this forward's bits */
-        if (want_gx && (!relu_in || bits)) {
+        if (use_x3_layer(m, ly->input_size, ly->output_size)) {
+            phip_linear_x3_bwd_w(ly->d_grad_weights, ly->d_grad_biases, g, x, m, ly->input_size, ly->output_size, 1);
+            if (want_gx && (!relu_in || bits))
+                phip_linear_x3_bwd_x(ly->d_grad_x, g, ly->d_weights, bits, m, ly->input_size, ly->output_size);
+            else if (want_gx)
+                phip_linear_bwd_x_bits(ly->d_grad_x, g, ly->d_weights, ly->d_input, NULL, m, ly->input_size,
+                                       ly->output_size);
+        } else if (want_gx && (!relu_in || bits)) {
             phip_linear_bwd_pair(ly->d_grad_weights, ly->d_grad_biases, ly->d_grad_x, g, x, ly->d_weights, bits, m,
                                  ly->input_size, ly->output_size, 1);
         } else {

@@ -66,7 +66,7 @@ def main():
         res = {"launches": n,
                "fetch_size_kb_sum": sum(f), "write_size_kb_sum": sum(w),
                "hbm_bytes_per_launch": (2 * sum(f) + sum(w)) * 1024 / max(1, n),
-               "note": "(2*FETCH_SIZE + WRITE_SIZE)*1024 per GEMM launch (gemm_f32_kernel / gemm_pair_kernel, a pair "
+               "note": "(2*FETCH_SIZE + WRITE_SIZE)*1024 per GEMM launch (gemm_f32_kernel / gemm_pair_kernel / gemm_bf16_kernel, a pair "
                        "launch counting once as in bench.py's roofline), averaged over one "
                        "bench.py update (+ synthetic fill); separate --pmc passes for each counter"}
         json.dump(res, open(os.path.join(out, f"{args.tag}_pmc_gemm.json"), "w"), indent=1)

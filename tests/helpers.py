@@ -28,6 +28,60 @@ def assert_gemm_close(got, ref, K, what=""):
     assert err <= tol, f"{what}: max |err| {err:.3g} > tol {tol:.3g} (K={K})"
 
 
+def gpu_relu_masks(lib, nn_ptr, x_rows):
+    """The ReLU′ masks libppo's last forward used (NeuralNetwork.d_act_bits: one [act_cap_m, ⌈w/32⌉]
+    u32 block per layer input, bit c%32 of word c/32), for every hidden layer input, re-ordered to
+    the rows of `x_rows`: the forward's rows are matched to x_rows through the layer-0 input copy
+    (nn.d_x0, the gathered minibatch)."""
+    nn = nn_ptr.contents
+    L = nn.num_layers - 1
+    sizes = [nn.layers[i].input_size for i in range(L)] + [nn.output_size]
+    m, cap = nn.bits_m, nn.act_cap_m
+    if m != x_rows.shape[0] or not nn.d_x0 or not nn.d_act_bits:
+        return None          # the last forward was not this one (e.g. the single-workgroup path)
+    x0 = ppo_ffi.d2h(lib, nn.d_x0, F32, m * sizes[0]).reshape(m, sizes[0])
+    where = {r.tobytes(): i for i, r in enumerate(np.ascontiguousarray(x_rows, F32))}
+    order = np.array([where[r.tobytes()] for r in x0])      # forward row j = reference row order[j]
+    total = sum(cap * ((s + 31) // 32) for s in sizes)
+    words = ppo_ffi.d2h(lib, nn.d_act_bits, np.uint32, total)
+    masks, off = [], 0
+    for i, s in enumerate(sizes):
+        wpr = (s + 31) // 32
+        if 0 < i < L:
+            blk = words[off:off + m * wpr].reshape(m, wpr)
+            bits = (blk[:, np.arange(s) // 32] >> (np.arange(s) % 32).astype(np.uint32)) & 1
+            mk = np.empty((m, s), bool)
+            mk[order] = bits.astype(bool)
+            masks.append(mk)
+        off += cap * wpr
+    return masks
+
+
+def oracle_grads_with_masks(oracle, sizes, relu, params, x, gout, masks, what=""):
+    """The oracle's MLP gradients (reference neural_network.cu:192-231) evaluated with libppo's ReLU′
+    masks.  Where the two forwards disagree on a mask bit, the pre-activation lies within fp32
+    rounding of 0 (asserted: |y| ≤ 1e-5·max|y|, at most 16 such units per layer), both sides are
+    valid fp32 evaluations, and the GPU's choice is used so the gradients compare strictly."""
+    m = x.shape[0]
+    acts = oracle.mlp_forward(sizes, relu, params, x).copy()
+    if masks is None:
+        return oracle.mlp_backward(sizes, relu, params, x, acts, gout), 0
+    outs = oracle.mlp_layer_outputs(sizes, acts, m)
+    flips = 0
+    for i, mk in enumerate(masks):                    # hidden layer i+1's input = output of layer i
+        y = outs[i]
+        diff = mk != (y > 0)
+        n = int(diff.sum())
+        flips += n
+        if n:
+            worst = float(np.abs(y[diff]).max())
+            assert worst <= 1e-5 * float(np.abs(y).max()), f"{what}: mask disagreement at |y| = {worst:.3g}"
+            assert n <= 16, f"{what}: {n} mask disagreements in layer {i}"
+        y[mk & ~(y > 0)] = np.float32(1e-30)          # GPU kept the unit: positive, negligible value
+        y[~mk] = 0
+    return oracle.mlp_backward(sizes, relu, params, x, acts, gout), flips
+
+
 def assert_rel_close(got, ref, rtol, atol, what=""):
     got = np.asarray(got, np.float64)
     ref = np.asarray(ref, np.float64)

@@ -22,8 +22,11 @@ SHAPES = [(4096, 376, 512), (1000, 512, 256), (257, 64, 36), (513, 130, 67), (30
 
 @pytest.fixture(scope="module")
 def ncfg(lib):
+    """the exact fp32-MFMA engine's configurations (the x3 engine has its own test: test_gpu_x3.py)"""
     n = lib.ppo_gemm_tune(-1, 0)
+    old = lib.ppo_gemm_f32_engine(0)
     yield n
+    lib.ppo_gemm_f32_engine(old)
     lib.ppo_gemm_tune(-1, 0)
 
 
@@ -100,7 +103,7 @@ def _mlp_grads_f64(sizes, params, x, gout):
 
 
 @pytest.mark.parametrize("sizes,m", [([376, 512, 512, 512, 17], 16384), ([64, 1024, 1024, 8], 8192)])
-def test_mlp_paired_backward(lib, sizes, m):
+def test_mlp_paired_backward(lib, ncfg, sizes, m):
     """grad_W + grad_x of a layer as one launch (gemm_pair_kernel: hidden layers, and the 17-wide
     output layer) vs two launches (flag 4):
     grad_x identical bit for bit (same tiles, same k order), grad_W up to the split-K atomics'
