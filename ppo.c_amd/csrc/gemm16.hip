@@ -23,6 +23,8 @@
 //    k-tile behind this tile's MFMAs, XCD-aware block remap — as in gemm.hip.
 #include "dev.h"
 
+#include <algorithm>
+
 namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -45,6 +47,7 @@ struct Args {
     float* gbias;
     int kchunk, splits, tiles_m, tiles_n;
     int vec;
+    long psA, psB, psC;                   // x3 engine: plane strides (elements) of pre-split operands / output
 };
 
 // fp32 → bf16, round to nearest even (NaN stays NaN: v_cvt_pk_bf16_f32)
@@ -56,6 +59,17 @@ __device__ __forceinline__ unsigned pack2(float lo, float hi) {
 __device__ __forceinline__ float bf_lo(unsigned u) { return __builtin_bit_cast(float, u << 16); }
 __device__ __forceinline__ float bf_hi(unsigned u) { return __builtin_bit_cast(float, u & 0xffff0000u); }
 
+// x3 output: v = h0 + h1 + h2 exactly (each bf16, round-to-nearest), plane q at dst + q·ps
+__device__ __forceinline__ void store_planes(unsigned short* dst, long ps, float v) {
+    const unsigned a = pack2(v, 0.f);
+    const float r = v - bf_lo(a);
+    const unsigned b = pack2(r, 0.f);
+    const unsigned c = pack2(r - bf_lo(b), 0.f);
+    dst[0] = (unsigned short)a;
+    dst[ps] = (unsigned short)b;
+    dst[2 * ps] = (unsigned short)c;
+}
+
 // ---------------------------------------------------------------------------
 // Staging of one operand tile (R rows × BK k) into a bf16 LDS image.  T = float or unsigned short
 // (bf16 bits).  One 16-B global load per slot: 4 fp32 or 8 bf16 elements.
@@ -63,7 +77,7 @@ __device__ __forceinline__ float bf_hi(unsigned u) { return __builtin_bit_cast(f
 template <int R, int BK, bool MN, typename T, int P = 1>
 struct Stage16 {
     static constexpr bool F32 = sizeof(T) == 4;
-    static_assert(P == 1 || (P == 3 && sizeof(T) == 4), "3-plane split needs fp32 operands");
+    static_assert(P == 1 || P == 3, "one bf16 image or three planes");
     static constexpr int EPL = F32 ? 4 : 8;                 // elements per 16-B load
     static constexpr int PK = BK + 8;                       // kcont pitch (elements) = 80 B
     static constexpr int PR = ((R / 2) % 64 == 16 || (R / 2) % 64 == 48) ? R : R + 32;   // mncont pitch
@@ -72,7 +86,9 @@ struct Stage16 {
     static constexpr int TOTAL = MN ? BK * PER_ROW : R * PER_ROW;
     static constexpr int ITERS = (TOTAL + NT_ - 1) / NT_;
     static_assert(R % EPL == 0 && R >= 32, "tile rows");
-    u32x4 v[ITERS];
+    static constexpr bool PL = P == 3 && !F32;              // operand stored as three bf16 planes
+    static constexpr int NV = PL ? 3 : 1;                   // 16-B loads per slot
+    u32x4 v[ITERS * NV];
     bool kok[ITERS];
     int src[ITERS];
 
@@ -91,13 +107,16 @@ struct Stage16 {
         }
     }
 
-    // vec: every contiguous extent and ld are multiples of EPL and the base is 16-B aligned
+    // vec: every contiguous extent and ld are multiples of EPL and the base is 16-B aligned.
+    // Pre-split planes (P == 3, bf16 storage): the three planes sit at src_p + q·pstride.
     __device__ __forceinline__ void load(const T* __restrict__ src_p, int ld, int r0, int Rmax, int k0, int kend,
-                                         bool vec, int tid) {
+                                         bool vec, int tid, long pstride = 0) {
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) {
             const int idx = tid + it * NT_;
-            u32x4 x = {0u, 0u, 0u, 0u};
+            u32x4 x[NV];
+#pragma unroll
+            for (int q = 0; q < NV; ++q) x[q] = u32x4{0u, 0u, 0u, 0u};
             kok[it] = true;
             if (TOTAL % NT_ == 0 || idx < TOTAL) {
                 int row, k;
@@ -107,28 +126,33 @@ struct Stage16 {
                     kok[it] = gk < kend;
                     const T* p = MN ? src_p + (long)(gk < kend ? gk : kend - 1) * ld + (gr < Rmax ? gr : Rmax - EPL)
                                     : src_p + (long)src[it] * ld + (gk < kend ? gk : kend - EPL);
-                    x = *reinterpret_cast<const u32x4*>(p);
+#pragma unroll
+                    for (int q = 0; q < NV; ++q) x[q] = *reinterpret_cast<const u32x4*>(p + q * pstride);
                 } else {
-                    T e[EPL];
 #pragma unroll
-                    for (int q = 0; q < EPL; ++q) e[q] = T(0);
-                    if (MN) {
-                        if (gk < kend) {
-                            const T* p = src_p + (long)gk * ld + gr;
+                    for (int q = 0; q < NV; ++q) {
+                        T e[EPL];
 #pragma unroll
-                            for (int q = 0; q < EPL; ++q)
-                                if (gr + q < Rmax) e[q] = p[q];
+                        for (int c = 0; c < EPL; ++c) e[c] = T(0);
+                        if (MN) {
+                            if (gk < kend) {
+                                const T* p = src_p + q * pstride + (long)gk * ld + gr;
+#pragma unroll
+                                for (int c = 0; c < EPL; ++c)
+                                    if (gr + c < Rmax) e[c] = p[c];
+                            }
+                        } else if (gr < Rmax) {
+                            const T* p = src_p + q * pstride + (long)src[it] * ld + gk;
+#pragma unroll
+                            for (int c = 0; c < EPL; ++c)
+                                if (gk + c < kend) e[c] = p[c];
                         }
-                    } else if (gr < Rmax) {
-                        const T* p = src_p + (long)src[it] * ld + gk;
-#pragma unroll
-                        for (int q = 0; q < EPL; ++q)
-                            if (gk + q < kend) e[q] = p[q];
+                        x[q] = __builtin_bit_cast(u32x4, e);
                     }
-                    x = __builtin_bit_cast(u32x4, e);
                 }
             }
-            v[it] = x;
+#pragma unroll
+            for (int q = 0; q < NV; ++q) v[it * NV + q] = x[q];
         }
     }
 
@@ -141,8 +165,12 @@ struct Stage16 {
                 coords(idx, row, k);
                 unsigned short* d = img + (MN ? k * PR + row : row * PK + k);
                 const u32x4 z = {0u, 0u, 0u, 0u};
-                const u32x4 x = kok[it] ? v[it] : z;
-                if (F32 && P == 3) {
+                const u32x4 x = kok[it] ? v[it * NV] : z;
+                if (PL) {
+#pragma unroll
+                    for (int q = 0; q < NV; ++q)
+                        *reinterpret_cast<u32x4*>(d + q * IMG) = kok[it] ? v[it * NV + q] : z;
+                } else if (F32 && P == 3) {
                     // exact 3-way split x = x0 + x1 + x2 (each bf16, round-to-nearest): x0 holds the
                     // top 8 significant bits, the residual x − x0 has ≤ 16 and x1 takes 8 of them, so
                     // x − x0 − x1 has ≤ 8 and is exactly a bf16 (fp32 subtractions are exact here)
@@ -171,6 +199,7 @@ struct Stage16 {
     // or (3-plane split mode) as the fp32 values themselves
     __device__ __forceinline__ void copy_out(void* __restrict__ dstv, int ldd, int r0, int Rmax, int k0,
                                              int kend, int tid) const {
+        if (PL) return;                      // (host never asks for a copy of pre-split planes)
         if (P == 3) {
             float* __restrict__ dst = static_cast<float*>(dstv);
 #pragma unroll
@@ -273,6 +302,7 @@ __global__ __launch_bounds__(NT_, 2) void gemm_bf16_kernel(Args a) {
     using SB = Stage16<BN, BK, B_MN, TB, P>;
     static_assert(TM >= 1 && TN >= 1, "wave tile must be a multiple of 32x32");
     static_assert(!(OP == OP_TN) || sizeof(TC) == 4, "grad_W accumulates in fp32");
+    constexpr bool OUT_PL = P == 3 && sizeof(TC) == 2;      // x3: output written as three bf16 planes
 
     __shared__ __attribute__((aligned(16))) unsigned short lds[(SA::IMG + SB::IMG) * P];
 
@@ -314,8 +344,8 @@ __global__ __launch_bounds__(NT_, 2) void gemm_bf16_kernel(Args a) {
     const TB* __restrict__ PB = static_cast<const TB*>(a.B);
 
     auto load = [&](int k0) {
-        sa.load(PA, a.lda, m0, a.M, k0, kend, vec, tid);
-        sb.load(PB, a.ldb, n0, a.N, k0, kend, vec, tid);
+        sa.load(PA, a.lda, m0, a.M, k0, kend, vec, tid, a.psA);
+        sb.load(PB, a.ldb, n0, a.N, k0, kend, vec, tid, a.psB);
     };
 
     if (kbeg < kend) load(kbeg);
@@ -399,7 +429,9 @@ __global__ __launch_bounds__(NT_, 2) void gemm_bf16_kernel(Args a) {
                 if (OP == OP_NT) {
                     v += bcol;
                     if (a.relu) v = v > 0.f ? v : 0.f;
-                    if (Bits<TC>::code == 1) {
+                    if (OUT_PL) {
+                        if (ok) store_planes(static_cast<unsigned short*>(a.C) + off, a.psC, v);
+                    } else if (Bits<TC>::code == 1) {
                         const unsigned short hv = (unsigned short)(pack2(v, 0.f) & 0xffffu);
                         v = bf_lo(hv);                  // bits describe the stored (rounded) value
                         if (ok) static_cast<unsigned short*>(a.C)[off] = hv;
@@ -413,7 +445,8 @@ __global__ __launch_bounds__(NT_, 2) void gemm_bf16_kernel(Args a) {
                 } else if (OP == OP_NN) {
                     if (ok) {
                         v = keep[e] ? v : 0.f;
-                        if (Bits<TC>::code == 1) static_cast<unsigned short*>(a.C)[off] =
+                        if (OUT_PL) store_planes(static_cast<unsigned short*>(a.C) + off, a.psC, v);
+                        else if (Bits<TC>::code == 1) static_cast<unsigned short*>(a.C)[off] =
                             (unsigned short)(pack2(v, 0.f) & 0xffffu);
                         else static_cast<float*>(a.C)[off] = v;
                     }
@@ -493,13 +526,13 @@ int pick16(int M, int N, int op = OP_NT) {
 int g_force3 = -1;
 int g_split3 = 0;
 
-template <int OP>
+template <int OP, typename TA, typename TB, typename TC>
 void launch_cfg3(int c, const Args& a) {
     switch (c) {
-        case 1: launch<OP, 128, 32, 4, 32, f32, f32, f32, 3>(a); break;
-        case 2: launch<OP, 32, 128, 1, 32, f32, f32, f32, 3>(a); break;
-        case 3: launch<OP, 64, 64, 2, 32, f32, f32, f32, 3>(a); break;
-        default: launch<OP, 128, 128, 2, 32, f32, f32, f32, 3>(a); break;
+        case 1: launch<OP, 128, 32, 4, 32, TA, TB, TC, 3>(a); break;
+        case 2: launch<OP, 32, 128, 1, 32, TA, TB, TC, 3>(a); break;
+        case 3: launch<OP, 64, 64, 2, 32, TA, TB, TC, 3>(a); break;
+        default: launch<OP, 128, 128, 2, 32, TA, TB, TC, 3>(a); break;
     }
 }
 constexpr Cfg kCfgs3[] = {{128, 128, 32}, {128, 32, 32}, {32, 128, 32}, {64, 64, 32}};
@@ -513,6 +546,36 @@ int pick3(int M, int N) {
 }
 
 inline bool al16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+// dst planes (stride m·S) of the rows src[rows[i]] (rows == nullptr: row i), 4 elements per thread
+__global__ void gather_rows_x3_kernel(unsigned short* __restrict__ dst, const float* __restrict__ src,
+                                      const int* __restrict__ rows, int m, int S, int vec) {
+    const long ps = (long)m * S;
+    const int per_row = vec ? S / 4 : S;
+    const long total = (long)m * per_row;
+    for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+        const int i = (int)(t / per_row), c = (int)(t % per_row);
+        const long srow = rows ? rows[i] : i;
+        if (vec) {
+            const f32x4 f = *reinterpret_cast<const f32x4*>(src + srow * S + 4 * c);
+            const unsigned a0 = pack2(f[0], f[1]), b0 = pack2(f[2], f[3]);
+            const float r0 = f[0] - bf_lo(a0), r1 = f[1] - bf_hi(a0), r2 = f[2] - bf_lo(b0), r3 = f[3] - bf_hi(b0);
+            const unsigned a1 = pack2(r0, r1), b1 = pack2(r2, r3);
+            const unsigned a2 = pack2(r0 - bf_lo(a1), r1 - bf_hi(a1)), b2 = pack2(r2 - bf_lo(b1), r3 - bf_hi(b1));
+            unsigned short* d = dst + (long)i * S + 4 * c;
+            *reinterpret_cast<u32x2*>(d) = u32x2{a0, b0};
+            *reinterpret_cast<u32x2*>(d + ps) = u32x2{a1, b1};
+            *reinterpret_cast<u32x2*>(d + 2 * ps) = u32x2{a2, b2};
+        } else {
+            store_planes(dst + (long)i * S + c, ps, src[srow * S + c]);
+        }
+    }
+}
+
+__global__ void split_x3_kernel(unsigned short* __restrict__ dst, long stride, const float* __restrict__ p, long n) {
+    for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+        store_planes(dst + i, stride, p[i]);
+}
 inline int epl(int t) { return t ? 8 : 4; }
 
 }  // namespace
@@ -592,36 +655,58 @@ void phip_linear16_bwd_w(float* gW, float* gb, const void* g, int tg, const void
     else launch_cfg<OP_TN, b16, b16, f32>(c, a);
 }
 
-// fp32 storage everywhere; fp32-accurate products on the bf16 MFMA (x3 engine, above)
-void phip_linear_x3_fwd(float* y, const float* x, const int* ridx, float* xcopy, const float* W, const float* b,
+// fp32-accurate products on the bf16 MFMA (x3 engine, above).  Operands are fp32 (split on the way
+// into LDS) or pre-split (phip_opnd.planes: three bf16 planes at p + q·pstride); outputs of the
+// forward and grad_x likewise (written split in the epilogue).  Supported storage combinations
+// (everything else is a host bug): forward x ∈ {fp32, planes} with W planes, or all fp32 (the
+// mat_mul API); grad_x g ∈ {fp32, planes} with W planes, or all fp32; grad_W any.
+static inline bool al16o(const phip_opnd& o) { return al16(o.p) && (!o.planes || o.pstride % 8 == 0); }
+static inline int eplo(const phip_opnd& o) { return o.planes ? 8 : 4; }
+
+void phip_linear_x3_fwd(phip_opnd y, phip_opnd x, const int* ridx, float* xcopy, phip_opnd W, const float* b,
                         int m, int n, int l, int relu, unsigned* bits) {
     if (m <= 0 || l <= 0) return;
-    PPO_REQUIRE(y && x && W && n > 0, "phip_linear_x3_fwd: null operand");
+    PPO_REQUIRE(y.p && x.p && W.p && n > 0, "phip_linear_x3_fwd: null operand");
+    PPO_REQUIRE(!(ridx && x.planes), "phip_linear_x3_fwd: fused gather from pre-split planes");
+    PPO_REQUIRE(W.planes || (!x.planes && !y.planes), "phip_linear_x3_fwd: unsupported storage combination");
     ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l);
     Args a{};
-    a.A = x; a.lda = n; a.B = W; a.ldb = n; a.C = y; a.ldc = l;
+    a.A = x.p; a.lda = n; a.B = W.p; a.ldb = n; a.C = y.p; a.ldc = l;
+    a.psA = x.pstride; a.psB = W.pstride; a.psC = y.pstride;
     a.M = m; a.N = l; a.K = n; a.kchunk = n; a.splits = 1;
     a.bias = b; a.relu = relu; a.ridx = ridx; a.acopy = ridx ? xcopy : nullptr;
     a.bits_out = relu ? bits : nullptr; a.wpr = ppo_divup(l, 32);
-    a.vec = n % 4 == 0 && al16(x) && al16(W);
-    launch_cfg3<OP_NT>(pick3(m, l), a);
+    a.vec = n % eplo(x) == 0 && n % eplo(W) == 0 && al16o(x) && al16o(W);
+    const int c = pick3(m, l);
+    if (!W.planes) launch_cfg3<OP_NT, f32, f32, f32>(c, a);
+    else if (!x.planes && !y.planes) launch_cfg3<OP_NT, f32, b16, f32>(c, a);
+    else if (!x.planes) launch_cfg3<OP_NT, f32, b16, b16>(c, a);
+    else if (!y.planes) launch_cfg3<OP_NT, b16, b16, f32>(c, a);
+    else launch_cfg3<OP_NT, b16, b16, b16>(c, a);
 }
 
-void phip_linear_x3_bwd_x(float* gx, const float* g, const float* W, const unsigned* bits, int m, int n, int l) {
+void phip_linear_x3_bwd_x(phip_opnd gx, phip_opnd g, phip_opnd W, const unsigned* bits, int m, int n, int l) {
     if (m <= 0 || n <= 0) return;
-    PPO_REQUIRE(gx && g && W && l > 0, "phip_linear_x3_bwd_x: null operand");
+    PPO_REQUIRE(gx.p && g.p && W.p && l > 0, "phip_linear_x3_bwd_x: null operand");
+    PPO_REQUIRE(W.planes || (!g.planes && !gx.planes), "phip_linear_x3_bwd_x: unsupported storage combination");
     ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l);
     Args a{};
-    a.A = g; a.lda = l; a.B = W; a.ldb = n; a.C = gx; a.ldc = n;
+    a.A = g.p; a.lda = l; a.B = W.p; a.ldb = n; a.C = gx.p; a.ldc = n;
+    a.psA = g.pstride; a.psB = W.pstride; a.psC = gx.pstride;
     a.M = m; a.N = n; a.K = l; a.kchunk = l; a.splits = 1;
     a.bits_in = bits; a.wpr = ppo_divup(n, 32);
-    a.vec = l % 4 == 0 && n % 4 == 0 && al16(g) && al16(W);
-    launch_cfg3<OP_NN>(pick3(m, n), a);
+    a.vec = l % eplo(g) == 0 && n % eplo(W) == 0 && al16o(g) && al16o(W);
+    const int c = pick3(m, n);
+    if (!W.planes) launch_cfg3<OP_NN, f32, f32, f32>(c, a);
+    else if (!g.planes && !gx.planes) launch_cfg3<OP_NN, f32, b16, f32>(c, a);
+    else if (!g.planes) launch_cfg3<OP_NN, f32, b16, b16>(c, a);
+    else if (!gx.planes) launch_cfg3<OP_NN, b16, b16, f32>(c, a);
+    else launch_cfg3<OP_NN, b16, b16, b16>(c, a);
 }
 
-void phip_linear_x3_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, int n, int l, int zeroed) {
+void phip_linear_x3_bwd_w(float* gW, float* gb, phip_opnd g, phip_opnd x, int m, int n, int l, int zeroed) {
     if (l <= 0 || n <= 0) return;
-    PPO_REQUIRE(gW && g && x, "phip_linear_x3_bwd_w: null operand");
+    PPO_REQUIRE(gW && g.p && x.p, "phip_linear_x3_bwd_w: null operand");
     ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l);
     if (m <= 0) {
         if (!zeroed) {
@@ -641,15 +726,36 @@ void phip_linear_x3_bwd_w(float* gW, float* gb, const float* g, const float* x, 
     int kchunk = ppo_divup(ppo_divup(m, splits), BK) * BK;
     splits = ppo_divup(m, kchunk);
     Args a{};
-    a.A = g; a.lda = l; a.B = x; a.ldb = n; a.C = gW; a.ldc = n;
+    a.A = g.p; a.lda = l; a.B = x.p; a.ldb = n; a.C = gW; a.ldc = n;
+    a.psA = g.pstride; a.psB = x.pstride;
     a.M = l; a.N = n; a.K = m; a.kchunk = kchunk; a.splits = splits;
     a.gbias = gb;
-    a.vec = l % 4 == 0 && n % 4 == 0 && al16(g) && al16(x);
+    a.vec = l % eplo(g) == 0 && n % eplo(x) == 0 && al16o(g) && al16o(x);
     if (splits > 1 && !zeroed) {
         phip_memset(gW, 0, sizeof(float) * (size_t)l * n);
         if (gb) phip_memset(gb, 0, sizeof(float) * (size_t)l);
     }
-    launch_cfg3<OP_TN>(c, a);
+    if (!g.planes && !x.planes) launch_cfg3<OP_TN, f32, f32, f32>(c, a);
+    else if (!g.planes) launch_cfg3<OP_TN, f32, b16, f32>(c, a);
+    else if (!x.planes) launch_cfg3<OP_TN, b16, f32, f32>(c, a);
+    else launch_cfg3<OP_TN, b16, b16, f32>(c, a);
+}
+
+void phip_gather_rows_x3(unsigned short* dst, const float* src, const int* rows, int m, int S) {
+    if (m <= 0 || S <= 0) return;
+    ppo::ProfScope ps(PPO_K_GATHER, 10.0 * m * S);
+    const int vec = S % 4 == 0 && al16(src) && ((uintptr_t)dst & 7u) == 0 && ((long)m * S) % 4 == 0;
+    const long total = (long)m * (vec ? S / 4 : S);
+    const int grid = (int)std::min<long>((total + 255) / 256, 4096);
+    hipLaunchKernelGGL(gather_rows_x3_kernel, dim3(grid), dim3(256), 0, ppo::stream(), dst, src, rows, m, S, vec);
+    PPO_LAUNCH_CHECK();
+}
+
+void phip_split_x3(unsigned short* dst, long stride, const float* p, long n) {
+    if (n <= 0) return;
+    const int grid = (int)std::min<long>((n + 255) / 256, 2048);
+    hipLaunchKernelGGL(split_x3_kernel, dim3(grid), dim3(256), 0, ppo::stream(), dst, stride, p, n);
+    PPO_LAUNCH_CHECK();
 }
 
 int ppo_gemm_x3_tune(int force_cfg, int splitk_target) {
@@ -662,25 +768,34 @@ int ppo_gemm_x3_tune(int force_cfg, int splitk_target) {
 double ppo_bench_gemm_x3(int op, int m, int n, int l, int iters, int cfg, int splitk_target) {
     ppo::ensure_device();
     const size_t sx = (size_t)m * n, sw = (size_t)l * n, sy = (size_t)m * l;
-    float* x = (float*)phip_malloc(4 * sx);
-    float* W = (float*)phip_malloc(4 * sw);
-    float* y = (float*)phip_malloc(4 * (sy > sx ? sy : sx));
+    float* x = (float*)phip_malloc(6 * sx);
+    float* W = (float*)phip_malloc(6 * sw);
+    float* y = (float*)phip_malloc(6 * (sy > sx ? sy : sx));
     float* b = (float*)phip_malloc(4 * (size_t)(l > n ? l : n));
     float* gw = (float*)phip_malloc(4 * sw);
     unsigned* bits = (unsigned*)phip_malloc(4 * (size_t)m * ppo_divup(l > n ? l : n, 32));
-    phip_fill_uniform(x, (long)sx, 1, -1.f, 1.f);
-    phip_fill_uniform(W, (long)sw, 2, -0.1f, 0.1f);
-    phip_fill_uniform(y, (long)(sy > sx ? sy : sx), 3, -1.f, 1.f);
+    phip_fill_uniform(x, (long)(sx * 3 / 2), 1, -1.f, 1.f);
+    phip_fill_uniform(W, (long)(sw * 3 / 2), 2, -0.1f, 0.1f);
+    phip_fill_uniform(y, (long)((sy > sx ? sy : sx) * 3 / 2), 3, -1.f, 1.f);
+    void* w3 = W;
     phip_fill_uniform(b, (long)(l > n ? l : n), 4, -0.1f, 0.1f);
     phip_memset(bits, 0xff, 4 * (size_t)m * ppo_divup(l > n ? l : n, 32));
     const int saved = g_force3, saved_split = g_split3;
     g_force3 = cfg;
     g_split3 = splitk_target;
+    // op ≥ 10: the same product with pre-split operands (planes in the buffers' first 6 B/elem
+    // view: x, y hold 1.5x their fp32 size) and W planes — the x3 engine's update-path storage
+    const bool pl = op >= 10;
+    const int o = op % 10;
+    auto F = [](void* p) { return phip_opnd{p, 0, 0}; };
+    auto PLo = [&](void* p, long cnt) { return pl ? phip_opnd{p, 1, cnt} : phip_opnd{p, 0, 0}; };
     auto run = [&]() {
-        if (op == 0) phip_linear_x3_fwd(y, x, nullptr, nullptr, W, b, m, n, l, 1, bits);
-        else if (op == 3) phip_linear_x3_fwd(y, x, nullptr, nullptr, W, b, m, n, l, 0, nullptr);
-        else if (op == 1) phip_linear_x3_bwd_x(x, y, W, bits, m, n, l);
-        else phip_linear_x3_bwd_w(gw, b, y, x, m, n, l, 0);
+        if (o == 0) phip_linear_x3_fwd(PLo(y, (long)sy), PLo(x, (long)sx), nullptr, nullptr, PLo(w3, (long)sw), b, m, n,
+                                       l, 1, bits);
+        else if (o == 3) phip_linear_x3_fwd(F(y), PLo(x, (long)sx), nullptr, nullptr, PLo(w3, (long)sw), b, m, n, l,
+                                            0, nullptr);
+        else if (o == 1) phip_linear_x3_bwd_x(PLo(x, (long)sx), PLo(y, (long)sy), PLo(w3, (long)sw), bits, m, n, l);
+        else phip_linear_x3_bwd_w(gw, b, PLo(y, (long)sy), PLo(x, (long)sx), m, n, l, 0);
     };
     for (int i = 0; i < 3; ++i) run();
     hipEvent_t e0, e1;

@@ -69,13 +69,21 @@ void phip_linear16_bwd_x(void* gx, int tgx, const void* g, int tg, const void* W
 /* gW[l,n] (+)= gᵀ·x, gb (+)= Σ g in fp32 (zeroed != 0: outputs already zero) */
 void phip_linear16_bwd_w(float* gW, float* gb, const void* g, int tg, const void* x, int tx, int m, int n, int l,
                          int zeroed);
-/* fp32 storage, fp32-accurate products on the bf16 MFMA (exact 3-plane bf16 split, 6 products):
- * the "x3" engine of fp32 mode.  Forward with optional fused gather (ridx; xcopy = fp32 copy of the
- * gathered rows) + bias/ReLU/ReLU' bits; grad_x with the bit mask; grad_W (+gb) split-K. */
-void phip_linear_x3_fwd(float* y, const float* x, const int* ridx, float* xcopy, const float* W, const float* b,
+/* fp32-accurate products on the bf16 MFMA (exact 3-plane bf16 split, 6 products): the "x3" engine
+ * of fp32 mode.  An operand is fp32 (planes = 0: split on the way into LDS) or pre-split (planes = 1:
+ * three bf16 planes whose sum is the fp32 value exactly, plane q at p + q·pstride elements).
+ * Forward with optional fused gather (fp32 x only; xcopy = fp32 copy of the gathered rows) +
+ * bias/ReLU/ReLU' bits; grad_x with the bit mask; grad_W (+gb) split-K. */
+typedef struct { void* p; int planes; long pstride; } phip_opnd;
+void phip_linear_x3_fwd(phip_opnd y, phip_opnd x, const int* ridx, float* xcopy, phip_opnd W, const float* b,
                         int m, int n, int l, int relu, unsigned* bits);
-void phip_linear_x3_bwd_x(float* gx, const float* g, const float* W, const unsigned* bits, int m, int n, int l);
-void phip_linear_x3_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, int n, int l, int zeroed);
+void phip_linear_x3_bwd_x(phip_opnd gx, phip_opnd g, phip_opnd W, const unsigned* bits, int m, int n, int l);
+void phip_linear_x3_bwd_w(float* gW, float* gb, phip_opnd g, phip_opnd x, int m, int n, int l, int zeroed);
+/* dst (three bf16 planes, plane stride m·S) = split(src[rows[i], :]) for i < m: layer 0's gather
+ * in the x3 engine's update path; rows == NULL: rows 0..m-1 */
+void phip_gather_rows_x3(unsigned short* dst, const float* src, const int* rows, int m, int S);
+/* three bf16 planes of p[0, n) at dst + q·stride (the x3 engine's weight planes) */
+void phip_split_x3(unsigned short* dst, long stride, const float* p, long n);
 /* dst[i, :] = bf16(src[rows[i], :]) for i < m (S % 4 == 0): layer 0's gather in bf16 mode */
 void phip_gather_rows_bf16(unsigned short* dst, const float* src, const int* rows, int m, int S);
 void phip_f32_to_bf16(unsigned short* dst, const float* src, long count);

@@ -32,6 +32,13 @@ static inline long align4(long n) { return (n + 3) & ~3L; }
 
 /* fp32 GEMM engine used when PPO_F32_GEMM is unset (ppo_ext.h ppo_gemm_f32_engine): 1 = x3 */
 #define PPO_F32_ENGINE_DEFAULT 1
+/* bytes per element of activation / gradient caches and gathered-row workspaces: room for the x3
+ * engine's pre-split storage (three bf16 planes) */
+#define X3_BYTES 6
+void nn_set_x3_planar(int on);                 /* pre-split storage inside ppo_update (neural_network.c) */
+int  nn_x3_planar(void);
+void nn_sync_w3(NeuralNetwork* nn);            /* refresh the x3 weight planes from d_params */
+int  ppo_gemm_f32_engine(int engine);
 /* linear-layer products of the reference API through the engine choice (neural_network.c) */
 void lin_fwd(float* y, const float* x, const float* W, const float* b, int m, int n, int l);
 void lin_bwd_x(float* gx, const float* g, const float* W, int m, int n, int l);

@@ -92,8 +92,8 @@ static PPODev* dev_ws(PPO* ppo, int B) {
         phip_free(d->rows_p); phip_free(d->states_p);
         d->rows = (int*)phip_malloc(sizeof(int) * (size_t)B);
         d->rows_p = (int*)phip_malloc(sizeof(int) * (size_t)B);
-        d->states = (float*)phip_malloc(sizeof(float) * (size_t)B * S);
-        d->states_p = (float*)phip_malloc(sizeof(float) * (size_t)B * S);
+        d->states = (float*)phip_malloc(X3_BYTES * (size_t)B * S);
+        d->states_p = (float*)phip_malloc(X3_BYTES * (size_t)B * S);
         d->actions = (float*)phip_malloc(sizeof(float) * (size_t)B * A);
         d->old_lp = (float*)phip_malloc(sizeof(float) * (size_t)B);
         d->adv = (float*)phip_malloc(sizeof(float) * (size_t)B);
@@ -315,6 +315,7 @@ static void adam_update_net(Adam* adam, float lr, NeuralNetwork* nn) {
     const int fused = nn->dtype == 1 && adam->flat && adam->weights[0] == nn->d_params;
     if (!adam_update_cuda_w16(adam, lr, fused ? nn->d_w16 : NULL, nn->num_params) && nn->dtype == 1)
         nn_sync_w16(nn);
+    if (nn->dtype == 0 && nn->d_w3 && nn_x3_planar()) nn_sync_w3(nn);     /* x3 weight planes */
 }
 
 static float* tiny_steps(PPODev* d, int slot, Adam* adam, float lr, int n) {
@@ -418,9 +419,31 @@ static int ppo_update_tiny(PPO* ppo, PPODev* d, int B, int n_epochs_policy, int 
     return 0;
 }
 
+static void ppo_update_body(PPO* ppo, float gamma, int batch_size, int n_epochs_policy, int n_epochs_value,
+                            int shuffle_mode, unsigned long long seed);
+
+/* The x3 engine's pre-split storage (neural_network.c) applies for the duration of an update when
+ * PPO_X3_PLANAR=1 (weights, activations, gradients and gathered rows as three bf16 planes) or 2
+ * (weight planes only): weight planes refreshed here and after every Adam step.  Off by default:
+ * measured slower at C4 (update 409 -> 442 ms with 1, -> 414 ms with 2; the planes are 1.5x the
+ * fp32 bytes and the split it saves is not what bounds the x3 GEMM — DESIGN.md §4). */
 void ppo_update(void* vppo, float gamma, int batch_size, int n_epochs_policy, int n_epochs_value, int shuffle_mode,
                 unsigned long long seed) {
     PPO* ppo = (PPO*)vppo;
+    const char* e = getenv("PPO_X3_PLANAR");
+    const int mode = e && (*e == '1' || *e == '2') ? *e - '0' : 0;
+    const int planar = mode && ppo->V->dtype == 0 && ppo_gemm_f32_engine(-1) == 1;
+    if (planar) {
+        nn_sync_w3(ppo->V);
+        nn_sync_w3(ppo->policy->mu);
+    }
+    nn_set_x3_planar(planar ? mode : 0);
+    ppo_update_body(ppo, gamma, batch_size, n_epochs_policy, n_epochs_value, shuffle_mode, seed);
+    nn_set_x3_planar(0);
+}
+
+static void ppo_update_body(PPO* ppo, float gamma, int batch_size, int n_epochs_policy, int n_epochs_value,
+                            int shuffle_mode, unsigned long long seed) {
     TrajectoryBuffer* buf = ppo->buffer;
     if (!buf->on_device) die("ppo_update: buffer must be device-resident (buffer_to_device / ppo_fill_synthetic)");
     if (batch_size <= 0) die("ppo_update: batch_size must be positive");

@@ -3,7 +3,8 @@
 fp32-MFMA engine, on the MI355X: device µs and algorithmic fp32 TFLOP/s per (op, shape, config).
 
     python ppo.c_amd/tools/gemm_x3_sweep.py [--shapes 32768,512,512;32768,376,512] [--cfgs -1,0,3]
-op 0 = forward (bias+ReLU+bits), 1 = grad_x (bit mask), 2 = grad_W (split-K), 3 = forward, no activation.
+op 0 = forward (bias+ReLU+bits), 1 = grad_x (bit mask), 2 = grad_W (split-K), 3 = forward, no activation;
+op + 10 = the same with pre-split (three bf16 plane) operands and outputs, the update path's storage.
 """
 import argparse
 import os
@@ -30,7 +31,7 @@ def main():
             if op == 0 and l < 32:
                 op = 3
             flop = 2.0 * m * n * l
-            ex = lib.ppo_bench_gemm(op, m, n, l, 20, -1)
+            ex = lib.ppo_bench_gemm(op % 10, m, n, l, 20, -1)
             print(f"op{op} m={m} n={n} l={l} exact-f32 auto        {ex:9.1f} us {flop / ex / 1e6:8.1f} TF/s", flush=True)
             for cfg in (int(c) for c in args.cfgs.split(",")):
                 for tgt in ([int(s) for s in args.splits.split(",")] if op == 2 else [0]):
