@@ -48,6 +48,7 @@ struct Args {
     int kchunk, splits, tiles_m, tiles_n;
     int vec;
     long psA, psB, psC;                   // x3 engine: plane strides (elements) of pre-split operands / output
+    int flags;                            // x3 experiment bits (PPO_X3_FLAGS): 1 = s_setprio 1 around the MFMAs
 };
 
 // fp32 → bf16, round to nearest even (NaN stays NaN: v_cvt_pk_bf16_f32)
@@ -74,7 +75,7 @@ __device__ __forceinline__ void store_planes(unsigned short* dst, long ps, float
 // Staging of one operand tile (R rows × BK k) into a bf16 LDS image.  T = float or unsigned short
 // (bf16 bits).  One 16-B global load per slot: 4 fp32 or 8 bf16 elements.
 // ---------------------------------------------------------------------------
-template <int R, int BK, bool MN, typename T, int P = 1>
+template <int R, int BK, bool MN, typename T, int P = 1, bool FPI = false>
 struct Stage16 {
     static constexpr bool F32 = sizeof(T) == 4;
     static_assert(P == 1 || P == 3, "one bf16 image or three planes");
@@ -87,6 +88,11 @@ struct Stage16 {
     static constexpr int ITERS = (TOTAL + NT_ - 1) / NT_;
     static_assert(R % EPL == 0 && R >= 32, "tile rows");
     static constexpr bool PL = P == 3 && !F32;              // operand stored as three bf16 planes
+    // FPI (x3, k-contiguous fp32 operand): the LDS image holds the fp32 values ([row][BK+4] floats)
+    // and each wave splits its fragments after reading them (split at read, not at store)
+    static_assert(!FPI || (F32 && !MN && P == 3), "fp32 image: fp32 k-contiguous x3 operands only");
+    static constexpr int PKF = BK + 4;                      // fp32 pitch: 36 dwords at BK 32 (conflict-free b128)
+    static constexpr int LDSZ = FPI ? R * PKF * 2 : IMG * P;   // LDS footprint in 16-bit units
     static constexpr int NV = PL ? 3 : 1;                   // 16-B loads per slot
     u32x4 v[ITERS * NV];
     bool kok[ITERS];
@@ -166,7 +172,9 @@ struct Stage16 {
                 unsigned short* d = img + (MN ? k * PR + row : row * PK + k);
                 const u32x4 z = {0u, 0u, 0u, 0u};
                 const u32x4 x = kok[it] ? v[it * NV] : z;
-                if (PL) {
+                if (FPI) {
+                    *reinterpret_cast<u32x4*>(reinterpret_cast<float*>(img) + row * PKF + k) = x;
+                } else if (PL) {
 #pragma unroll
                     for (int q = 0; q < NV; ++q)
                         *reinterpret_cast<u32x4*>(d + q * IMG) = kok[it] ? v[it * NV + q] : z;
@@ -272,6 +280,27 @@ struct Stage16 {
         return __builtin_bit_cast(bf16x8, f);
     }
 
+    // FPI: the three bf16 planes of the k-step-ks fragment of image row `row` (k = 16·ks + 8h + j)
+    __device__ __forceinline__ static void frag3(const unsigned short* img, int row, int ks, int lane, bf16x8& f0,
+                                                 bf16x8& f1, bf16x8& f2) {
+        const float* s = reinterpret_cast<const float*>(img) + row * PKF + 16 * ks + 8 * (lane >> 5);
+        const f32x4 x = *reinterpret_cast<const f32x4*>(s), y = *reinterpret_cast<const f32x4*>(s + 4);
+        const float e[8] = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+        u32x4 p0, p1, p2;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const unsigned a0 = pack2(e[2 * q], e[2 * q + 1]);
+            const float r0 = e[2 * q] - bf_lo(a0), r1 = e[2 * q + 1] - bf_hi(a0);
+            const unsigned a1 = pack2(r0, r1);
+            p0[q] = a0;
+            p1[q] = a1;
+            p2[q] = pack2(r0 - bf_lo(a1), r1 - bf_hi(a1));
+        }
+        f0 = __builtin_bit_cast(bf16x8, p0);
+        f1 = __builtin_bit_cast(bf16x8, p1);
+        f2 = __builtin_bit_cast(bf16x8, p2);
+    }
+
     // Σ over this tile's k of image row `row` (fp32), k ∈ [k_lo, k_lo + n); in 3-plane mode each
     // element is recombined exactly (x0 + x1 + x2) before it is added
     __device__ __forceinline__ static float rowsum(const unsigned short* img, int row, int k_lo, int n) {
@@ -292,19 +321,29 @@ template <typename T> struct Bits;
 template <> struct Bits<float> { static constexpr int code = 0; };
 template <> struct Bits<unsigned short> { static constexpr int code = 1; };
 
-template <int OP, int BM, int BN, int WARPS_M, int BK, typename TA, typename TB, typename TC, int P>
+// VAR (x3 only): 0 = operands split into plane images at LDS-store time; 1 = k-contiguous fp32
+// operands staged as fp32 and split at fragment read; 2 = as 1 with a double-buffered LDS image (one
+// barrier per k-tile, the next tile's LDS write after this tile's MFMAs).  EOP = epilogue op (grad_x
+// computed as an NT product against Wᵀ uses OP_NT staging with the OP_NN epilogue).
+template <int OP, int BM, int BN, int WARPS_M, int BK, typename TA, typename TB, typename TC, int P, int VAR = 0,
+          int EOP = OP>
 __global__ __launch_bounds__(NT_, 2) void gemm_bf16_kernel(Args a) {
     constexpr int WARPS_N = 4 / WARPS_M;
     constexpr int WM = BM / WARPS_M, WN = BN / WARPS_N;
     constexpr int TM = WM / 32, TN = WN / 32;
     constexpr bool A_MN = OP == OP_TN, B_MN = OP != OP_NT;
-    using SA = Stage16<BM, BK, A_MN, TA, P>;
-    using SB = Stage16<BN, BK, B_MN, TB, P>;
+    constexpr bool FPA = VAR >= 1 && !A_MN && sizeof(TA) == 4, FPB = VAR >= 1 && !B_MN && sizeof(TB) == 4;
+    constexpr bool DB = VAR == 2;
+    using SA = Stage16<BM, BK, A_MN, TA, P, FPA>;
+    using SB = Stage16<BN, BK, B_MN, TB, P, FPB>;
+    constexpr int BUF = SA::LDSZ + SB::LDSZ;                  // one LDS image (16-bit units)
+    static_assert(!(DB && OP == OP_TN), "double-buffered image: no bias-gradient row sums");
     static_assert(TM >= 1 && TN >= 1, "wave tile must be a multiple of 32x32");
     static_assert(!(OP == OP_TN) || sizeof(TC) == 4, "grad_W accumulates in fp32");
     constexpr bool OUT_PL = P == 3 && sizeof(TC) == 2;      // x3: output written as three bf16 planes
 
-    __shared__ __attribute__((aligned(16))) unsigned short lds[(SA::IMG + SB::IMG) * P];
+    extern __shared__ __attribute__((aligned(16))) unsigned short lds[];     // (SA::IMG + SB::IMG) * P
+    const bool prio = (a.flags & 1) != 0;
 
     const int nwg = gridDim.x, b = blockIdx.x;
     const int xcd = b & 7, qq = nwg >> 3, rr = nwg & 7;
@@ -331,7 +370,7 @@ __global__ __launch_bounds__(NT_, 2) void gemm_bf16_kernel(Args a) {
 
     constexpr int TPR = NT_ / BM > 0 ? NT_ / BM : 1;
     constexpr int KPT = BK / TPR > 0 ? BK / TPR : 1;
-    const bool do_bsum = OP == OP_TN && a.gbias != nullptr && tn == 0 && (NT_ % BM == 0);
+    const bool do_bsum = OP == OP_TN && EOP == OP_TN && a.gbias != nullptr && tn == 0 && (NT_ % BM == 0);
     float bsum = 0.f;
 
     SA sa;
@@ -348,25 +387,31 @@ __global__ __launch_bounds__(NT_, 2) void gemm_bf16_kernel(Args a) {
         sb.load(PB, a.ldb, n0, a.N, k0, kend, vec, tid, a.psB);
     };
 
-    if (kbeg < kend) load(kbeg);
-    for (int k0 = kbeg; k0 < kend; k0 += BK) {
-        if (do_copy) sa.copy_out(a.acopy, a.K, m0, a.M, k0, kend, tid);
-        sa.store(lds, tid);
-        sb.store(lds + P * SA::IMG, tid);
-        __syncthreads();
-        if (k0 + BK < kend) load(k0 + BK);            // in flight during this tile's MFMAs
-        const unsigned short* As = lds;
-        const unsigned short* Bs = lds + P * SA::IMG;
-        if (do_bsum) bsum += SA::rowsum(As, tid / TPR, (tid % TPR) * KPT, KPT);
+    // one k-tile of MFMAs on the image at `img`
+    auto compute = [&](const unsigned short* img) {
+        const unsigned short* As = img;
+        const unsigned short* Bs = img + SA::LDSZ;
+        if (prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int ks = 0; ks < BK / 16; ++ks) {
             bf16x8 fa[P][TM], fb[P][TN];
 #pragma unroll
-            for (int p = 0; p < P; ++p) {
+            for (int i = 0; i < TM; ++i) {
+                if constexpr (FPA) {
+                    SA::frag3(As, wm * WM + i * 32 + r, ks, lane, fa[0][i], fa[P - 2][i], fa[P - 1][i]);
+                } else {
 #pragma unroll
-                for (int i = 0; i < TM; ++i) fa[p][i] = SA::frag(As + p * SA::IMG, wm * WM + i * 32 + r, ks, lane);
+                    for (int p = 0; p < P; ++p) fa[p][i] = SA::frag(As + p * SA::IMG, wm * WM + i * 32 + r, ks, lane);
+                }
+            }
 #pragma unroll
-                for (int j = 0; j < TN; ++j) fb[p][j] = SB::frag(Bs + p * SB::IMG, wn * WN + j * 32 + r, ks, lane);
+            for (int j = 0; j < TN; ++j) {
+                if constexpr (FPB) {
+                    SB::frag3(Bs, wn * WN + j * 32 + r, ks, lane, fb[0][j], fb[P - 2][j], fb[P - 1][j]);
+                } else {
+#pragma unroll
+                    for (int p = 0; p < P; ++p) fb[p][j] = SB::frag(Bs + p * SB::IMG, wn * WN + j * 32 + r, ks, lane);
+                }
             }
             // 3-plane mode: the six products whose planes sum to ≤ 2 (smallest first); the three
             // dropped ones are below 2^-24 relative to the product
@@ -381,7 +426,41 @@ __global__ __launch_bounds__(NT_, 2) void gemm_bf16_kernel(Args a) {
                         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[pa][i], fb[pb][j], acc[i][j], 0, 0, 0);
             }
         }
+        if (prio) __builtin_amdgcn_s_setprio(0);
+    };
+    auto stage = [&](unsigned short* img, int k0) {
+        if (do_copy) sa.copy_out(a.acopy, a.K, m0, a.M, k0, kend, tid);
+        sa.store(img, tid);
+        sb.store(img + SA::LDSZ, tid);
+    };
+
+    if constexpr (DB) {
+        // double-buffered image: tile t+1's loads fly during tile t's MFMAs and are written into the
+        // other image right after them; one barrier per k-tile
+        if (kbeg < kend) {
+            load(kbeg);
+            stage(lds, kbeg);
+        }
         __syncthreads();
+        int cur = 0;
+        for (int k0 = kbeg; k0 < kend; k0 += BK) {
+            const bool more = k0 + BK < kend;
+            if (more) load(k0 + BK);
+            compute(lds + cur * BUF);
+            if (more) stage(lds + (cur ^ 1) * BUF, k0 + BK);
+            __syncthreads();
+            cur ^= 1;
+        }
+    } else {
+        if (kbeg < kend) load(kbeg);
+        for (int k0 = kbeg; k0 < kend; k0 += BK) {
+            stage(lds, k0);
+            __syncthreads();
+            if (k0 + BK < kend) load(k0 + BK);            // in flight during this tile's MFMAs
+            if (do_bsum) bsum += SA::rowsum(lds, tid / TPR, (tid % TPR) * KPT, KPT);
+            compute(lds);
+            __syncthreads();
+        }
     }
 
     if (do_bsum) {
@@ -404,9 +483,9 @@ __global__ __launch_bounds__(NT_, 2) void gemm_bf16_kernel(Args a) {
             const int r0 = m0 + wm * WM + i * 32 + 4 * h;
             const bool col_ok = col < a.N;
             float bcol = 0.f;
-            if (OP == OP_NT && a.bias) bcol = a.bias[col_ok ? col : a.N - 1];
+            if (EOP == OP_NT && a.bias) bcol = a.bias[col_ok ? col : a.N - 1];
             bool keep[16];
-            if (OP == OP_NN) {
+            if (EOP == OP_NN) {
                 if (a.bits_in) {
                     unsigned wv[16];
 #pragma unroll
@@ -426,7 +505,7 @@ __global__ __launch_bounds__(NT_, 2) void gemm_bf16_kernel(Args a) {
                 const bool ok = col_ok && row < a.M;
                 float v = acc[i][j][e];
                 const long off = (long)row * a.ldc + col;
-                if (OP == OP_NT) {
+                if (EOP == OP_NT) {
                     v += bcol;
                     if (a.relu) v = v > 0.f ? v : 0.f;
                     if (OUT_PL) {
@@ -442,7 +521,7 @@ __global__ __launch_bounds__(NT_, 2) void gemm_bf16_kernel(Args a) {
                         const unsigned long long bb = __ballot(ok && v > 0.f);
                         if (r == e) word = h ? (unsigned)(bb >> 32) : (unsigned)bb;
                     }
-                } else if (OP == OP_NN) {
+                } else if (EOP == OP_NN) {
                     if (ok) {
                         v = keep[e] ? v : 0.f;
                         if (OUT_PL) store_planes(static_cast<unsigned short*>(a.C) + off, a.psC, v);
@@ -456,7 +535,7 @@ __global__ __launch_bounds__(NT_, 2) void gemm_bf16_kernel(Args a) {
                     else *dst = v;
                 }
             }
-            if (OP == OP_NT && a.bits_out && r < 16) {
+            if (EOP == OP_NT && a.bits_out && r < 16) {
                 const int row = r0 + (r & 3) + 8 * (r >> 2);
                 if (row < a.M && c0 < a.N) a.bits_out[(long)row * a.wpr + (c0 >> 5)] = word;
             }
@@ -466,15 +545,28 @@ __global__ __launch_bounds__(NT_, 2) void gemm_bf16_kernel(Args a) {
 using f32 = float;
 using b16 = unsigned short;
 
-template <int OP, int BM, int BN, int WM_, int BK, typename TA, typename TB, typename TC, int P = 1>
+template <int OP, int BM, int BN, int WM_, int BK, typename TA, typename TB, typename TC, int P = 1, int VAR = 0,
+          int EOP = OP>
 void launch(Args a) {
     a.tiles_m = ppo_divup(a.M, BM);
     a.tiles_n = ppo_divup(a.N, BN);
     if (a.splits < 1) a.splits = 1;
     const long grid = (long)a.tiles_m * a.tiles_n * a.splits;
     PPO_REQUIRE(grid > 0 && grid < (1L << 31), "gemm16: grid out of range");
-    hipLaunchKernelGGL((gemm_bf16_kernel<OP, BM, BN, WM_, BK, TA, TB, TC, P>), dim3((unsigned)grid), dim3(NT_), 0,
-                       ppo::stream(), a);
+    constexpr bool A_MN = OP == OP_TN, B_MN = OP != OP_NT;
+    constexpr size_t lds = sizeof(unsigned short) * (VAR == 2 ? 2 : 1) *
+                           (Stage16<BM, BK, A_MN, TA, P, VAR >= 1 && !A_MN && sizeof(TA) == 4>::LDSZ +
+                            Stage16<BN, BK, B_MN, TB, P, VAR >= 1 && !B_MN && sizeof(TB) == 4>::LDSZ);
+    static_assert(lds <= 160 * 1024, "gemm16: LDS image exceeds 160 KiB");
+    auto kern = gemm_bf16_kernel<OP, BM, BN, WM_, BK, TA, TB, TC, P, VAR, EOP>;
+    if (lds > 64 * 1024) {
+        static bool attr = false;                      // once per instantiation
+        if (!attr) {
+            PPO_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            attr = true;
+        }
+    }
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT_), lds, ppo::stream(), a);
     PPO_LAUNCH_CHECK();
 }
 
@@ -526,16 +618,31 @@ int pick16(int M, int N, int op = OP_NT) {
 int g_force3 = -1;
 int g_split3 = 0;
 
-template <int OP, typename TA, typename TB, typename TC>
+template <int OP, typename TA, typename TB, typename TC, int EOP = OP>
 void launch_cfg3(int c, const Args& a) {
     switch (c) {
-        case 1: launch<OP, 128, 32, 4, 32, TA, TB, TC, 3>(a); break;
-        case 2: launch<OP, 32, 128, 1, 32, TA, TB, TC, 3>(a); break;
-        case 3: launch<OP, 64, 64, 2, 32, TA, TB, TC, 3>(a); break;
-        default: launch<OP, 128, 128, 2, 32, TA, TB, TC, 3>(a); break;
+        case 1: launch<OP, 128, 32, 4, 32, TA, TB, TC, 3, 0, EOP>(a); break;
+        case 2: launch<OP, 32, 128, 1, 32, TA, TB, TC, 3, 0, EOP>(a); break;
+        case 3: launch<OP, 64, 64, 2, 32, TA, TB, TC, 3, 0, EOP>(a); break;
+        case 4: launch<OP, 128, 128, 2, 64, TA, TB, TC, 3, 0, EOP>(a); break;   // 110 KiB LDS: 1 workgroup per CU
+        case 5: launch<OP, 128, 128, 2, 32, TA, TB, TC, 3, 1, EOP>(a); break;   // fp32 images, split at read
+        case 6:                                                                  // + double-buffered image
+            if constexpr (OP == OP_TN) launch<OP, 128, 128, 2, 32, TA, TB, TC, 3, 0, EOP>(a);
+            else launch<OP, 128, 128, 2, 32, TA, TB, TC, 3, 2, EOP>(a);
+            break;
+        default: launch<OP, 128, 128, 2, 32, TA, TB, TC, 3, 0, EOP>(a); break;
     }
 }
-constexpr Cfg kCfgs3[] = {{128, 128, 32}, {128, 32, 32}, {32, 128, 32}, {64, 64, 32}};
+constexpr Cfg kCfgs3[] = {{128, 128, 32}, {128, 32, 32}, {32, 128, 32}, {64, 64, 32}, {128, 128, 64},
+                          {128, 128, 32}, {128, 128, 32}};
+int g_flags3 = -1;          // PPO_X3_FLAGS (read once)
+int flags3() {
+    if (g_flags3 < 0) {
+        const char* e = getenv("PPO_X3_FLAGS");
+        g_flags3 = e ? atoi(e) : 0;
+    }
+    return g_flags3;
+}
 
 int pick3(int M, int N) {
     if (g_force3 >= 0) return g_force3;
@@ -671,6 +778,7 @@ void phip_linear_x3_fwd(phip_opnd y, phip_opnd x, const int* ridx, float* xcopy,
     PPO_REQUIRE(W.planes || (!x.planes && !y.planes), "phip_linear_x3_fwd: unsupported storage combination");
     ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l);
     Args a{};
+    a.flags = flags3();
     a.A = x.p; a.lda = n; a.B = W.p; a.ldb = n; a.C = y.p; a.ldc = l;
     a.psA = x.pstride; a.psB = W.pstride; a.psC = y.pstride;
     a.M = m; a.N = l; a.K = n; a.kchunk = n; a.splits = 1;
@@ -685,12 +793,26 @@ void phip_linear_x3_fwd(phip_opnd y, phip_opnd x, const int* ridx, float* xcopy,
     else launch_cfg3<OP_NT, b16, b16, b16>(c, a);
 }
 
-void phip_linear_x3_bwd_x(phip_opnd gx, phip_opnd g, phip_opnd W, const unsigned* bits, int m, int n, int l) {
+void phip_linear_x3_bwd_x(phip_opnd gx, phip_opnd g, phip_opnd W, const float* Wt, const unsigned* bits, int m,
+                          int n, int l) {
     if (m <= 0 || n <= 0) return;
     PPO_REQUIRE(gx.p && g.p && W.p && l > 0, "phip_linear_x3_bwd_x: null operand");
+    if (Wt && !g.planes && !gx.planes) {
+        // gx = g·W as an NT product against Wᵀ [n, l]: both operands k-contiguous fp32
+        ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l);
+        Args a{};
+        a.flags = flags3();
+        a.A = g.p; a.lda = l; a.B = Wt; a.ldb = l; a.C = gx.p; a.ldc = n;
+        a.M = m; a.N = n; a.K = l; a.kchunk = l; a.splits = 1;
+        a.bits_in = bits; a.wpr = ppo_divup(n, 32);
+        a.vec = l % 4 == 0 && al16(g.p) && al16(Wt);
+        launch_cfg3<OP_NT, f32, f32, f32, OP_NN>(pick3(m, n), a);
+        return;
+    }
     PPO_REQUIRE(W.planes || (!g.planes && !gx.planes), "phip_linear_x3_bwd_x: unsupported storage combination");
     ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l);
     Args a{};
+    a.flags = flags3();
     a.A = g.p; a.lda = l; a.B = W.p; a.ldb = n; a.C = gx.p; a.ldc = n;
     a.psA = g.pstride; a.psB = W.pstride; a.psC = gx.pstride;
     a.M = m; a.N = n; a.K = l; a.kchunk = l; a.splits = 1;
@@ -726,6 +848,7 @@ void phip_linear_x3_bwd_w(float* gW, float* gb, phip_opnd g, phip_opnd x, int m,
     int kchunk = ppo_divup(ppo_divup(m, splits), BK) * BK;
     splits = ppo_divup(m, kchunk);
     Args a{};
+    a.flags = flags3();
     a.A = g.p; a.lda = l; a.B = x.p; a.ldb = n; a.C = gW; a.ldc = n;
     a.psA = g.pstride; a.psB = x.pstride;
     a.M = l; a.N = n; a.K = m; a.kchunk = kchunk; a.splits = splits;
@@ -794,7 +917,9 @@ double ppo_bench_gemm_x3(int op, int m, int n, int l, int iters, int cfg, int sp
                                        l, 1, bits);
         else if (o == 3) phip_linear_x3_fwd(F(y), PLo(x, (long)sx), nullptr, nullptr, PLo(w3, (long)sw), b, m, n, l,
                                             0, nullptr);
-        else if (o == 1) phip_linear_x3_bwd_x(PLo(x, (long)sx), PLo(y, (long)sy), PLo(w3, (long)sw), bits, m, n, l);
+        else if (o == 1) phip_linear_x3_bwd_x(PLo(x, (long)sx), PLo(y, (long)sy), PLo(w3, (long)sw), nullptr, bits, m,
+                                              n, l);
+        else if (o == 4) phip_linear_x3_bwd_x(F(x), F(y), F(W), W, bits, m, n, l);     // grad_x against Wᵀ
         else phip_linear_x3_bwd_w(gw, b, PLo(y, (long)sy), PLo(x, (long)sx), m, n, l, 0);
     };
     for (int i = 0; i < 3; ++i) run();

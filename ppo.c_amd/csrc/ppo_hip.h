@@ -77,7 +77,9 @@ void phip_linear16_bwd_w(float* gW, float* gb, const void* g, int tg, const void
 typedef struct { void* p; int planes; long pstride; } phip_opnd;
 void phip_linear_x3_fwd(phip_opnd y, phip_opnd x, const int* ridx, float* xcopy, phip_opnd W, const float* b,
                         int m, int n, int l, int relu, unsigned* bits);
-void phip_linear_x3_bwd_x(phip_opnd gx, phip_opnd g, phip_opnd W, const unsigned* bits, int m, int n, int l);
+/* Wt (optional, fp32 [n, l]): grad_x computed as an NT product against Wᵀ (fp32 g and gx only) */
+void phip_linear_x3_bwd_x(phip_opnd gx, phip_opnd g, phip_opnd W, const float* Wt, const unsigned* bits, int m,
+                          int n, int l);
 void phip_linear_x3_bwd_w(float* gW, float* gb, phip_opnd g, phip_opnd x, int m, int n, int l, int zeroed);
 /* dst (three bf16 planes, plane stride m·S) = split(src[rows[i], :]) for i < m: layer 0's gather
  * in the x3 engine's update path; rows == NULL: rows 0..m-1 */

@@ -196,7 +196,7 @@ void lin_fwd(float* y, const float* x, const float* W, const float* b, int m, in
     else phip_linear_fwd(y, x, W, b, m, n, l, 0);
 }
 void lin_bwd_x(float* gx, const float* g, const float* W, int m, int n, int l) {
-    if (use_x3(m)) phip_linear_x3_bwd_x(opf(gx), opf(g), opf(W), NULL, m, n, l);
+    if (use_x3(m)) phip_linear_x3_bwd_x(opf(gx), opf(g), opf(W), NULL, NULL, m, n, l);
     else phip_linear_bwd_x(gx, g, W, NULL, m, n, l);
 }
 void lin_bwd_w(float* gW, const float* g, const float* x, int m, int n, int l) {
@@ -311,7 +311,7 @@ void nn_backward_dev(NeuralNetwork* nn, const float* d_grad_out, int m, int want
             if (want_gx && (!relu_in || bits)) {
                 gx_pl = planar && g_x3_planar != 2 && i > 0 && use_x3_layer(m, nn->layers[i - 1].input_size, n);
                 const phip_opnd W = planar ? oppl(nn->d_w3 + nn->param_offset[i], w3_stride(nn)) : opf(ly->d_weights);
-                phip_linear_x3_bwd_x(gx_pl ? oppl(ly->d_grad_x, (long)m * n) : opf(ly->d_grad_x), go, W, bits, m, n, l);
+                phip_linear_x3_bwd_x(gx_pl ? oppl(ly->d_grad_x, (long)m * n) : opf(ly->d_grad_x), go, W, NULL, bits, m, n, l);
             } else if (want_gx) {
                 if (g_pl || xo.planes) die("nn_backward_dev: pre-split operands without this forward's ReLU bits");
                 phip_linear_bwd_x_bits(ly->d_grad_x, g, ly->d_weights, ly->d_input, NULL, m, n, l);

@@ -3,7 +3,8 @@
 fp32-MFMA engine, on the MI355X: device µs and algorithmic fp32 TFLOP/s per (op, shape, config).
 
     python ppo.c_amd/tools/gemm_x3_sweep.py [--shapes 32768,512,512;32768,376,512] [--cfgs -1,0,3]
-op 0 = forward (bias+ReLU+bits), 1 = grad_x (bit mask), 2 = grad_W (split-K), 3 = forward, no activation;
+op 0 = forward (bias+ReLU+bits), 1 = grad_x (bit mask), 2 = grad_W (split-K), 3 = forward, no activation,
+4 = grad_x as an NT product against a transposed fp32 weight copy;
 op + 10 = the same with pre-split (three bf16 plane) operands and outputs, the update path's storage.
 """
 import argparse
@@ -13,7 +14,8 @@ import sys
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 import ppo_ffi  # noqa: E402
 
-NAMES = {-1: "auto", 0: "128x128/bk32", 1: "128x32/bk32", 2: "32x128/bk32", 3: "64x64/bk32"}
+NAMES = {-1: "auto", 0: "128x128/bk32", 1: "128x32/bk32", 2: "32x128/bk32", 3: "64x64/bk32", 4: "128x128/bk64",
+         5: "128x128 fp32img", 6: "128x128 fp32img db"}
 
 
 def main():
@@ -31,7 +33,7 @@ def main():
             if op == 0 and l < 32:
                 op = 3
             flop = 2.0 * m * n * l
-            ex = lib.ppo_bench_gemm(op % 10, m, n, l, 20, -1)
+            ex = lib.ppo_bench_gemm(1 if op % 10 == 4 else op % 10, m, n, l, 20, -1)
             print(f"op{op} m={m} n={n} l={l} exact-f32 auto        {ex:9.1f} us {flop / ex / 1e6:8.1f} TF/s", flush=True)
             for cfg in (int(c) for c in args.cfgs.split(",")):
                 for tgt in ([int(s) for s in args.splits.split(",")] if op == 2 else [0]):
