@@ -645,7 +645,7 @@ Args bwd_w_args(float* gW, float* gb, const float* g, const float* x, int m, int
     a.vec_a = (l % 4 == 0) && aligned16(g);             // mncont, extent M = l, ld = l
     a.vec_b = (n % 4 == 0) && aligned16(x);             // mncont, extent N = n, ld = n
     const long tiles = (long)ppo_divup(l, tc.bm) * ppo_divup(n, tc.bn);
-    int splits = (int)((target + tiles - 1) / tiles);
+    int splits = (int)(target / tiles);                 // the grid stays within the target's rounds
     const int max_splits = m / (8 * tc.bk) > 0 ? m / (8 * tc.bk) : 1;     // ≥ 8 k-tiles per split
     if (splits > max_splits) splits = max_splits;
     if (splits < 1) splits = 1;

@@ -741,7 +741,7 @@ void phip_linear16_bwd_w(float* gW, float* gb, const void* g, int tg, const void
     const int BK = kCfgs[c].bk;
     const long tiles = (long)ppo_divup(l, kCfgs[c].bm) * ppo_divup(n, kCfgs[c].bn);
     const int target = g_split16 > 0 ? g_split16 : (c == 6 ? 256 : 512);
-    int splits = (int)((target + tiles - 1) / tiles);
+    int splits = (int)(target / tiles);                 // at or below one round (see x3 bwd_w)
     const int max_splits = m / (4 * BK) > 0 ? m / (4 * BK) : 1;          // ≥ 4 k-tiles per split
     if (splits > max_splits) splits = max_splits;
     if (splits < 1) splits = 1;
@@ -840,8 +840,11 @@ void phip_linear_x3_bwd_w(float* gW, float* gb, phip_opnd g, phip_opnd x, int m,
     const int c = pick3(l, n);
     const int BK = kCfgs3[c].bk;
     const long tiles = (long)ppo_divup(l, kCfgs3[c].bm) * ppo_divup(n, kCfgs3[c].bn);
+    // target = workgroup slots of one round (2 per CU): the grid stays at or below it (rounding
+    // the split count up would put the last few workgroups into a second round — 516 workgroups
+    // for the 512 x 376 layer-0 gradient, 142 us instead of ~100)
     const int target = g_split3 > 0 ? g_split3 : 512;
-    int splits = (int)((target + tiles - 1) / tiles);
+    int splits = (int)(target / tiles);
     const int max_splits = m / (4 * BK) > 0 ? m / (4 * BK) : 1;          // ≥ 4 k-tiles per split
     if (splits > max_splits) splits = max_splits;
     if (splits < 1) splits = 1;

@@ -1,1 +1,6 @@
-for f in 0 1; do echo "PPO_X3_FLAGS=$f"; PPO_X3_FLAGS=$f timeout -k 10 200 python ppo.c_amd/tools/gemm_x3_sweep.py --ops=0,1,4,2 --cfgs=0,5,6 --shapes="32768,512,512;32768,376,512" || exit 1; done > gpurun_out/x3_sweep4.txt 2>&1
+for i in 1 2; do
+timeout -k 10 400 python bench.py --no-rollout --no-cpu-baseline --steps 8 > gpurun_out/ab_floor$i.json 2>/dev/null || exit 1
+PPO_SPLIT_CEIL=1 timeout -k 10 400 python bench.py --no-rollout --no-cpu-baseline --steps 8 > gpurun_out/ab_ceil$i.json 2>/dev/null || exit 1
+PPO_SERIAL=1 timeout -k 10 400 python bench.py --no-rollout --no-cpu-baseline --steps 8 > gpurun_out/ab_sfloor$i.json 2>/dev/null || exit 1
+PPO_SERIAL=1 PPO_SPLIT_CEIL=1 timeout -k 10 400 python bench.py --no-rollout --no-cpu-baseline --steps 8 > gpurun_out/ab_sceil$i.json 2>/dev/null || exit 1
+done
