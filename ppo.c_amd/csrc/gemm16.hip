@@ -162,7 +162,7 @@ struct Stage16 {
         }
     }
 
-    __device__ __forceinline__ void store(unsigned short* img, int tid) const {
+    __device__ __forceinline__ void store(unsigned short* img, int tid, bool nosplit = false) const {
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) {
             const int idx = tid + it * NT_;
@@ -178,6 +178,12 @@ struct Stage16 {
 #pragma unroll
                     for (int q = 0; q < NV; ++q)
                         *reinterpret_cast<u32x4*>(d + q * IMG) = kok[it] ? v[it * NV + q] : z;
+                } else if (F32 && P == 3 && nosplit) {          // ablation (PPO_X3_FLAGS & 8): no split
+                    const f32x4 f = __builtin_bit_cast(f32x4, x);
+                    const u32x2 p = {pack2(f[0], f[1]), pack2(f[2], f[3])};
+                    *reinterpret_cast<u32x2*>(d) = p;
+                    *reinterpret_cast<u32x2*>(d + IMG) = p;
+                    *reinterpret_cast<u32x2*>(d + 2 * IMG) = p;
                 } else if (F32 && P == 3) {
                     // exact 3-way split x = x0 + x1 + x2 (each bf16, round-to-nearest): x0 holds the
                     // top 8 significant bits, the residual x − x0 has ≤ 16 and x1 takes 8 of them, so
@@ -327,7 +333,7 @@ template <> struct Bits<unsigned short> { static constexpr int code = 1; };
 // computed as an NT product against Wᵀ uses OP_NT staging with the OP_NN epilogue).
 template <int OP, int BM, int BN, int WARPS_M, int BK, typename TA, typename TB, typename TC, int P, int VAR = 0,
           int EOP = OP>
-__global__ __launch_bounds__(NT_, 2) void gemm_bf16_kernel(Args a) {
+__global__ __launch_bounds__(VAR == 3 ? 2 * NT_ : NT_, VAR == 3 ? 1 : 2) void gemm_bf16_kernel(Args a) {
     constexpr int WARPS_N = 4 / WARPS_M;
     constexpr int WM = BM / WARPS_M, WN = BN / WARPS_N;
     constexpr int TM = WM / 32, TN = WN / 32;
@@ -345,18 +351,34 @@ __global__ __launch_bounds__(NT_, 2) void gemm_bf16_kernel(Args a) {
     extern __shared__ __attribute__((aligned(16))) unsigned short lds[];     // (SA::IMG + SB::IMG) * P
     const bool prio = (a.flags & 1) != 0;
 
+    // VAR 3 (ping-pong): a 512-thread workgroup holds two independent 256-thread groups, each with
+    // its own output tile (tiles 2·t' and 2·t' + 1) and LDS image; one group splits and stages
+    // while the other runs its MFMAs, then they swap (see the VAR 3 loop below)
+    constexpr bool PP = VAR == 3;
+    const int grp = PP ? (int)(threadIdx.x >> 8) : 0;
     const int nwg = gridDim.x, b = blockIdx.x;
     const int xcd = b & 7, qq = nwg >> 3, rr = nwg & 7;
-    const int t = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (b >> 3);
+    const int t1 = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (b >> 3);
+    const int total = a.tiles_m * a.tiles_n * a.splits;
+    auto tile_k = [&](int tt, int& kb, int& ke) {        // k range of linear tile tt (empty if none)
+        if (tt >= total) { kb = ke = 0; return; }
+        kb = (tt / (a.tiles_n * a.tiles_m)) * a.kchunk;
+        ke = min(a.K, kb + a.kchunk);
+    };
+    const int t = PP ? 2 * t1 + grp : t1;
+    const bool has_tile = !PP || t < total;
     const int tn = t % a.tiles_n;
     const int rest = t / a.tiles_n;
     const int tm = rest % a.tiles_m;
-    const int split = rest / a.tiles_m;
     const int m0 = tm * BM, n0 = tn * BN;
-    const int kbeg = split * a.kchunk;
-    const int kend = min(a.K, kbeg + a.kchunk);
+    int kbeg, kend;
+    tile_k(PP ? t : 0, kbeg, kend);
+    if (!PP) {
+        kbeg = (rest / a.tiles_m) * a.kchunk;
+        kend = min(a.K, kbeg + a.kchunk);
+    }
 
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x & (NT_ - 1), lane = tid & 63, w = tid >> 6;
     const int wm = w / WARPS_N, wn = w % WARPS_N;
     const int r = lane & 31, h = lane >> 5;
 
@@ -370,14 +392,14 @@ __global__ __launch_bounds__(NT_, 2) void gemm_bf16_kernel(Args a) {
 
     constexpr int TPR = NT_ / BM > 0 ? NT_ / BM : 1;
     constexpr int KPT = BK / TPR > 0 ? BK / TPR : 1;
-    const bool do_bsum = OP == OP_TN && EOP == OP_TN && a.gbias != nullptr && tn == 0 && (NT_ % BM == 0);
+    const bool do_bsum = OP == OP_TN && EOP == OP_TN && a.gbias != nullptr && tn == 0 && (NT_ % BM == 0) && has_tile;
     float bsum = 0.f;
 
     SA sa;
     SB sb;
     if (!A_MN) sa.prep(OP == OP_NT ? a.ridx : nullptr, m0, a.M, tid);
     if (!B_MN) sb.prep(nullptr, n0, a.N, tid);
-    const bool do_copy = OP == OP_NT && a.acopy != nullptr && tn == 0;
+    const bool do_copy = OP == OP_NT && a.acopy != nullptr && tn == 0 && has_tile;
     const bool vec = a.vec != 0;
     const TA* __restrict__ PA = static_cast<const TA*>(a.A);
     const TB* __restrict__ PB = static_cast<const TB*>(a.B);
@@ -428,13 +450,57 @@ __global__ __launch_bounds__(NT_, 2) void gemm_bf16_kernel(Args a) {
         }
         if (prio) __builtin_amdgcn_s_setprio(0);
     };
+    // PPO_X3_FLAGS ablations (timing diagnostics only, results wrong): 4 = no reload after the first
+    // k-tile, 8 = no split (plane 0 in every plane), 16 = no MFMAs
+    const bool nosplit = (a.flags & 8) != 0, noreload = (a.flags & 4) != 0, nomfma = (a.flags & 16) != 0;
     auto stage = [&](unsigned short* img, int k0) {
         if (do_copy) sa.copy_out(a.acopy, a.K, m0, a.M, k0, kend, tid);
-        sa.store(img, tid);
-        sb.store(img + SA::LDSZ, tid);
+        sa.store(img, tid, nosplit);
+        sb.store(img + SA::LDSZ, tid, nosplit);
     };
 
-    if constexpr (DB) {
+    if constexpr (PP) {
+        // Ping-pong over two groups (one wave of each on every SIMD).  Phase A: group 0 splits and
+        // stages its tile it while group 1 multiplies its tile it−1; phase B: group 0 multiplies tile
+        // it while group 1 stages tile it.  The barrier between phases orders each group's LDS
+        // write before its reads and its reads before its next write (one image per group), and
+        // keeps the two groups half a k-tile apart, so one SIMD's MFMA pipe runs one group's
+        // products while the other group's split (VALU) and LDS stores issue beside them.
+        unsigned short* img = lds + grp * BUF;
+        int kb0, ke0, kb1, ke1;
+        tile_k(2 * t1, kb0, ke0);
+        tile_k(2 * t1 + 1, kb1, ke1);
+        const int nk0 = ke0 > kb0 ? (ke0 - kb0 + BK - 1) / BK : 0;
+        const int nk1 = ke1 > kb1 ? (ke1 - kb1 + BK - 1) / BK : 0;
+        const int nk = grp ? nk1 : nk0, nkmax = max(nk0, nk1);
+        if (nk > 0) load(kbeg);
+        auto stage_it = [&](int it) {
+            const int k0 = kbeg + it * BK;
+            stage(img, k0);
+            if (it + 1 < nk && !noreload) load(k0 + BK);   // in flight through the partner's phase
+        };
+        auto compute_it = [&]() {
+            if (do_bsum) bsum += SA::rowsum(img, tid / TPR, (tid % TPR) * KPT, KPT);
+            if (!nomfma) compute(img);
+        };
+        for (int it = 0; it < nkmax; ++it) {
+            if (grp == 0) {
+                if (it < nk) stage_it(it);
+            } else if (it >= 1 && it <= nk) {
+                compute_it();
+            }
+            __syncthreads();
+            if (grp == 0) {
+                if (it < nk) compute_it();
+            } else if (it < nk) {
+                stage_it(it);
+            }
+            __syncthreads();
+        }
+        // group 1's last tile runs beside group 0's epilogue (no barrier after this point)
+        if (grp == 1 && nk > 0 && nk == nkmax) compute_it();
+        if (!has_tile) return;
+    } else if constexpr (DB) {
         // double-buffered image: tile t+1's loads fly during tile t's MFMAs and are written into the
         // other image right after them; one barrier per k-tile
         if (kbeg < kend) {
@@ -456,9 +522,9 @@ __global__ __launch_bounds__(NT_, 2) void gemm_bf16_kernel(Args a) {
         for (int k0 = kbeg; k0 < kend; k0 += BK) {
             stage(lds, k0);
             __syncthreads();
-            if (k0 + BK < kend) load(k0 + BK);            // in flight during this tile's MFMAs
+            if (k0 + BK < kend && !noreload) load(k0 + BK);   // in flight during this tile's MFMAs
             if (do_bsum) bsum += SA::rowsum(lds, tid / TPR, (tid % TPR) * KPT, KPT);
-            compute(lds);
+            if (!nomfma) compute(lds);
             __syncthreads();
         }
     }
@@ -551,10 +617,11 @@ void launch(Args a) {
     a.tiles_m = ppo_divup(a.M, BM);
     a.tiles_n = ppo_divup(a.N, BN);
     if (a.splits < 1) a.splits = 1;
-    const long grid = (long)a.tiles_m * a.tiles_n * a.splits;
-    PPO_REQUIRE(grid > 0 && grid < (1L << 31), "gemm16: grid out of range");
+    const long tiles = (long)a.tiles_m * a.tiles_n * a.splits;
+    const long grid = VAR == 3 ? (tiles + 1) / 2 : tiles;
+    PPO_REQUIRE(grid > 0 && tiles < (1L << 31), "gemm16: grid out of range");
     constexpr bool A_MN = OP == OP_TN, B_MN = OP != OP_NT;
-    constexpr size_t lds = sizeof(unsigned short) * (VAR == 2 ? 2 : 1) *
+    constexpr size_t lds = sizeof(unsigned short) * (VAR == 2 || VAR == 3 ? 2 : 1) *
                            (Stage16<BM, BK, A_MN, TA, P, VAR >= 1 && !A_MN && sizeof(TA) == 4>::LDSZ +
                             Stage16<BN, BK, B_MN, TB, P, VAR >= 1 && !B_MN && sizeof(TB) == 4>::LDSZ);
     static_assert(lds <= 160 * 1024, "gemm16: LDS image exceeds 160 KiB");
@@ -566,7 +633,7 @@ void launch(Args a) {
             attr = true;
         }
     }
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NT_), lds, ppo::stream(), a);
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(VAR == 3 ? 2 * NT_ : NT_), lds, ppo::stream(), a);
     PPO_LAUNCH_CHECK();
 }
 
@@ -630,11 +697,12 @@ void launch_cfg3(int c, const Args& a) {
             if constexpr (OP == OP_TN) launch<OP, 128, 128, 2, 32, TA, TB, TC, 3, 0, EOP>(a);
             else launch<OP, 128, 128, 2, 32, TA, TB, TC, 3, 2, EOP>(a);
             break;
+        case 7: launch<OP, 128, 128, 2, 32, TA, TB, TC, 3, 3, EOP>(a); break;   // ping-pong pair of tiles
         default: launch<OP, 128, 128, 2, 32, TA, TB, TC, 3, 0, EOP>(a); break;
     }
 }
 constexpr Cfg kCfgs3[] = {{128, 128, 32}, {128, 32, 32}, {32, 128, 32}, {64, 64, 32}, {128, 128, 64},
-                          {128, 128, 32}, {128, 128, 32}};
+                          {128, 128, 32}, {128, 128, 32}, {128, 128, 32}};
 int g_flags3 = -1;          // PPO_X3_FLAGS (read once)
 int flags3() {
     if (g_flags3 < 0) {
