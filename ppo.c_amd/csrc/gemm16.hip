@@ -327,18 +327,22 @@ template <typename T> struct Bits;
 template <> struct Bits<float> { static constexpr int code = 0; };
 template <> struct Bits<unsigned short> { static constexpr int code = 1; };
 
+constexpr bool var_fpi(int v) { return v == 1 || v == 2 || v == 4 || v == 6; }   // fp32 images, split at read
+constexpr bool var_pp(int v) { return v == 3 || v == 6; }                          // ping-pong tile pair
+constexpr bool var_pipe(int v) { return v == 4 || v == 6; }                        // pipelined split at read
+
 // VAR (x3 only): 0 = operands split into plane images at LDS-store time; 1 = k-contiguous fp32
 // operands staged as fp32 and split at fragment read; 2 = as 1 with a double-buffered LDS image (one
 // barrier per k-tile, the next tile's LDS write after this tile's MFMAs).  EOP = epilogue op (grad_x
 // computed as an NT product against Wᵀ uses OP_NT staging with the OP_NN epilogue).
 template <int OP, int BM, int BN, int WARPS_M, int BK, typename TA, typename TB, typename TC, int P, int VAR = 0,
           int EOP = OP>
-__global__ __launch_bounds__(VAR == 3 ? 2 * NT_ : NT_, VAR == 3 ? 1 : 2) void gemm_bf16_kernel(Args a) {
+__global__ __launch_bounds__(var_pp(VAR) ? 2 * NT_ : NT_, var_pp(VAR) ? 1 : 2) void gemm_bf16_kernel(Args a) {
     constexpr int WARPS_N = 4 / WARPS_M;
     constexpr int WM = BM / WARPS_M, WN = BN / WARPS_N;
     constexpr int TM = WM / 32, TN = WN / 32;
     constexpr bool A_MN = OP == OP_TN, B_MN = OP != OP_NT;
-    constexpr bool FPA = VAR >= 1 && !A_MN && sizeof(TA) == 4, FPB = VAR >= 1 && !B_MN && sizeof(TB) == 4;
+    constexpr bool FPA = var_fpi(VAR) && !A_MN && sizeof(TA) == 4, FPB = var_fpi(VAR) && !B_MN && sizeof(TB) == 4;
     constexpr bool DB = VAR == 2;
     using SA = Stage16<BM, BK, A_MN, TA, P, FPA>;
     using SB = Stage16<BN, BK, B_MN, TB, P, FPB>;
@@ -354,7 +358,7 @@ __global__ __launch_bounds__(VAR == 3 ? 2 * NT_ : NT_, VAR == 3 ? 1 : 2) void ge
     // VAR 3 (ping-pong): a 512-thread workgroup holds two independent 256-thread groups, each with
     // its own output tile (tiles 2·t' and 2·t' + 1) and LDS image; one group splits and stages
     // while the other runs its MFMAs, then they swap (see the VAR 3 loop below)
-    constexpr bool PP = VAR == 3;
+    constexpr bool PP = var_pp(VAR);
     const int grp = PP ? (int)(threadIdx.x >> 8) : 0;
     const int nwg = gridDim.x, b = blockIdx.x;
     const int xcd = b & 7, qq = nwg >> 3, rr = nwg & 7;
@@ -414,6 +418,56 @@ __global__ __launch_bounds__(VAR == 3 ? 2 * NT_ : NT_, VAR == 3 ? 1 : 2) void ge
         const unsigned short* As = img;
         const unsigned short* Bs = img + SA::LDSZ;
         if (prio) __builtin_amdgcn_s_setprio(1);
+        if constexpr (var_pipe(VAR)) {
+            // fp32 images split at read, software-pipelined: k-step 1's fragment reads and splits
+            // are interleaved with k-step 0's MFMAs (≈ 6 VALU per MFMA fill the MFMA's issue gap)
+            static_assert(BK == 32, "two k-steps per tile");
+            bf16x8 fa[2][P][TM], fb[2][P][TN];
+            auto frags = [&](int ks, bf16x8 (&xa)[P][TM], bf16x8 (&xb)[P][TN]) {
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    if constexpr (FPA) SA::frag3(As, wm * WM + i * 32 + r, ks, lane, xa[0][i], xa[1][i], xa[2][i]);
+                    else
+#pragma unroll
+                        for (int p = 0; p < P; ++p) xa[p][i] = SA::frag(As + p * SA::IMG, wm * WM + i * 32 + r, ks, lane);
+                }
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    if constexpr (FPB) SB::frag3(Bs, wn * WN + j * 32 + r, ks, lane, xb[0][j], xb[1][j], xb[2][j]);
+                    else
+#pragma unroll
+                        for (int p = 0; p < P; ++p) xb[p][j] = SB::frag(Bs + p * SB::IMG, wn * WN + j * 32 + r, ks, lane);
+                }
+            };
+            auto mfmas = [&](const bf16x8 (&xa)[P][TM], const bf16x8 (&xb)[P][TN]) {
+#pragma unroll
+                for (int q = 0; q < 6; ++q) {
+                    constexpr int pa_[6] = {2, 0, 1, 1, 0, 0}, pb_[6] = {0, 2, 1, 0, 1, 0};
+#pragma unroll
+                    for (int i = 0; i < TM; ++i)
+#pragma unroll
+                        for (int j = 0; j < TN; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(xa[pa_[q]][i], xb[pb_[q]][j], acc[i][j],
+                                                                                0, 0, 0);
+                }
+            };
+            frags(0, fa[0], fb[0]);
+            frags(1, fa[1], fb[1]);
+            mfmas(fa[0], fb[0]);
+            mfmas(fa[1], fb[1]);
+            constexpr int NM = 6 * TM * TN;                 // MFMAs per k-step
+            __builtin_amdgcn_sched_group_barrier(0x100, 4 * (TM + TN), 0);   // k-step 0 reads
+            __builtin_amdgcn_sched_group_barrier(0x002, 200, 0);             // k-step 0 splits
+            __builtin_amdgcn_sched_group_barrier(0x100, 4 * (TM + TN), 0);   // k-step 1 reads
+#pragma unroll
+            for (int q = 0; q < NM; ++q) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 7, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
+            if (prio) __builtin_amdgcn_s_setprio(0);
+            return;
+        }
 #pragma unroll
         for (int ks = 0; ks < BK / 16; ++ks) {
             bf16x8 fa[P][TM], fb[P][TN];
@@ -618,12 +672,12 @@ void launch(Args a) {
     a.tiles_n = ppo_divup(a.N, BN);
     if (a.splits < 1) a.splits = 1;
     const long tiles = (long)a.tiles_m * a.tiles_n * a.splits;
-    const long grid = VAR == 3 ? (tiles + 1) / 2 : tiles;
+    const long grid = var_pp(VAR) ? (tiles + 1) / 2 : tiles;
     PPO_REQUIRE(grid > 0 && tiles < (1L << 31), "gemm16: grid out of range");
     constexpr bool A_MN = OP == OP_TN, B_MN = OP != OP_NT;
-    constexpr size_t lds = sizeof(unsigned short) * (VAR == 2 || VAR == 3 ? 2 : 1) *
-                           (Stage16<BM, BK, A_MN, TA, P, VAR >= 1 && !A_MN && sizeof(TA) == 4>::LDSZ +
-                            Stage16<BN, BK, B_MN, TB, P, VAR >= 1 && !B_MN && sizeof(TB) == 4>::LDSZ);
+    constexpr size_t lds = sizeof(unsigned short) * (VAR == 2 || var_pp(VAR) ? 2 : 1) *
+                           (Stage16<BM, BK, A_MN, TA, P, var_fpi(VAR) && !A_MN && sizeof(TA) == 4>::LDSZ +
+                            Stage16<BN, BK, B_MN, TB, P, var_fpi(VAR) && !B_MN && sizeof(TB) == 4>::LDSZ);
     static_assert(lds <= 160 * 1024, "gemm16: LDS image exceeds 160 KiB");
     auto kern = gemm_bf16_kernel<OP, BM, BN, WM_, BK, TA, TB, TC, P, VAR, EOP>;
     if (lds > 64 * 1024) {
@@ -633,7 +687,7 @@ void launch(Args a) {
             attr = true;
         }
     }
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(VAR == 3 ? 2 * NT_ : NT_), lds, ppo::stream(), a);
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(var_pp(VAR) ? 2 * NT_ : NT_), lds, ppo::stream(), a);
     PPO_LAUNCH_CHECK();
 }
 
@@ -698,11 +752,13 @@ void launch_cfg3(int c, const Args& a) {
             else launch<OP, 128, 128, 2, 32, TA, TB, TC, 3, 2, EOP>(a);
             break;
         case 7: launch<OP, 128, 128, 2, 32, TA, TB, TC, 3, 3, EOP>(a); break;   // ping-pong pair of tiles
+        case 8: launch<OP, 128, 128, 2, 32, TA, TB, TC, 3, 4, EOP>(a); break;   // fp32 images, pipelined split
+        case 9: launch<OP, 128, 128, 2, 32, TA, TB, TC, 3, 6, EOP>(a); break;   // ping-pong + cfg 8
         default: launch<OP, 128, 128, 2, 32, TA, TB, TC, 3, 0, EOP>(a); break;
     }
 }
 constexpr Cfg kCfgs3[] = {{128, 128, 32}, {128, 32, 32}, {32, 128, 32}, {64, 64, 32}, {128, 128, 64},
-                          {128, 128, 32}, {128, 128, 32}, {128, 128, 32}};
+                          {128, 128, 32}, {128, 128, 32}, {128, 128, 32}, {128, 128, 32}, {128, 128, 32}};
 int g_flags3 = -1;          // PPO_X3_FLAGS (read once)
 int flags3() {
     if (g_flags3 < 0) {
@@ -712,12 +768,17 @@ int flags3() {
     return g_flags3;
 }
 
-int pick3(int M, int N) {
+// cfg 8 (fp32 images split at fragment read, pipelined behind the MFMAs) is 3-6 % faster per
+// isolated NT / NN launch (C4 forward 138 -> 129 us, grad_x 118 -> 114 us) but the whole C4 update
+// measured 1 % slower with it (profiles/r01_x3_pipelined.txt): PPO_X3_PIPE=1 selects it, cfg 0 is
+// the default
+int pick3(int M, int N, int op = OP_TN) {
     if (g_force3 >= 0) return g_force3;
     if (N <= 32 && M > 32) return 1;
     if (M <= 32 && N > 32) return 2;
     if (M <= 64 || N <= 64) return 3;
-    return 0;
+    static const int pipe = getenv("PPO_X3_PIPE") ? 8 : 0;
+    return op == OP_TN ? 0 : pipe;
 }
 
 inline bool al16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
@@ -853,7 +914,7 @@ void phip_linear_x3_fwd(phip_opnd y, phip_opnd x, const int* ridx, float* xcopy,
     a.bias = b; a.relu = relu; a.ridx = ridx; a.acopy = ridx ? xcopy : nullptr;
     a.bits_out = relu ? bits : nullptr; a.wpr = ppo_divup(l, 32);
     a.vec = n % eplo(x) == 0 && n % eplo(W) == 0 && al16o(x) && al16o(W);
-    const int c = pick3(m, l);
+    const int c = pick3(m, l, OP_NT);
     if (!W.planes) launch_cfg3<OP_NT, f32, f32, f32>(c, a);
     else if (!x.planes && !y.planes) launch_cfg3<OP_NT, f32, b16, f32>(c, a);
     else if (!x.planes) launch_cfg3<OP_NT, f32, b16, b16>(c, a);
@@ -874,7 +935,7 @@ void phip_linear_x3_bwd_x(phip_opnd gx, phip_opnd g, phip_opnd W, const float* W
         a.M = m; a.N = n; a.K = l; a.kchunk = l; a.splits = 1;
         a.bits_in = bits; a.wpr = ppo_divup(n, 32);
         a.vec = l % 4 == 0 && al16(g.p) && al16(Wt);
-        launch_cfg3<OP_NT, f32, f32, f32, OP_NN>(pick3(m, n), a);
+        launch_cfg3<OP_NT, f32, f32, f32, OP_NN>(pick3(m, n, OP_NT), a);
         return;
     }
     PPO_REQUIRE(W.planes || (!g.planes && !gx.planes), "phip_linear_x3_bwd_x: unsupported storage combination");
@@ -886,7 +947,7 @@ void phip_linear_x3_bwd_x(phip_opnd gx, phip_opnd g, phip_opnd W, const float* W
     a.M = m; a.N = n; a.K = l; a.kchunk = l; a.splits = 1;
     a.bits_in = bits; a.wpr = ppo_divup(n, 32);
     a.vec = l % eplo(g) == 0 && n % eplo(W) == 0 && al16o(g) && al16o(W);
-    const int c = pick3(m, n);
+    const int c = pick3(m, n, OP_NN);
     if (!W.planes) launch_cfg3<OP_NN, f32, f32, f32>(c, a);
     else if (!g.planes && !gx.planes) launch_cfg3<OP_NN, f32, b16, f32>(c, a);
     else if (!g.planes) launch_cfg3<OP_NN, f32, b16, b16>(c, a);

@@ -1,2 +1,5 @@
-timeout -k 10 200 python ppo.c_amd/tools/gemm_x3_sweep.py --ops=0,1,2 --cfgs=0,7 --shapes="32768,512,512;32768,376,512;8192,512,512" > gpurun_out/x3_pp.txt 2>&1 && \
-timeout -k 10 300 python -u -m pytest tests/test_gpu_x3.py -x -q --timeout 120 --timeout-method thread > gpurun_out/x3_pp_test.log 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || exit 1
+for i in 1 2; do
+timeout -k 10 400 python bench.py --no-rollout --no-cpu-baseline --steps 8 > gpurun_out/ab_pipe$i.json 2>/dev/null || exit 1
+PPO_X3_NOPIPE=1 timeout -k 10 400 python bench.py --no-rollout --no-cpu-baseline --steps 8 > gpurun_out/ab_nopipe$i.json 2>/dev/null || exit 1
+done
