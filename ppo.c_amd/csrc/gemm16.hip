@@ -329,6 +329,8 @@ template <> struct Bits<unsigned short> { static constexpr int code = 1; };
 
 constexpr bool var_fpi(int v) { return v == 1 || v == 2 || v == 4 || v == 6; }   // fp32 images, split at read
 constexpr bool var_pp(int v) { return v == 3 || v == 6; }                          // ping-pong tile pair
+constexpr bool var_pc(int v) { return v == 7; }                     // producer / consumer waves, one tile
+constexpr bool var_wide(int v) { return var_pp(v) || var_pc(v); }   // 512-thread workgroups, two images
 constexpr bool var_pipe(int v) { return v == 4 || v == 6; }                        // pipelined split at read
 
 // VAR (x3 only): 0 = operands split into plane images at LDS-store time; 1 = k-contiguous fp32
@@ -337,7 +339,7 @@ constexpr bool var_pipe(int v) { return v == 4 || v == 6; }                     
 // computed as an NT product against Wᵀ uses OP_NT staging with the OP_NN epilogue).
 template <int OP, int BM, int BN, int WARPS_M, int BK, typename TA, typename TB, typename TC, int P, int VAR = 0,
           int EOP = OP>
-__global__ __launch_bounds__(var_pp(VAR) ? 2 * NT_ : NT_, var_pp(VAR) ? 1 : 2) void gemm_bf16_kernel(Args a) {
+__global__ __launch_bounds__(var_wide(VAR) ? 2 * NT_ : NT_, var_wide(VAR) ? 1 : 2) void gemm_bf16_kernel(Args a) {
     constexpr int WARPS_N = 4 / WARPS_M;
     constexpr int WM = BM / WARPS_M, WN = BN / WARPS_N;
     constexpr int TM = WM / 32, TN = WN / 32;
@@ -513,7 +515,58 @@ __global__ __launch_bounds__(var_pp(VAR) ? 2 * NT_ : NT_, var_pp(VAR) ? 1 : 2) v
         sb.store(img + SA::LDSZ, tid, nosplit);
     };
 
-    if constexpr (PP) {
+    if constexpr (var_pc(VAR)) {
+        // Producer / consumer waves (VAR 7): waves 4–7 only load, split and stage; waves 0–3 only
+        // read fragments and run the MFMAs, one wave of each kind per SIMD, so the split VALU and
+        // the LDS stores issue in the MFMA pipe's gaps.  Two plane images; one barrier per k-tile:
+        // in iteration it the producers write tile it into image it&1 while the consumers multiply
+        // tile it−1 from the other image (written before the previous barrier, and read before this
+        // one ends, so the next write into it comes after).
+        const bool producer = (threadIdx.x >> 8) != 0;
+        const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+        if (producer) {
+            // two register sets: tile it+2's loads are issued as tile it is staged, so each load
+            // has two phases (≈ 2 × 48 MFMAs) to arrive
+            SA sa1 = sa;
+            SB sb1 = sb;
+            auto load_set = [&](SA& xa, SB& xb, int k0) {
+                xa.load(PA, a.lda, m0, a.M, k0, kend, vec, tid, a.psA);
+                xb.load(PB, a.ldb, n0, a.N, k0, kend, vec, tid, a.psB);
+            };
+            auto stage_set = [&](SA& xa, SB& xb, unsigned short* img, int k0) {
+                if (do_copy) xa.copy_out(a.acopy, a.K, m0, a.M, k0, kend, tid);
+                xa.store(img, tid, nosplit);
+                xb.store(img + SA::LDSZ, tid, nosplit);
+            };
+            if (nk > 0) load_set(sa, sb, kbeg);
+            if (nk > 1) load_set(sa1, sb1, kbeg + BK);
+            for (int it = 0; it < nk; ++it) {
+                const int k0 = kbeg + it * BK;
+                if (it & 1) {
+                    stage_set(sa1, sb1, lds + BUF, k0);
+                    if (it + 2 < nk) load_set(sa1, sb1, k0 + 2 * BK);
+                } else {
+                    stage_set(sa, sb, lds, k0);
+                    if (it + 2 < nk) load_set(sa, sb, k0 + 2 * BK);
+                }
+                __syncthreads();
+            }
+            return;                                         // consumers run the epilogue
+        }
+        for (int it = 0; it < nk; ++it) {
+            if (it >= 1) {
+                const unsigned short* img = lds + ((it - 1) & 1) * BUF;
+                if (do_bsum) bsum += SA::rowsum(img, tid / TPR, (tid % TPR) * KPT, KPT);
+                if (!nomfma) compute(img);
+            }
+            __syncthreads();
+        }
+        if (nk > 0) {
+            const unsigned short* img = lds + ((nk - 1) & 1) * BUF;
+            if (do_bsum) bsum += SA::rowsum(img, tid / TPR, (tid % TPR) * KPT, KPT);
+            compute(img);
+        }
+    } else if constexpr (PP) {
         // Ping-pong over two groups (one wave of each on every SIMD).  Phase A: group 0 splits and
         // stages its tile it while group 1 multiplies its tile it−1; phase B: group 0 multiplies tile
         // it while group 1 stages tile it.  The barrier between phases orders each group's LDS
@@ -675,7 +728,7 @@ void launch(Args a) {
     const long grid = var_pp(VAR) ? (tiles + 1) / 2 : tiles;
     PPO_REQUIRE(grid > 0 && tiles < (1L << 31), "gemm16: grid out of range");
     constexpr bool A_MN = OP == OP_TN, B_MN = OP != OP_NT;
-    constexpr size_t lds = sizeof(unsigned short) * (VAR == 2 || var_pp(VAR) ? 2 : 1) *
+    constexpr size_t lds = sizeof(unsigned short) * (VAR == 2 || var_wide(VAR) ? 2 : 1) *
                            (Stage16<BM, BK, A_MN, TA, P, var_fpi(VAR) && !A_MN && sizeof(TA) == 4>::LDSZ +
                             Stage16<BN, BK, B_MN, TB, P, var_fpi(VAR) && !B_MN && sizeof(TB) == 4>::LDSZ);
     static_assert(lds <= 160 * 1024, "gemm16: LDS image exceeds 160 KiB");
@@ -687,7 +740,7 @@ void launch(Args a) {
             attr = true;
         }
     }
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(var_pp(VAR) ? 2 * NT_ : NT_), lds, ppo::stream(), a);
+    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(var_wide(VAR) ? 2 * NT_ : NT_), lds, ppo::stream(), a);
     PPO_LAUNCH_CHECK();
 }
 
@@ -754,11 +807,13 @@ void launch_cfg3(int c, const Args& a) {
         case 7: launch<OP, 128, 128, 2, 32, TA, TB, TC, 3, 3, EOP>(a); break;   // ping-pong pair of tiles
         case 8: launch<OP, 128, 128, 2, 32, TA, TB, TC, 3, 4, EOP>(a); break;   // fp32 images, pipelined split
         case 9: launch<OP, 128, 128, 2, 32, TA, TB, TC, 3, 6, EOP>(a); break;   // ping-pong + cfg 8
+        case 10: launch<OP, 128, 128, 2, 32, TA, TB, TC, 3, 7, EOP>(a); break;  // producer / consumer waves
         default: launch<OP, 128, 128, 2, 32, TA, TB, TC, 3, 0, EOP>(a); break;
     }
 }
 constexpr Cfg kCfgs3[] = {{128, 128, 32}, {128, 32, 32}, {32, 128, 32}, {64, 64, 32}, {128, 128, 64},
-                          {128, 128, 32}, {128, 128, 32}, {128, 128, 32}, {128, 128, 32}, {128, 128, 32}};
+                          {128, 128, 32}, {128, 128, 32}, {128, 128, 32}, {128, 128, 32}, {128, 128, 32},
+                          {128, 128, 32}};
 int g_flags3 = -1;          // PPO_X3_FLAGS (read once)
 int flags3() {
     if (g_flags3 < 0) {
