@@ -75,7 +75,7 @@ __device__ __forceinline__ void store_planes(unsigned short* dst, long ps, float
 // Staging of one operand tile (R rows × BK k) into a bf16 LDS image.  T = float or unsigned short
 // (bf16 bits).  One 16-B global load per slot: 4 fp32 or 8 bf16 elements.
 // ---------------------------------------------------------------------------
-template <int R, int BK, bool MN, typename T, int P = 1, bool FPI = false>
+template <int R, int BK, bool MN, typename T, int P = 1, bool FPI = false, int NTS = NT_>
 struct Stage16 {
     static constexpr bool F32 = sizeof(T) == 4;
     static_assert(P == 1 || P == 3, "one bf16 image or three planes");
@@ -85,7 +85,7 @@ struct Stage16 {
     static constexpr int IMG = MN ? BK * PR : R * PK;       // bf16 elements
     static constexpr int PER_ROW = MN ? R / EPL : BK / EPL; // loads along the contiguous dimension
     static constexpr int TOTAL = MN ? BK * PER_ROW : R * PER_ROW;
-    static constexpr int ITERS = (TOTAL + NT_ - 1) / NT_;
+    static constexpr int ITERS = (TOTAL + NTS - 1) / NTS;
     static_assert(R % EPL == 0 && R >= 32, "tile rows");
     static constexpr bool PL = P == 3 && !F32;              // operand stored as three bf16 planes
     // FPI (x3, k-contiguous fp32 operand): the LDS image holds the fp32 values ([row][BK+4] floats)
@@ -107,7 +107,7 @@ struct Stage16 {
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) {
             int row, k;
-            coords(tid + it * NT_, row, k);
+            coords(tid + it * NTS, row, k);
             const int gr = min(r0 + row, Rmax - 1);
             src[it] = ridx ? ridx[gr] : gr;
         }
@@ -119,12 +119,12 @@ struct Stage16 {
                                          bool vec, int tid, long pstride = 0) {
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) {
-            const int idx = tid + it * NT_;
+            const int idx = tid + it * NTS;
             u32x4 x[NV];
 #pragma unroll
             for (int q = 0; q < NV; ++q) x[q] = u32x4{0u, 0u, 0u, 0u};
             kok[it] = true;
-            if (TOTAL % NT_ == 0 || idx < TOTAL) {
+            if (TOTAL % NTS == 0 || idx < TOTAL) {
                 int row, k;
                 coords(idx, row, k);
                 const int gr = r0 + row, gk = k0 + k;
@@ -165,8 +165,8 @@ struct Stage16 {
     __device__ __forceinline__ void store(unsigned short* img, int tid, bool nosplit = false) const {
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) {
-            const int idx = tid + it * NT_;
-            if (TOTAL % NT_ == 0 || idx < TOTAL) {
+            const int idx = tid + it * NTS;
+            if (TOTAL % NTS == 0 || idx < TOTAL) {
                 int row, k;
                 coords(idx, row, k);
                 unsigned short* d = img + (MN ? k * PR + row : row * PK + k);
@@ -218,8 +218,8 @@ struct Stage16 {
             float* __restrict__ dst = static_cast<float*>(dstv);
 #pragma unroll
             for (int it = 0; it < ITERS; ++it) {
-                const int idx = tid + it * NT_;
-                if (TOTAL % NT_ == 0 || idx < TOTAL) {
+                const int idx = tid + it * NTS;
+                if (TOTAL % NTS == 0 || idx < TOTAL) {
                     int row, k;
                     coords(idx, row, k);
                     const int gr = r0 + row, gk = k0 + k;
@@ -240,8 +240,8 @@ struct Stage16 {
         unsigned short* __restrict__ dst = static_cast<unsigned short*>(dstv);
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) {
-            const int idx = tid + it * NT_;
-            if (TOTAL % NT_ == 0 || idx < TOTAL) {
+            const int idx = tid + it * NTS;
+            if (TOTAL % NTS == 0 || idx < TOTAL) {
                 int row, k;
                 coords(idx, row, k);
                 const int gr = r0 + row, gk = k0 + k;
@@ -330,7 +330,8 @@ template <> struct Bits<unsigned short> { static constexpr int code = 1; };
 constexpr bool var_fpi(int v) { return v == 1 || v == 2 || v == 4 || v == 6; }   // fp32 images, split at read
 constexpr bool var_pp(int v) { return v == 3 || v == 6; }                          // ping-pong tile pair
 constexpr bool var_pc(int v) { return v == 7; }                     // producer / consumer waves, one tile
-constexpr bool var_wide(int v) { return var_pp(v) || var_pc(v); }   // 512-thread workgroups, two images
+constexpr bool var_w8(int v) { return v == 8; }                     // one tile over all 8 waves
+constexpr bool var_wide(int v) { return var_pp(v) || var_pc(v) || var_w8(v); }   // 512-thread workgroups
 constexpr bool var_pipe(int v) { return v == 4 || v == 6; }                        // pipelined split at read
 
 // VAR (x3 only): 0 = operands split into plane images at LDS-store time; 1 = k-contiguous fp32
@@ -340,14 +341,15 @@ constexpr bool var_pipe(int v) { return v == 4 || v == 6; }                     
 template <int OP, int BM, int BN, int WARPS_M, int BK, typename TA, typename TB, typename TC, int P, int VAR = 0,
           int EOP = OP>
 __global__ __launch_bounds__(var_wide(VAR) ? 2 * NT_ : NT_, var_wide(VAR) ? 1 : 2) void gemm_bf16_kernel(Args a) {
-    constexpr int WARPS_N = 4 / WARPS_M;
+    constexpr int NTH = var_w8(VAR) ? 2 * NT_ : NT_;          // threads sharing one tile
+    constexpr int WARPS_N = NTH / 64 / WARPS_M;
     constexpr int WM = BM / WARPS_M, WN = BN / WARPS_N;
     constexpr int TM = WM / 32, TN = WN / 32;
     constexpr bool A_MN = OP == OP_TN, B_MN = OP != OP_NT;
     constexpr bool FPA = var_fpi(VAR) && !A_MN && sizeof(TA) == 4, FPB = var_fpi(VAR) && !B_MN && sizeof(TB) == 4;
     constexpr bool DB = VAR == 2;
-    using SA = Stage16<BM, BK, A_MN, TA, P, FPA>;
-    using SB = Stage16<BN, BK, B_MN, TB, P, FPB>;
+    using SA = Stage16<BM, BK, A_MN, TA, P, FPA, NTH>;
+    using SB = Stage16<BN, BK, B_MN, TB, P, FPB, NTH>;
     constexpr int BUF = SA::LDSZ + SB::LDSZ;                  // one LDS image (16-bit units)
     static_assert(!(DB && OP == OP_TN), "double-buffered image: no bias-gradient row sums");
     static_assert(TM >= 1 && TN >= 1, "wave tile must be a multiple of 32x32");
@@ -384,7 +386,7 @@ __global__ __launch_bounds__(var_wide(VAR) ? 2 * NT_ : NT_, var_wide(VAR) ? 1 : 
         kend = min(a.K, kbeg + a.kchunk);
     }
 
-    const int tid = threadIdx.x & (NT_ - 1), lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x & (NTH - 1), lane = tid & 63, w = tid >> 6;
     const int wm = w / WARPS_N, wn = w % WARPS_N;
     const int r = lane & 31, h = lane >> 5;
 
@@ -396,9 +398,9 @@ __global__ __launch_bounds__(var_wide(VAR) ? 2 * NT_ : NT_, var_wide(VAR) ? 1 : 
 #pragma unroll
             for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
-    constexpr int TPR = NT_ / BM > 0 ? NT_ / BM : 1;
+    constexpr int TPR = NTH / BM > 0 ? NTH / BM : 1;
     constexpr int KPT = BK / TPR > 0 ? BK / TPR : 1;
-    const bool do_bsum = OP == OP_TN && EOP == OP_TN && a.gbias != nullptr && tn == 0 && (NT_ % BM == 0) && has_tile;
+    const bool do_bsum = OP == OP_TN && EOP == OP_TN && a.gbias != nullptr && tn == 0 && (NTH % BM == 0) && has_tile;
     float bsum = 0.f;
 
     SA sa;
@@ -728,7 +730,7 @@ void launch(Args a) {
     const long grid = var_pp(VAR) ? (tiles + 1) / 2 : tiles;
     PPO_REQUIRE(grid > 0 && tiles < (1L << 31), "gemm16: grid out of range");
     constexpr bool A_MN = OP == OP_TN, B_MN = OP != OP_NT;
-    constexpr size_t lds = sizeof(unsigned short) * (VAR == 2 || var_wide(VAR) ? 2 : 1) *
+    constexpr size_t lds = sizeof(unsigned short) * (VAR == 2 || var_pp(VAR) || var_pc(VAR) ? 2 : 1) *
                            (Stage16<BM, BK, A_MN, TA, P, var_fpi(VAR) && !A_MN && sizeof(TA) == 4>::LDSZ +
                             Stage16<BN, BK, B_MN, TB, P, var_fpi(VAR) && !B_MN && sizeof(TB) == 4>::LDSZ);
     static_assert(lds <= 160 * 1024, "gemm16: LDS image exceeds 160 KiB");
@@ -808,12 +810,14 @@ void launch_cfg3(int c, const Args& a) {
         case 8: launch<OP, 128, 128, 2, 32, TA, TB, TC, 3, 4, EOP>(a); break;   // fp32 images, pipelined split
         case 9: launch<OP, 128, 128, 2, 32, TA, TB, TC, 3, 6, EOP>(a); break;   // ping-pong + cfg 8
         case 10: launch<OP, 128, 128, 2, 32, TA, TB, TC, 3, 7, EOP>(a); break;  // producer / consumer waves
+        case 11: launch<OP, 128, 256, 2, 32, TA, TB, TC, 3, 8, EOP>(a); break;  // 8 waves of 64x64
+        case 12: launch<OP, 256, 128, 4, 32, TA, TB, TC, 3, 8, EOP>(a); break;  // 8 waves of 64x64
         default: launch<OP, 128, 128, 2, 32, TA, TB, TC, 3, 0, EOP>(a); break;
     }
 }
 constexpr Cfg kCfgs3[] = {{128, 128, 32}, {128, 32, 32}, {32, 128, 32}, {64, 64, 32}, {128, 128, 64},
                           {128, 128, 32}, {128, 128, 32}, {128, 128, 32}, {128, 128, 32}, {128, 128, 32},
-                          {128, 128, 32}};
+                          {128, 128, 32}, {128, 256, 32}, {256, 128, 32}};
 int g_flags3 = -1;          // PPO_X3_FLAGS (read once)
 int flags3() {
     if (g_flags3 < 0) {
@@ -823,17 +827,22 @@ int flags3() {
     return g_flags3;
 }
 
-// cfg 8 (fp32 images split at fragment read, pipelined behind the MFMAs) is 3-6 % faster per
-// isolated NT / NN launch (C4 forward 138 -> 129 us, grad_x 118 -> 114 us) but the whole C4 update
-// measured 1 % slower with it (profiles/r01_x3_pipelined.txt): PPO_X3_PIPE=1 selects it, cfg 0 is
-// the default
+// Forward and grad_x with wide output (N a multiple of 128, large M): 256x128 tiles over 8 waves
+// (cfg 12) stage 25 % fewer elements per output than two 128x128 workgroups (C4 512x512 forward
+// 143 -> 120 us, grad_x 121 -> 112 us; profiles/r01_x3_8wave.txt); grad_W keeps the 128x128 tile
+// (its split-K grid of 8-wave tiles measured slower).  cfg 8 (fp32 images split at fragment read,
+// pipelined; 3-6 % faster per isolated launch than cfg 0, 1 % slower per C4 update) is opt-in via
+// PPO_X3_PIPE=1 for the shapes cfg 12 does not take.
 int pick3(int M, int N, int op = OP_TN) {
     if (g_force3 >= 0) return g_force3;
     if (N <= 32 && M > 32) return 1;
     if (M <= 32 && N > 32) return 2;
     if (M <= 64 || N <= 64) return 3;
+    if (op == OP_TN) return 0;
+    static const int wide = getenv("PPO_X3_NOWIDE") ? 0 : 12;      // A/B switch
+    if (wide && M >= 2048 && N % 128 == 0) return wide;
     static const int pipe = getenv("PPO_X3_PIPE") ? 8 : 0;
-    return op == OP_TN ? 0 : pipe;
+    return pipe;
 }
 
 inline bool al16(const void* p) { return ((uintptr_t)p & 15u) == 0; }

@@ -15,7 +15,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import ppo_ffi  # noqa: E402
 
 NAMES = {-1: "auto", 0: "128x128/bk32", 1: "128x32/bk32", 2: "32x128/bk32", 3: "64x64/bk32", 4: "128x128/bk64",
-         5: "128x128 fp32img", 6: "128x128 fp32img db", 7: "128x128 pingpong", 8: "fp32img pipelined", 9: "pingpong fp32img pipe", 10: "producer/consumer"}
+         5: "128x128 fp32img", 6: "128x128 fp32img db", 7: "128x128 pingpong", 8: "fp32img pipelined", 9: "pingpong fp32img pipe", 10: "producer/consumer", 11: "128x256 8 waves", 12: "256x128 8 waves"}
 
 
 def main():

@@ -1,1 +1,5 @@
-for f in 0 8 16 24; do echo "PPO_X3_FLAGS=$f"; PPO_X3_FLAGS=$f timeout -k 10 100 python ppo.c_amd/tools/gemm_x3_sweep.py --ops=0 --cfgs=0,10 --shapes="8192,512,512;8192,2048,512" || exit 1; done > gpurun_out/x3_pc_abl.txt 2>&1
+cd /tmp && export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+B="python3 $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-kernel-events --no-rollout"
+PPO_SERIAL=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/wide/s -o run --output-format csv -- $B > $R/gpurun_out/wide_s.log 2>&1 && \
+PPO_SERIAL=1 PPO_X3_NOWIDE=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/wide/n -o run --output-format csv -- $B > $R/gpurun_out/wide_n.log 2>&1
