@@ -111,18 +111,33 @@ def cpu_baseline(lib, ppo, S, H, A, N, B, sample_envs=16, steps=2):
     mu0 = packed(pol.mu)
     ls0 = ppo_ffi.d2h(lib, pol.d_log_std, np.float32, A)
     v0 = packed(ppo.contents.V)
-    r = oracle_ffi.ppo_update(sizes, [1] * len(H) + [0], mu0, ls0, v0, buf, batch_size=Bs, shuffle_mode=1,
-                              seed=1, max_value_steps=steps, max_policy_steps=steps)
     nb = N // B
-    t_update = r["t_gae"] * (N / Ns) + 10 * nb * (r["t_value"] / max(1, r["n_v"])) * (B / Bs) \
-        + 4 * nb * (r["t_policy"] / max(1, r["n_p"])) * (B / Bs)
-    sample_s = r["t_gae"] + r["t_value"] + r["t_policy"]
+
+    def timed(threads):
+        olib.ref_blas_threads(threads)
+        try:
+            r = oracle_ffi.ppo_update(sizes, [1] * len(H) + [0], mu0, ls0, v0, buf, batch_size=Bs, shuffle_mode=1,
+                                      seed=1, max_value_steps=steps, max_policy_steps=steps)
+        finally:
+            olib.ref_blas_threads(1)
+        t = r["t_gae"] * (N / Ns) + 10 * nb * (r["t_value"] / max(1, r["n_v"])) * (B / Bs) \
+            + 4 * nb * (r["t_policy"] / max(1, r["n_p"])) * (B / Bs)
+        return r, t, r["t_gae"] + r["t_value"] + r["t_policy"]
+
+    r, t_update, sample_s = timed(1)
+    # SURVEY §8d also asks for an all-cores run: the same sample with OpenBLAS on every core this
+    # process may use (the box's share: OMP_NUM_THREADS; GAE and the element-wise code stay serial C)
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    _, t_all, sample_all = timed(cores)
     return {
         "value": N / t_update, "unit": "env-steps/s", "cores": 1, "kind": "port",
         "sample": (f"oracle (C restatement of the reference CPU path, {blas}, 1 thread): GAE over {Ns} "
                    f"transitions + {r['n_v']} value + {r['n_p']} policy minibatches at B={Bs}, "
                    f"extrapolated to a full update (t={t_update:.1f}s); sample took {sample_s:.1f}s"),
         "cpu": platform.processor() or platform.machine(),
+        "all_cores": {"value": N / t_all, "unit": "env-steps/s", "cores": cores,
+                      "sample": f"same sample, OpenBLAS on {cores} threads (t={t_all:.1f}s extrapolated; "
+                                f"sample took {sample_all:.1f}s)"},
     }
 
 
@@ -311,7 +326,7 @@ def main():
                               "traffic_source": traffic_src,
                               "kernel": {"bf16": "gemm_bf16_kernel",
                                          "x3": "gemm_bf16_kernel<P=3> (x3 engine: hidden and input layers) + "
-                                               "gemm_f32_kernel (1- and A-wide output layers)",
+                                               "gemm_f32_kernel / gemm_pair_kernel (1- and A-wide output layers)",
                                          "exact": "gemm_f32_kernel"}[engine] +
                                         " (linear-layer launches; Σ 2MNK / Σ HIP-event time over every "
                                         "event_stride-th launch of one serialised update after the timed region)",

@@ -55,6 +55,10 @@ void nn_forward_dev(NeuralNetwork* nn, const float* d_x, int m);
 void nn_forward_dev_rows(NeuralNetwork* nn, const float* d_x, const int* d_rows, float* d_xcopy, int m);
 /* device backward from d_grad_out (no copy unless the output activation needs masking) */
 void nn_backward_dev(NeuralNetwork* nn, const float* d_grad_out, int m, int want_grad_x0);
+int  nn_out_fusable(const NeuralNetwork* nn, int m);
+void nn_out_fused_step(NeuralNetwork* nn, int head, const float* d_x, const int* d_rows, float* d_xcopy, int m,
+                       int extra, const float* tgt, const float* log_std, const float* action, const float* adv,
+                       const float* old_lp, float eps, float ent_coeff, float* grad_log_std, float* loss_accum);
 
 NeuralNetwork* nn_load_ex(FILE* file, long extra_floats);
 void nn_sync_w16(NeuralNetwork* nn);       /* bf16 mode: refresh the bf16 weight shadow */

@@ -204,6 +204,9 @@ void lin_bwd_w(float* gW, const float* g, const float* x, int m, int n, int l) {
     else phip_linear_bwd_w(gW, NULL, g, x, m, n, l);
 }
 
+/* set by nn_out_fused_step: the forward stops before the output layer (run fused with the head) */
+static int g_skip_out = 0;
+
 void nn_forward_dev_rows(NeuralNetwork* nn, const float* d_x, const int* d_rows, float* d_xcopy, int m) {
     nn_ensure_act(nn, m);
     const int L = nn->num_layers - 1;
@@ -227,7 +230,7 @@ void nn_forward_dev_rows(NeuralNetwork* nn, const float* d_x, const int* d_rows,
         d_rows = NULL;
         pl_in = 1u;
     }
-    for (int i = 0; i < L; i++) {
+    for (int i = 0; i < L - g_skip_out; i++) {
         Layer* ly = &nn->layers[i];
         float* out = nn->layers[i + 1].d_input;
         const int n = ly->input_size, l = ly->output_size;
@@ -257,6 +260,45 @@ void nn_forward_dev_rows(NeuralNetwork* nn, const float* d_x, const int* d_rows,
 
 void nn_forward_dev(NeuralNetwork* nn, const float* d_x, int m) { nn_forward_dev_rows(nn, d_x, NULL, NULL, m); }
 
+/* The output layer runs fused with the loss head (out_head.hip) when: fp32 storage (no bf16 mode,
+ * no pre-split planes), at least one hidden layer, identity output activation, a supported
+ * (width, A), a minibatch past the small-M regime, and PPO_OUT_FUSED=1. */
+int nn_out_fusable(const NeuralNetwork* nn, int m) {
+    /* opt-in (PPO_OUT_FUSED=1, read per update): measured slower than the separate launches at C4 —
+     * the A = 17 kernel spills its 136 grad_W accumulators (profiles/r01_out_fused.txt) */
+    const char* e = getenv("PPO_OUT_FUSED");
+    const int env = e && e[0] == '1';
+    const int L = nn->num_layers - 1;
+    if (!env || nn->dtype != 0 || g_x3_planar || L < 2 || m <= 1024) return 0;
+    if (nn_is_relu(nn, L - 1) || !nn_is_relu(nn, L - 2)) return 0;
+    return phip_out_fused_supported(nn->layers[L - 1].input_size, nn->layers[L - 1].output_size);
+}
+
+/* One minibatch step's forward + head + backward with the output layer fused (nn_out_fusable):
+ * hidden forward, one memset of the gradients (plus `extra` trailing floats: the policy's logσ
+ * gradient), the fused output layer + head, then the hidden layers' backward.  Same results as
+ * nn_forward_dev_rows → head kernel → nn_backward_dev up to fp32 re-association of the output
+ * layer's dot products. */
+void nn_out_fused_step(NeuralNetwork* nn, int head, const float* d_x, const int* d_rows, float* d_xcopy, int m,
+                       int extra, const float* tgt, const float* log_std, const float* action, const float* adv,
+                       const float* old_lp, float eps, float ent_coeff, float* grad_log_std, float* loss_accum) {
+    const int L = nn->num_layers - 1;
+    g_skip_out = 1;
+    nn_forward_dev_rows(nn, d_x, d_rows, d_xcopy, m);
+    g_skip_out = 0;
+    nn_ensure_grad(nn, m);
+    phip_memset(nn->d_grads, 0, sizeof(float) * (size_t)(nn->num_params + extra));
+    Layer* ly = &nn->layers[L - 1];
+    const int n = ly->input_size, A = ly->output_size;
+    phip_out_fused(head, ly->d_input, act_bits(nn, L - 1), ly->d_weights, ly->d_biases, m, n, A, tgt, log_std, action,
+                   adv, old_lp, eps, ent_coeff, nn->layers[L].d_input, ly->d_grad_x, ly->d_grad_weights,
+                   ly->d_grad_biases, grad_log_std, loss_accum);
+    nn->d_output = nn->layers[L].d_input;
+    g_skip_out = 1;
+    nn_backward_dev(nn, NULL, m, 0);
+    g_skip_out = 0;
+}
+
 void nn_backward_dev(NeuralNetwork* nn, const float* d_grad_out, int m, int want_grad_x0) {
     nn_ensure_grad(nn, m);
     const int L = nn->num_layers - 1;
@@ -268,8 +310,10 @@ void nn_backward_dev(NeuralNetwork* nn, const float* d_grad_out, int m, int want
         g = top;
     }
     /* one memset for every layer's gradient (split-K grad_W accumulates atomically);
-     * the trailing extra_floats (policy log_std grad) are owned by the caller and left alone */
-    phip_memset(nn->d_grads, 0, sizeof(float) * (size_t)nn->num_params);
+     * the trailing extra_floats (policy log_std grad) are owned by the caller and left alone.
+     * nn_out_fused_step: the output layer's gradients and grad_x are already written, the memset
+     * came before them */
+    if (!g_skip_out) phip_memset(nn->d_grads, 0, sizeof(float) * (size_t)nn->num_params);
     if (nn->dtype == 1) {      /* bf16 mode: hidden gradients stored bf16, the top one (heads) fp32 */
         if (nn->bits_m != m) die("nn_backward_dev (bf16): backward must follow a forward over the same rows");
         int tg = 0;
@@ -296,7 +340,8 @@ void nn_backward_dev(NeuralNetwork* nn, const float* d_grad_out, int m, int want
      * (measured: grad_W on a second queue beside grad_x was slower than back to back) */
     const int planar = g_x3_planar && nn->d_w3;
     int g_pl = 0;                                         /* g (gradient at layer i's output) pre-split */
-    for (int i = L - 1; i >= 0; i--) {
+    if (g_skip_out) g = nn->layers[L - 1].d_grad_x;
+    for (int i = L - 1 - g_skip_out; i >= 0; i--) {
         Layer* ly = &nn->layers[i];
         const float* x = i == 0 ? nn->d_x0 : ly->d_input;
         const int n = ly->input_size, l = ly->output_size;

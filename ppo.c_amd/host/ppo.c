@@ -488,6 +488,7 @@ static void ppo_update_body(PPO* ppo, float gamma, int batch_size, int n_epochs_
     const char* serial_env = getenv("PPO_SERIAL");
     const int concurrent = nv > 0 && np > 0 && world == 1 && !(serial_env && *serial_env && *serial_env != '0');
     if (concurrent) phip_side_fork();
+    const int fuse_v = nn_out_fusable(V, B), fuse_p = nn_out_fusable(mu, B);
     long iv = 0, ip = 0;
     while (iv < nv || ip < np) {
         /* serial: every value step first (the reference's order); concurrent: issue in proportion */
@@ -499,9 +500,14 @@ static void ppo_update_body(PPO* ppo, float gamma, int batch_size, int n_epochs_
              * reads the buffer rows through them and leaves the gathered copy for its grad_W */
             phip_gather_rows(perm, keys_v[j], k * B, limit, B, S, A, buf->state_p, buf->action_p, buf->logprob_p,
                              buf->advantage_p, buf->adv_target_p, NULL, NULL, NULL, NULL, d->tgt, d->rows);
-            nn_forward_dev_rows(V, buf->state_p, d->rows, d->states, B);
-            phip_mse(V->d_output, d->tgt, B, d->gv, NULL, d->stats + 0);
-            nn_backward_dev(V, d->gv, B, 0);
+            if (fuse_v) {       /* output layer + MSE head in one pass (out_head.hip) */
+                nn_out_fused_step(V, 0, buf->state_p, d->rows, d->states, B, 0, d->tgt, NULL, NULL, NULL, NULL, 0.f,
+                                  0.f, NULL, d->stats + 0);
+            } else {
+                nn_forward_dev_rows(V, buf->state_p, d->rows, d->states, B);
+                phip_mse(V->d_output, d->tgt, B, d->gv, NULL, d->stats + 0);
+                nn_backward_dev(V, d->gv, B, 0);
+            }
             phip_allreduce_sum_f32(V->d_grads, V->num_params);
             adam_update_net(ppo->adam_V, ppo->lr_V, V);
             d->n_v++;
@@ -513,10 +519,16 @@ static void ppo_update_body(PPO* ppo, float gamma, int batch_size, int n_epochs_
             phip_gather_rows(perm, keys_p[j], k * B, limit, B, S, A, buf->state_p, buf->action_p, buf->logprob_p,
                              buf->advantage_p, buf->adv_target_p, NULL, d->actions, d->old_lp, d->adv, NULL,
                              d->rows_p);
-            nn_forward_dev_rows(mu, buf->state_p, d->rows_p, d->states_p, B);
-            phip_policy_head(mu->d_output, pol->d_log_std, d->actions, d->adv, d->old_lp, B, A, ppo->epsilon,
-                             ppo->ent_coeff, d->gmu, pol->d_log_std_grad, d->stats + 1);
-            nn_backward_dev(mu, d->gmu, B, 0);
+            if (fuse_p) {       /* output layer + clipped-surrogate head in one pass (out_head.hip) */
+                nn_out_fused_step(mu, 1, buf->state_p, d->rows_p, d->states_p, B, A, NULL, pol->d_log_std,
+                                  d->actions, d->adv, d->old_lp, ppo->epsilon, ppo->ent_coeff, pol->d_log_std_grad,
+                                  d->stats + 1);
+            } else {
+                nn_forward_dev_rows(mu, buf->state_p, d->rows_p, d->states_p, B);
+                phip_policy_head(mu->d_output, pol->d_log_std, d->actions, d->adv, d->old_lp, B, A, ppo->epsilon,
+                                 ppo->ent_coeff, d->gmu, pol->d_log_std_grad, d->stats + 1);
+                nn_backward_dev(mu, d->gmu, B, 0);
+            }
             phip_allreduce_sum_f32(mu->d_grads, mu->num_params + align4(A));   /* μ grads + log_std grad */
             adam_update_cuda(ppo->adam_entropy, ppo->lr_policy);               /* ppo.cu:440-442 order */
             adam_update_net(ppo->adam_policy, ppo->lr_policy, mu);
