@@ -179,6 +179,12 @@ def main():
         dist.broadcast_object_list(obj, src=0)
         if LIB.ppo_comm_init(rank, world, obj[0]) != 0:                  # RCCL over xGMI for the data path
             raise SystemExit(f"ppo_comm_init failed: {LIB.ppo_last_error().decode()}")
+    comm_self = world == 1 and os.environ.get("PPO_COMM_SELF", "0") not in ("", "0")
+    if comm_self:
+        # rehearsal of the data-parallel path on one GPU: a one-rank RCCL communicator, so every
+        # gradient all-reduce goes through the comm stream exactly as at world > 1
+        if LIB.ppo_comm_init(0, 1, None) != 0:
+            raise SystemExit(f"ppo_comm_init (self) failed: {LIB.ppo_last_error().decode()}")
 
     S, H, A, T, E, B = CONFIGS[args.config]
     if args.strong and world > 1:
@@ -302,6 +308,7 @@ def main():
         "config": {"workload": f"{args.config}: {S}->{'x'.join(map(str, H))}->{A} MLP (policy + value), "
                                f"{T} steps x {E} envs per GPU, B={B}, 10 value + 4 policy epochs",
                    "global_batch": B * world, "rollout_per_gpu": N, "parallelism": f"dp{world}",
+                   "comm": "rccl-self (1-rank rehearsal)" if comm_self else ("rccl" if world > 1 else "none"),
                    "shuffle": "device-feistel" if args.shuffle else "host-rand"},
         "updates_per_sec": 1.0 / t_update,
         "rollout_env_steps_per_sec": (world * N / t_rollout) if t_rollout else None,
@@ -344,8 +351,8 @@ def main():
         result["cpu_baseline"] = cpu_baseline(LIB, ppo, S, H, A, N, B)
         result["cpu_baseline"]["gpu_over_cpu"] = result["value"] / result["cpu_baseline"]["value"]
     LIB.free_ppo(ppo)
+    LIB.ppo_comm_finalize()
     if world > 1:
-        LIB.ppo_comm_finalize()
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(result), flush=True)

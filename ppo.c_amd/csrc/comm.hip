@@ -3,8 +3,15 @@
 // The reference has no multi-GPU code.  libppo shards the rollout buffer by whole
 // environments: GAE needs no exchange; advantage statistics need one all-gather of
 // a 24-byte Welford triple per update; every minibatch step all-reduces the flat gradient buffer
-// of the network being trained (one call per network, on libppo's stream, so it is ordered after
-// the backward kernels and before Adam with no host synchronisation).
+// of the network being trained (one call per network).
+//
+// Every collective runs on ONE dedicated comm stream, in host issue order, on ONE communicator:
+// the issuing stream (libppo's main stream for the value loop, its side stream for the policy loop)
+// records an event the comm stream waits on, and then waits on the comm stream's completion event
+// before Adam.  The cross-rank order of collectives is therefore the host order, identical on every
+// rank, so the value and policy loops can run concurrently at world > 1 without a second
+// communicator, and each all-reduce overlaps the other loop's kernels.  PPO_COMM_SELF=1 at world 1
+// builds a one-rank communicator so this exact stream/event/RCCL path runs on a single GPU.
 #include "dev.h"
 #include "../../include/ppo_ext.h"
 
@@ -14,6 +21,34 @@
 namespace {
 ncclComm_t g_comm = nullptr;
 int g_rank = 0, g_world = 1;
+hipStream_t g_comm_stream = nullptr;
+constexpr int kEvents = 16;                  // ring: a wait captures the record at enqueue time
+hipEvent_t g_ready[kEvents], g_done[kEvents];
+int g_ev = 0;
+
+void comm_stream_init() {
+    if (g_comm_stream) return;
+    PPO_CHECK(hipStreamCreateWithFlags(&g_comm_stream, hipStreamNonBlocking));
+    for (int i = 0; i < kEvents; i++) {
+        PPO_CHECK(hipEventCreateWithFlags(&g_ready[i], hipEventDisableTiming));
+        PPO_CHECK(hipEventCreateWithFlags(&g_done[i], hipEventDisableTiming));
+    }
+}
+
+// comm stream waits for the issuing stream's queued work
+hipStream_t comm_enter(int* slot) {
+    *slot = g_ev;
+    g_ev = (g_ev + 1) % kEvents;
+    PPO_CHECK(hipEventRecord(g_ready[*slot], ppo::stream()));
+    PPO_CHECK(hipStreamWaitEvent(g_comm_stream, g_ready[*slot], 0));
+    return g_comm_stream;
+}
+
+// the issuing stream waits for the collective
+void comm_leave(int slot) {
+    PPO_CHECK(hipEventRecord(g_done[slot], g_comm_stream));
+    PPO_CHECK(hipStreamWaitEvent(ppo::stream(), g_done[slot], 0));
+}
 
 void nccl_check(ncclResult_t r, const char* what, int line) {
     if (r == ncclSuccess) return;
@@ -36,9 +71,16 @@ int ppo_comm_unique_id(unsigned char* out, int cap) {
 
 int ppo_comm_init(int rank, int world, const unsigned char* id) {
     ppo::ensure_device();
-    if (world <= 1) { g_rank = 0; g_world = 1; return 0; }
+    const char* self = getenv("PPO_COMM_SELF");
+    const bool self_comm = world <= 1 && self && *self && *self != '0';
+    if (world <= 1 && !self_comm) { g_rank = 0; g_world = 1; return 0; }
+    if (g_comm) { phip_record_error("ppo_comm_init: communicator already initialised"); return -1; }
     ncclUniqueId uid;
-    memcpy(&uid, id, sizeof(uid));
+    if (id) memcpy(&uid, id, sizeof(uid));
+    else if (world <= 1) nccl_check(ncclGetUniqueId(&uid), "ncclGetUniqueId", __LINE__);
+    else { phip_record_error("ppo_comm_init: null unique id at world > 1"); return -1; }
+    if (world <= 1) { world = 1; rank = 0; }
+    comm_stream_init();
     ncclResult_t r = ncclCommInitRank(&g_comm, world, uid, rank);
     if (r != ncclSuccess) {
         phip_record_error(ncclGetErrorString(r));
@@ -55,6 +97,7 @@ int ppo_comm_world(void) { return g_world; }
 void ppo_comm_finalize(void) {
     if (g_comm) {
         phip_sync();
+        PPO_CHECK(hipStreamSynchronize(g_comm_stream));
         ncclCommDestroy(g_comm);
         g_comm = nullptr;
     }
@@ -66,22 +109,28 @@ int phip_comm_world(void) { return g_world; }
 int phip_comm_rank(void) { return g_rank; }
 
 void phip_allreduce_sum_f32(float* d_buf, long n) {
-    if (g_world <= 1 || n <= 0) return;
-    ppo::ProfScope ps(PPO_K_COMM, 4.0 * n);
-    nccl_check(ncclAllReduce(d_buf, d_buf, (size_t)n, ncclFloat32, ncclSum, g_comm, ppo::stream()),
-               "ncclAllReduce", __LINE__);
+    if (!g_comm || n <= 0) return;
+    ppo::ProfScope ps(PPO_K_COMM, 4.0 * n);   // issuing stream: ready -> collective done
+    int slot;
+    hipStream_t cs = comm_enter(&slot);
+    nccl_check(ncclAllReduce(d_buf, d_buf, (size_t)n, ncclFloat32, ncclSum, g_comm, cs), "ncclAllReduce",
+               __LINE__);
+    comm_leave(slot);
 }
 
 void ppo_comm_allreduce_f32(float* d_buf, long n) { phip_allreduce_sum_f32(d_buf, n); }
 
 void phip_allgather_f64(const double* d_send, double* d_recv, long n_per_rank) {
-    if (g_world <= 1) {
+    if (!g_comm) {
         phip_d2d(d_recv, d_send, sizeof(double) * (size_t)n_per_rank);
         return;
     }
     ppo::ProfScope ps(PPO_K_COMM, 8.0 * n_per_rank * g_world);
-    nccl_check(ncclAllGather(d_send, d_recv, (size_t)n_per_rank, ncclFloat64, g_comm, ppo::stream()),
-               "ncclAllGather", __LINE__);
+    int slot;
+    hipStream_t cs = comm_enter(&slot);
+    nccl_check(ncclAllGather(d_send, d_recv, (size_t)n_per_rank, ncclFloat64, g_comm, cs), "ncclAllGather",
+               __LINE__);
+    comm_leave(slot);
 }
 
 }  // extern "C"

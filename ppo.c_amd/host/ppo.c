@@ -476,9 +476,10 @@ static void ppo_update_body(PPO* ppo, float gamma, int batch_size, int n_epochs_
      * so on one GPU the two run concurrently: value steps on libppo's stream, policy steps on its
      * side stream (own workspaces), issued interleaved.  Every network sees exactly the reference's
      * sequence of minibatches and Adam steps; epochs' shuffles are drawn up front in the
-     * reference's order (value epochs first).  PPO_SERIAL=1 runs them one after the other, and so
-     * does data parallelism (world > 1): RCCL collectives from two streams would need a second
-     * communicator and a cross-rank execution order that cannot be rehearsed on one GPU. */
+     * reference's order (value epochs first).  PPO_SERIAL=1 runs them one after the other.  Under
+     * data parallelism (world > 1) both loops hand their gradient all-reduces to comm.hip's single
+     * comm stream in this host issue order, identical on every rank, so they stay concurrent and
+     * each collective overlaps the other loop's kernels. */
     const long nv = (long)n_epochs_value * num_batches, np = (long)n_epochs_policy * num_batches;
     uint64_t* keys = (uint64_t*)xmalloc(sizeof(uint64_t) * (size_t)(n_epochs_value + n_epochs_policy + 1));
     uint64_t* keys_v = keys;
@@ -486,7 +487,7 @@ static void ppo_update_body(PPO* ppo, float gamma, int batch_size, int n_epochs_
     const int* perms_v = phase_perms(ppo, d, shuffle_mode, n_epochs_value, limit, 0, keys_v);
     const int* perms_p = phase_perms(ppo, d, shuffle_mode, n_epochs_policy, limit, 1, keys_p);
     const char* serial_env = getenv("PPO_SERIAL");
-    const int concurrent = nv > 0 && np > 0 && world == 1 && !(serial_env && *serial_env && *serial_env != '0');
+    const int concurrent = nv > 0 && np > 0 && !(serial_env && *serial_env && *serial_env != '0');
     if (concurrent) phip_side_fork();
     const int fuse_v = nn_out_fusable(V, B), fuse_p = nn_out_fusable(mu, B);
     long iv = 0, ip = 0;

@@ -315,6 +315,44 @@ def test_concurrent_value_policy_loops(lib, oracle, shuffle_mode, monkeypatch):
         assert (err > 1e-6).mean() < 0.01, (k, (err > 1e-6).mean())
 
 
+def test_comm_stream_rehearsal(lib, oracle, monkeypatch):
+    """The data-parallel path on one GPU: a one-rank RCCL communicator (PPO_COMM_SELF=1) routes every
+    gradient all-reduce through comm.hip's comm stream (issuing stream -> event -> comm stream ->
+    event -> Adam) while the value and policy loops run concurrently, exactly as at world > 1.  The
+    one-rank sum is the identity, so the update must equal the update without a communicator: value
+    network bit for bit (split-K forced off), policy within the log σ-gradient atomics bound."""
+    sizes, N, B = [17, 256, 256, 6], 4096, 512
+    lib.ppo_gemm_tune(-1, 1)
+    monkeypatch.delenv("PPO_SERIAL", raising=False)
+    out = {}
+    for mode in ("plain", "comm"):
+        if mode == "comm":
+            monkeypatch.setenv("PPO_COMM_SELF", "1")
+            assert lib.ppo_comm_init(0, 1, None) == 0, lib.ppo_last_error()
+        ppo = make_ppo(lib, oracle, sizes, N)
+        mu0, ls0 = policy_state(lib, ppo)
+        buf = synthetic_buffer(oracle, sizes, mu0, ls0, N, seed=5, n_envs=8)
+        load_buffer(lib, ppo, buf)
+        lib.ppo_reset_stats(ppo)
+        oracle.srand(43)
+        lib.ppo_update(ppo, 0.99, B, 2, 3, 1, 9)
+        st = (C.c_double * 7)()
+        lib.ppo_read_stats(ppo, st, 7)
+        mu, ls = policy_state(lib, ppo)
+        out[mode] = dict(stats=np.array(st[:4]), v=nn_params_packed(lib, ppo.contents.V), mu=mu, ls=ls)
+        lib.free_ppo(ppo)
+        if mode == "comm":
+            lib.ppo_comm_finalize()
+    lib.ppo_gemm_tune(-1, 0)
+    a, b = out["plain"], out["comm"]
+    np.testing.assert_allclose(a["stats"], b["stats"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_array_equal(a["v"], b["v"])
+    for k in ("mu", "ls"):
+        err = np.abs(a[k] - b[k])
+        assert err.max() <= 2 * 3e-4, (k, err.max())
+        assert (err > 1e-6).mean() < 0.01, (k, (err > 1e-6).mean())
+
+
 @pytest.mark.parametrize("cap,filled,B", [(4096, 3000, 512), (4096, 4096, 1000)])
 def test_partial_and_ragged_buffer(lib, oracle, cap, filled, B):
     """A partly filled buffer (idx = filled < capacity, full = false) and a batch size that does not
