@@ -89,6 +89,12 @@ typedef struct {
     long   tiny_wt_cap;
     unsigned short* d_w3;   /* x3 engine (fp32 mode): d_params as three bf16 planes (plane stride num_params rounded up to 8) */
     int    x3_in_planes;    /* bit i: layers[i].d_input (bit 0: d_x0) held three bf16 planes in the last forward */
+    /* host mirror <-> HBM reconciliation for the host-pointer entry points (forward_propagation,
+     * sample_action, ...): HBM parameters changed by Adam / ppo_update are pulled to the host
+     * mirrors, host mirrors edited by the caller are pushed to HBM — never blindly overwritten */
+    float* h_sync;          /* host-mirror snapshot at the last sync: packed [W0,b0,...] then extra_floats */
+    long   dev_version;     /* bumped by every HBM parameter update */
+    long   host_version;    /* dev_version the host mirrors last matched */
 } NeuralNetwork;
 
 typedef struct {

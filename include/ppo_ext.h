@@ -46,6 +46,9 @@ int  ppo_comm_world(void);
 void ppo_comm_finalize(void);
 /* sum-all-reduce of n floats in place on libppo's stream (no-op at world 1) */
 void ppo_comm_allreduce_f32(float* d_buf, long n);
+/* the advantage-statistics combine after the all-gather: `count` device triples (n, mean, M2) in
+ * double → one triple (Chan et al. pairwise combine; empty parts skipped).  Synchronises. */
+void ppo_welford_combine(const double* d_parts, int count, double* d_out);
 
 /* ---------------- the PPO update ---------------- */
 enum { PPO_SHUFFLE_HOST_RAND = 0,   /* reference shuffle_buffer: swap(i, rand()%N), host rand() */
@@ -65,6 +68,10 @@ void ppo_update(void* ppo, float gamma, int batch_size, int n_epochs_policy, int
  * out[3]=#policy steps, out[4]=entropy, out[5]=advantage mean, out[6]=advantage std */
 void ppo_read_stats(void* ppo, double* out, int n);
 void ppo_reset_stats(void* ppo);
+/* Parity testing at full size: cap the value / policy minibatch steps of the following ppo_update
+ * calls (−1 = no cap).  GAE, the shuffles and their rand() consumption are unchanged; only the
+ * loops stop early (so one step of a 1M-row, B = 32768 update can be checked against the oracle). */
+void ppo_set_step_limit(void* ppo, long max_value_steps, long max_policy_steps);
 
 /* Batched policy sample on device: a = μ(s) + σ·ε, ε ~ N(0,1) (counter-based
  * Philox + Box–Muller), log_prob per row.  d_* are device pointers. */

@@ -324,3 +324,61 @@ def libc():
 
 def srand(seed):
     libc().srand(C.c_uint(seed))
+
+
+def save_ppo_bytes(hyper, S, A, capacity, log_std, mu_sizes, mu_acts, mu_params, v_sizes, v_acts, v_params,
+                   adams):
+    """The reference checkpoint writer, restated byte for byte (test infrastructure only).
+
+    ppo.cu:585-611 save_ppo: lambda, epsilon, ent_coeff, lr_policy, lr_V (f32), state_size,
+    action_size, capacity (i32); then save_policy (policy.cu:207-211: log_std[A] f32, then μ's
+    save_neural_network), save_neural_network(V) (neural_network.cu:283-300: num_layers,
+    output_size, per activation (strlen+1, chars incl. NUL), per layer (in, out, W[out·in], b[out])),
+    and save_adam for adam_policy, adam_V, adam_entropy (adam.cu:172-189: size, time_step, beta1,
+    beta2, num_layers, m[size], v[size]).  Everything native-endian (x86: little).
+    hyper = (lambda, epsilon, ent_coeff, lr_policy, lr_V); adams = three dicts with keys
+    size, t, b1, b2, n, m, v (m/v packed in tensor order).
+    """
+    import struct
+
+    out = bytearray()
+    out += struct.pack("<5f", *hyper)
+    out += struct.pack("<3i", S, A, capacity)
+
+    def nn(sizes, acts, params):
+        b = bytearray(struct.pack("<2i", len(sizes), sizes[-1]))
+        for a in acts:
+            raw = a.encode() + b"\0"
+            b += struct.pack("<i", len(raw)) + raw
+        off = 0
+        for i in range(len(sizes) - 1):
+            n_in, n_out = sizes[i], sizes[i + 1]
+            b += struct.pack("<2i", n_in, n_out)
+            b += np.asarray(params[off:off + n_in * n_out + n_out], "<f4").tobytes()
+            off += n_in * n_out + n_out
+        assert off == len(params)
+        return b
+
+    out += np.asarray(log_std, "<f4").tobytes()
+    out += nn(mu_sizes, mu_acts, mu_params)
+    out += nn(v_sizes, v_acts, v_params)
+    for ad in adams:
+        out += struct.pack("<2i2fi", ad["size"], ad["t"], ad["b1"], ad["b2"], ad["n"])
+        out += np.asarray(ad["m"], "<f4").tobytes() + np.asarray(ad["v"], "<f4").tobytes()
+    return bytes(out)
+
+
+def splitmix64(z):
+    """libppo's key derivation (host/ppo.c splitmix64), for predicting device-shuffle permutations."""
+    M = (1 << 64) - 1
+    z = (z + 0x9E3779B97F4A7C15) & M
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+    return z ^ (z >> 31)
+
+
+def gaussian_noise(n):
+    """ref_gaussian_noise (policy.cu:46-65, D3: every element filled); consumes libc rand()."""
+    out = np.empty(n, _f32)
+    load().ref_gaussian_noise(_p(out), n)
+    return out

@@ -12,6 +12,12 @@
 // rank, so the value and policy loops can run concurrently at world > 1 without a second
 // communicator, and each all-reduce overlaps the other loop's kernels.  PPO_COMM_SELF=1 at world 1
 // builds a one-rank communicator so this exact stream/event/RCCL path runs on a single GPU.
+//
+// PPO_COMM_LOOPBACK=k (k > 1, at world 1): an in-process stand-in for k ranks holding IDENTICAL
+// shards.  ppo_comm_world() reports k, so every world > 1 branch of the update runs (grad_scale
+// 1/k, the Welford all-gather + Chan combine, the limit agreement, the comm stream); the all-reduce
+// is the exact k-fold sum of identical buffers (×k on the comm stream) and the all-gather
+// replicates the local block k times.  For k a power of two an update must equal the 1-GPU update.
 #include "dev.h"
 #include "../../include/ppo_ext.h"
 
@@ -21,6 +27,18 @@
 namespace {
 ncclComm_t g_comm = nullptr;
 int g_rank = 0, g_world = 1;
+int g_loopback = 0;                          // k > 1: PPO_COMM_LOOPBACK stand-in for k identical ranks
+int* g_i32 = nullptr;                        // scratch for host-visible integer collectives
+
+__global__ void scale_kernel(float* __restrict__ x, long n, float s) {
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+        x[i] *= s;
+}
+
+__global__ void replicate_kernel(const double* __restrict__ src, double* __restrict__ dst, long n, int k) {
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < n * k; i += (long)gridDim.x * 256)
+        dst[i] = src[i % n];
+}
 hipStream_t g_comm_stream = nullptr;
 constexpr int kEvents = 16;                  // ring: a wait captures the record at enqueue time
 hipEvent_t g_ready[kEvents], g_done[kEvents];
@@ -73,6 +91,16 @@ int ppo_comm_init(int rank, int world, const unsigned char* id) {
     ppo::ensure_device();
     const char* self = getenv("PPO_COMM_SELF");
     const bool self_comm = world <= 1 && self && *self && *self != '0';
+    const char* lb = getenv("PPO_COMM_LOOPBACK");
+    const int k = lb ? atoi(lb) : 0;
+    if (world <= 1 && k > 1) {
+        if (g_comm || g_loopback) { phip_record_error("ppo_comm_init: communicator already initialised"); return -1; }
+        comm_stream_init();
+        g_loopback = k;
+        g_rank = 0;
+        g_world = k;
+        return 0;
+    }
     if (world <= 1 && !self_comm) { g_rank = 0; g_world = 1; return 0; }
     if (g_comm) { phip_record_error("ppo_comm_init: communicator already initialised"); return -1; }
     ncclUniqueId uid;
@@ -95,6 +123,11 @@ int ppo_comm_rank(void) { return g_rank; }
 int ppo_comm_world(void) { return g_world; }
 
 void ppo_comm_finalize(void) {
+    if (g_loopback) {
+        phip_sync();
+        PPO_CHECK(hipStreamSynchronize(g_comm_stream));
+        g_loopback = 0;
+    }
     if (g_comm) {
         phip_sync();
         PPO_CHECK(hipStreamSynchronize(g_comm_stream));
@@ -109,10 +142,18 @@ int phip_comm_world(void) { return g_world; }
 int phip_comm_rank(void) { return g_rank; }
 
 void phip_allreduce_sum_f32(float* d_buf, long n) {
-    if (!g_comm || n <= 0) return;
+    if ((!g_comm && !g_loopback) || n <= 0) return;
     ppo::ProfScope ps(PPO_K_COMM, 4.0 * n);   // issuing stream: ready -> collective done
     int slot;
     hipStream_t cs = comm_enter(&slot);
+    if (g_loopback) {                          // k identical ranks: the sum is k·x
+        int grid = ppo_divup(n, 256);
+        if (grid > 2048) grid = 2048;
+        hipLaunchKernelGGL(scale_kernel, dim3(grid), dim3(256), 0, cs, d_buf, n, (float)g_loopback);
+        PPO_LAUNCH_CHECK();
+        comm_leave(slot);
+        return;
+    }
     nccl_check(ncclAllReduce(d_buf, d_buf, (size_t)n, ncclFloat32, ncclSum, g_comm, cs), "ncclAllReduce",
                __LINE__);
     comm_leave(slot);
@@ -121,16 +162,37 @@ void phip_allreduce_sum_f32(float* d_buf, long n) {
 void ppo_comm_allreduce_f32(float* d_buf, long n) { phip_allreduce_sum_f32(d_buf, n); }
 
 void phip_allgather_f64(const double* d_send, double* d_recv, long n_per_rank) {
-    if (!g_comm) {
+    if (!g_comm && !g_loopback) {
         phip_d2d(d_recv, d_send, sizeof(double) * (size_t)n_per_rank);
         return;
     }
     ppo::ProfScope ps(PPO_K_COMM, 8.0 * n_per_rank * g_world);
     int slot;
     hipStream_t cs = comm_enter(&slot);
+    if (g_loopback) {                          // every rank holds the same block
+        hipLaunchKernelGGL(replicate_kernel, dim3(1), dim3(256), 0, cs, d_send, d_recv, n_per_rank, g_loopback);
+        PPO_LAUNCH_CHECK();
+        comm_leave(slot);
+        return;
+    }
     nccl_check(ncclAllGather(d_send, d_recv, (size_t)n_per_rank, ncclFloat64, g_comm, cs), "ncclAllGather",
                __LINE__);
     comm_leave(slot);
+}
+
+// min over ranks of a host integer (synchronous; a few µs per call).  The update uses it to agree
+// on whether any rank has an empty shard, so either every rank trains or none does.
+int phip_comm_min_i32(int v) {
+    if (!g_comm) return v;                     // world 1 or loopback (identical ranks)
+    if (!g_i32) g_i32 = (int*)phip_malloc(sizeof(int));
+    phip_h2d(g_i32, &v, sizeof(int));
+    int slot;
+    hipStream_t cs = comm_enter(&slot);
+    nccl_check(ncclAllReduce(g_i32, g_i32, 1, ncclInt32, ncclMin, g_comm, cs), "ncclAllReduce(min)", __LINE__);
+    comm_leave(slot);
+    int out = v;
+    phip_d2h(&out, g_i32, sizeof(int));
+    return out;
 }
 
 }  // extern "C"

@@ -166,6 +166,7 @@ __global__ void welford_combine_kernel(const double* __restrict__ parts, int cou
     for (int i = 0; i < count; ++i) {
         const double nb = parts[3 * i], mb = parts[3 * i + 1], m2b = parts[3 * i + 2];
         if (nb <= 0.0) continue;
+        if (n <= 0.0) { n = nb; mean = mb; m2 = m2b; continue; }     // first non-empty part taken as is
         const double nn = n + nb, d = mb - mean;
         mean += d * nb / nn;
         m2 += m2b + d * d * n * nb / nn;
@@ -266,6 +267,11 @@ void phip_welford_combine(const double* d_welford_all, int world, double* d_welf
     hipLaunchKernelGGL(welford_combine_kernel, dim3(1), dim3(64), 0, ppo::stream(), d_welford_all, world,
                        d_welford);
     PPO_LAUNCH_CHECK();
+}
+
+void ppo_welford_combine(const double* d_parts, int count, double* d_out) {
+    phip_welford_combine(d_parts, count, d_out);
+    phip_sync();
 }
 
 void phip_normalize(float* adv, int n, const double* d_welford, float* d_stats_out) {

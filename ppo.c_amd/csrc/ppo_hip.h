@@ -215,6 +215,7 @@ void phip_link_next_state(float* next_state, const float* state, const uint8_t* 
 /* ---------------- data parallel (comm.hip, RCCL) ---------------- */
 int  phip_comm_world(void);
 int  phip_comm_rank(void);
+int  phip_comm_min_i32(int v);      /* min over ranks (synchronous); identity at world 1 */
 void phip_allreduce_sum_f32(float* d_buf, long n);
 void phip_allgather_f64(const double* d_send, double* d_recv, long n_per_rank);
 

@@ -169,6 +169,7 @@ void adam_update_cuda(Adam* adam, float lr) { adam_update_cuda_w16(adam, lr, NUL
 int adam_update_cuda_w16(Adam* adam, float lr, unsigned short* w16, long n16) {
     float bc1, bc2;
     bias_corrections(adam, &bc1, &bc2);
+    nn_note_device_update(adam->weights[0]);          /* the network's host mirrors are now stale */
     if (adam->flat) {
         phip_adam_flat_w16(adam->weights[0], adam->grad_weights[0], adam->m, adam->v, adam->span, lr, adam->beta1,
                            adam->beta2, bc1, bc2, adam->grad_scale, w16, w16 ? n16 : 0);
@@ -214,13 +215,23 @@ void save_adam(Adam* adam, FILE* file, bool cuda) {
     free(v);
 }
 
-Adam* load_adam(FILE* file, float** weights, float** grad_weights, int* length, bool cuda) {
+/* n_expected: tensors the caller's arrays hold (−1: unknown, the reference signature) — a checkpoint
+ * whose tensor count or size disagrees is rejected before anything is allocated or copied */
+Adam* load_adam_ex(FILE* file, float** weights, float** grad_weights, int* length, int n_expected, bool cuda) {
     int size, t, n;
     float b1, b2;
     if (fread(&size, sizeof(int), 1, file) != 1 || fread(&t, sizeof(int), 1, file) != 1 ||
         fread(&b1, sizeof(float), 1, file) != 1 || fread(&b2, sizeof(float), 1, file) != 1 ||
         fread(&n, sizeof(int), 1, file) != 1)
         die("checkpoint: unexpected end of file");
+    if (n <= 0 || (n_expected >= 0 && n != n_expected))
+        die("checkpoint: Adam tensor count does not match the network");
+    long total = 0;
+    for (int i = 0; i < n; i++) {
+        if (length[i] < 0) die("checkpoint: negative Adam tensor length");
+        total += length[i];
+    }
+    if (size < 0 || (long)size != total) die("checkpoint: Adam size does not match the tensor lengths");
     float* m = (float*)xmalloc(sizeof(float) * (size_t)size);
     float* v = (float*)xmalloc(sizeof(float) * (size_t)size);
     if (fread(m, sizeof(float), (size_t)size, file) != (size_t)size ||
@@ -249,6 +260,10 @@ Adam* load_adam(FILE* file, float** weights, float** grad_weights, int* length, 
     return a;
 }
 
+Adam* load_adam(FILE* file, float** weights, float** grad_weights, int* length, bool cuda) {
+    return load_adam_ex(file, weights, grad_weights, length, -1, cuda);
+}
+
 Adam* load_adam_from_nn(FILE* file, NeuralNetwork* nn, bool cuda) {
     const int L = nn->num_layers - 1;
     float** w = (float**)xmalloc(sizeof(float*) * (size_t)(2 * L));
@@ -263,7 +278,7 @@ Adam* load_adam_from_nn(FILE* file, NeuralNetwork* nn, bool cuda) {
         len[2 * i] = ly->input_size * ly->output_size;
         len[2 * i + 1] = ly->output_size;
     }
-    Adam* a = load_adam(file, w, g, len, cuda);
+    Adam* a = load_adam_ex(file, w, g, len, 2 * L, cuda);
     free(w); free(g); free(len);
     return a;
 }

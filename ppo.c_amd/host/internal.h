@@ -61,12 +61,20 @@ void nn_out_fused_step(NeuralNetwork* nn, int head, const float* d_x, const int*
                        const float* old_lp, float eps, float ent_coeff, float* grad_log_std, float* loss_accum);
 
 NeuralNetwork* nn_load_ex(FILE* file, long extra_floats);
+/* host mirror <-> HBM reconciliation (neural_network.c) */
+void nn_note_device_update(const float* d_ptr);   /* an HBM parameter update touched d_ptr's network */
+void nn_host_sync(NeuralNetwork* nn, float* extra); /* before a host-pointer entry point computes */
+void nn_sync_extra_snapshot(NeuralNetwork* nn, const float* extra);
+void policy_host_sync(GaussianPolicy* p);
 void nn_sync_w16(NeuralNetwork* nn);       /* bf16 mode: refresh the bf16 weight shadow */
 
 /* adam.c */
 void adam_next_step(Adam* a, float lr, float* step, float* bc2);
 /* device Adam that also writes the bf16 shadow w16[0, n16) in the same pass; returns 1 when it did */
 int adam_update_cuda_w16(Adam* adam, float lr, unsigned short* w16, long n16);
+
+/* checkpoint Adam with a known tensor count (n_expected < 0: unknown); rejects mismatches */
+Adam* load_adam_ex(FILE* file, float** weights, float** grad_weights, int* length, int n_expected, bool cuda);
 
 /* trajectory_buffer.c */
 void buffer_point_device(TrajectoryBuffer* b);

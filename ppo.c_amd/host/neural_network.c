@@ -21,6 +21,84 @@ int nn_is_relu(const NeuralNetwork* nn, int layer) {
     return a && a->activation != NULL;
 }
 
+/* ---- host mirror <-> HBM reconciliation ------------------------------------------------------
+ * The reference's host-pointer functions compute from the host mirrors (Layer.weights, log_std);
+ * libppo computes from HBM.  Every live network is registered so a device Adam step can mark the
+ * network whose parameters it moved (dev_version); the host entry points then pull newer HBM
+ * parameters into the mirrors, and push only mirror tensors the caller edited since the last sync
+ * (compared with the h_sync snapshot) — HBM is never overwritten with stale host values. */
+static NeuralNetwork** g_nets = NULL;
+static int g_nets_n = 0, g_nets_cap = 0;
+
+static void nn_registry_add(NeuralNetwork* nn) {
+    if (g_nets_n == g_nets_cap) {
+        g_nets_cap = g_nets_cap ? 2 * g_nets_cap : 16;
+        NeuralNetwork** p = (NeuralNetwork**)realloc(g_nets, sizeof(NeuralNetwork*) * (size_t)g_nets_cap);
+        if (!p) die("host allocation failed");
+        g_nets = p;
+    }
+    g_nets[g_nets_n++] = nn;
+}
+
+static void nn_registry_remove(NeuralNetwork* nn) {
+    for (int i = 0; i < g_nets_n; i++)
+        if (g_nets[i] == nn) { g_nets[i] = g_nets[--g_nets_n]; return; }
+}
+
+void nn_note_device_update(const float* d_ptr) {
+    for (int i = 0; i < g_nets_n; i++) {
+        NeuralNetwork* nn = g_nets[i];
+        if (d_ptr >= nn->d_params && d_ptr < nn->d_params + nn->num_params + nn->extra_floats) nn->dev_version++;
+    }
+}
+
+/* h_sync offset of layer i's weights in the packed order */
+static long packed_offset(const NeuralNetwork* nn, int layer) {
+    long off = 0;
+    for (int i = 0; i < layer; i++) off += (long)nn->layers[i].input_size * nn->layers[i].output_size + nn->layers[i].output_size;
+    return off;
+}
+
+void nn_host_sync(NeuralNetwork* nn, float* extra) {
+    const int L = nn->num_layers - 1;
+    const long ne = extra ? nn->extra_floats : 0;
+    if (nn->dev_version != nn->host_version) {            /* HBM is newer: pull */
+        nn_write_weights_to_host(nn);
+        if (ne) {
+            phip_d2h(extra, nn->d_params + nn->num_params, sizeof(float) * (size_t)ne);
+            memcpy(nn->h_sync + nn->num_params_packed, extra, sizeof(float) * (size_t)ne);
+        }
+        if (ne || !nn->extra_floats) nn->host_version = nn->dev_version;
+        return;
+    }
+    int pushed = 0;                                       /* push the tensors the caller edited */
+    for (int i = 0; i < L; i++) {
+        Layer* ly = &nn->layers[i];
+        const size_t nw = (size_t)ly->input_size * ly->output_size, nb = (size_t)ly->output_size;
+        float* sw = nn->h_sync + packed_offset(nn, i);
+        if (memcmp(sw, ly->weights, sizeof(float) * nw)) {
+            phip_h2d(ly->d_weights, ly->weights, sizeof(float) * nw);
+            memcpy(sw, ly->weights, sizeof(float) * nw);
+            pushed = 1;
+        }
+        if (memcmp(sw + nw, ly->biases, sizeof(float) * nb)) {
+            phip_h2d(ly->d_biases, ly->biases, sizeof(float) * nb);
+            memcpy(sw + nw, ly->biases, sizeof(float) * nb);
+            pushed = 1;
+        }
+    }
+    if (ne && memcmp(nn->h_sync + nn->num_params_packed, extra, sizeof(float) * (size_t)ne)) {
+        phip_h2d(nn->d_params + nn->num_params, extra, sizeof(float) * (size_t)ne);
+        memcpy(nn->h_sync + nn->num_params_packed, extra, sizeof(float) * (size_t)ne);
+    }
+    if (pushed) nn_sync_w16(nn);
+}
+
+/* the caller's extra floats were written to HBM and the mirror (policy log_std at creation / load) */
+void nn_sync_extra_snapshot(NeuralNetwork* nn, const float* extra) {
+    if (nn->extra_floats) memcpy(nn->h_sync + nn->num_params_packed, extra, sizeof(float) * (size_t)nn->extra_floats);
+}
+
 /* neural_network.cu:40-51 restated: He-uniform hidden layers, Xavier-uniform output layer. */
 static void init_layer_from_rand(Layer* ly, int is_last) {
     const int in = ly->input_size, out = ly->output_size;
@@ -79,6 +157,8 @@ NeuralNetwork* nn_create_ex(int* layer_sizes, char** activation_functions, int n
         ly->d_grad_weights = nn->d_grads + nn->param_offset[i];
         ly->d_grad_biases = nn->d_grads + nn->bias_offset[i];
     }
+    nn->h_sync = (float*)xcalloc((size_t)(packed + extra_floats), sizeof(float));
+    nn_registry_add(nn);
     if (init_from_rand) nn_write_weights_to_device(nn);
     nn->cublas_handle = NULL;
     return nn;
@@ -391,11 +471,11 @@ void backward_propagation_cuda(NeuralNetwork* nn, float* grad_in, int m) {
     nn_backward_dev(nn, nn->layers[L].d_grad_x, m, 1);
 }
 
-/* Host-pointer entry points (reference CPU path, neural_network.cu:163-231): the host
- * weight arrays are the source of truth, so they are uploaded first; the output and
- * gradients come back into the host mirrors. */
+/* Host-pointer entry points (reference CPU path, neural_network.cu:163-231): host mirrors and HBM
+ * are reconciled first (nn_host_sync: newer HBM parameters pulled, caller-edited mirror tensors
+ * pushed); the output and gradients come back into the host mirrors. */
 void forward_propagation(NeuralNetwork* nn, float* input, int m) {
-    nn_write_weights_to_device(nn);
+    nn_host_sync(nn, NULL);
     nn_ensure_act(nn, m);
     phip_h2d(nn->layers[0].d_input, input, sizeof(float) * (size_t)m * nn->layers[0].input_size);
     nn_forward_dev(nn, nn->layers[0].d_input, m);
@@ -405,6 +485,7 @@ void forward_propagation(NeuralNetwork* nn, float* input, int m) {
 }
 
 void backward_propagation(NeuralNetwork* nn, float* grad_in, int m) {
+    nn_host_sync(nn, NULL);
     nn_ensure_grad(nn, m);
     const int L = nn->num_layers - 1;
     phip_h2d(nn->layers[L].d_grad_x, grad_in, sizeof(float) * (size_t)m * nn->output_size);
@@ -419,10 +500,15 @@ void backward_propagation(NeuralNetwork* nn, float* grad_in, int m) {
 void nn_sync_w16(NeuralNetwork* nn);
 
 void nn_write_weights_to_device(NeuralNetwork* nn) {
+    long off = 0;
     for (int i = 0; i < nn->num_layers - 1; i++) {
         Layer* ly = &nn->layers[i];
-        phip_h2d(ly->d_weights, ly->weights, sizeof(float) * (size_t)ly->input_size * ly->output_size);
-        phip_h2d(ly->d_biases, ly->biases, sizeof(float) * (size_t)ly->output_size);
+        const size_t nw = (size_t)ly->input_size * ly->output_size, nb = (size_t)ly->output_size;
+        phip_h2d(ly->d_weights, ly->weights, sizeof(float) * nw);
+        phip_h2d(ly->d_biases, ly->biases, sizeof(float) * nb);
+        memcpy(nn->h_sync + off, ly->weights, sizeof(float) * nw);
+        memcpy(nn->h_sync + off + nw, ly->biases, sizeof(float) * nb);
+        off += (long)(nw + nb);
     }
     nn_sync_w16(nn);
 }
@@ -443,11 +529,17 @@ int nn_set_compute_dtype(void* vnn, int dtype) {
 }
 
 void nn_write_weights_to_host(NeuralNetwork* nn) {
+    long off = 0;
     for (int i = 0; i < nn->num_layers - 1; i++) {
         Layer* ly = &nn->layers[i];
-        phip_d2h(ly->weights, ly->d_weights, sizeof(float) * (size_t)ly->input_size * ly->output_size);
-        phip_d2h(ly->biases, ly->d_biases, sizeof(float) * (size_t)ly->output_size);
+        const size_t nw = (size_t)ly->input_size * ly->output_size, nb = (size_t)ly->output_size;
+        phip_d2h(ly->weights, ly->d_weights, sizeof(float) * nw);
+        phip_d2h(ly->biases, ly->d_biases, sizeof(float) * nb);
+        memcpy(nn->h_sync + off, ly->weights, sizeof(float) * nw);
+        memcpy(nn->h_sync + off + nw, ly->biases, sizeof(float) * nb);
+        off += (long)(nw + nb);
     }
+    if (!nn->extra_floats) nn->host_version = nn->dev_version;   /* with extras: the owner syncs them too */
 }
 
 void free_neural_network(NeuralNetwork* nn) {
@@ -474,6 +566,8 @@ void free_neural_network(NeuralNetwork* nn) {
     phip_free(nn->d_tiny_wt);
     phip_free(nn->d_params);
     phip_free(nn->d_grads);
+    nn_registry_remove(nn);
+    free(nn->h_sync);
     free(nn->activation_functions);
     free(nn->param_offset);
     free(nn->bias_offset);
@@ -485,6 +579,7 @@ void free_neural_network(NeuralNetwork* nn) {
 /* neural_network.cu:284-300 byte layout: num_layers, output_size, per activation
  * (len incl. NUL, chars), per layer (in, out, W[out·in], b[out]). */
 void save_neural_network(NeuralNetwork* nn, FILE* file) {
+    nn_host_sync(nn, NULL);
     fwrite(&nn->num_layers, sizeof(int), 1, file);
     fwrite(&nn->output_size, sizeof(int), 1, file);
     for (int i = 0; i < nn->num_layers - 1; i++) {

@@ -27,6 +27,7 @@ GaussianPolicy* policy_create_ex(int* layer_sizes, char** activation_functions, 
     attach_log_std(p);
     for (int i = 0; i < p->action_size; i++) p->log_std[i] = logf(init_std);      /* policy.cu:22-24 */
     phip_h2d(p->d_log_std, p->log_std, sizeof(float) * (size_t)p->action_size);
+    nn_sync_extra_snapshot(p->mu, p->log_std);
     p->input_action = NULL;
     p->d_input_action = NULL;
     return p;
@@ -67,8 +68,8 @@ static void gaussian_noise_from_rand(float* out, int n) {
  * reference's seeded rand() stream. */
 void sample_action(GaussianPolicy* policy, float* state, float* action, float* log_prob, int m) {
     const int A = policy->action_size;
+    policy_host_sync(policy);
     forward_propagation(policy->mu, state, m);
-    phip_h2d(policy->d_log_std, policy->log_std, sizeof(float) * (size_t)A);
     float* noise = (float*)xmalloc(sizeof(float) * (size_t)m * A);
     gaussian_noise_from_rand(noise, m * A);
     float* d_noise = stage_up(ST_E, noise, (size_t)m * A);
@@ -84,8 +85,8 @@ void sample_action(GaussianPolicy* policy, float* state, float* action, float* l
 void compute_log_prob(GaussianPolicy* policy, float* out, float* state, float* action, int m) {
     const int A = policy->action_size;
     policy->input_action = action;
+    policy_host_sync(policy);
     forward_propagation(policy->mu, state, m);
-    phip_h2d(policy->d_log_std, policy->log_std, sizeof(float) * (size_t)A);
     float* d_act = stage_up(ST_E, action, (size_t)m * A);
     float* d_out = (float*)stage(ST_F, sizeof(float) * (size_t)m);
     phip_log_prob(policy->mu->d_output, policy->d_log_std, d_act, d_out, m, A);
@@ -95,6 +96,7 @@ void compute_log_prob(GaussianPolicy* policy, float* out, float* state, float* a
 /* policy.cu:101-111 with D2 (grad_in per sample) */
 void log_prob_backwards(GaussianPolicy* policy, float* grad_in, float* grad_mu, float* grad_log_std, int m) {
     const int A = policy->action_size;
+    policy_host_sync(policy);
     float* d_act = stage_up(ST_E, policy->input_action, (size_t)m * A);
     float* d_g = stage_up(ST_F, grad_in, (size_t)m);
     float* d_gmu = (float*)stage(ST_G, sizeof(float) * (size_t)m * A);
@@ -128,6 +130,7 @@ float compute_entropy_cuda(GaussianPolicy* policy) {
 
 /* policy.cu:171-178 — reads the host log_std mirror, evaluated on the GPU */
 float compute_entropy(GaussianPolicy* policy) {
+    policy_host_sync(policy);
     float* d_ls = stage_up(ST_G, policy->log_std, (size_t)policy->action_size);
     float* d = (float*)stage(ST_H, 16);
     phip_entropy(d_ls, policy->action_size, d);
@@ -139,10 +142,16 @@ float compute_entropy(GaussianPolicy* policy) {
 void policy_to_host(GaussianPolicy* policy) {
     nn_write_weights_to_host(policy->mu);
     phip_d2h(policy->log_std, policy->d_log_std, sizeof(float) * (size_t)policy->action_size);
+    nn_sync_extra_snapshot(policy->mu, policy->log_std);
+    policy->mu->host_version = policy->mu->dev_version;
 }
+
+/* before a host-pointer entry point: μ's mirrors and log_std reconciled with HBM (nn_host_sync) */
+void policy_host_sync(GaussianPolicy* policy) { nn_host_sync(policy->mu, policy->log_std); }
 
 /* policy.cu:201-227 */
 void save_policy(GaussianPolicy* policy, FILE* file) {
+    policy_host_sync(policy);
     fwrite(policy->log_std, sizeof(float), (size_t)policy->action_size, file);
     save_neural_network(policy->mu, file);
 }
@@ -158,5 +167,7 @@ GaussianPolicy* load_policy(FILE* file, int state_size, int action_size) {
     p->mu = nn_load_ex(file, action_size);
     attach_log_std(p);
     phip_h2d(p->d_log_std, p->log_std, sizeof(float) * (size_t)action_size);
+    nn_sync_extra_snapshot(p->mu, p->log_std);
+    p->mu->host_version = p->mu->dev_version;
     return p;
 }

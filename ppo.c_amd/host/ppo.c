@@ -38,6 +38,7 @@ typedef struct {
     uint64_t key;                 /* device-shuffle epoch key */
     unsigned long long seed;
     int seeded;
+    long max_v, max_p;            /* ppo_set_step_limit: cap on value / policy minibatch steps (−1: none) */
 } PPODev;
 
 static float* g_v = NULL;         /* V(state), V(next_state) for compute_gae_cuda */
@@ -84,6 +85,7 @@ static PPODev* dev_ws(PPO* ppo, int B) {
     if (!d) {
         d = (PPODev*)xcalloc(1, sizeof(PPODev));
         d->stats = (float*)phip_malloc(4 * sizeof(float));
+        d->max_v = d->max_p = -1;
         ppo->dev = d;
     }
     if (B > d->cap_B) {
@@ -368,6 +370,7 @@ static int ppo_update_tiny(PPO* ppo, PPODev* d, int B, int n_epochs_policy, int 
     const int limit = buf->full ? buf->capacity : buf->idx;
     const int num_batches = buf->capacity / B;
     if (getenv("PPO_NO_TINY") || phip_comm_world() > 1 || n_epochs_value > 16 || n_epochs_policy > 16) return -1;
+    if (d->max_v >= 0 || d->max_p >= 0) return -1;          /* step caps: the multi-launch path */
     PhipTinyNet nv, np;
     if (tiny_net(ppo->V, ppo->adam_V, &nv) || tiny_net(ppo->policy->mu, ppo->adam_policy, &np)) return -1;
     if (!ppo->adam_entropy->flat) return -1;
@@ -440,6 +443,8 @@ void ppo_update(void* vppo, float gamma, int batch_size, int n_epochs_policy, in
     nn_set_x3_planar(planar ? mode : 0);
     ppo_update_body(ppo, gamma, batch_size, n_epochs_policy, n_epochs_value, shuffle_mode, seed);
     nn_set_x3_planar(0);
+    ppo->V->dev_version++;               /* HBM parameters moved (also by the single-workgroup path) */
+    ppo->policy->mu->dev_version++;
 }
 
 static void ppo_update_body(PPO* ppo, float gamma, int batch_size, int n_epochs_policy, int n_epochs_value,
@@ -467,8 +472,10 @@ static void ppo_update_body(PPO* ppo, float gamma, int batch_size, int n_epochs_
 
     ppo_gae_device(V, buf, gamma, ppo->lambda);
     /* D19: an empty buffer (idx = 0, not full) has nothing to train on; the reference would divide
-     * by zero (rand() % 0 in shuffle_buffer, % limit in get_batch) — here the update ends after GAE */
-    if (limit <= 0) return;
+     * by zero (rand() % 0 in shuffle_buffer, % limit in get_batch) — here the update ends after GAE.
+     * At world > 1 the ranks agree first (min over ranks): one empty shard ends the update on every
+     * rank, so no rank waits in a gradient all-reduce the others never issue. */
+    if ((world > 1 ? phip_comm_min_i32(limit) : limit) <= 0) return;
 
     if (ppo_update_tiny(ppo, d, B, n_epochs_policy, n_epochs_value, shuffle_mode) == 0) return;
 
@@ -480,7 +487,9 @@ static void ppo_update_body(PPO* ppo, float gamma, int batch_size, int n_epochs_
      * data parallelism (world > 1) both loops hand their gradient all-reduces to comm.hip's single
      * comm stream in this host issue order, identical on every rank, so they stay concurrent and
      * each collective overlaps the other loop's kernels. */
-    const long nv = (long)n_epochs_value * num_batches, np = (long)n_epochs_policy * num_batches;
+    long nv = (long)n_epochs_value * num_batches, np = (long)n_epochs_policy * num_batches;
+    if (d->max_v >= 0 && nv > d->max_v) nv = d->max_v;
+    if (d->max_p >= 0 && np > d->max_p) np = d->max_p;
     uint64_t* keys = (uint64_t*)xmalloc(sizeof(uint64_t) * (size_t)(n_epochs_value + n_epochs_policy + 1));
     uint64_t* keys_v = keys;
     uint64_t* keys_p = keys + n_epochs_value;
@@ -540,6 +549,12 @@ static void ppo_update_body(PPO* ppo, float gamma, int batch_size, int n_epochs_
     }
     if (concurrent) phip_side_join();
     free(keys);
+}
+
+void ppo_set_step_limit(void* vppo, long max_value_steps, long max_policy_steps) {
+    PPODev* d = dev_ws((PPO*)vppo, 1);
+    d->max_v = max_value_steps;
+    d->max_p = max_policy_steps;
 }
 
 void ppo_reset_stats(void* vppo) {
@@ -703,12 +718,18 @@ PPO* load_ppo(const char* filename, bool use_cuda) {
         fread(&ppo->lr_V, sizeof(float), 1, f) != 1 || fread(&S, sizeof(int), 1, f) != 1 ||
         fread(&A, sizeof(int), 1, f) != 1 || fread(&cap, sizeof(int), 1, f) != 1)
         die("load_ppo: unexpected end of file");
+    if (S <= 0 || A <= 0 || cap < 0) die("load_ppo: bad header");
     ppo->buffer = create_trajectory_buffer(cap, S, A);
     ppo->policy = load_policy(f, S, A);
     ppo->V = load_neural_network(f);
+    if (ppo->policy->mu->layers[0].input_size != S || ppo->policy->mu->output_size != A ||
+        ppo->V->layers[0].input_size != S || ppo->V->output_size != 1)
+        die("load_ppo: network shapes do not match the header");
+    /* optimiser state always lives in HBM (use_cuda is kept for the ABI; both values run the HIP
+     * path), so the moments are loaded as device Adams whatever use_cuda says */
     ppo->adam_policy = load_adam_from_nn(f, ppo->policy->mu, true);
     ppo->adam_V = load_adam_from_nn(f, ppo->V, true);
-    ppo->adam_entropy = load_adam(f, &ppo->policy->d_log_std, &ppo->policy->d_log_std_grad, &A, true);
+    ppo->adam_entropy = load_adam_ex(f, &ppo->policy->d_log_std, &ppo->policy->d_log_std_grad, &A, 1, true);
     fclose(f);
     return ppo;
 }

@@ -42,7 +42,8 @@ class NeuralNetwork(C.Structure):
                 ("extra_floats", C.c_long), ("d_x0", c_float_p), ("d_act_bits", C.POINTER(C.c_uint)),
                 ("bits_m", C.c_int), ("dtype", C.c_int), ("x0_dtype", C.c_int), ("d_w16", C.c_void_p),
                 ("d_tiny_wt", c_float_p), ("tiny_wt_cap", C.c_long), ("d_w3", C.c_void_p),
-                ("x3_in_planes", C.c_int)]
+                ("x3_in_planes", C.c_int), ("h_sync", c_float_p), ("dev_version", C.c_long),
+                ("host_version", C.c_long)]
 
 
 class GaussianPolicy(C.Structure):
@@ -127,9 +128,11 @@ _SIGS = {
     "ppo_comm_world": (C.c_int, []),
     "ppo_comm_finalize": (None, []),
     "ppo_comm_allreduce_f32": (None, [_P, C.c_long]),
+    "ppo_welford_combine": (None, [_P, C.c_int, _P]),
     "ppo_update": (None, [_P, C.c_float, C.c_int, C.c_int, C.c_int, C.c_int, C.c_ulonglong]),
     "ppo_read_stats": (None, [_P, C.POINTER(C.c_double), C.c_int]),
     "ppo_reset_stats": (None, [_P]),
+    "ppo_set_step_limit": (None, [_P, C.c_long, C.c_long]),
     "ppo_sample_action_device": (None, [_P, _P, _P, _P, C.c_int, C.c_ulonglong, C.c_ulonglong]),
     "ppo_fill_synthetic": (None, [_P, C.c_int, C.c_int, C.c_ulonglong, C.c_float]),
     "ppo_prof_enable": (None, [C.c_int]),

@@ -61,7 +61,7 @@ def gpu_relu_masks(lib, nn_ptr, x_rows):
     return masks
 
 
-def oracle_grads_with_masks(oracle, sizes, relu, params, x, gout, masks, what=""):
+def oracle_grads_with_masks(oracle, sizes, relu, params, x, gout, masks, what="", max_flips=16):
     """The oracle's MLP gradients (reference neural_network.cu:192-231) evaluated with libppo's ReLU′
     masks.  Where the two forwards disagree on a mask bit, the pre-activation lies within fp32
     rounding of 0 (asserted: |y| ≤ 1e-5·max|y|, at most 16 such units per layer), both sides are
@@ -80,7 +80,7 @@ def oracle_grads_with_masks(oracle, sizes, relu, params, x, gout, masks, what=""
         if n:
             worst = float(np.abs(y[diff]).max())
             assert worst <= 1e-5 * float(np.abs(y).max()), f"{what}: mask disagreement at |y| = {worst:.3g}"
-            assert n <= 16, f"{what}: {n} mask disagreements in layer {i}"
+            assert n <= max_flips, f"{what}: {n} mask disagreements in layer {i}"
         y[mk & ~(y > 0)] = np.float32(1e-30)          # GPU kept the unit: positive, negligible value
         y[~mk] = 0
     return oracle.mlp_backward(sizes, relu, params, x, acts, gout), flips

@@ -60,6 +60,22 @@ def test_x3_every_cfg(lib, oracle, x3, m, n, l):
         lib.ppo_gemm_x3_tune(-1, 0)
 
 
+@pytest.mark.parametrize("m,n,l", [(32768, 512, 512), (32768, 376, 512)])
+def test_x3_production_c4_shapes(lib, oracle, x3, m, n, l):
+    """The bench's C4 minibatch products (B = 32768) with the automatic tile choice and the production
+    split-K grids of grad_W (the ones the timed update launches), against the oracle (OpenBLAS)."""
+    oracle.load(use_openblas=True)
+    oracle.load().ref_blas_threads(16)
+    rng = np.random.default_rng(m + n + l + 1)
+    x, W, b, g = _rand(rng, (m, n)), _rand(rng, (l, n), -0.1, 0.1), _rand(rng, l, -0.1, 0.1), _rand(rng, (m, l))
+    lib.ppo_gemm_x3_tune(-1, 0)
+    y, gx, gW = _products(lib, x, W, b, g)
+    assert_gemm_close(y, oracle.mat_mul(x, W, b), n, "C4 forward")
+    gx_ref, gW_ref = oracle.mat_mul_backwards(g, x, W)
+    assert_gemm_close(gx, gx_ref, l, "C4 grad_x")
+    assert_gemm_close(gW, gW_ref, m, "C4 grad_W (split-K)")
+
+
 @pytest.mark.parametrize("m,n,l", [(8192, 512, 512), (4096, 376, 512), (8192, 512, 17)])
 def test_x3_as_accurate_as_exact_fp32(lib, x3, m, n, l):
     """Max and RMS error against float64, x3 vs the exact fp32-MFMA engine on the same inputs:
