@@ -11,6 +11,7 @@ inside libppo each minibatch, advantage statistics are global.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c3|c2|c5|c5f32] [--batch B]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+    (torch.distributed.run is only the launcher: this process never imports torch)
 
 Prints ONE JSON line (rank 0).  `value` = learner env-steps/s over all ranks = world·N / t_update.
 """
@@ -25,16 +26,15 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "ppo.c_amd"))
 
-# torch first: libppo then binds to the HIP runtime torch already loaded (same soname), so the
-# process holds ONE runtime.  Loading libppo first makes torch pull a second one, which aborts
-# at interpreter exit (measured on the MI355X box).
+# No torch in this process: libppo owns the device, the stream and RCCL, so the process maps ONE HIP
+# runtime (torch's wheel bundles a second one).  torch.distributed.run is only the
+# launcher; ranks exchange the RCCL unique id through a file (exchange_unique_id) and the barrier /
+# max-over-ranks timing run over libppo's communicator.
 import numpy as np  # noqa: E402
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
 
 import ppo_ffi  # noqa: E402
 
-LIB = ppo_ffi.load()
+LIB = ppo_ffi.load() if __name__ == "__main__" else None
 
 CONFIGS = {
     # name: (S, hidden, A, T, E, batch)   — BASELINE.json configs
@@ -61,6 +61,37 @@ def algorithmic_flops(S, H, A, N, B, n_v=10, n_p=4):
     P_mu, P_v = P([S] + H + [A]), P([S] + H + [1])
     nb = (N // B) * B
     return 4 * N * P_v + n_v * nb * (6 * P_v - 2 * S * H[0]) + n_p * nb * (6 * P_mu - 2 * S * H[0])
+
+
+def uid_path(world):
+    """Rendezvous file of one launch: torch.distributed.run starts every local rank as a child of one
+    agent process, so (agent pid, master port, run id) names this launch and nothing else."""
+    tag = f"{os.getppid()}_{os.environ.get('MASTER_PORT', '0')}_{os.environ.get('TORCHELASTIC_RUN_ID', 'none')}"
+    return os.path.join(os.environ.get("PPO_RDZV_DIR", "/tmp"), f"ppo_rccl_uid_{tag}_w{world}")
+
+
+def exchange_unique_id(rank, world, make_id, timeout_s=300.0, path=None):
+    """Rank 0 publishes the RCCL unique id (atomic rename); the other ranks poll for it."""
+    path = path or uid_path(world)
+    if rank == 0:
+        uid = make_id()
+        tmp = f"{path}.tmp{os.getpid()}"
+        with open(tmp, "wb") as f:
+            f.write(uid)
+        os.replace(tmp, path)
+        return uid
+    t0 = time.time()
+    while True:
+        try:
+            with open(path, "rb") as f:
+                uid = f.read()
+            if uid:
+                return uid
+        except FileNotFoundError:
+            pass
+        if time.time() - t0 > timeout_s:
+            raise SystemExit(f"rank {rank}: no RCCL unique id at {path} after {timeout_s:.0f}s")
+        time.sleep(0.01)
 
 
 def pmc_traffic():
@@ -168,17 +199,21 @@ def main():
             raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one process per GPU)")
     if LIB.ppo_set_device(local) != 0:
         raise SystemExit(f"libppo: cannot select device {local}: {LIB.ppo_last_error().decode()}")
-    torch.cuda.set_device(local)
 
     if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)      # control plane only
-        uid = C.create_string_buffer(256)
-        n = LIB.ppo_comm_unique_id(uid, 256) if rank == 0 else 0
-        obj = [bytes(uid.raw[:n])] if rank == 0 else [None]
-        dist.broadcast_object_list(obj, src=0)
-        if LIB.ppo_comm_init(rank, world, obj[0]) != 0:                  # RCCL over xGMI for the data path
+        def make_id():
+            buf = C.create_string_buffer(256)
+            n = LIB.ppo_comm_unique_id(buf, 256)
+            return bytes(buf.raw[:n])
+
+        uid = exchange_unique_id(rank, world, make_id)
+        if LIB.ppo_comm_init(rank, world, uid) != 0:                      # RCCL over xGMI for the data path
             raise SystemExit(f"ppo_comm_init failed: {LIB.ppo_last_error().decode()}")
+        if rank == 0:                                                    # every rank has joined: tidy up
+            try:
+                os.remove(uid_path(world))
+            except OSError:
+                pass
     comm_self = world == 1 and os.environ.get("PPO_COMM_SELF", "0") not in ("", "0")
     if comm_self:
         # rehearsal of the data-parallel path on one GPU: a one-rank RCCL communicator, so every
@@ -211,9 +246,7 @@ def main():
 
     def barrier():
         LIB.ppo_synchronize()
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
+        LIB.ppo_comm_barrier()
 
     for _ in range(args.warmup):
         LIB.ppo_update(ppo, 0.99, B, 4, 10, args.shuffle, args.seed)
@@ -230,10 +263,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     LIB.ppo_prof_enable(0)
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = LIB.ppo_comm_max_f64(elapsed)                              # max over ranks
 
     # batched device rollout of the same E x T (SURVEY §8d "rollout env-steps/s", reported beside
     # the learner throughput; not part of `value`): one warm call, then one timed call
@@ -246,10 +276,7 @@ def main():
         LIB.ppo_rollout_device(ppo, E, T, env_kind, args.seed + rank)
         barrier()
         t_rollout = time.perf_counter() - r0
-        if world > 1:
-            tr = torch.tensor([t_rollout], dtype=torch.float64)
-            dist.all_reduce(tr, op=dist.ReduceOp.MAX)
-            t_rollout = float(tr.item())
+        t_rollout = LIB.ppo_comm_max_f64(t_rollout)
 
     def prof_snapshot():
         ms, work, launches = (C.c_double * 7)(), (C.c_double * 7)(), (C.c_long * 7)()
@@ -268,9 +295,11 @@ def main():
     # the chip the other stream held.  One more update with the loops serialised (PPO_SERIAL=1)
     # times every event_stride-th launch running alone.
     serial = None
+    shapes = []
     if not args.no_kernel_events:
         os.environ["PPO_SERIAL"] = "1"
         LIB.ppo_prof_reset()
+        LIB.ppo_prof_kernel_events(1)          # GEMMs: the kernel's own duration (dispatch-stamped)
         LIB.ppo_prof_enable(max(1, args.event_stride))
         barrier()
         s0 = time.perf_counter()
@@ -278,11 +307,31 @@ def main():
         barrier()
         serial_s = time.perf_counter() - s0
         LIB.ppo_prof_enable(0)
+        LIB.ppo_prof_kernel_events(0)
         del os.environ["PPO_SERIAL"]
         serial = list(prof_snapshot()) + [serial_s]
+        cap = 256
+        keys, kms, kl, kw = (C.c_longlong * cap)(), (C.c_double * cap)(), (C.c_long * cap)(), (C.c_double * cap)()
+        n_sh = min(cap, LIB.ppo_prof_shapes(keys, kms, kl, kw, cap))
+        ops = ["forward", "grad_x", "grad_W", "grad_W+grad_x"]
+        engines = ["exact-fp32", "x3", "bf16"]
+        for i in range(n_sh):
+            k = keys[i]
+            shapes.append({"op": ops[(k >> 58) & 0xF], "engine": engines[(k >> 54) & 0xF], "m": (k >> 24) & 0x3FFFFFFF,
+                           "n": (k >> 12) & 0xFFF, "l": k & 0xFFF, "launches": kl[i], "ms": kms[i],
+                           "avg_us": 1000.0 * kms[i] / kl[i], "tflops": kw[i] / (kms[i] * 1e-3) / 1e12})
+        shapes.sort(key=lambda d: -d["ms"])
 
     t_update = elapsed / args.steps
-    flops = algorithmic_flops(S, H, A, N, B)
+    # algorithmic FLOPs of the update: SURVEY §8(d)'s formula counts two full-buffer value forwards for
+    # GAE; V(next_state[t]) = V(state[t+1]) is reused wherever the rows are equal, so only the rows of
+    # the own next-state forward (stats[7]) are work the update does
+    stats_all = (C.c_double * 8)()
+    LIB.ppo_read_stats(ppo, stats_all, 8)
+    gae_own = int(stats_all[7])
+    sv = [S] + H + [1]
+    P_v = sum(a * b for a, b in zip(sv[:-1], sv[1:]))
+    flops = algorithmic_flops(S, H, A, N, B) - 2.0 * (N - gae_own) * P_v
     # sampled launches: class time per update = mean sampled launch time × launches issued
     # per-class breakdown from the serialised kernel pass (one update) when it ran
     k_ms, k_launches, k_issued, k_updates = (serial[0], serial[2], serial[3], 1) if serial else \
@@ -317,6 +366,7 @@ def main():
                     "ms": 1000.0 * t_rollout if t_rollout else None},
         "minibatch_steps_per_sec": 14 * (N // B) / t_update,
         "algorithmic_tflop_per_update": flops / 1e12,
+        "gae_next_state_forward_rows": gae_own,
         "mfma_frac_whole_update": flops / t_update / (peak * 1e12),
         "kernels": kernels,
         "loss": {"value_mean": stats[0] / max(1.0, stats[1]), "policy_mean": stats[2] / max(1.0, stats[3])},
@@ -335,8 +385,12 @@ def main():
                                          "x3": "gemm_bf16_kernel<P=3> (x3 engine: hidden and input layers) + "
                                                "gemm_f32_kernel / gemm_pair_kernel (1- and A-wide output layers)",
                                          "exact": "gemm_f32_kernel"}[engine] +
-                                        " (linear-layer launches; Σ 2MNK / Σ HIP-event time over every "
-                                        "event_stride-th launch of one serialised update after the timed region)",
+                                        " (every linear-layer launch of one serialised update after the timed "
+                                        "region; Σ 2MNK / Σ kernel duration, each duration stamped by the "
+                                        "kernel's own dispatch (hipExtLaunchKernel events), as rocprofv3 "
+                                        "--kernel-trace measures it)",
+                              "dominant": ({**shapes[0], "frac": shapes[0]["tflops"] / peak} if shapes else None),
+                              "by_shape": shapes[:12],
                               "gemm_engine": engine,
                               "peak_basis": {"bf16": "dense bf16 MFMA spec",
                                              "x3": "dense bf16 MFMA spec / 6 (six bf16 products per fp32 product)",
@@ -352,8 +406,6 @@ def main():
         result["cpu_baseline"]["gpu_over_cpu"] = result["value"] / result["cpu_baseline"]["value"]
     LIB.free_ppo(ppo)
     LIB.ppo_comm_finalize()
-    if world > 1:
-        dist.destroy_process_group()
     if rank == 0:
         print(json.dumps(result), flush=True)
 

@@ -46,6 +46,10 @@ int  ppo_comm_world(void);
 void ppo_comm_finalize(void);
 /* sum-all-reduce of n floats in place on libppo's stream (no-op at world 1) */
 void ppo_comm_allreduce_f32(float* d_buf, long n);
+/* host-synchronous helpers over the communicator (identity at world 1): a barrier (every rank's
+ * queued work drained, then one collective), and the max over ranks of a host double */
+void   ppo_comm_barrier(void);
+double ppo_comm_max_f64(double v);
 /* the advantage-statistics combine after the all-gather: `count` device triples (n, mean, M2) in
  * double → one triple (Chan et al. pairwise combine; empty parts skipped).  Synchronises. */
 void ppo_welford_combine(const double* d_parts, int count, double* d_out);
@@ -65,7 +69,8 @@ void ppo_update(void* ppo, float gamma, int batch_size, int n_epochs_policy, int
 
 /* stats accumulated by ppo_update since the last reset (synchronises):
  * out[0]=Σ value loss, out[1]=#value steps, out[2]=Σ policy loss,
- * out[3]=#policy steps, out[4]=entropy, out[5]=advantage mean, out[6]=advantage std */
+ * out[3]=#policy steps, out[4]=entropy, out[5]=advantage mean, out[6]=advantage std,
+ * out[7]=rows of the last GAE's own V(next_state) forward (those not reused from V(state[t+1])) */
 void ppo_read_stats(void* ppo, double* out, int n);
 void ppo_reset_stats(void* ppo);
 /* Parity testing at full size: cap the value / policy minibatch steps of the following ppo_update
@@ -140,6 +145,14 @@ void ppo_prof_reset(void);
 /* per class: out_ms[k] = Σ kernel time (ms), out_work[k] = Σ algorithmic FLOPs (GEMM) or bytes,
  * out_launches[k] = launches.  Synchronises. */
 void ppo_prof_read(double* out_ms, double* out_work, long* out_launches);
+/* on != 0: sampled GEMM launches are timed by events the kernel dispatch itself stamps
+ * (hipExtLaunchKernel) instead of event packets around the launch — the kernel's own duration, as
+ * rocprofv3 --kernel-trace reports it (default off: event pairs around every sampled launch) */
+void ppo_prof_kernel_events(int on);
+/* per GEMM shape since the last reset: key = op<<58 | engine<<54 | m<<24 | n<<12 | l (op 0 forward,
+ * 1 grad_x, 2 grad_W, 3 paired grad_W + grad_x; engine 0 exact fp32, 1 x3, 2 bf16), Σ ms, sampled
+ * launches and Σ algorithmic FLOPs.  Returns the number of shapes (fills at most cap).  Synchronises. */
+int  ppo_prof_shapes(long long* keys, double* ms, long* launches, double* work, int cap);
 /* per class: launches issued while profiling was enabled (sampled or not) */
 void ppo_prof_counts(long* out_total);
 /* per class: Σ algorithmic work of every launch issued while profiling was enabled */

@@ -180,6 +180,29 @@ void phip_allgather_f64(const double* d_send, double* d_recv, long n_per_rank) {
     comm_leave(slot);
 }
 
+// host-level helpers for drivers (bench.py) that keep torch out of the process: a barrier and a
+// max-over-ranks of a double, both over the RCCL communicator (synchronous)
+static double* g_f64 = nullptr;
+
+double ppo_comm_max_f64(double v) {
+    if (!g_comm) return v;
+    if (!g_f64) g_f64 = (double*)phip_malloc(sizeof(double));
+    phip_h2d(g_f64, &v, sizeof(double));
+    int slot;
+    hipStream_t cs = comm_enter(&slot);
+    nccl_check(ncclAllReduce(g_f64, g_f64, 1, ncclFloat64, ncclMax, g_comm, cs), "ncclAllReduce(max)", __LINE__);
+    comm_leave(slot);
+    double out = v;
+    phip_d2h(&out, g_f64, sizeof(double));
+    return out;
+}
+
+void ppo_comm_barrier(void) {
+    phip_sync();
+    (void)ppo_comm_max_f64(0.0);
+    phip_sync();
+}
+
 // min over ranks of a host integer (synchronous; a few µs per call).  The update uses it to agree
 // on whether any rank has an empty shard, so either every rank trains or none does.
 int phip_comm_min_i32(int v) {

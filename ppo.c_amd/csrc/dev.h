@@ -5,6 +5,7 @@
 // event timing used by bench.py's roofline (ppo_prof_*).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <cstdint>
 #include <cstdio>
 
@@ -22,11 +23,30 @@ void        fail(const char* msg, const char* file, int line);   // records + ab
 // records the stop event and attributes `work` (FLOPs or bytes) to class k.
 struct ProfScope {
     int k; double work; int slot;
-    ProfScope(int k_, double work_);
+    ProfScope(int k_, double work_, long long key = 0);   // key: shape tag (gemm_key) for per-shape stats
     ~ProfScope();
 };
 
+// Kernel-attached timing (ppo_prof_kernel_events): a sampled GEMM scope records no events of its own;
+// its one kernel is launched through PPO_TIMED_LAUNCH, whose start/stop events are stamped by the
+// dispatch itself (hipExtLaunchKernel) — the kernel's own duration, as rocprofv3 reports it.
+bool take_kernel_events(hipEvent_t* start, hipEvent_t* stop);
+
+// shape tag of a GEMM launch: op (0 fwd, 1 grad_x, 2 grad_W, 3 paired bwd) | engine | m | n | l
+inline long long gemm_key(int op, int engine, long m, long n, long l) {
+    return ((long long)op << 58) | ((long long)engine << 54) | ((long long)m << 24) | ((long long)n << 12) | l;
+}
+
 }  // namespace ppo
+
+#define PPO_TIMED_LAUNCH(kernel, grid, block, lds, strm, ...)                                         \
+    do {                                                                                           \
+        hipEvent_t ppo_e0_, ppo_e1_;                                                               \
+        if (::ppo::take_kernel_events(&ppo_e0_, &ppo_e1_))                                         \
+            hipExtLaunchKernelGGL(kernel, grid, block, lds, strm, ppo_e0_, ppo_e1_, 0, __VA_ARGS__); \
+        else                                                                                       \
+            hipLaunchKernelGGL(kernel, grid, block, lds, strm, __VA_ARGS__);                       \
+    } while (0)
 
 #define PPO_CHECK(x) ::ppo::check((x), #x, __FILE__, __LINE__)
 #define PPO_LAUNCH_CHECK() ::ppo::check(hipGetLastError(), "kernel launch", __FILE__, __LINE__)

@@ -515,10 +515,10 @@ void launch(Args a) {
     const long grid = (long)a.tiles_m * a.tiles_n * a.splits;
     PPO_REQUIRE(grid > 0 && grid < (1L << 31), "gemm: grid out of range");
     if (a.vec_a && a.vec_b)
-        hipLaunchKernelGGL((gemm_f32_kernel<OP, BM, BN, WARPS_M, BK, true, DBUF>), dim3((unsigned)grid), dim3(NT_),
+        PPO_TIMED_LAUNCH((gemm_f32_kernel<OP, BM, BN, WARPS_M, BK, true, DBUF>), dim3((unsigned)grid), dim3(NT_),
                            0, ppo::stream(), a);
     else
-        hipLaunchKernelGGL((gemm_f32_kernel<OP, BM, BN, WARPS_M, BK, false, DBUF>), dim3((unsigned)grid), dim3(NT_),
+        PPO_TIMED_LAUNCH((gemm_f32_kernel<OP, BM, BN, WARPS_M, BK, false, DBUF>), dim3((unsigned)grid), dim3(NT_),
                            0, ppo::stream(), a);
     PPO_LAUNCH_CHECK();
 }
@@ -602,9 +602,9 @@ void fwd(float* y, const float* x, const float* W, const float* b, int m, int n,
         a.tiles_n = ppo_divup(l, 32);
         const int grid = ppo_divup(m, 32) * a.tiles_n;
         if (a.vec_a && a.vec_b)
-            hipLaunchKernelGGL(gemm_smallm_kernel<true>, dim3(grid), dim3(64 * SM_WAVES), 0, ppo::stream(), a);
+            PPO_TIMED_LAUNCH(gemm_smallm_kernel<true>, dim3(grid), dim3(64 * SM_WAVES), 0, ppo::stream(), a);
         else
-            hipLaunchKernelGGL(gemm_smallm_kernel<false>, dim3(grid), dim3(64 * SM_WAVES), 0, ppo::stream(), a);
+            PPO_TIMED_LAUNCH(gemm_smallm_kernel<false>, dim3(grid), dim3(64 * SM_WAVES), 0, ppo::stream(), a);
         PPO_LAUNCH_CHECK();
         return;
     }
@@ -702,10 +702,10 @@ void bwd_pair(float* gW, float* gb, float* gx, const float* g, const float* x, c
         const dim3 grid((unsigned)(g1 + g2));
         const bool vw = aw.vec_a && aw.vec_b, vx = ax.vec_a && ax.vec_b;
         if (hidden && vw && vx) {
-            hipLaunchKernelGGL((gemm_pair_kernel<128, 128, 2, true, 128, 128, 2, true>), grid, dim3(NT_), 0,
+            PPO_TIMED_LAUNCH((gemm_pair_kernel<128, 128, 2, true, 128, 128, 2, true>), grid, dim3(NT_), 0,
                                ppo::stream(), aw, ax, (int)g1);
         } else if (output && !vw && !vx) {
-            hipLaunchKernelGGL((gemm_pair_kernel<32, 128, 1, false, 128, 128, 2, false>), grid, dim3(NT_), 0,
+            PPO_TIMED_LAUNCH((gemm_pair_kernel<32, 128, 1, false, 128, 128, 2, false>), grid, dim3(NT_), 0,
                                ppo::stream(), aw, ax, (int)g1);
         } else {
             launch_cfg<OP_TN>(c, aw);           // arguments built (and output zeroed) already
@@ -727,7 +727,7 @@ void phip_linear_fwd_bits(float* y, const float* x, const float* W, const float*
                           unsigned* bits) {
     if (m <= 0 || l <= 0) return;
     PPO_REQUIRE(y && x && W && n > 0, "phip_linear_fwd: null operand");
-    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l);
+    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l, ppo::gemm_key(0, 0, m, n, l));
     fwd(y, x, W, b, m, n, l, relu, relu ? bits : nullptr, -1);
 }
 
@@ -739,7 +739,7 @@ void phip_linear_fwd_gather(float* y, const float* x, const int* ridx, float* xc
                             int m, int n, int l, int relu, unsigned* bits) {
     if (m <= 0 || l <= 0) return;
     PPO_REQUIRE(y && x && ridx && W && n > 0, "phip_linear_fwd_gather: null operand");
-    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l);
+    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l, ppo::gemm_key(0, 0, m, n, l));
     fwd(y, x, W, b, m, n, l, relu, relu ? bits : nullptr, -1, ridx, xcopy);
 }
 
@@ -747,7 +747,7 @@ void phip_linear_bwd_x_bits(float* gx, const float* g, const float* W, const flo
                             int n, int l) {
     if (m <= 0 || n <= 0) return;
     PPO_REQUIRE(gx && g && W && l > 0, "phip_linear_bwd_x: null operand");
-    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l);
+    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l, ppo::gemm_key(1, 0, m, n, l));
     bwd_x(gx, g, W, mask, bits, m, n, l, -1);
 }
 
@@ -758,7 +758,7 @@ void phip_linear_bwd_x(float* gx, const float* g, const float* W, const float* m
 void phip_linear_bwd_w_ex(float* gW, float* gb, const float* g, const float* x, int m, int n, int l, int zeroed) {
     if (l <= 0 || n <= 0) return;
     PPO_REQUIRE(gW && g && x, "phip_linear_bwd_w: null operand");
-    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l);
+    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l, ppo::gemm_key(2, 0, m, n, l));
     bwd_w(gW, gb, g, x, m, n, l, zeroed, -1);
 }
 
@@ -770,7 +770,7 @@ void phip_linear_bwd_pair(float* gW, float* gb, float* gx, const float* g, const
                           const unsigned* bits, int m, int n, int l, int zeroed) {
     if (l <= 0 || n <= 0) return;
     PPO_REQUIRE(gW && gx && g && x && W, "phip_linear_bwd_pair: null operand");
-    ppo::ProfScope ps(PPO_K_GEMM, 4.0 * m * n * l);
+    ppo::ProfScope ps(PPO_K_GEMM, 4.0 * m * n * l, ppo::gemm_key(3, 0, m, n, l));
     bwd_pair(gW, gb, gx, g, x, W, bits, m, n, l, zeroed);
 }
 

@@ -742,7 +742,7 @@ void launch(Args a) {
             attr = true;
         }
     }
-    hipLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(var_wide(VAR) ? 2 * NT_ : NT_), lds, ppo::stream(), a);
+    PPO_TIMED_LAUNCH(kern, dim3((unsigned)grid), dim3(var_wide(VAR) ? 2 * NT_ : NT_), lds, ppo::stream(), a);
     PPO_LAUNCH_CHECK();
 }
 
@@ -887,7 +887,7 @@ void phip_linear16_fwd(void* y, int ty, const void* x, int tx, const int* ridx, 
                        const float* b, int m, int n, int l, int relu, unsigned* bits) {
     if (m <= 0 || l <= 0) return;
     PPO_REQUIRE(y && x && W16 && n > 0, "phip_linear16_fwd: null operand");
-    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l);
+    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l, ppo::gemm_key(0, 2, m, n, l));
     Args a{};
     a.A = x; a.lda = n; a.B = W16; a.ldb = n; a.C = y; a.ldc = l;
     a.M = m; a.N = l; a.K = n; a.kchunk = n; a.splits = 1;
@@ -905,7 +905,7 @@ void phip_linear16_bwd_x(void* gx, int tgx, const void* g, int tg, const void* W
                          int n, int l) {
     if (m <= 0 || n <= 0) return;
     PPO_REQUIRE(gx && g && W16 && l > 0, "phip_linear16_bwd_x: null operand");
-    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l);
+    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l, ppo::gemm_key(1, 2, m, n, l));
     Args a{};
     a.A = g; a.lda = l; a.B = W16; a.ldb = n; a.C = gx; a.ldc = n;
     a.M = m; a.N = n; a.K = l; a.kchunk = l; a.splits = 1;
@@ -922,7 +922,7 @@ void phip_linear16_bwd_w(float* gW, float* gb, const void* g, int tg, const void
                          int zeroed) {
     if (l <= 0 || n <= 0) return;
     PPO_REQUIRE(gW && g && x, "phip_linear16_bwd_w: null operand");
-    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l);
+    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l, ppo::gemm_key(2, 2, m, n, l));
     if (m <= 0) {
         if (!zeroed) {
             phip_memset(gW, 0, sizeof(float) * (size_t)l * n);
@@ -969,7 +969,7 @@ void phip_linear_x3_fwd(phip_opnd y, phip_opnd x, const int* ridx, float* xcopy,
     PPO_REQUIRE(y.p && x.p && W.p && n > 0, "phip_linear_x3_fwd: null operand");
     PPO_REQUIRE(!(ridx && x.planes), "phip_linear_x3_fwd: fused gather from pre-split planes");
     PPO_REQUIRE(W.planes || (!x.planes && !y.planes), "phip_linear_x3_fwd: unsupported storage combination");
-    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l);
+    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l, ppo::gemm_key(0, 1, m, n, l));
     Args a{};
     a.flags = flags3();
     a.A = x.p; a.lda = n; a.B = W.p; a.ldb = n; a.C = y.p; a.ldc = l;
@@ -1003,7 +1003,7 @@ void phip_linear_x3_bwd_x(phip_opnd gx, phip_opnd g, phip_opnd W, const float* W
         return;
     }
     PPO_REQUIRE(W.planes || (!g.planes && !gx.planes), "phip_linear_x3_bwd_x: unsupported storage combination");
-    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l);
+    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l, ppo::gemm_key(1, 1, m, n, l));
     Args a{};
     a.flags = flags3();
     a.A = g.p; a.lda = l; a.B = W.p; a.ldb = n; a.C = gx.p; a.ldc = n;
@@ -1022,7 +1022,7 @@ void phip_linear_x3_bwd_x(phip_opnd gx, phip_opnd g, phip_opnd W, const float* W
 void phip_linear_x3_bwd_w(float* gW, float* gb, phip_opnd g, phip_opnd x, int m, int n, int l, int zeroed) {
     if (l <= 0 || n <= 0) return;
     PPO_REQUIRE(gW && g.p && x.p, "phip_linear_x3_bwd_w: null operand");
-    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l);
+    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l, ppo::gemm_key(2, 1, m, n, l));
     if (m <= 0) {
         if (!zeroed) {
             phip_memset(gW, 0, sizeof(float) * (size_t)l * n);

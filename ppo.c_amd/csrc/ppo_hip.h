@@ -222,6 +222,7 @@ void phip_allgather_f64(const double* d_send, double* d_recv, long n_per_rank);
 /* ---------------- profiling ---------------- */
 /* host C wrappers bracket launches: slot = phip_prof_begin(cls, work); ...; phip_prof_end(slot) */
 int  phip_prof_begin(int cls, double work);
+int  phip_prof_begin_key(int cls, double work, long long key);
 void phip_prof_end(int slot);
 
 #ifdef __cplusplus

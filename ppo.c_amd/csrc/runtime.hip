@@ -71,8 +71,12 @@ hipStream_t stream() {
 }
 
 // ---------------- per-launch event timing ----------------
-struct ProfSlot { hipEvent_t a, b; int k; double work; };
+struct ProfSlot { hipEvent_t a, b; int k; double work; long long key; int ext; };   // ext: 1 awaiting, 2 stamped
 static bool                  g_prof_on = false;
+static bool                  g_prof_kattach = false;      // GEMM scopes timed by their kernel's dispatch
+static int                   g_pending = -1;              // slot awaiting a PPO_TIMED_LAUNCH
+struct ShapeStat { long long key; double ms; long launches; double work; };
+static std::vector<ShapeStat> g_shapes;
 static int                   g_prof_stride = 1;
 static long                  g_issued[PPO_K_COUNT];
 static double                g_issued_work[PPO_K_COUNT];   // algorithmic work of every issued launch
@@ -93,19 +97,41 @@ static void harvest() {
     PPO_CHECK(hipStreamSynchronize(g_stream));
     PPO_CHECK(hipStreamSynchronize(g_side));
     for (auto& s : g_slots) {
+        g_free_events.push_back(s.a);
+        g_free_events.push_back(s.b);
+        if (s.ext == 1) continue;                 // its scope launched no timed kernel: not measured
         float ms = 0.f;
         PPO_CHECK(hipEventElapsedTime(&ms, s.a, s.b));
         g_ms[s.k] += ms;
         g_work[s.k] += s.work;
         g_launches[s.k] += 1;
-        g_free_events.push_back(s.a);
-        g_free_events.push_back(s.b);
+        if (s.key) {
+            ShapeStat* st = nullptr;
+            for (auto& x : g_shapes) if (x.key == s.key) { st = &x; break; }
+            if (!st) { g_shapes.push_back(ShapeStat{s.key, 0.0, 0, 0.0}); st = &g_shapes.back(); }
+            st->ms += ms;
+            st->launches += 1;
+            st->work += s.work;
+        }
     }
     g_slots.clear();
 }
 
-ProfScope::ProfScope(int k_, double work_) : k(k_), work(work_), slot(-1) { slot = phip_prof_begin(k, work); }
+ProfScope::ProfScope(int k_, double work_, long long key) : k(k_), work(work_), slot(-1) {
+    slot = phip_prof_begin_key(k, work, key);
+}
 ProfScope::~ProfScope() { phip_prof_end(slot); }
+
+bool take_kernel_events(hipEvent_t* start, hipEvent_t* stop) {
+    if (g_pending < 0 || g_pending >= (int)g_slots.size()) return false;
+    ProfSlot& s = g_slots[g_pending];
+    g_pending = -1;
+    if (s.ext != 1) return false;
+    s.ext = 2;
+    *start = s.a;
+    *stop = s.b;
+    return true;
+}
 
 }  // namespace ppo
 
@@ -113,19 +139,26 @@ using namespace ppo;
 
 extern "C" {
 
-int phip_prof_begin(int cls, double work) {
+int phip_prof_begin_key(int cls, double work, long long key) {
     if (!g_prof_on) return -1;
     g_issued_work[cls] += work;
     if (g_issued[cls]++ % g_prof_stride != 0) return -1;
     if (g_slots.size() >= (1u << 16)) harvest();
-    ProfSlot s{take_event(), take_event(), cls, work};
-    PPO_CHECK(hipEventRecord(s.a, stream()));
+    const int ext = g_prof_kattach && cls == PPO_K_GEMM ? 1 : 0;
+    ProfSlot s{take_event(), take_event(), cls, work, key, ext};
+    if (!ext) PPO_CHECK(hipEventRecord(s.a, stream()));
     g_slots.push_back(s);
-    return (int)g_slots.size() - 1;
+    const int idx = (int)g_slots.size() - 1;
+    if (ext) g_pending = idx;
+    return idx;
 }
+
+int phip_prof_begin(int cls, double work) { return phip_prof_begin_key(cls, work, 0); }
 
 void phip_prof_end(int slot) {
     if (slot < 0 || !g_prof_on || slot >= (int)g_slots.size()) return;
+    if (slot == g_pending) g_pending = -1;
+    if (g_slots[slot].ext) return;               // stamped by the kernel's dispatch (or unmeasured)
     PPO_CHECK(hipEventRecord(g_slots[slot].b, stream()));
 }
 
@@ -241,8 +274,23 @@ void ppo_prof_issued_work(double* out_work) {
     for (int k = 0; k < PPO_K_COUNT; k++) out_work[k] = g_issued_work[k];
 }
 
+void ppo_prof_kernel_events(int on) { g_prof_kattach = on != 0; }
+
+int ppo_prof_shapes(long long* keys, double* ms, long* launches, double* work, int cap) {
+    harvest();
+    const int n = (int)g_shapes.size();
+    for (int i = 0; i < n && i < cap; i++) {
+        keys[i] = g_shapes[i].key;
+        ms[i] = g_shapes[i].ms;
+        launches[i] = g_shapes[i].launches;
+        work[i] = g_shapes[i].work;
+    }
+    return n;
+}
+
 void ppo_prof_reset(void) {
     harvest();
+    g_shapes.clear();
     for (int k = 0; k < PPO_K_COUNT; k++) { g_ms[k] = 0; g_work[k] = 0; g_launches[k] = 0; g_issued[k] = 0; g_issued_work[k] = 0; }
 }
 

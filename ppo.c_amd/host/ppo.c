@@ -49,6 +49,7 @@ static double* g_welford = NULL;  /* (n, mean, M2) */
 static double* g_welford_all = NULL;
 static int g_welford_world = 0;
 static float* g_adv_stats = NULL; /* (mean, std) as used for normalisation */
+static long g_gae_own_rows = 0;   /* rows of the last GAE's own V(next_state) forward */
 
 static uint64_t splitmix64(uint64_t z) {
     z += 0x9E3779B97F4A7C15ULL;
@@ -202,6 +203,7 @@ void ppo_gae_device(NeuralNetwork* V, TrajectoryBuffer* b, float gamma, float la
     if (n > 0 && gae_full_forwards()) {     /* the reference's two full forwards (ppo.cu:333-336) */
         nn_forward_dev(V, b->next_state_p, n);
         phip_d2d(g_vn, V->d_output, sizeof(float) * (size_t)n);
+        g_gae_own_rows = n;
         nn_forward_dev(V, b->state_p, n);
         phip_d2d(g_v, V->d_output, sizeof(float) * (size_t)n);
     } else if (n > 0) {
@@ -210,6 +212,7 @@ void ppo_gae_device(NeuralNetwork* V, TrajectoryBuffer* b, float gamma, float la
         nn_forward_dev(V, b->state_p, n);
         phip_d2d(g_v, V->d_output, sizeof(float) * (size_t)n);
         const int own = phip_next_value_map(b->next_state_p, b->state_p, g_v, g_vn, g_own, n, V->layers[0].input_size);
+        g_gae_own_rows = own;
         if (own > 0) {
             nn_forward_dev_rows(V, b->next_state_p, g_own, NULL, own);
             phip_scatter_values(g_vn, g_own, V->d_output, own);
@@ -570,8 +573,9 @@ void ppo_read_stats(void* vppo, double* out, int n) {
     float s[4] = {0, 0, 0, 0}, a[2] = {0, 0};
     phip_d2h(s, d->stats, sizeof(s));
     if (g_adv_stats) phip_d2h(a, g_adv_stats, sizeof(a));
-    double v[7] = {s[0], (double)d->n_v, s[1], (double)d->n_p, compute_entropy_cuda(ppo->policy), a[0], a[1]};
-    for (int i = 0; i < n && i < 7; i++) out[i] = v[i];
+    double v[8] = {s[0], (double)d->n_v, s[1], (double)d->n_p, compute_entropy_cuda(ppo->policy), a[0], a[1],
+                   (double)g_gae_own_rows};
+    for (int i = 0; i < n && i < 8; i++) out[i] = v[i];
 }
 
 /* ppo.cu:451-558 */

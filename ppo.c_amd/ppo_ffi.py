@@ -129,6 +129,8 @@ _SIGS = {
     "ppo_comm_finalize": (None, []),
     "ppo_comm_allreduce_f32": (None, [_P, C.c_long]),
     "ppo_welford_combine": (None, [_P, C.c_int, _P]),
+    "ppo_comm_barrier": (None, []),
+    "ppo_comm_max_f64": (C.c_double, [C.c_double]),
     "ppo_update": (None, [_P, C.c_float, C.c_int, C.c_int, C.c_int, C.c_int, C.c_ulonglong]),
     "ppo_read_stats": (None, [_P, C.POINTER(C.c_double), C.c_int]),
     "ppo_reset_stats": (None, [_P]),
@@ -137,6 +139,9 @@ _SIGS = {
     "ppo_fill_synthetic": (None, [_P, C.c_int, C.c_int, C.c_ulonglong, C.c_float]),
     "ppo_prof_enable": (None, [C.c_int]),
     "ppo_prof_reset": (None, []),
+    "ppo_prof_kernel_events": (None, [C.c_int]),
+    "ppo_prof_shapes": (C.c_int, [C.POINTER(C.c_longlong), C.POINTER(C.c_double), c_long_p, C.POINTER(C.c_double),
+                                  C.c_int]),
     "ppo_prof_read": (None, [C.POINTER(C.c_double), C.POINTER(C.c_double), c_long_p]),
     "ppo_prof_counts": (None, [c_long_p]),
     "ppo_prof_issued_work": (None, [C.POINTER(C.c_double)]),
