@@ -1077,65 +1077,6 @@ void phip_split_x3(unsigned short* dst, long stride, const float* p, long n) {
     PPO_LAUNCH_CHECK();
 }
 
-int ppo_gemm_x3_tune(int force_cfg, int splitk_target) {
-    g_force3 = force_cfg;
-    if (splitk_target >= 0) g_split3 = splitk_target;
-    return (int)(sizeof(kCfgs3) / sizeof(kCfgs3[0]));
-}
-
-// average device µs of one x3 launch (fp32 operands; op as ppo_bench_gemm)
-double ppo_bench_gemm_x3(int op, int m, int n, int l, int iters, int cfg, int splitk_target) {
-    ppo::ensure_device();
-    const size_t sx = (size_t)m * n, sw = (size_t)l * n, sy = (size_t)m * l;
-    float* x = (float*)phip_malloc(6 * sx);
-    float* W = (float*)phip_malloc(6 * sw);
-    float* y = (float*)phip_malloc(6 * (sy > sx ? sy : sx));
-    float* b = (float*)phip_malloc(4 * (size_t)(l > n ? l : n));
-    float* gw = (float*)phip_malloc(4 * sw);
-    unsigned* bits = (unsigned*)phip_malloc(4 * (size_t)m * ppo_divup(l > n ? l : n, 32));
-    phip_fill_uniform(x, (long)(sx * 3 / 2), 1, -1.f, 1.f);
-    phip_fill_uniform(W, (long)(sw * 3 / 2), 2, -0.1f, 0.1f);
-    phip_fill_uniform(y, (long)((sy > sx ? sy : sx) * 3 / 2), 3, -1.f, 1.f);
-    void* w3 = W;
-    phip_fill_uniform(b, (long)(l > n ? l : n), 4, -0.1f, 0.1f);
-    phip_memset(bits, 0xff, 4 * (size_t)m * ppo_divup(l > n ? l : n, 32));
-    const int saved = g_force3, saved_split = g_split3;
-    g_force3 = cfg;
-    g_split3 = splitk_target;
-    // op ≥ 10: the same product with pre-split operands (planes in the buffers' first 6 B/elem
-    // view: x, y hold 1.5x their fp32 size) and W planes — the x3 engine's update-path storage
-    const bool pl = op >= 10;
-    const int o = op % 10;
-    auto F = [](void* p) { return phip_opnd{p, 0, 0}; };
-    auto PLo = [&](void* p, long cnt) { return pl ? phip_opnd{p, 1, cnt} : phip_opnd{p, 0, 0}; };
-    auto run = [&]() {
-        if (o == 0) phip_linear_x3_fwd(PLo(y, (long)sy), PLo(x, (long)sx), nullptr, nullptr, PLo(w3, (long)sw), b, m, n,
-                                       l, 1, bits);
-        else if (o == 3) phip_linear_x3_fwd(F(y), PLo(x, (long)sx), nullptr, nullptr, PLo(w3, (long)sw), b, m, n, l,
-                                            0, nullptr);
-        else if (o == 1) phip_linear_x3_bwd_x(PLo(x, (long)sx), PLo(y, (long)sy), PLo(w3, (long)sw), nullptr, bits, m,
-                                              n, l);
-        else if (o == 4) phip_linear_x3_bwd_x(F(x), F(y), F(W), W, bits, m, n, l);     // grad_x against Wᵀ
-        else phip_linear_x3_bwd_w(gw, b, PLo(y, (long)sy), PLo(x, (long)sx), m, n, l, 0);
-    };
-    for (int i = 0; i < 3; ++i) run();
-    hipEvent_t e0, e1;
-    PPO_CHECK(hipEventCreate(&e0));
-    PPO_CHECK(hipEventCreate(&e1));
-    PPO_CHECK(hipEventRecord(e0, ppo::stream()));
-    for (int i = 0; i < iters; ++i) run();
-    PPO_CHECK(hipEventRecord(e1, ppo::stream()));
-    PPO_CHECK(hipEventSynchronize(e1));
-    float ms = 0.f;
-    PPO_CHECK(hipEventElapsedTime(&ms, e0, e1));
-    PPO_CHECK(hipEventDestroy(e0));
-    PPO_CHECK(hipEventDestroy(e1));
-    g_force3 = saved;
-    g_split3 = saved_split;
-    phip_free(x); phip_free(W); phip_free(y); phip_free(b); phip_free(gw); phip_free(bits);
-    return 1000.0 * ms / (iters > 0 ? iters : 1);
-}
-
 int ppo_gemm16_tune(int force_cfg) {
     g_force16 = force_cfg;
     return (int)(sizeof(kCfgs) / sizeof(kCfgs[0]));

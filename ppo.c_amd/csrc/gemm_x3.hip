@@ -1,0 +1,675 @@
+// gemm_x3.hip — fp32 linear-layer GEMMs on the bf16 MFMA (the "x3" engine of fp32 mode).
+//
+// Reference products (mat_mul.cu:122-217 with the fused bias / ReLU of activation_function.cu:17-29
+// and the bias-gradient sum of neural_network.cu:108-118):
+//   forward   y  = x·Wᵀ + b (+ReLU, +ReLU′ bit mask, + the minibatch gather of x's rows)   NT
+//   grad_x    gx = (g·W) ⊙ 1[y_prev > 0]                                                   NN
+//   grad_W    gW = gᵀ·x, gb = Σ_rows g      (split-K over the batch, f32 atomics)          TN
+//
+// Arithmetic.  Every fp32 operand value splits exactly into three bf16 planes x = x0 + x1 + x2
+// (round-to-nearest v_cvt_pk_bf16_f32 of x, of the residual, of the second residual: x0 carries 8
+// significant bits, x − x0 ≤ 16 of which x1 takes 8, so x − x0 − x1 is itself a bf16).  A product
+// a·b is Σ_{p+q≤2} a_p·b_q: six v_mfma_f32_32x32x16_bf16 with fp32 accumulation per fp32 product;
+// the dropped terms (1,2), (2,1), (2,2) are below 2^-24 of |a·b|, so the engine is as accurate as
+// the exact fp32 MFMA (tests/test_gpu_x3.py).  Ceiling: 2.5 PF/s ÷ 6 = 417 TF/s fp32-equivalent.
+//
+// Pipeline (one workgroup per CU for the wide products, two for grad_W's 128×128 tiles):
+//   * BK = 16 k-tiles; the three planes of both operand tiles live in an LDS image that is DOUBLE
+//     buffered, so each k-tile costs ONE barrier and the split + LDS stores of tile t+1 and the
+//     global loads of tile t+2 are issued in the same basic block as tile t's MFMAs (the
+//     scheduler interleaves them; nothing waits for a whole staging phase);
+//   * the split happens once per staged element (at LDS-store time), not once per wave reading it;
+//   * k-contiguous operands (x and W of the forward) are staged [row][24] bf16 per plane — a
+//     fragment is one conflict-free ds_read_b128 (48-B pitch: every 16-lane group of the read hits
+//     each of the 64 banks once); row-contiguous operands (W in grad_x, g and x in grad_W) are staged
+//     [k][R+pad] as loaded and read with two ds_read_b64_tr_b16 hardware transposes per fragment;
+//   * XCD-aware block remap: tiles that share an operand panel run on one XCD's L2.
+#include "dev.h"
+
+#include <algorithm>
+#include <type_traits>
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int BK = 16;
+enum { OP_NT = 0, OP_NN = 1, OP_TN = 2 };
+
+// diagnostic stamps (ABL & 32): s_memtime of wave 0 of each workgroup at kernel start, after the
+// prologue, after the mainloop, at the end
+__device__ unsigned long long g_x3_stamps[8192 * 4];
+
+struct X3Args {
+    const float* A; const float* B; float* C;
+    int M, N, K, lda, ldb, ldc;
+    const float* bias; int relu;
+    const int* ridx; float* acopy;        // forward: fused gather of A's rows + the gathered copy
+    unsigned* bits_out; const unsigned* bits_in; int wpr;
+    float* gbias;                         // grad_W: bias gradient (Σ over the batch of g)
+    int kchunk, splits, tiles_m, tiles_n;
+};
+
+// fp32 → bf16 round to nearest even (NaN stays NaN): v_cvt_pk_bf16_f32
+__device__ __forceinline__ unsigned pack2(float lo, float hi) {
+    typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+    bf16x2 p = {(__bf16)lo, (__bf16)hi};
+    return __builtin_bit_cast(unsigned, p);
+}
+__device__ __forceinline__ float bf_lo(unsigned u) { return __builtin_bit_cast(float, u << 16); }
+__device__ __forceinline__ float bf_hi(unsigned u) { return __builtin_bit_cast(float, u & 0xffff0000u); }
+
+// exact three-plane split of 4 values: plane q gets 4 bf16 (2 dwords)
+__device__ __forceinline__ void split4(f32x4 f, u32x2& p0, u32x2& p1, u32x2& p2) {
+    const unsigned a0 = pack2(f[0], f[1]), b0 = pack2(f[2], f[3]);
+    const float r0 = f[0] - bf_lo(a0), r1 = f[1] - bf_hi(a0);
+    const float r2 = f[2] - bf_lo(b0), r3 = f[3] - bf_hi(b0);
+    const unsigned a1 = pack2(r0, r1), b1 = pack2(r2, r3);
+    p0 = u32x2{a0, b0};
+    p1 = u32x2{a1, b1};
+    p2 = u32x2{pack2(r0 - bf_lo(a1), r1 - bf_hi(a1)), pack2(r2 - bf_lo(b1), r3 - bf_hi(b1))};
+}
+
+// ---------------------------------------------------------------------------------------------
+// One operand tile: R rows × BK k, fp32 in HBM → three bf16 planes in LDS.  NTH threads, each
+// owning NV float4 loads.  MN = the operand is contiguous along its rows (its k is the HBM row).
+// ---------------------------------------------------------------------------------------------
+template <int R, bool MN, int NTH>
+struct StageX3 {
+    static constexpr int NV = R * BK / (4 * NTH);            // float4 loads per thread
+    static_assert(NV >= 1 && R * BK == 4 * NTH * NV, "tile / thread count");
+    static constexpr int PK = BK + 8;                        // k-contiguous pitch (bf16) = 48 B
+    static constexpr int PR = ((R / 2) % 64 == 16 || (R / 2) % 64 == 48) ? R : R + 32;   // row-contiguous pitch
+    static constexpr int PLANE = MN ? BK * PR : R * PK;      // bf16 elements per plane
+    static constexpr int SIZE = 3 * PLANE;
+    static constexpr int TPR = BK / (4 * NV);                // k-contiguous: threads per row
+    static constexpr int KSTEP = 4 * NTH / R;                // row-contiguous: k distance of the q-th load
+    static_assert(MN || TPR >= 1, "k-contiguous mapping");
+
+    f32x4 v[NV];
+    const float* base;                                       // this thread's element (row, k) at k0 = 0
+    int row, k;                                              // this thread's first element in the tile
+    int ld;
+
+    // src row (k-contiguous: after the gather, clamped into the operand); rows past the end read row
+    // Rmax − 1 (their products land in output rows that are never stored)
+    __device__ __forceinline__ void init(const float* __restrict__ p, int ld_, const int* __restrict__ ridx, int r0,
+                                         int Rmax, int tid) {
+        ld = ld_;
+        if (MN) {
+            row = (tid % (R / 4)) * 4;
+            k = tid / (R / 4);
+            base = p + (long)k * ld + min(r0 + row, Rmax - 4);
+        } else {
+            row = tid / TPR;
+            k = (tid % TPR) * 4 * NV;
+            const int gr = min(r0 + row, Rmax - 1);
+            base = p + (long)(ridx ? ridx[gr] : gr) * ld + k;
+        }
+    }
+    // FULL: the whole k-tile lies inside [kbeg, kend) — no clamping
+    template <bool FULL>
+    __device__ __forceinline__ void load(int k0, int kend) {
+        if (MN) {
+#pragma unroll
+            for (int q = 0; q < NV; ++q) {
+                const int dk = FULL ? k0 + q * KSTEP : min(k0 + k + q * KSTEP, kend - 1) - k;
+                v[q] = *reinterpret_cast<const f32x4*>(base + (long)dk * ld);
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < NV; ++q) {
+                const int dk = FULL ? k0 + 4 * q : min(k0 + k + 4 * q, kend - 4) - k;
+                v[q] = *reinterpret_cast<const f32x4*>(base + dk);
+            }
+        }
+    }
+    __device__ __forceinline__ bool kvalid(int q, int k0, int kend) const {
+        return MN ? k0 + k + q * KSTEP < kend : k0 + k + 4 * q < kend;
+    }
+    template <bool FULL>
+    __device__ __forceinline__ void store(unsigned short* img, int k0, int kend) {
+        if (!FULL) {
+#pragma unroll
+            for (int q = 0; q < NV; ++q)
+                if (!kvalid(q, k0, kend)) v[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        if (MN) {
+#pragma unroll
+            for (int q = 0; q < NV; ++q) {
+                u32x2 p0, p1, p2;
+                split4(v[q], p0, p1, p2);
+                unsigned short* d = img + (k + q * KSTEP) * PR + row;
+                *reinterpret_cast<u32x2*>(d) = p0;
+                *reinterpret_cast<u32x2*>(d + PLANE) = p1;
+                *reinterpret_cast<u32x2*>(d + 2 * PLANE) = p2;
+            }
+        } else if (NV == 2) {                                 // 8 consecutive k: one ds_write_b128 per plane
+            u32x2 a0, a1, a2, b0, b1, b2;
+            split4(v[0], a0, a1, a2);
+            split4(v[NV - 1], b0, b1, b2);
+            unsigned short* d = img + row * PK + k;
+            *reinterpret_cast<u32x4*>(d) = u32x4{a0[0], a0[1], b0[0], b0[1]};
+            *reinterpret_cast<u32x4*>(d + PLANE) = u32x4{a1[0], a1[1], b1[0], b1[1]};
+            *reinterpret_cast<u32x4*>(d + 2 * PLANE) = u32x4{a2[0], a2[1], b2[0], b2[1]};
+        } else {
+#pragma unroll
+            for (int q = 0; q < NV; ++q) {
+                u32x2 p0, p1, p2;
+                split4(v[q], p0, p1, p2);
+                unsigned short* d = img + row * PK + k + 4 * q;
+                *reinterpret_cast<u32x2*>(d) = p0;
+                *reinterpret_cast<u32x2*>(d + PLANE) = p1;
+                *reinterpret_cast<u32x2*>(d + 2 * PLANE) = p2;
+            }
+        }
+    }
+    // forward's fused gather: the staged rows written to dst (rows < Rmax, k < kend)
+    __device__ __forceinline__ void copy_out(float* __restrict__ dst, int ldd, int r0, int Rmax, int k0,
+                                             int kend) const {
+        if (MN || r0 + row >= Rmax) return;
+#pragma unroll
+        for (int q = 0; q < NV; ++q)
+            if (kvalid(q, k0, kend))
+                *reinterpret_cast<f32x4*>(dst + (long)(r0 + row) * ldd + k0 + k + 4 * q) = v[q];
+    }
+    // MFMA fragment (32 rows × 16 k, bf16x8 per lane: row `rr`, k = 8h..8h+7) of one plane
+    __device__ __forceinline__ static bf16x8 frag(const unsigned short* plane, int rr, int lane) {
+        const int h = lane >> 5;
+        if (!MN) return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(plane + rr * PK + 8 * h));
+        // hardware transpose: in each 16-lane group lane 4q+p addresses k-row q, rows 4p..4p+3 of
+        // the group's 16; lane i receives row i of the 4 k-rows (two reads: k 8h+0..3, 8h+4..7)
+        const int gi = lane & 15, q = gi >> 2, p = gi & 3;
+        typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+        const unsigned short* a0 = plane + (8 * h + q) * PR + (rr - gi) + 4 * p;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 4 * PR));
+        const s16x8 f = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        return __builtin_bit_cast(bf16x8, f);
+    }
+};
+
+// ---------------------------------------------------------------------------------------------
+// The kernel.  BM×BN output tile per workgroup of NTH threads (WARPS_M × WARPS_N waves), k range
+// [kbeg, kend) of the workgroup's split.
+// ---------------------------------------------------------------------------------------------
+// ABL (timing ablations, results wrong; PPO_X3_ABLATE, forward cfg 0 only): 1 = no MFMAs, 2 = no
+// split / LDS stores, 4 = no epilogue stores, 8 = no global loads after the prologue
+template <int OP, int BM, int BN, int WARPS_M, int NTH, int OCC, int ABL = 0>
+__global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
+    constexpr int NW = NTH / 64, WARPS_N = NW / WARPS_M;
+    constexpr int WM = BM / WARPS_M, WN = BN / WARPS_N;
+    constexpr int TM = WM / 32, TN = WN / 32;
+    static_assert(TM >= 1 && TN >= 1 && WARPS_M * WARPS_N == NW, "wave tiling");
+    constexpr bool A_MN = OP == OP_TN, B_MN = OP != OP_NT;
+    using SA = StageX3<BM, A_MN, NTH>;
+    using SB = StageX3<BN, B_MN, NTH>;
+    constexpr int BUF = SA::SIZE + SB::SIZE;
+
+    extern __shared__ __attribute__((aligned(16))) unsigned short lds[];     // 2 × BUF
+
+    // XCD-aware remap: hardware deals blocks round-robin over the 8 XCDs; give each XCD a
+    // contiguous range of linear tiles (n fastest), so tiles sharing an A panel share an L2
+    const int nwg = gridDim.x, b = blockIdx.x;
+    const int xcd = b & 7, qq = nwg >> 3, rr = nwg & 7;
+    const int t = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (b >> 3);
+    const int tn = t % a.tiles_n;
+    const int rest = t / a.tiles_n;
+    const int tm = rest % a.tiles_m;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int kbeg = (rest / a.tiles_m) * a.kchunk;
+    const int kend = min(a.K, kbeg + a.kchunk);
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = w / WARPS_N, wn = w % WARPS_N;
+    auto stamp = [&](int slot) {
+        if (tid == 0 && b < 8192) g_x3_stamps[b * 4 + slot] = __builtin_amdgcn_s_memtime();
+    };
+    if (ABL & 32) stamp(0);
+    const int r = lane & 31, h = lane >> 5;
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+    SA sa;
+    SB sb;
+    sa.init(a.A, a.lda, OP == OP_NT ? a.ridx : nullptr, m0, a.M, tid);
+    sb.init(a.B, a.ldb, nullptr, n0, a.N, tid);
+    const bool do_copy = OP == OP_NT && a.acopy != nullptr && tn == 0;
+    // grad_W bias: Σ over this split's k of the A (= g) tile, from the staging registers
+    const bool do_bsum = OP == OP_TN && a.gbias != nullptr && tn == 0;
+    f32x4 bs[SA::NV];
+#pragma unroll
+    for (int q = 0; q < SA::NV; ++q) bs[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // fragments of one k-tile, read in the order the plane products use them
+    bf16x8 fa[3][TM], fb[3][TN];
+    auto read_frags = [&](const unsigned short* img) {
+        const unsigned short* As = img;
+        const unsigned short* Bs = img + SA::SIZE;
+        constexpr int order[6][2] = {{0, 2}, {1, 0}, {0, 0}, {1, 2}, {0, 1}, {1, 1}};   // (operand, plane)
+#pragma unroll
+        for (int o = 0; o < 6; ++o) {
+            const int p = order[o][1];
+            if (order[o][0] == 0) {
+#pragma unroll
+                for (int i = 0; i < TM; ++i) fa[p][i] = SA::frag(As + p * SA::PLANE, wm * WM + i * 32 + r, lane);
+            } else {
+#pragma unroll
+                for (int j = 0; j < TN; ++j) fb[p][j] = SB::frag(Bs + p * SB::PLANE, wn * WN + j * 32 + r, lane);
+            }
+        }
+    };
+    // plane product q of the six with pa + pb ≤ 2 (smallest first)
+    auto mfma_group = [&](int q) {
+        constexpr int pa_[6] = {2, 0, 1, 1, 0, 0}, pb_[6] = {0, 2, 1, 0, 1, 0};
+        if (ABL & 1) {               // keep the fragment reads live
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) acc[i][j][0] += (float)fa[pa_[q]][i][0] + (float)fb[pb_[q]][j][1];
+            return;
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[pa_[q]][i], fb[pb_[q]][j], acc[i][j], 0, 0, 0);
+    };
+    auto compute = [&](const unsigned short* img) {
+        read_frags(img);
+#pragma unroll
+        for (int q = 0; q < 6; ++q) mfma_group(q);
+    };
+    // split + LDS store of the staged tile at k0 (FULL: no k tail); COPY: also the gathered rows
+    auto stage_a = [&](auto FULLc, auto COPYc, unsigned short* img, int k0) {
+        constexpr bool FULL = decltype(FULLc)::value, COPY = decltype(COPYc)::value;
+        if ((ABL & 2) && k0 != kbeg) return;
+        if (COPY) sa.copy_out(a.acopy, a.K, m0, a.M, k0, kend);
+        sa.template store<FULL>(img, k0, kend);
+        if (do_bsum) {
+#pragma unroll
+            for (int q = 0; q < SA::NV; ++q) bs[q] += sa.v[q];
+        }
+    };
+    auto stage_b = [&](auto FULLc, unsigned short* img, int k0) {
+        constexpr bool FULL = decltype(FULLc)::value;
+        if ((ABL & 2) && k0 != kbeg) return;
+        sb.template store<FULL>(img + SA::SIZE, k0, kend);
+    };
+    auto stage = [&](auto FULLc, auto COPYc, unsigned short* img, int k0) {
+        stage_a(FULLc, COPYc, img, k0);
+        stage_b(FULLc, img, k0);
+    };
+    auto load = [&](auto FULLc, int k0) {
+        constexpr bool FULL = decltype(FULLc)::value;
+        if (ABL & 8) return;
+        sa.template load<FULL>(k0, kend);
+        sb.template load<FULL>(k0, kend);
+    };
+    using T = std::true_type;
+    using F = std::false_type;
+
+    const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+    const bool tail = kbeg + nk * BK > kend;                  // the last k-tile is partial
+    unsigned short* const buf0 = lds;
+    unsigned short* const buf1 = lds + BUF;
+    // tile t is full unless it is the last one and K is ragged
+    auto is_full = [&](int t_) { return !(tail && t_ == nk - 1); };
+
+    // steady state, one basic block per k-tile: MFMAs of tile it from one image; the split + LDS
+    // stores of tile it+1 (loaded one iteration ago) into the other; the loads of tile it+2; one
+    // barrier.  Tiles it+1 and it+2 are full here (it+2 < nk−1 unless K is ragged: then the loop
+    // stops one tile earlier and the tail is handled below).
+    auto mainloop = [&](auto COPYc) {
+        int it = 0;
+        if (nk > 0) {
+            if (is_full(0)) load(T{}, kbeg); else load(F{}, kbeg);
+            if (is_full(0)) stage(T{}, COPYc, buf0, kbeg); else stage(F{}, COPYc, buf0, kbeg);
+        }
+        if (nk > 1) {
+            if (is_full(1)) load(T{}, kbeg + BK); else load(F{}, kbeg + BK);
+        }
+        __syncthreads();
+        if (ABL & 32) stamp(1);
+        const int steady = tail ? nk - 3 : nk - 2;            // iterations whose it+1, it+2 tiles are full
+        for (; it < steady; ++it) {
+            const unsigned short* cur = (it & 1) ? buf1 : buf0;
+            unsigned short* nxt = (it & 1) ? buf0 : buf1;
+            const int k1 = kbeg + (it + 1) * BK;
+            // interleave in program order (sched_barrier fences): each plane-product group of MFMAs
+            // shares its scheduling region with one slice of the staging work
+            read_frags(cur);
+            mfma_group(0);
+            __builtin_amdgcn_sched_barrier(0);
+            mfma_group(1);
+            stage_a(T{}, COPYc, nxt, k1);
+            __builtin_amdgcn_sched_barrier(0);
+            mfma_group(2);
+            stage_b(T{}, nxt, k1);
+            __builtin_amdgcn_sched_barrier(0);
+            mfma_group(3);
+            load(T{}, k1 + BK);
+            __builtin_amdgcn_sched_barrier(0);
+            mfma_group(4);
+            mfma_group(5);
+            __syncthreads();
+        }
+        for (; it < nk; ++it) {                               // the last one or two tiles
+            const unsigned short* cur = (it & 1) ? buf1 : buf0;
+            unsigned short* nxt = (it & 1) ? buf0 : buf1;
+            const int k1 = kbeg + (it + 1) * BK;
+            compute(cur);
+            if (it + 1 < nk) {
+                if (is_full(it + 1)) stage(T{}, COPYc, nxt, k1); else stage(F{}, COPYc, nxt, k1);
+            }
+            if (it + 2 < nk) {
+                if (is_full(it + 2)) load(T{}, k1 + BK); else load(F{}, k1 + BK);
+            }
+            __syncthreads();
+        }
+    };
+    if (do_copy) mainloop(T{});
+    else mainloop(F{});
+
+    if (do_bsum) {
+        // rows of this thread's float4s: row .. row+3; reduce over the threads sharing them
+        // (tid ≡ tid' mod BM/4), through LDS (the images are no longer read after this barrier)
+        __syncthreads();
+        float* red = reinterpret_cast<float*>(lds);
+        constexpr int G = BM / 4;                       // float4 row groups
+        constexpr int S = NTH / G;                      // threads per group (one per k-row slot)
+#pragma unroll
+        for (int q = 0; q < SA::NV; ++q) {
+            // (NV > 1: the q-th float4 is a different k of the same rows — already summed into bs[0..])
+            if (q > 0) bs[0] += bs[q];
+        }
+        *reinterpret_cast<f32x4*>(red + (tid / G) * BM + (tid % G) * 4) = bs[0];
+        __syncthreads();
+        if (tid < BM) {
+            float s = 0.f;
+            for (int j = 0; j < S; ++j) s += red[j * BM + tid];
+            if (m0 + tid < a.M) {
+                if (a.splits > 1) atomicAdd(a.gbias + m0 + tid, s);
+                else a.gbias[m0 + tid] = s;
+            }
+        }
+    }
+
+    if (ABL & 32) stamp(2);
+    if (ABL & 4) {
+        float t = 0.f;                                          // keep every accumulator live
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) t += acc[i][j][e];
+        if (t == 12345.678f) a.C[tid] = 1.f;
+        return;
+    }
+    // epilogue: 32×32 accumulator block (i, j): lane (r, h) holds column r, rows 4h + (e&3) + 8(e>>2);
+    // every load a block needs (bias, ReLU′ bit words) is issued before its stores
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int c0 = n0 + wn * WN + j * 32;
+            const int col = c0 + r;
+            const int r0 = m0 + wm * WM + i * 32 + 4 * h;
+            const bool col_ok = col < a.N;
+            float bcol = 0.f;
+            if (OP == OP_NT && a.bias) bcol = a.bias[col_ok ? col : a.N - 1];
+            bool keep[16];
+            if (OP == OP_NN) {
+                if (a.bits_in) {
+                    unsigned wv[16];
+#pragma unroll
+                    for (int e = 0; e < 16; ++e)
+                        wv[e] = a.bits_in[(long)min(r0 + (e & 3) + 8 * (e >> 2), a.M - 1) * a.wpr + (c0 >> 5)];
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) keep[e] = (wv[e] >> r) & 1u;
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) keep[e] = true;
+                }
+            }
+            unsigned word = 0;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int row = r0 + (e & 3) + 8 * (e >> 2);
+                const bool ok = col_ok && row < a.M;
+                float v = acc[i][j][e];
+                float* dst = a.C + (long)row * a.ldc + col;
+                if (OP == OP_NT) {
+                    v += bcol;
+                    if (a.relu) v = v > 0.f ? v : 0.f;
+                    if (ok) *dst = v;
+                    if (a.bits_out) {
+                        const unsigned long long bb = __ballot(ok && v > 0.f);
+                        if (r == e) word = h ? (unsigned)(bb >> 32) : (unsigned)bb;
+                    }
+                } else if (OP == OP_NN) {
+                    if (ok) *dst = keep[e] ? v : 0.f;
+                } else if (ok) {
+                    if (a.splits > 1) atomicAdd(dst, v);
+                    else *dst = v;
+                }
+            }
+            if (OP == OP_NT && a.bits_out && r < 16) {
+                const int row = r0 + (r & 3) + 8 * (r >> 2);
+                if (row < a.M && c0 < a.N) a.bits_out[(long)row * a.wpr + (c0 >> 5)] = word;
+            }
+        }
+    if (ABL & 32) stamp(3);
+}
+
+int g_x3_ablate = -1;
+
+template <int OP, int BM, int BN, int WARPS_M, int NTH, int OCC, int ABL = 0>
+void launch_x3(X3Args a) {
+    a.tiles_m = ppo_divup(a.M, BM);
+    a.tiles_n = ppo_divup(a.N, BN);
+    if (a.splits < 1) a.splits = 1;
+    const long grid = (long)a.tiles_m * a.tiles_n * a.splits;
+    PPO_REQUIRE(grid > 0 && grid < (1L << 31), "gemm_x3: grid out of range");
+    using SA = StageX3<BM, OP == OP_TN, NTH>;
+    using SB = StageX3<BN, OP != OP_NT, NTH>;
+    constexpr size_t lds = 2 * sizeof(unsigned short) * (SA::SIZE + SB::SIZE);
+    static_assert(lds <= 160 * 1024, "gemm_x3: LDS images exceed 160 KiB");
+    auto kern = gemm_x3_kernel<OP, BM, BN, WARPS_M, NTH, OCC, ABL>;
+    if (lds > 64 * 1024) {
+        static bool attr = false;                      // once per instantiation
+        if (!attr) {
+            PPO_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            attr = true;
+        }
+    }
+    PPO_TIMED_LAUNCH(kern, dim3((unsigned)grid), dim3(NTH), lds, ppo::stream(), a);
+    PPO_LAUNCH_CHECK();
+}
+
+// tile configurations {BM, BN}: 0 = 256×256 over 8 waves of 64×128 (forward, grad_x), 1 = 128×128
+// over 4 waves of 64×64, two workgroups per CU (grad_W, narrow products), 2 = 128×128 over 8 waves
+// of 64×32
+struct CfgX3 { int bm, bn; };
+constexpr CfgX3 kCfgX3[] = {{256, 256}, {128, 128}, {128, 128}};
+int g_force_x3 = -1;
+int g_split_x3 = 0;
+
+template <int OP>
+void launch_cfg_x3(int c, const X3Args& a) {
+    if (g_x3_ablate < 0) {
+        const char* e = getenv("PPO_X3_ABLATE");
+        g_x3_ablate = e ? atoi(e) : 0;
+    }
+    if (OP == OP_NT && c == 0 && g_x3_ablate) {
+        switch (g_x3_ablate) {
+            case 1: launch_x3<OP, 256, 256, 4, 512, 2, 1>(a); return;
+            case 2: launch_x3<OP, 256, 256, 4, 512, 2, 2>(a); return;
+            case 3: launch_x3<OP, 256, 256, 4, 512, 2, 3>(a); return;
+            case 4: launch_x3<OP, 256, 256, 4, 512, 2, 4>(a); return;
+            case 8: launch_x3<OP, 256, 256, 4, 512, 2, 8>(a); return;
+            case 10: launch_x3<OP, 256, 256, 4, 512, 2, 10>(a); return;
+            case 14: launch_x3<OP, 256, 256, 4, 512, 2, 14>(a); return;
+            case 5: launch_x3<OP, 256, 256, 4, 512, 2, 5>(a); return;
+            case 7: launch_x3<OP, 256, 256, 4, 512, 2, 7>(a); return;
+            case 32: launch_x3<OP, 256, 256, 4, 512, 2, 32>(a); return;
+            default: break;
+        }
+    }
+    switch (c) {
+        case 0: launch_x3<OP, 256, 256, 4, 512, 2>(a); break;
+        case 2: launch_x3<OP, 128, 128, 4, 512, 2>(a); break;
+        default: launch_x3<OP, 128, 128, 2, 256, 2>(a); break;
+    }
+}
+
+int pick_x3(int M, int N, int op) {
+    if (g_force_x3 >= 0) return g_force_x3;
+    if (op != OP_TN && M >= 4096 && N >= 256) return 0;
+    return 1;
+}
+
+inline bool al16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+}  // namespace
+
+extern "C" {
+
+// Shapes the engine takes (neural_network.c routes the rest to the exact fp32 kernels): the k
+// extent and every leading dimension a multiple of 4 floats, 16-B aligned operands, and for
+// row-contiguous operands a row extent that is a multiple of 4.
+int phip_x3_supported(int op, int m, int n, int l) {
+    if (m <= 0 || n <= 0 || l <= 0) return 0;
+    if (op == OP_NT) return n % 4 == 0 && l % 4 == 0;          // K = n; W rows l (k-contiguous)
+    if (op == OP_NN) return l % 4 == 0 && n % 4 == 0;          // K = l; W row-contiguous along n
+    return n % 4 == 0 && l % 4 == 0;                           // K = m; g rows l, x rows n
+}
+
+void phip_x3_fwd(float* y, const float* x, const int* ridx, float* xcopy, const float* W, const float* b, int m,
+                 int n, int l, int relu, unsigned* bits) {
+    if (m <= 0 || l <= 0) return;
+    PPO_REQUIRE(y && x && W && n > 0 && n % 4 == 0 && al16(x) && al16(W), "phip_x3_fwd: unsupported operands");
+    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l, ppo::gemm_key(0, 1, m, n, l));
+    X3Args a{};
+    a.A = x; a.lda = n; a.B = W; a.ldb = n; a.C = y; a.ldc = l;
+    a.M = m; a.N = l; a.K = n; a.kchunk = n; a.splits = 1;
+    a.bias = b; a.relu = relu; a.ridx = ridx; a.acopy = ridx ? xcopy : nullptr;
+    a.bits_out = relu ? bits : nullptr; a.wpr = ppo_divup(l, 32);
+    launch_cfg_x3<OP_NT>(pick_x3(m, l, OP_NT), a);
+}
+
+void phip_x3_bwd_x(float* gx, const float* g, const float* W, const unsigned* bits, int m, int n, int l) {
+    if (m <= 0 || n <= 0) return;
+    PPO_REQUIRE(gx && g && W && l > 0 && l % 4 == 0 && n % 4 == 0 && al16(g) && al16(W),
+                "phip_x3_bwd_x: unsupported operands");
+    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l, ppo::gemm_key(1, 1, m, n, l));
+    X3Args a{};
+    a.A = g; a.lda = l; a.B = W; a.ldb = n; a.C = gx; a.ldc = n;
+    a.M = m; a.N = n; a.K = l; a.kchunk = l; a.splits = 1;
+    a.bits_in = bits; a.wpr = ppo_divup(n, 32);
+    launch_cfg_x3<OP_NN>(pick_x3(m, n, OP_NN), a);
+}
+
+// zeroed: gW / gb already hold zeros (one memset per backward); otherwise they are cleared here
+void phip_x3_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, int n, int l, int zeroed) {
+    if (l <= 0 || n <= 0) return;
+    PPO_REQUIRE(gW && g && x && n % 4 == 0 && l % 4 == 0 && al16(g) && al16(x), "phip_x3_bwd_w: unsupported operands");
+    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l, ppo::gemm_key(2, 1, m, n, l));
+    if (m <= 0) {
+        if (!zeroed) {
+            phip_memset(gW, 0, sizeof(float) * (size_t)l * n);
+            if (gb) phip_memset(gb, 0, sizeof(float) * (size_t)l);
+        }
+        return;
+    }
+    const int c = pick_x3(l, n, OP_TN);
+    const long tiles = (long)ppo_divup(l, kCfgX3[c].bm) * ppo_divup(n, kCfgX3[c].bn);
+    // split-K over the batch: the grid stays within one round of workgroup slots (2 per CU), each
+    // split ≥ 8 k-tiles
+    const int target = g_split_x3 > 0 ? g_split_x3 : 512;
+    int splits = (int)(target / tiles);
+    const int max_splits = m / (8 * BK) > 0 ? m / (8 * BK) : 1;
+    splits = std::max(1, std::min(splits, max_splits));
+    int kchunk = ppo_divup(ppo_divup(m, splits), BK) * BK;
+    splits = ppo_divup(m, kchunk);
+    X3Args a{};
+    a.A = g; a.lda = l; a.B = x; a.ldb = n; a.C = gW; a.ldc = n;
+    a.M = l; a.N = n; a.K = m; a.kchunk = kchunk; a.splits = splits;
+    a.gbias = gb;
+    if (splits > 1 && !zeroed) {
+        phip_memset(gW, 0, sizeof(float) * (size_t)l * n);
+        if (gb) phip_memset(gb, 0, sizeof(float) * (size_t)l);
+    }
+    launch_cfg_x3<OP_TN>(c, a);
+}
+
+int ppo_gemm_x3_tune(int force_cfg, int splitk_target) {
+    g_force_x3 = force_cfg;
+    if (splitk_target >= 0) g_split_x3 = splitk_target;
+    return (int)(sizeof(kCfgX3) / sizeof(kCfgX3[0]));
+}
+
+// average device µs of one launch (op 0 forward + bias + ReLU + bits, 1 grad_x with bits, 2 grad_W
+// + bias grad (split-K from zero), 3 forward without activation); cfg −1 = automatic
+double ppo_bench_gemm_x3(int op, int m, int n, int l, int iters, int cfg, int splitk_target) {
+    ppo::ensure_device();
+    const size_t sx = (size_t)m * n, sw = (size_t)l * n, sy = (size_t)m * l;
+    float* x = (float*)phip_malloc(4 * sx);
+    float* W = (float*)phip_malloc(4 * sw);
+    float* y = (float*)phip_malloc(4 * sy);
+    float* b = (float*)phip_malloc(4 * (size_t)std::max(l, n));
+    float* gw = (float*)phip_malloc(4 * sw);
+    unsigned* bits = (unsigned*)phip_malloc(4 * (size_t)m * ppo_divup(std::max(l, n), 32));
+    phip_fill_uniform(x, (long)sx, 1, -1.f, 1.f);
+    phip_fill_uniform(W, (long)sw, 2, -0.1f, 0.1f);
+    phip_fill_uniform(y, (long)sy, 3, -1.f, 1.f);
+    phip_fill_uniform(b, (long)std::max(l, n), 4, -0.1f, 0.1f);
+    phip_memset(bits, 0xff, 4 * (size_t)m * ppo_divup(std::max(l, n), 32));
+    const int saved = g_force_x3, saved_split = g_split_x3;
+    g_force_x3 = cfg;
+    g_split_x3 = splitk_target;
+    auto run = [&]() {
+        if (op == 0) phip_x3_fwd(y, x, nullptr, nullptr, W, b, m, n, l, 1, bits);
+        else if (op == 3) phip_x3_fwd(y, x, nullptr, nullptr, W, b, m, n, l, 0, nullptr);
+        else if (op == 1) phip_x3_bwd_x(x, y, W, bits, m, n, l);
+        else phip_x3_bwd_w(gw, b, y, x, m, n, l, 0);
+    };
+    for (int i = 0; i < 3; ++i) run();
+    hipEvent_t e0, e1;
+    PPO_CHECK(hipEventCreate(&e0));
+    PPO_CHECK(hipEventCreate(&e1));
+    PPO_CHECK(hipEventRecord(e0, ppo::stream()));
+    for (int i = 0; i < iters; ++i) run();
+    PPO_CHECK(hipEventRecord(e1, ppo::stream()));
+    PPO_CHECK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    PPO_CHECK(hipEventElapsedTime(&ms, e0, e1));
+    PPO_CHECK(hipEventDestroy(e0));
+    PPO_CHECK(hipEventDestroy(e1));
+    g_force_x3 = saved;
+    g_split_x3 = saved_split;
+    phip_free(x); phip_free(W); phip_free(y); phip_free(b); phip_free(gw); phip_free(bits);
+    return 1000.0 * ms / (iters > 0 ? iters : 1);
+}
+
+// diagnostic: the stamps of the last PPO_X3_ABLATE=32 launch (4 per workgroup)
+int ppo_x3_stamps(unsigned long long* out, int n) {
+    phip_sync();
+    PPO_CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_x3_stamps), sizeof(unsigned long long) * (size_t)std::min(n, 8192 * 4)));
+    return 8192 * 4;
+}
+
+}  // extern "C"

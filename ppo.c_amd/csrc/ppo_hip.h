@@ -84,6 +84,12 @@ void phip_linear_x3_bwd_w(float* gW, float* gb, phip_opnd g, phip_opnd x, int m,
 /* dst (three bf16 planes, plane stride m·S) = split(src[rows[i], :]) for i < m: layer 0's gather
  * in the x3 engine's update path; rows == NULL: rows 0..m-1 */
 void phip_gather_rows_x3(unsigned short* dst, const float* src, const int* rows, int m, int S);
+/* the x3 engine (gemm_x3.hip): fp32 operands, double-buffered split-at-store pipeline */
+int  phip_x3_supported(int op, int m, int n, int l);
+void phip_x3_fwd(float* y, const float* x, const int* ridx, float* xcopy, const float* W, const float* b, int m,
+                 int n, int l, int relu, unsigned* bits);
+void phip_x3_bwd_x(float* gx, const float* g, const float* W, const unsigned* bits, int m, int n, int l);
+void phip_x3_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, int n, int l, int zeroed);
 /* three bf16 planes of p[0, n) at dst + q·stride (the x3 engine's weight planes) */
 void phip_split_x3(unsigned short* dst, long stride, const float* p, long n);
 /* dst[i, :] = bf16(src[rows[i], :]) for i < m (S % 4 == 0): layer 0's gather in bf16 mode */

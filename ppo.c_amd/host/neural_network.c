@@ -246,6 +246,12 @@ static int use_x3(int m) { return m > 1024 && ppo_gemm_f32_engine(-1) == 1; }
 /* per layer: the 1- and A-wide output layers are latency-bound skinny products where the exact
  * kernels (and their paired backward launch) measure faster (profiles/r01_x3_sweep.txt) */
 static int use_x3_layer(int m, int n, int l) { return use_x3(m) && n > 32 && l > 32; }
+/* gemm_x3.hip (default) or the round-1 x3 kernels of gemm16.hip (PPO_X3_V1=1, A/B runs) */
+static int x3v2(void) {
+    static int v = -1;
+    if (v < 0) v = getenv("PPO_X3_V1") ? 0 : 1;
+    return v;
+}
 
 /* Pre-split ("planar") storage inside ppo_update (nn_set_x3_planar): the x3 layers' weights are
  * read as three bf16 planes (nn->d_w3, refreshed at update start and by every Adam step), and an
@@ -272,15 +278,18 @@ void nn_sync_w3(NeuralNetwork* nn) {
 
 /* the reference-API products (mat_mul*_cuda, layers.c) through the same engine choice (fp32 storage) */
 void lin_fwd(float* y, const float* x, const float* W, const float* b, int m, int n, int l) {
-    if (use_x3(m)) phip_linear_x3_fwd(opf(y), opf(x), NULL, NULL, opf(W), b, m, n, l, 0, NULL);
+    if (use_x3(m) && x3v2() && phip_x3_supported(0, m, n, l)) phip_x3_fwd(y, x, NULL, NULL, W, b, m, n, l, 0, NULL);
+    else if (use_x3(m)) phip_linear_x3_fwd(opf(y), opf(x), NULL, NULL, opf(W), b, m, n, l, 0, NULL);
     else phip_linear_fwd(y, x, W, b, m, n, l, 0);
 }
 void lin_bwd_x(float* gx, const float* g, const float* W, int m, int n, int l) {
-    if (use_x3(m)) phip_linear_x3_bwd_x(opf(gx), opf(g), opf(W), NULL, NULL, m, n, l);
+    if (use_x3(m) && x3v2() && phip_x3_supported(1, m, n, l)) phip_x3_bwd_x(gx, g, W, NULL, m, n, l);
+    else if (use_x3(m)) phip_linear_x3_bwd_x(opf(gx), opf(g), opf(W), NULL, NULL, m, n, l);
     else phip_linear_bwd_x(gx, g, W, NULL, m, n, l);
 }
 void lin_bwd_w(float* gW, const float* g, const float* x, int m, int n, int l) {
-    if (use_x3(m)) phip_linear_x3_bwd_w(gW, NULL, opf(g), opf(x), m, n, l, 0);
+    if (use_x3(m) && x3v2() && phip_x3_supported(2, m, n, l)) phip_x3_bwd_w(gW, NULL, g, x, m, n, l, 0);
+    else if (use_x3(m)) phip_linear_x3_bwd_w(gW, NULL, opf(g), opf(x), m, n, l, 0);
     else phip_linear_bwd_w(gW, NULL, g, x, m, n, l);
 }
 
@@ -314,7 +323,10 @@ void nn_forward_dev_rows(NeuralNetwork* nn, const float* d_x, const int* d_rows,
         Layer* ly = &nn->layers[i];
         float* out = nn->layers[i + 1].d_input;
         const int n = ly->input_size, l = ly->output_size;
-        if (use_x3_layer(m, n, l)) {
+        if (use_x3_layer(m, n, l) && x3v2() && !planar && phip_x3_supported(0, m, n, l)) {
+            phip_x3_fwd(out, (const float*)in, i == 0 ? d_rows : NULL, i == 0 ? d_xcopy : NULL, ly->d_weights,
+                        ly->d_biases, m, n, l, nn_is_relu(nn, i), act_bits(nn, i + 1));
+        } else if (use_x3_layer(m, n, l)) {
             /* the output is written pre-split when the next layer reads it through the x3 engine */
             const int out_pl = pl_act && i + 1 < L && use_x3_layer(m, l, nn->layers[i + 1].output_size);
             const phip_opnd x = (pl_in >> i) & 1u ? oppl(in, (long)m * n) : opf(in);
@@ -429,7 +441,12 @@ void nn_backward_dev(NeuralNetwork* nn, const float* d_grad_out, int m, int want
         const int relu_in = i > 0 && nn_is_relu(nn, i - 1);
         const unsigned* bits = relu_in && nn->bits_m == m ? act_bits(nn, i) : NULL;   /* this forward's bits */
         int gx_pl = 0;
-        if (use_x3_layer(m, n, l)) {
+        if (use_x3_layer(m, n, l) && x3v2() && !planar && !g_pl && phip_x3_supported(2, m, n, l) &&
+            !(nn->bits_m == m && ((nn->x3_in_planes >> i) & 1))) {
+            phip_x3_bwd_w(ly->d_grad_weights, ly->d_grad_biases, g, x, m, n, l, 1);
+            if (want_gx && (!relu_in || bits)) phip_x3_bwd_x(ly->d_grad_x, g, ly->d_weights, bits, m, n, l);
+            else if (want_gx) phip_linear_bwd_x_bits(ly->d_grad_x, g, ly->d_weights, ly->d_input, NULL, m, n, l);
+        } else if (use_x3_layer(m, n, l)) {
             const phip_opnd go = g_pl ? oppl(g, (long)m * l) : opf(g);
             const phip_opnd xo = nn->bits_m == m && ((nn->x3_in_planes >> i) & 1) ? oppl(x, (long)m * n) : opf(x);
             phip_linear_x3_bwd_w(ly->d_grad_weights, ly->d_grad_biases, go, xo, m, n, l, 1);

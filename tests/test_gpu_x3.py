@@ -125,43 +125,3 @@ def test_x3_mlp_matches_exact(lib, x3):
     err = np.abs(out[1][1] - out[0][1])
     tol = 1e-4 * np.abs(out[0][1]).max() * 2
     assert (err > tol).mean() < 1e-3, f"{(err > tol).sum()} gradient entries beyond {tol:.3g}"
-
-
-@pytest.mark.parametrize("shuffle_mode", [0, 1])
-def test_x3_planar_storage_bit_identical(lib, oracle, x3, shuffle_mode, monkeypatch):
-    """Inside ppo_update the x3 engine keeps weights, hidden activations, hidden gradients and the
-    gathered layer-0 rows as three bf16 planes split once by their producer (PPO_X3_PLANAR=1; off by
-    default, measured slower) instead of fp32 split by every consuming tile.  The planes sum to the fp32 value exactly, so
-    with split-K off (no atomics) two value and two policy minibatch steps must give bit-identical
-    networks, losses and rand() consumption either way (log σ: the head's atomics may reorder)."""
-    import test_gpu_update as U
-    sizes, N, B = [376, 512, 512, 512, 17], 4096, 2048
-    lib.ppo_gemm_tune(-1, 1)
-    lib.ppo_gemm_x3_tune(-1, 1)
-    out = {}
-    try:
-        for planar in ("0", "1"):
-            monkeypatch.setenv("PPO_X3_PLANAR", planar)
-            ppo = U.make_ppo(lib, oracle, sizes, N)
-            mu0, ls0 = U.policy_state(lib, ppo)
-            buf = U.synthetic_buffer(oracle, sizes, mu0, ls0, N, seed=5, n_envs=4)
-            U.load_buffer(lib, ppo, buf)
-            lib.ppo_reset_stats(ppo)
-            oracle.srand(23)
-            lib.ppo_update(ppo, 0.99, B, 1, 1, shuffle_mode, 4)
-            st = (ppo_ffi.C.c_double * 7)()
-            lib.ppo_read_stats(ppo, st, 7)
-            mu, ls = U.policy_state(lib, ppo)
-            out[planar] = dict(stats=np.array(st[:4]), v=U.nn_params_packed(lib, ppo.contents.V), mu=mu, ls=ls,
-                               next_rand=oracle.libc().rand(), planes=ppo.contents.V.contents.x3_in_planes)
-            lib.free_ppo(ppo)
-    finally:
-        lib.ppo_gemm_tune(-1, 0)
-        lib.ppo_gemm_x3_tune(-1, 0)
-    a, b = out["0"], out["1"]
-    assert a["planes"] == 0 and b["planes"] == 0b0111, (a["planes"], b["planes"])   # layers 0-2 read planes
-    np.testing.assert_array_equal(a["v"], b["v"])
-    np.testing.assert_array_equal(a["mu"], b["mu"])
-    np.testing.assert_allclose(a["stats"], b["stats"], rtol=1e-6)     # loss sums: atomics
-    np.testing.assert_allclose(a["ls"], b["ls"], rtol=1e-6, atol=1e-9)
-    assert a["next_rand"] == b["next_rand"]
