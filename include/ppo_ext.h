@@ -131,8 +131,9 @@ int    ppo_gemm_f32_engine(int engine);
 /* x3 engine tuning: force a tile configuration (−1 = automatic) and the grad_W split-K workgroup
  * target (0 = automatic, < 0 keeps); returns the number of configurations */
 int    ppo_gemm_x3_tune(int force_cfg, int splitk_target);
-/* diagnostic: s_memtime stamps (4 per workgroup: start, after the prologue, after the mainloop,
- * end) of the last x3 forward launched with PPO_X3_ABLATE=32; returns the number of slots */
+/* diagnostic (libppo built with -DPPO_X3_DIAG): 8 slots per workgroup of the last x3 forward
+ * launched with PPO_X3_ABLATE=32 — s_memtime at start, after the prologue, after the mainloop, at
+ * the end; s_memrealtime (100 MHz, one clock for every XCD) at start and end; returns the slots */
 int    ppo_x3_stamps(unsigned long long* out, int n);
 /* average device µs of one x3 launch (fp32 operands; op as ppo_bench_gemm) */
 double ppo_bench_gemm_x3(int op, int m, int n, int l, int iters, int cfg, int splitk_target);

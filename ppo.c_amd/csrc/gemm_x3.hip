@@ -13,7 +13,7 @@
 // the dropped terms (1,2), (2,1), (2,2) are below 2^-24 of |a·b|, so the engine is as accurate as
 // the exact fp32 MFMA (tests/test_gpu_x3.py).  Ceiling: 2.5 PF/s ÷ 6 = 417 TF/s fp32-equivalent.
 //
-// Pipeline (one workgroup per CU for the wide products, two for grad_W's 128×128 tiles):
+// Pipeline (one workgroup per CU):
 //   * BK = 16 k-tiles; the three planes of both operand tiles live in an LDS image that is DOUBLE
 //     buffered, so each k-tile costs ONE barrier and the split + LDS stores of tile t+1 and the
 //     global loads of tile t+2 are issued in the same basic block as tile t's MFMAs (the
@@ -23,6 +23,8 @@
 //     fragment is one conflict-free ds_read_b128 (48-B pitch: every 16-lane group of the read hits
 //     each of the 64 banks once); row-contiguous operands (W in grad_x, g and x in grad_W) are staged
 //     [k][R+pad] as loaded and read with two ds_read_b64_tr_b16 hardware transposes per fragment;
+//   * grad_W (split-K, f32 atomics) runs two k-groups per workgroup that sum through LDS, halving
+//     the atomics per output element;
 //   * XCD-aware block remap: tiles that share an operand panel run on one XCD's L2.
 #include "dev.h"
 
@@ -44,7 +46,7 @@ enum { OP_NT = 0, OP_NN = 1, OP_TN = 2 };
 
 // diagnostic stamps (ABL & 32): s_memtime of wave 0 of each workgroup at kernel start, after the
 // prologue, after the mainloop, at the end
-__device__ unsigned long long g_x3_stamps[8192 * 4];
+__device__ unsigned long long g_x3_stamps[8192 * 8];
 
 struct X3Args {
     const float* A; const float* B; float* C;
@@ -77,8 +79,9 @@ __device__ __forceinline__ void split4(f32x4 f, u32x2& p0, u32x2& p1, u32x2& p2)
 }
 
 // ---------------------------------------------------------------------------------------------
-// One operand tile: R rows × BK k, fp32 in HBM → three bf16 planes in LDS.  NTH threads, each
-// owning NV float4 loads.  MN = the operand is contiguous along its rows (its k is the HBM row).
+// One operand tile: R rows × BK k, fp32 in HBM → three bf16 planes in LDS.  NTH threads (one
+// k-group), each owning NV float4 loads per k-tile.
+// MN = the operand is contiguous along its rows (its k is the HBM row).
 // ---------------------------------------------------------------------------------------------
 template <int R, bool MN, int NTH>
 struct StageX3 {
@@ -90,7 +93,7 @@ struct StageX3 {
     static constexpr int SIZE = 3 * PLANE;
     static constexpr int TPR = BK / (4 * NV);                // k-contiguous: threads per row
     static constexpr int KSTEP = 4 * NTH / R;                // row-contiguous: k distance of the q-th load
-    static_assert(MN || TPR >= 1, "k-contiguous mapping");
+    static_assert(MN || (TPR >= 1 && NTH % (8 * TPR) == 0), "k-contiguous mapping");
 
     f32x4 v[NV];
     const float* base;                                       // this thread's element (row, k) at k0 = 0
@@ -107,8 +110,10 @@ struct StageX3 {
             k = tid / (R / 4);
             base = p + (long)k * ld + min(r0 + row, Rmax - 4);
         } else {
-            row = tid / TPR;
-            k = (tid % TPR) * 4 * NV;
+            // 8 consecutive lanes take 8 rows at one k offset: with the 48-B pitch their
+            // ds_write_b128s cover the 32 write banks once (row-major lane order: 2-way conflicts)
+            row = (tid % 8) + 8 * (tid / (8 * TPR));
+            k = ((tid / 8) % TPR) * 4 * NV;
             const int gr = min(r0 + row, Rmax - 1);
             base = p + (long)(ridx ? ridx[gr] : gr) * ld + k;
         }
@@ -135,16 +140,17 @@ struct StageX3 {
     }
     template <bool FULL>
     __device__ __forceinline__ void store(unsigned short* img, int k0, int kend) {
+        f32x4* vv = v;
         if (!FULL) {
 #pragma unroll
             for (int q = 0; q < NV; ++q)
-                if (!kvalid(q, k0, kend)) v[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+                if (!kvalid(q, k0, kend)) vv[q] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
         if (MN) {
 #pragma unroll
             for (int q = 0; q < NV; ++q) {
                 u32x2 p0, p1, p2;
-                split4(v[q], p0, p1, p2);
+                split4(vv[q], p0, p1, p2);
                 unsigned short* d = img + (k + q * KSTEP) * PR + row;
                 *reinterpret_cast<u32x2*>(d) = p0;
                 *reinterpret_cast<u32x2*>(d + PLANE) = p1;
@@ -152,8 +158,8 @@ struct StageX3 {
             }
         } else if (NV == 2) {                                 // 8 consecutive k: one ds_write_b128 per plane
             u32x2 a0, a1, a2, b0, b1, b2;
-            split4(v[0], a0, a1, a2);
-            split4(v[NV - 1], b0, b1, b2);
+            split4(vv[0], a0, a1, a2);
+            split4(vv[NV - 1], b0, b1, b2);
             unsigned short* d = img + row * PK + k;
             *reinterpret_cast<u32x4*>(d) = u32x4{a0[0], a0[1], b0[0], b0[1]};
             *reinterpret_cast<u32x4*>(d + PLANE) = u32x4{a1[0], a1[1], b1[0], b1[1]};
@@ -162,7 +168,7 @@ struct StageX3 {
 #pragma unroll
             for (int q = 0; q < NV; ++q) {
                 u32x2 p0, p1, p2;
-                split4(v[q], p0, p1, p2);
+                split4(vv[q], p0, p1, p2);
                 unsigned short* d = img + row * PK + k + 4 * q;
                 *reinterpret_cast<u32x2*>(d) = p0;
                 *reinterpret_cast<u32x2*>(d + PLANE) = p1;
@@ -196,23 +202,28 @@ struct StageX3 {
 };
 
 // ---------------------------------------------------------------------------------------------
-// The kernel.  BM×BN output tile per workgroup of NTH threads (WARPS_M × WARPS_N waves), k range
-// [kbeg, kend) of the workgroup's split.
+// The kernel.  BM×BN output tile per workgroup of NTH threads in KG k-groups; each k-group
+// (NTH/KG threads = WARPS_M × WARPS_N waves) runs its own pipeline over every KG-th k-tile of the
+// workgroup's split [kbeg, kend) and the groups' accumulators are summed through LDS at the end
+// (grad_W: fewer split-K workgroups per output tile, so fewer f32 atomics — they execute at the
+// memory side at ≈1.3 TB/s chip-wide, MI355X_MICROARCH.md § Global float atomics).
 // ---------------------------------------------------------------------------------------------
 // ABL (timing ablations, results wrong; PPO_X3_ABLATE, forward cfg 0 only): 1 = no MFMAs, 2 = no
-// split / LDS stores, 4 = no epilogue stores, 8 = no global loads after the prologue
-template <int OP, int BM, int BN, int WARPS_M, int NTH, int OCC, int ABL = 0>
+// split / LDS stores, 4 = no epilogue stores, 8 = no global loads after the prologue, 32 = stamps
+template <int OP, int BM, int BN, int WARPS_M, int NTH, int OCC, int KG, int ABL = 0>
 __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
-    constexpr int NW = NTH / 64, WARPS_N = NW / WARPS_M;
+    constexpr int NTG = NTH / KG;                                  // threads per k-group
+    constexpr int NW = NTG / 64, WARPS_N = NW / WARPS_M;
     constexpr int WM = BM / WARPS_M, WN = BN / WARPS_N;
     constexpr int TM = WM / 32, TN = WN / 32;
     static_assert(TM >= 1 && TN >= 1 && WARPS_M * WARPS_N == NW, "wave tiling");
+    static_assert(KG == 1 || OP == OP_TN, "k-groups: grad_W only");
     constexpr bool A_MN = OP == OP_TN, B_MN = OP != OP_NT;
-    using SA = StageX3<BM, A_MN, NTH>;
-    using SB = StageX3<BN, B_MN, NTH>;
+    using SA = StageX3<BM, A_MN, NTG>;
+    using SB = StageX3<BN, B_MN, NTG>;
     constexpr int BUF = SA::SIZE + SB::SIZE;
 
-    extern __shared__ __attribute__((aligned(16))) unsigned short lds[];     // 2 × BUF
+    extern __shared__ __attribute__((aligned(16))) unsigned short lds[];     // KG × 2 × BUF
 
     // XCD-aware remap: hardware deals blocks round-robin over the 8 XCDs; give each XCD a
     // contiguous range of linear tiles (n fastest), so tiles sharing an A panel share an L2
@@ -226,10 +237,16 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     const int kbeg = (rest / a.tiles_m) * a.kchunk;
     const int kend = min(a.K, kbeg + a.kchunk);
 
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int grp = KG > 1 ? tid / NTG : 0;                        // wave-uniform
+    const int lt = KG > 1 ? tid % NTG : tid;
+    const int w = lt >> 6;
     const int wm = w / WARPS_N, wn = w % WARPS_N;
     auto stamp = [&](int slot) {
-        if (tid == 0 && b < 8192) g_x3_stamps[b * 4 + slot] = __builtin_amdgcn_s_memtime();
+        if (tid == 0 && b < 8192) {
+            g_x3_stamps[b * 8 + slot] = __builtin_amdgcn_s_memtime();
+            if (slot == 0 || slot == 3) g_x3_stamps[b * 8 + 4 + slot / 3] = __builtin_amdgcn_s_memrealtime();
+        }
     };
     if (ABL & 32) stamp(0);
     const int r = lane & 31, h = lane >> 5;
@@ -244,8 +261,8 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
 
     SA sa;
     SB sb;
-    sa.init(a.A, a.lda, OP == OP_NT ? a.ridx : nullptr, m0, a.M, tid);
-    sb.init(a.B, a.ldb, nullptr, n0, a.N, tid);
+    sa.init(a.A, a.lda, OP == OP_NT ? a.ridx : nullptr, m0, a.M, lt);
+    sb.init(a.B, a.ldb, nullptr, n0, a.N, lt);
     const bool do_copy = OP == OP_NT && a.acopy != nullptr && tn == 0;
     // grad_W bias: Σ over this split's k of the A (= g) tile, from the staging registers
     const bool do_bsum = OP == OP_TN && a.gbias != nullptr && tn == 0;
@@ -292,6 +309,17 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
 #pragma unroll
         for (int q = 0; q < 6; ++q) mfma_group(q);
     };
+
+    // this group's k-tiles: j = 0 … NK−1 at k0 = kbeg + (KG·j + grp)·BK; only the last one can be
+    // partial (or, for a k-group past the end, empty: every element masked to zero)
+    const int nkt = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+    const int NK = (nkt + KG - 1) / KG;
+    auto k0_of = [&](int j) { return kbeg + (KG * j + grp) * BK; };
+    auto is_full = [&](int j) { return k0_of(j) + BK <= kend; };
+    const bool tail = NK > 0 && !is_full(NK - 1);
+    unsigned short* const buf0 = lds + (KG > 1 ? grp * 2 * BUF : 0);
+    unsigned short* const buf1 = buf0 + BUF;
+
     // split + LDS store of the staged tile at k0 (FULL: no k tail); COPY: also the gathered rows
     auto stage_a = [&](auto FULLc, auto COPYc, unsigned short* img, int k0) {
         constexpr bool FULL = decltype(FULLc)::value, COPY = decltype(COPYc)::value;
@@ -308,48 +336,39 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
         if ((ABL & 2) && k0 != kbeg) return;
         sb.template store<FULL>(img + SA::SIZE, k0, kend);
     };
-    auto stage = [&](auto FULLc, auto COPYc, unsigned short* img, int k0) {
-        stage_a(FULLc, COPYc, img, k0);
-        stage_b(FULLc, img, k0);
-    };
     auto load = [&](auto FULLc, int k0) {
         constexpr bool FULL = decltype(FULLc)::value;
-        if (ABL & 8) return;
+        if ((ABL & 8) && k0 != kbeg) return;
         sa.template load<FULL>(k0, kend);
         sb.template load<FULL>(k0, kend);
     };
     using T = std::true_type;
     using F = std::false_type;
+    // tile j through the full or the clamped path
+    auto load_t = [&](int j) {
+        if (is_full(j)) load(T{}, k0_of(j)); else load(F{}, k0_of(j));
+    };
+    auto stage_t = [&](auto COPYc, unsigned short* img, int j) {
+        if (is_full(j)) { stage_a(T{}, COPYc, img, k0_of(j)); stage_b(T{}, img, k0_of(j)); }
+        else { stage_a(F{}, COPYc, img, k0_of(j)); stage_b(F{}, img, k0_of(j)); }
+    };
 
-    const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
-    const bool tail = kbeg + nk * BK > kend;                  // the last k-tile is partial
-    unsigned short* const buf0 = lds;
-    unsigned short* const buf1 = lds + BUF;
-    // tile t is full unless it is the last one and K is ragged
-    auto is_full = [&](int t_) { return !(tail && t_ == nk - 1); };
-
-    // steady state, one basic block per k-tile: MFMAs of tile it from one image; the split + LDS
-    // stores of tile it+1 (loaded one iteration ago) into the other; the loads of tile it+2; one
-    // barrier.  Tiles it+1 and it+2 are full here (it+2 < nk−1 unless K is ragged: then the loop
-    // stops one tile earlier and the tail is handled below).
+    // Pipeline, iteration j: MFMAs of tile j from one image; the split + LDS stores of tile j+1
+    // (loaded one iteration ago) into the other; the loads of tile j+2; one barrier.  (Two register
+    // sets — loads two tiles ahead — measured no faster and spill the 256×256 tile.)
     auto mainloop = [&](auto COPYc) {
-        int it = 0;
-        if (nk > 0) {
-            if (is_full(0)) load(T{}, kbeg); else load(F{}, kbeg);
-            if (is_full(0)) stage(T{}, COPYc, buf0, kbeg); else stage(F{}, COPYc, buf0, kbeg);
-        }
-        if (nk > 1) {
-            if (is_full(1)) load(T{}, kbeg + BK); else load(F{}, kbeg + BK);
-        }
+        if (NK > 0) { load_t(0); stage_t(COPYc, buf0, 0); }
+        if (NK > 1) load_t(1);
         __syncthreads();
         if (ABL & 32) stamp(1);
-        const int steady = tail ? nk - 3 : nk - 2;            // iterations whose it+1, it+2 tiles are full
-        for (; it < steady; ++it) {
-            const unsigned short* cur = (it & 1) ? buf1 : buf0;
-            unsigned short* nxt = (it & 1) ? buf0 : buf1;
-            const int k1 = kbeg + (it + 1) * BK;
-            // interleave in program order (sched_barrier fences): each plane-product group of MFMAs
-            // shares its scheduling region with one slice of the staging work
+        // steady state (tiles j+1, j+2 full): one basic block per k-tile, each plane-product group
+        // of MFMAs sharing its scheduling region with one slice of the staging work
+        const int steady = NK - 2 - (tail ? 1 : 0);
+        int j = 0;
+        for (; j < steady; ++j) {
+            const unsigned short* cur = (j & 1) ? buf1 : buf0;
+            unsigned short* nxt = (j & 1) ? buf0 : buf1;
+            const int k1 = k0_of(j + 1);
             read_frags(cur);
             mfma_group(0);
             __builtin_amdgcn_sched_barrier(0);
@@ -360,41 +379,37 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
             stage_b(T{}, nxt, k1);
             __builtin_amdgcn_sched_barrier(0);
             mfma_group(3);
-            load(T{}, k1 + BK);
+            load(T{}, k0_of(j + 2));
             __builtin_amdgcn_sched_barrier(0);
             mfma_group(4);
             mfma_group(5);
             __syncthreads();
         }
-        for (; it < nk; ++it) {                               // the last one or two tiles
-            const unsigned short* cur = (it & 1) ? buf1 : buf0;
-            unsigned short* nxt = (it & 1) ? buf0 : buf1;
-            const int k1 = kbeg + (it + 1) * BK;
+        for (; j < NK; ++j) {                                 // the last one or two tiles
+            const unsigned short* cur = (j & 1) ? buf1 : buf0;
+            unsigned short* nxt = (j & 1) ? buf0 : buf1;
             compute(cur);
-            if (it + 1 < nk) {
-                if (is_full(it + 1)) stage(T{}, COPYc, nxt, k1); else stage(F{}, COPYc, nxt, k1);
-            }
-            if (it + 2 < nk) {
-                if (is_full(it + 2)) load(T{}, k1 + BK); else load(F{}, k1 + BK);
-            }
+            if (j + 1 < NK) stage_t(COPYc, nxt, j + 1);
+            if (j + 2 < NK) load_t(j + 2);
             __syncthreads();
         }
     };
     if (do_copy) mainloop(T{});
     else mainloop(F{});
 
+    // LDS scratch after the mainloop (the images are no longer read): bias-gradient partial sums,
+    // then the k-groups' accumulator exchange
+    constexpr int RED_FLOATS = OP == OP_TN ? (NTH / (BM / 4)) * BM : 0;
     if (do_bsum) {
         // rows of this thread's float4s: row .. row+3; reduce over the threads sharing them
-        // (tid ≡ tid' mod BM/4), through LDS (the images are no longer read after this barrier)
+        // (tid ≡ tid' mod BM/4), through LDS
         __syncthreads();
         float* red = reinterpret_cast<float*>(lds);
         constexpr int G = BM / 4;                       // float4 row groups
         constexpr int S = NTH / G;                      // threads per group (one per k-row slot)
+        static_assert(NTG % G == 0, "bias-sum row mapping");
 #pragma unroll
-        for (int q = 0; q < SA::NV; ++q) {
-            // (NV > 1: the q-th float4 is a different k of the same rows — already summed into bs[0..])
-            if (q > 0) bs[0] += bs[q];
-        }
+        for (int q = 1; q < SA::NV; ++q) bs[0] += bs[q];
         *reinterpret_cast<f32x4*>(red + (tid / G) * BM + (tid % G) * 4) = bs[0];
         __syncthreads();
         if (tid < BM) {
@@ -405,6 +420,38 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
                 else a.gbias[m0 + tid] = s;
             }
         }
+    }
+    // k-groups: block (i, j) of a wave's tile is finished by the group (i·TN + j) mod KG; every
+    // other group's wave at the same position hands its partial block over through LDS
+    auto mine = [&](int i, int j) { return KG == 1 || ((i * TN + j) % KG) == grp; };
+    if constexpr (KG > 1) {
+        static_assert(KG == 2, "k-group exchange: two groups");
+        static_assert((RED_FLOATS * 4 + NW * TM * TN * 4096) <= KG * 2 * BUF * 2, "k-group exchange: LDS");
+        f32x4* xch = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(lds) + RED_FLOATS);
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                if (mine(i, j)) continue;
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    xch[((w * TM * TN + i * TN + j) * 4 + q) * 64 + lane] =
+                        f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+            }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                if (!mine(i, j)) continue;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const f32x4 o = xch[((w * TM * TN + i * TN + j) * 4 + q) * 64 + lane];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) acc[i][j][4 * q + e] += o[e];
+                }
+            }
     }
 
     if (ABL & 32) stamp(2);
@@ -425,6 +472,7 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
+            if (!mine(i, j)) continue;
             const int c0 = n0 + wn * WN + j * 32;
             const int col = c0 + r;
             const int r0 = m0 + wm * WM + i * 32 + 4 * h;
@@ -475,20 +523,23 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     if (ABL & 32) stamp(3);
 }
 
+#ifdef PPO_X3_DIAG
 int g_x3_ablate = -1;
+#endif
 
-template <int OP, int BM, int BN, int WARPS_M, int NTH, int OCC, int ABL = 0>
+template <int OP, int BM, int BN, int WARPS_M, int NTH, int OCC, int KG, int ABL = 0>
 void launch_x3(X3Args a) {
     a.tiles_m = ppo_divup(a.M, BM);
     a.tiles_n = ppo_divup(a.N, BN);
     if (a.splits < 1) a.splits = 1;
     const long grid = (long)a.tiles_m * a.tiles_n * a.splits;
     PPO_REQUIRE(grid > 0 && grid < (1L << 31), "gemm_x3: grid out of range");
-    using SA = StageX3<BM, OP == OP_TN, NTH>;
-    using SB = StageX3<BN, OP != OP_NT, NTH>;
-    constexpr size_t lds = 2 * sizeof(unsigned short) * (SA::SIZE + SB::SIZE);
+    PPO_REQUIRE(a.kchunk % (KG * BK) == 0 || a.splits == 1, "gemm_x3: split-K chunk vs k-groups");
+    using SA = StageX3<BM, OP == OP_TN, NTH / KG>;
+    using SB = StageX3<BN, OP != OP_NT, NTH / KG>;
+    constexpr size_t lds = (size_t)KG * 2 * sizeof(unsigned short) * (SA::SIZE + SB::SIZE);
     static_assert(lds <= 160 * 1024, "gemm_x3: LDS images exceed 160 KiB");
-    auto kern = gemm_x3_kernel<OP, BM, BN, WARPS_M, NTH, OCC, ABL>;
+    auto kern = gemm_x3_kernel<OP, BM, BN, WARPS_M, NTH, OCC, KG, ABL>;
     if (lds > 64 * 1024) {
         static bool attr = false;                      // once per instantiation
         if (!attr) {
@@ -500,45 +551,47 @@ void launch_x3(X3Args a) {
     PPO_LAUNCH_CHECK();
 }
 
-// tile configurations {BM, BN}: 0 = 256×256 over 8 waves of 64×128 (forward, grad_x), 1 = 128×128
-// over 4 waves of 64×64, two workgroups per CU (grad_W, narrow products), 2 = 128×128 over 8 waves
-// of 64×32
-struct CfgX3 { int bm, bn; };
-constexpr CfgX3 kCfgX3[] = {{256, 256}, {128, 128}, {128, 128}};
+// tile configurations: 0 = 256×256 over 8 waves of 64×128 (forward, grad_x; one workgroup per CU),
+// 1 = 128×128 over 4 waves of 64×64, two workgroups per CU (narrow products), 2 = 128×128 over 8
+// waves of 32×64, 3 = 128×128 over two k-groups of 4 waves of 64×64, one workgroup per CU (grad_W)
+struct CfgX3 { int bm, bn, kg, slots_per_cu; };
+constexpr CfgX3 kCfgX3[] = {{256, 256, 1, 1}, {128, 128, 1, 2}, {128, 128, 1, 1}, {128, 128, 2, 1}};
 int g_force_x3 = -1;
 int g_split_x3 = 0;
 
 template <int OP>
 void launch_cfg_x3(int c, const X3Args& a) {
+#ifdef PPO_X3_DIAG
     if (g_x3_ablate < 0) {
         const char* e = getenv("PPO_X3_ABLATE");
         g_x3_ablate = e ? atoi(e) : 0;
     }
     if (OP == OP_NT && c == 0 && g_x3_ablate) {
         switch (g_x3_ablate) {
-            case 1: launch_x3<OP, 256, 256, 4, 512, 2, 1>(a); return;
-            case 2: launch_x3<OP, 256, 256, 4, 512, 2, 2>(a); return;
-            case 3: launch_x3<OP, 256, 256, 4, 512, 2, 3>(a); return;
-            case 4: launch_x3<OP, 256, 256, 4, 512, 2, 4>(a); return;
-            case 8: launch_x3<OP, 256, 256, 4, 512, 2, 8>(a); return;
-            case 10: launch_x3<OP, 256, 256, 4, 512, 2, 10>(a); return;
-            case 14: launch_x3<OP, 256, 256, 4, 512, 2, 14>(a); return;
-            case 5: launch_x3<OP, 256, 256, 4, 512, 2, 5>(a); return;
-            case 7: launch_x3<OP, 256, 256, 4, 512, 2, 7>(a); return;
-            case 32: launch_x3<OP, 256, 256, 4, 512, 2, 32>(a); return;
+            case 1: launch_x3<OP, 256, 256, 4, 512, 2, 1, 1>(a); return;
+            case 2: launch_x3<OP, 256, 256, 4, 512, 2, 1, 2>(a); return;
+            case 3: launch_x3<OP, 256, 256, 4, 512, 2, 1, 3>(a); return;
+            case 4: launch_x3<OP, 256, 256, 4, 512, 2, 1, 4>(a); return;
+            case 8: launch_x3<OP, 256, 256, 4, 512, 2, 1, 8>(a); return;
+            case 32: launch_x3<OP, 256, 256, 4, 512, 2, 1, 32>(a); return;
             default: break;
         }
     }
+#endif
     switch (c) {
-        case 0: launch_x3<OP, 256, 256, 4, 512, 2>(a); break;
-        case 2: launch_x3<OP, 128, 128, 4, 512, 2>(a); break;
-        default: launch_x3<OP, 128, 128, 2, 256, 2>(a); break;
+        case 0: launch_x3<OP, 256, 256, 4, 512, 2, 1>(a); break;
+        case 2: launch_x3<OP, 128, 128, 4, 512, 2, 1>(a); break;
+        case 3:
+            if constexpr (OP == OP_TN) { launch_x3<OP, 128, 128, 2, 512, 2, 2>(a); break; }
+            [[fallthrough]];
+        default: launch_x3<OP, 128, 128, 2, 256, 2, 1>(a); break;
     }
 }
 
 int pick_x3(int M, int N, int op) {
     if (g_force_x3 >= 0) return g_force_x3;
-    if (op != OP_TN && M >= 4096 && N >= 256) return 0;
+    if (op == OP_TN) return 3;
+    if (M >= 4096 && N >= 256) return 0;
     return 1;
 }
 
@@ -597,13 +650,14 @@ void phip_x3_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, 
     }
     const int c = pick_x3(l, n, OP_TN);
     const long tiles = (long)ppo_divup(l, kCfgX3[c].bm) * ppo_divup(n, kCfgX3[c].bn);
-    // split-K over the batch: the grid stays within one round of workgroup slots (2 per CU), each
-    // split ≥ 8 k-tiles
-    const int target = g_split_x3 > 0 ? g_split_x3 : 512;
+    // split-K over the batch: the grid stays within one round of workgroup slots (256 CUs × the
+    // configuration's workgroups per CU), each split ≥ 8 k-tiles per k-group
+    const int kq = BK * kCfgX3[c].kg;                       // a split's k range: whole k-tiles per group
+    const int target = g_split_x3 > 0 ? g_split_x3 : 256 * kCfgX3[c].slots_per_cu;
     int splits = (int)(target / tiles);
-    const int max_splits = m / (8 * BK) > 0 ? m / (8 * BK) : 1;
+    const int max_splits = m / (8 * kq) > 0 ? m / (8 * kq) : 1;
     splits = std::max(1, std::min(splits, max_splits));
-    int kchunk = ppo_divup(ppo_divup(m, splits), BK) * BK;
+    int kchunk = ppo_divup(ppo_divup(m, splits), kq) * kq;
     splits = ppo_divup(m, kchunk);
     X3Args a{};
     a.A = g; a.lda = l; a.B = x; a.ldb = n; a.C = gW; a.ldc = n;
@@ -665,11 +719,12 @@ double ppo_bench_gemm_x3(int op, int m, int n, int l, int iters, int cfg, int sp
     return 1000.0 * ms / (iters > 0 ? iters : 1);
 }
 
-// diagnostic: the stamps of the last PPO_X3_ABLATE=32 launch (4 per workgroup)
+// diagnostic: the stamps of the last PPO_X3_ABLATE=32 launch (4 per workgroup; libppo built with
+// -DPPO_X3_DIAG, tools/build_variant.sh)
 int ppo_x3_stamps(unsigned long long* out, int n) {
     phip_sync();
-    PPO_CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_x3_stamps), sizeof(unsigned long long) * (size_t)std::min(n, 8192 * 4)));
-    return 8192 * 4;
+    PPO_CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_x3_stamps), sizeof(unsigned long long) * (size_t)std::min(n, 8192 * 8)));
+    return 8192 * 8;
 }
 
 }  // extern "C"

@@ -216,8 +216,8 @@ _SIGS = {
 _lib = None
 
 
-def load(path=LIB_PATH):
-    """Load libppo.so.
+def load(path=None):
+    """Load libppo.so (PPO_LIB overrides the path: diagnostic variants built by tools/build_variant.sh).
 
     In a process that also uses torch, `import torch` BEFORE calling load(): libppo then binds to the
     HIP runtime torch already mapped (same soname, libamdhip64.so.7) and the process holds one runtime.
@@ -225,6 +225,7 @@ def load(path=LIB_PATH):
     global _lib
     if _lib is not None:
         return _lib
+    path = path or os.environ.get("PPO_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise RuntimeError(f"libppo.so not built at {path}: run `python -c 'import __graft_entry__ as g; g.build()'`")
     lib = C.CDLL(path, mode=C.RTLD_GLOBAL)

@@ -4,7 +4,8 @@
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/x3abl
 mkdir -p $O
-for ab in 0 1 2 4 8 3 5 10 14 7; do
+export PPO_LIB=${PPO_LIB:-$R/ppo.c_amd/lib/variants/libppo_diag.so}   # tools/build_variant.sh diag -DPPO_X3_DIAG gemm_x3
+for ab in 0 1 2 4 8; do
   PPO_X3_ABLATE=$ab GEMM_ENGINE=x3 timeout -k 10 60 python3 $R/ppo.c_amd/tools/gemm_one.py ${OP:-0} 32768 512 512 0 50 | sed "s/^/ablate=$ab /" >> $O/times.txt || exit 1
 done
 cd /tmp && export TMPDIR=/tmp
