@@ -67,12 +67,20 @@ __device__ __forceinline__ unsigned pack2(float lo, float hi) {
 __device__ __forceinline__ float bf_lo(unsigned u) { return __builtin_bit_cast(float, u << 16); }
 __device__ __forceinline__ float bf_hi(unsigned u) { return __builtin_bit_cast(float, u & 0xffff0000u); }
 
+// the packed conversion, opaque: otherwise the compiler rebuilds bf_lo(pack2(lo, hi)) as a second
+// single-value v_cvt_pk_bf16_f32 + shift (16 extra VALU per k-tile per wave in the x3 mainloop)
+__device__ __forceinline__ unsigned pack2_opaque(float lo, float hi) {
+    unsigned u = pack2(lo, hi);
+    asm("" : "+v"(u));
+    return u;
+}
+
 // exact three-plane split of 4 values: plane q gets 4 bf16 (2 dwords)
 __device__ __forceinline__ void split4(f32x4 f, u32x2& p0, u32x2& p1, u32x2& p2) {
-    const unsigned a0 = pack2(f[0], f[1]), b0 = pack2(f[2], f[3]);
+    const unsigned a0 = pack2_opaque(f[0], f[1]), b0 = pack2_opaque(f[2], f[3]);
     const float r0 = f[0] - bf_lo(a0), r1 = f[1] - bf_hi(a0);
     const float r2 = f[2] - bf_lo(b0), r3 = f[3] - bf_hi(b0);
-    const unsigned a1 = pack2(r0, r1), b1 = pack2(r2, r3);
+    const unsigned a1 = pack2_opaque(r0, r1), b1 = pack2_opaque(r2, r3);
     p0 = u32x2{a0, b0};
     p1 = u32x2{a1, b1};
     p2 = u32x2{pack2(r0 - bf_lo(a1), r1 - bf_hi(a1)), pack2(r2 - bf_lo(b1), r3 - bf_hi(b1))};
@@ -494,6 +502,9 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
                 }
             }
             unsigned word = 0;
+            // element stores in the accumulator layout (each wave store: two 128-B row segments);
+            // a DPP quad transpose to 16-B stores measured slower: the store tail is HBM-write-bound
+            // (64 MB in ≈14 µs), not store-issue-bound
 #pragma unroll
             for (int e = 0; e < 16; ++e) {
                 const int row = r0 + (e & 3) + 8 * (e >> 2);
