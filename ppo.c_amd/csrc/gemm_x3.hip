@@ -146,7 +146,7 @@ struct StageX3 {
     __device__ __forceinline__ bool kvalid(int q, int k0, int kend) const {
         return MN ? k0 + k + q * KSTEP < kend : k0 + k + 4 * q < kend;
     }
-    template <bool FULL>
+    template <bool FULL, bool NOSPLIT = false>
     __device__ __forceinline__ void store(unsigned short* img, int k0, int kend) {
         f32x4* vv = v;
         if (!FULL) {
@@ -154,11 +154,16 @@ struct StageX3 {
             for (int q = 0; q < NV; ++q)
                 if (!kvalid(q, k0, kend)) vv[q] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
+        // NOSPLIT (timing ablation only): raw bits into the planes, no split VALU
+        auto split = [](f32x4 f, u32x2& p0, u32x2& p1, u32x2& p2) {
+            if (NOSPLIT) { p0 = p1 = p2 = u32x2{__builtin_bit_cast(unsigned, f[0]), __builtin_bit_cast(unsigned, f[3])}; }
+            else split4(f, p0, p1, p2);
+        };
         if (MN) {
 #pragma unroll
             for (int q = 0; q < NV; ++q) {
                 u32x2 p0, p1, p2;
-                split4(vv[q], p0, p1, p2);
+                split(vv[q], p0, p1, p2);
                 unsigned short* d = img + (k + q * KSTEP) * PR + row;
                 *reinterpret_cast<u32x2*>(d) = p0;
                 *reinterpret_cast<u32x2*>(d + PLANE) = p1;
@@ -166,8 +171,8 @@ struct StageX3 {
             }
         } else if (NV == 2) {                                 // 8 consecutive k: one ds_write_b128 per plane
             u32x2 a0, a1, a2, b0, b1, b2;
-            split4(vv[0], a0, a1, a2);
-            split4(vv[NV - 1], b0, b1, b2);
+            split(vv[0], a0, a1, a2);
+            split(vv[NV - 1], b0, b1, b2);
             unsigned short* d = img + row * PK + k;
             *reinterpret_cast<u32x4*>(d) = u32x4{a0[0], a0[1], b0[0], b0[1]};
             *reinterpret_cast<u32x4*>(d + PLANE) = u32x4{a1[0], a1[1], b1[0], b1[1]};
@@ -176,7 +181,7 @@ struct StageX3 {
 #pragma unroll
             for (int q = 0; q < NV; ++q) {
                 u32x2 p0, p1, p2;
-                split4(vv[q], p0, p1, p2);
+                split(vv[q], p0, p1, p2);
                 unsigned short* d = img + row * PK + k + 4 * q;
                 *reinterpret_cast<u32x2*>(d) = p0;
                 *reinterpret_cast<u32x2*>(d + PLANE) = p1;
@@ -216,8 +221,9 @@ struct StageX3 {
 // (grad_W: fewer split-K workgroups per output tile, so fewer f32 atomics — they execute at the
 // memory side at ≈1.3 TB/s chip-wide, MI355X_MICROARCH.md § Global float atomics).
 // ---------------------------------------------------------------------------------------------
-// ABL (timing ablations, results wrong; PPO_X3_ABLATE, forward cfg 0 only): 1 = no MFMAs, 2 = no
-// split / LDS stores, 4 = no epilogue stores, 8 = no global loads after the prologue, 32 = stamps
+// ABL (timing ablations, results wrong; PPO_X3_ABLATE, -DPPO_X3_DIAG builds, cfgs 0 and 3): 1 = no
+// MFMAs, 2 = no split / LDS stores, 4 = no epilogue stores, 8 = no global loads after the prologue,
+// 32 = stamps, 64 = no split (raw bits stored to the planes)
 template <int OP, int BM, int BN, int WARPS_M, int NTH, int OCC, int KG, int ABL = 0>
 __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     constexpr int NTG = NTH / KG;                                  // threads per k-group
@@ -333,7 +339,7 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
         constexpr bool FULL = decltype(FULLc)::value, COPY = decltype(COPYc)::value;
         if ((ABL & 2) && k0 != kbeg) return;
         if (COPY) sa.copy_out(a.acopy, a.K, m0, a.M, k0, kend);
-        sa.template store<FULL>(img, k0, kend);
+        sa.template store<FULL, (ABL & 64) != 0>(img, k0, kend);
         if (do_bsum) {
 #pragma unroll
             for (int q = 0; q < SA::NV; ++q) bs[q] += sa.v[q];
@@ -342,7 +348,7 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     auto stage_b = [&](auto FULLc, unsigned short* img, int k0) {
         constexpr bool FULL = decltype(FULLc)::value;
         if ((ABL & 2) && k0 != kbeg) return;
-        sb.template store<FULL>(img + SA::SIZE, k0, kend);
+        sb.template store<FULL, (ABL & 64) != 0>(img + SA::SIZE, k0, kend);
     };
     auto load = [&](auto FULLc, int k0) {
         constexpr bool FULL = decltype(FULLc)::value;
@@ -577,14 +583,19 @@ void launch_cfg_x3(int c, const X3Args& a) {
         const char* e = getenv("PPO_X3_ABLATE");
         g_x3_ablate = e ? atoi(e) : 0;
     }
-    if (OP == OP_NT && c == 0 && g_x3_ablate) {
+    if (g_x3_ablate && (c == 0 || (c == 3 && OP == OP_TN))) {
+        auto run = [&](auto ABLc) {
+            constexpr int A = decltype(ABLc)::value;
+            if constexpr (OP == OP_TN) launch_x3<OP, 128, 128, 2, 512, 2, 2, A>(a);
+            else launch_x3<OP, 256, 256, 4, 512, 2, 1, A>(a);
+        };
         switch (g_x3_ablate) {
-            case 1: launch_x3<OP, 256, 256, 4, 512, 2, 1, 1>(a); return;
-            case 2: launch_x3<OP, 256, 256, 4, 512, 2, 1, 2>(a); return;
-            case 3: launch_x3<OP, 256, 256, 4, 512, 2, 1, 3>(a); return;
-            case 4: launch_x3<OP, 256, 256, 4, 512, 2, 1, 4>(a); return;
-            case 8: launch_x3<OP, 256, 256, 4, 512, 2, 1, 8>(a); return;
-            case 32: launch_x3<OP, 256, 256, 4, 512, 2, 1, 32>(a); return;
+            case 1: run(std::integral_constant<int, 1>{}); return;
+            case 2: run(std::integral_constant<int, 2>{}); return;
+            case 4: run(std::integral_constant<int, 4>{}); return;
+            case 8: run(std::integral_constant<int, 8>{}); return;
+            case 32: run(std::integral_constant<int, 32>{}); return;
+            case 64: run(std::integral_constant<int, 64>{}); return;
             default: break;
         }
     }
