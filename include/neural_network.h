@@ -87,8 +87,6 @@ typedef struct {
     unsigned short* d_w16;  /* bf16 mode: bf16 shadow of d_params (same offsets), refreshed after updates */
     float* d_tiny_wt;       /* small-network update path: transposed weights scratch */
     long   tiny_wt_cap;
-    unsigned short* d_w3;   /* x3 engine (fp32 mode): d_params as three bf16 planes (plane stride num_params rounded up to 8) */
-    int    x3_in_planes;    /* bit i: layers[i].d_input (bit 0: d_x0) held three bf16 planes in the last forward */
     /* host mirror <-> HBM reconciliation for the host-pointer entry points (forward_propagation,
      * sample_action, ...): HBM parameters changed by Adam / ppo_update are pulled to the host
      * mirrors, host mirrors edited by the caller are pushed to HBM — never blindly overwritten */

@@ -26,9 +26,11 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
 
 // n elements: float4 body plus a scalar tail (a network's span ends with its unpadded output bias).
 // w16 (bf16 mode): the parameters' bf16 shadow for the first n16 elements, written in the same pass.
-__global__ void adam_flat_vec_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+// zero_g: the gradient is cleared once read (ppo_update: the next backward's split-K atomics then
+// accumulate into zeros without a memset launch per minibatch step).
+__global__ void adam_flat_vec_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
                                      float* __restrict__ v, long n, float step, float b1, float b2, float bc2,
-                                     float scale, __bf16* __restrict__ w16, long n16) {
+                                     float scale, __bf16* __restrict__ w16, long n16, int zero_g) {
     typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
     const long n4 = n >> 2;
     for (long i = blockIdx.x * (long)TPB + threadIdx.x; i < n4; i += (long)gridDim.x * TPB) {
@@ -41,6 +43,7 @@ __global__ void adam_flat_vec_kernel(float* __restrict__ p, const float* __restr
         reinterpret_cast<float4*>(p)[i] = pp;
         reinterpret_cast<float4*>(m)[i] = mm;
         reinterpret_cast<float4*>(v)[i] = vv;
+        if (zero_g) reinterpret_cast<float4*>(g)[i] = float4{0.f, 0.f, 0.f, 0.f};
         if (w16 && 4 * i < n16) {
             if (4 * i + 4 <= n16) {
                 bf16x4 o = {(__bf16)pp.x, (__bf16)pp.y, (__bf16)pp.z, (__bf16)pp.w};
@@ -56,6 +59,7 @@ __global__ void adam_flat_vec_kernel(float* __restrict__ p, const float* __restr
         float pp = p[j], mm = m[j], vv = v[j];
         adam_elem(pp, g[j], mm, vv, step, b1, b2, bc2, scale);
         p[j] = pp; m[j] = mm; v[j] = vv;
+        if (zero_g) g[j] = 0.f;
         if (w16 && j < n16) w16[j] = (__bf16)pp;
     }
 }
@@ -102,20 +106,20 @@ int grid_for(long n) {
 
 extern "C" {
 
-void phip_adam_flat_w16(float* p, const float* g, float* m, float* v, long n, float lr, float beta1, float beta2,
+void phip_adam_flat_w16(float* p, float* g, float* m, float* v, long n, float lr, float beta1, float beta2,
                         float bias_correction1, float bias_correction2, float grad_scale, unsigned short* w16,
-                        long n16) {
+                        long n16, int zero_g) {
     if (n <= 0) return;
     const float step = lr / bias_correction1;
-    ppo::ProfScope ps(PPO_K_ADAM, 28.0 * n + (w16 ? 2.0 * n16 : 0.0));
+    ppo::ProfScope ps(PPO_K_ADAM, 28.0 * n + (w16 ? 2.0 * n16 : 0.0) + (zero_g ? 4.0 * n : 0.0));
     const bool vec = (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15u) == 0 &&
                      ((uintptr_t)w16 & 7u) == 0;
     if (vec) {
         hipLaunchKernelGGL(adam_flat_vec_kernel, dim3(grid_for((n + 3) / 4)), dim3(TPB), 0, ppo::stream(), p, g, m,
                            v, n, step, beta1, beta2, bias_correction2, grad_scale,
-                           reinterpret_cast<__bf16*>(w16), n16);
+                           reinterpret_cast<__bf16*>(w16), n16, zero_g);
     } else {
-        PPO_REQUIRE(!w16, "phip_adam_flat_w16: unaligned span with a bf16 shadow");
+        PPO_REQUIRE(!w16 && !zero_g, "phip_adam_flat_w16: unaligned span with a bf16 shadow or gradient clear");
         hipLaunchKernelGGL(adam_flat_kernel, dim3(grid_for(n)), dim3(TPB), 0, ppo::stream(), p, g, m, v, n, step,
                            beta1, beta2, bias_correction2, grad_scale);
     }
@@ -124,7 +128,8 @@ void phip_adam_flat_w16(float* p, const float* g, float* m, float* v, long n, fl
 
 void phip_adam_flat(float* p, const float* g, float* m, float* v, long n, float lr, float beta1, float beta2,
                     float bias_correction1, float bias_correction2, float grad_scale) {
-    phip_adam_flat_w16(p, g, m, v, n, lr, beta1, beta2, bias_correction1, bias_correction2, grad_scale, nullptr, 0);
+    phip_adam_flat_w16(p, const_cast<float*>(g), m, v, n, lr, beta1, beta2, bias_correction1, bias_correction2,
+                       grad_scale, nullptr, 0, 0);
 }
 
 void phip_adam_multi(float* const* params, float* const* grads, const int* lengths, int num_tensors, float* m,

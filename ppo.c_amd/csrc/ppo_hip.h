@@ -69,29 +69,15 @@ void phip_linear16_bwd_x(void* gx, int tgx, const void* g, int tg, const void* W
 /* gW[l,n] (+)= gᵀ·x, gb (+)= Σ g in fp32 (zeroed != 0: outputs already zero) */
 void phip_linear16_bwd_w(float* gW, float* gb, const void* g, int tg, const void* x, int tx, int m, int n, int l,
                          int zeroed);
-/* fp32-accurate products on the bf16 MFMA (exact 3-plane bf16 split, 6 products): the "x3" engine
- * of fp32 mode.  An operand is fp32 (planes = 0: split on the way into LDS) or pre-split (planes = 1:
- * three bf16 planes whose sum is the fp32 value exactly, plane q at p + q·pstride elements).
- * Forward with optional fused gather (fp32 x only; xcopy = fp32 copy of the gathered rows) +
+/* fp32-accurate products on the bf16 MFMA (gemm_x3.hip, the "x3" engine of fp32 mode): every fp32
+ * operand splits exactly into three bf16 planes on its way into LDS, six plane products, fp32
+ * accumulation.  Forward with optional fused gather (xcopy = fp32 copy of the gathered rows) +
  * bias/ReLU/ReLU' bits; grad_x with the bit mask; grad_W (+gb) split-K. */
-typedef struct { void* p; int planes; long pstride; } phip_opnd;
-void phip_linear_x3_fwd(phip_opnd y, phip_opnd x, const int* ridx, float* xcopy, phip_opnd W, const float* b,
-                        int m, int n, int l, int relu, unsigned* bits);
-/* Wt (optional, fp32 [n, l]): grad_x computed as an NT product against Wᵀ (fp32 g and gx only) */
-void phip_linear_x3_bwd_x(phip_opnd gx, phip_opnd g, phip_opnd W, const float* Wt, const unsigned* bits, int m,
-                          int n, int l);
-void phip_linear_x3_bwd_w(float* gW, float* gb, phip_opnd g, phip_opnd x, int m, int n, int l, int zeroed);
-/* dst (three bf16 planes, plane stride m·S) = split(src[rows[i], :]) for i < m: layer 0's gather
- * in the x3 engine's update path; rows == NULL: rows 0..m-1 */
-void phip_gather_rows_x3(unsigned short* dst, const float* src, const int* rows, int m, int S);
-/* the x3 engine (gemm_x3.hip): fp32 operands, double-buffered split-at-store pipeline */
 int  phip_x3_supported(int op, int m, int n, int l);
 void phip_x3_fwd(float* y, const float* x, const int* ridx, float* xcopy, const float* W, const float* b, int m,
                  int n, int l, int relu, unsigned* bits);
 void phip_x3_bwd_x(float* gx, const float* g, const float* W, const unsigned* bits, int m, int n, int l);
 void phip_x3_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, int n, int l, int zeroed);
-/* three bf16 planes of p[0, n) at dst + q·stride (the x3 engine's weight planes) */
-void phip_split_x3(unsigned short* dst, long stride, const float* p, long n);
 /* dst[i, :] = bf16(src[rows[i], :]) for i < m (S % 4 == 0): layer 0's gather in bf16 mode */
 void phip_gather_rows_bf16(unsigned short* dst, const float* src, const int* rows, int m, int S);
 void phip_f32_to_bf16(unsigned short* dst, const float* src, long count);
@@ -139,14 +125,6 @@ void phip_axpy(float* y, const float* x, long count);
 /* d_loss[0] = Σ(t−y)²/count (written), d_loss_accum[0] += same (if non-NULL);
  * grad = 2(y−t)/count (if non-NULL).  loss.cu:25-83 fused, no host sync. */
 void phip_mse(const float* y, const float* t, long count, float* grad, float* d_loss, float* d_loss_accum);
-/* out_head.hip: output layer forward + loss head + output layer backward in one pass (ppo_update);
- * head 0 = value (A = 1, MSE against tgt), 1 = policy (clipped surrogate); gW / gb overwritten
- * (deterministic workgroup partials), grad_log_std accumulated (pre-zeroed) */
-int  phip_out_fused_supported(int n, int A);
-void phip_out_fused(int head, const float* x, const unsigned* bits, const float* W, const float* b, int m, int n,
-                    int A, const float* tgt, const float* log_std, const float* action, const float* adv,
-                    const float* old_lp, float eps, float ent_coeff, float* y, float* gx, float* gW, float* gb,
-                    float* grad_log_std, float* loss_accum);
 void phip_log_prob(const float* mu, const float* log_std, const float* action, float* out, int m, int A);
 void phip_log_prob_bwd(const float* mu, const float* log_std, const float* action, const float* grad_in,
                        float* grad_mu, float* grad_log_std, int m, int A);
@@ -196,10 +174,11 @@ void phip_gather(const int* perm, uint64_t key, int offset, int limit, int batch
 /* ---------------- Adam (adam.hip) ---------------- */
 void phip_adam_flat(float* p, const float* g, float* m, float* v, long n, float lr, float beta1,
                     float beta2, float bias_correction1, float bias_correction2, float grad_scale);
-/* the same, also writing bf16(p) into w16[0, n16) (bf16 mode's parameter shadow) */
-void phip_adam_flat_w16(float* p, const float* g, float* m, float* v, long n, float lr, float beta1, float beta2,
+/* the same, also writing bf16(p) into w16[0, n16) (bf16 mode's parameter shadow); zero_g: g is
+ * cleared once read (the next backward accumulates into it without a memset) */
+void phip_adam_flat_w16(float* p, float* g, float* m, float* v, long n, float lr, float beta1, float beta2,
                         float bias_correction1, float bias_correction2, float grad_scale, unsigned short* w16,
-                        long n16);
+                        long n16, int zero_g);
 /* multi-tensor: ptrs/lengths are HOST arrays describing device tensors; m/v are flat */
 void phip_adam_multi(float* const* params, float* const* grads, const int* lengths, int num_tensors,
                      float* m, float* v, float lr, float beta1, float beta2,

@@ -163,17 +163,19 @@ void free_adam_cuda(Adam* adam) {
     free(adam);
 }
 
-void adam_update_cuda(Adam* adam, float lr) { adam_update_cuda_w16(adam, lr, NULL, 0); }
+void adam_update_cuda(Adam* adam, float lr) { adam_update_cuda_w16(adam, lr, NULL, 0, 0); }
 
-/* w16 != NULL: also refresh the bf16 shadow of the first n16 parameters (flat spans only) */
-int adam_update_cuda_w16(Adam* adam, float lr, unsigned short* w16, long n16) {
+/* w16 != NULL: also refresh the bf16 shadow of the first n16 parameters (flat spans only).
+ * zero_g: clear the gradient span once read (flat spans only).  Returns bit 0: shadow refreshed,
+ * bit 1: gradients cleared. */
+int adam_update_cuda_w16(Adam* adam, float lr, unsigned short* w16, long n16, int zero_g) {
     float bc1, bc2;
     bias_corrections(adam, &bc1, &bc2);
     nn_note_device_update(adam->weights[0]);          /* the network's host mirrors are now stale */
     if (adam->flat) {
         phip_adam_flat_w16(adam->weights[0], adam->grad_weights[0], adam->m, adam->v, adam->span, lr, adam->beta1,
-                           adam->beta2, bc1, bc2, adam->grad_scale, w16, w16 ? n16 : 0);
-        return w16 != NULL;
+                           adam->beta2, bc1, bc2, adam->grad_scale, w16, w16 ? n16 : 0, zero_g);
+        return (w16 != NULL) | (zero_g ? 2 : 0);
     } else {
         phip_adam_multi(adam->weights, adam->grad_weights, adam->lengths, adam->num_layers, adam->m, adam->v, lr,
                         adam->beta1, adam->beta2, bc1, bc2, adam->grad_scale);

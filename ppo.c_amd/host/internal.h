@@ -32,12 +32,6 @@ static inline long align4(long n) { return (n + 3) & ~3L; }
 
 /* fp32 GEMM engine used when PPO_F32_GEMM is unset (ppo_ext.h ppo_gemm_f32_engine): 1 = x3 */
 #define PPO_F32_ENGINE_DEFAULT 1
-/* bytes per element of activation / gradient caches and gathered-row workspaces: room for the x3
- * engine's pre-split storage (three bf16 planes) */
-#define X3_BYTES 6
-void nn_set_x3_planar(int on);                 /* pre-split storage inside ppo_update (neural_network.c) */
-int  nn_x3_planar(void);
-void nn_sync_w3(NeuralNetwork* nn);            /* refresh the x3 weight planes from d_params */
 int  ppo_gemm_f32_engine(int engine);
 /* linear-layer products of the reference API through the engine choice (neural_network.c) */
 void lin_fwd(float* y, const float* x, const float* W, const float* b, int m, int n, int l);
@@ -55,10 +49,8 @@ void nn_forward_dev(NeuralNetwork* nn, const float* d_x, int m);
 void nn_forward_dev_rows(NeuralNetwork* nn, const float* d_x, const int* d_rows, float* d_xcopy, int m);
 /* device backward from d_grad_out (no copy unless the output activation needs masking) */
 void nn_backward_dev(NeuralNetwork* nn, const float* d_grad_out, int m, int want_grad_x0);
-int  nn_out_fusable(const NeuralNetwork* nn, int m);
-void nn_out_fused_step(NeuralNetwork* nn, int head, const float* d_x, const int* d_rows, float* d_xcopy, int m,
-                       int extra, const float* tgt, const float* log_std, const float* action, const float* adv,
-                       const float* old_lp, float eps, float ent_coeff, float* grad_log_std, float* loss_accum);
+/* the same; grads_zero: d_grads already hold zeros (cleared by the previous Adam step), no memset */
+void nn_backward_dev_z(NeuralNetwork* nn, const float* d_grad_out, int m, int want_grad_x0, int grads_zero);
 
 NeuralNetwork* nn_load_ex(FILE* file, long extra_floats);
 /* host mirror <-> HBM reconciliation (neural_network.c) */
@@ -71,7 +63,7 @@ void nn_sync_w16(NeuralNetwork* nn);       /* bf16 mode: refresh the bf16 weight
 /* adam.c */
 void adam_next_step(Adam* a, float lr, float* step, float* bc2);
 /* device Adam that also writes the bf16 shadow w16[0, n16) in the same pass; returns 1 when it did */
-int adam_update_cuda_w16(Adam* adam, float lr, unsigned short* w16, long n16);
+int adam_update_cuda_w16(Adam* adam, float lr, unsigned short* w16, long n16, int zero_g);
 
 /* checkpoint Adam with a known tensor count (n_expected < 0: unknown); rejects mismatches */
 Adam* load_adam_ex(FILE* file, float** weights, float** grad_weights, int* length, int n_expected, bool cuda);

@@ -181,7 +181,7 @@ void nn_ensure_act(NeuralNetwork* nn, int m) {
     if (m <= nn->act_cap_m) return;
     for (int i = 0; i < nn->num_layers; i++) {
         phip_free(nn->layers[i].d_input);
-        nn->layers[i].d_input = (float*)phip_malloc(X3_BYTES * (size_t)m * nn->layers[i].input_size);
+        nn->layers[i].d_input = (float*)phip_malloc(sizeof(float) * (size_t)m * nn->layers[i].input_size);
     }
     phip_free(nn->d_act_bits);
     nn->d_act_bits = (unsigned*)phip_malloc(sizeof(unsigned) * (size_t)bits_words(nn, nn->num_layers, m));
@@ -193,7 +193,7 @@ void nn_ensure_grad(NeuralNetwork* nn, int m) {
     if (m <= nn->grad_cap_m) return;
     for (int i = 0; i < nn->num_layers; i++) {
         phip_free(nn->layers[i].d_grad_x);
-        nn->layers[i].d_grad_x = (float*)phip_malloc(X3_BYTES * (size_t)m * nn->layers[i].input_size);
+        nn->layers[i].d_grad_x = (float*)phip_malloc(sizeof(float) * (size_t)m * nn->layers[i].input_size);
     }
     nn->grad_cap_m = m;
 }
@@ -246,55 +246,19 @@ static int use_x3(int m) { return m > 1024 && ppo_gemm_f32_engine(-1) == 1; }
 /* per layer: the 1- and A-wide output layers are latency-bound skinny products where the exact
  * kernels (and their paired backward launch) measure faster (profiles/r01_x3_sweep.txt) */
 static int use_x3_layer(int m, int n, int l) { return use_x3(m) && n > 32 && l > 32; }
-/* gemm_x3.hip (default) or the round-1 x3 kernels of gemm16.hip (PPO_X3_V1=1, A/B runs) */
-static int x3v2(void) {
-    static int v = -1;
-    if (v < 0) v = getenv("PPO_X3_V1") ? 0 : 1;
-    return v;
-}
-
-/* Pre-split ("planar") storage inside ppo_update (nn_set_x3_planar): the x3 layers' weights are
- * read as three bf16 planes (nn->d_w3, refreshed at update start and by every Adam step), and an
- * activation or gradient that an x3 layer consumes is written by its producer as three bf16 planes
- * (6 B/element) — the split is done once, in the producer's epilogue, instead of in every tile that
- * loads it.  The planes sum to the fp32 value exactly, so results are bit-identical to fp32 storage.
- * Outside ppo_update (the reference API entry points) every buffer stays fp32. */
-static int g_x3_planar = 0;
-
-void nn_set_x3_planar(int on) { g_x3_planar = on; }
-int nn_x3_planar(void) { return g_x3_planar; }
-
-static phip_opnd opf(const void* p) { phip_opnd o = {(void*)p, 0, 0}; return o; }
-static phip_opnd oppl(const void* p, long stride) { phip_opnd o = {(void*)p, 1, stride}; return o; }
-
-/* plane stride of d_w3: a multiple of 8 elements keeps every plane's W tiles 16-B aligned */
-static long w3_stride(const NeuralNetwork* nn) { return (nn->num_params + 7) & ~7L; }
-
-void nn_sync_w3(NeuralNetwork* nn) {
-    if (!nn || nn->dtype != 0) return;
-    if (!nn->d_w3) nn->d_w3 = (unsigned short*)phip_malloc(sizeof(unsigned short) * 3 * (size_t)w3_stride(nn));
-    phip_split_x3(nn->d_w3, w3_stride(nn), nn->d_params, nn->num_params);
-}
-
 /* the reference-API products (mat_mul*_cuda, layers.c) through the same engine choice (fp32 storage) */
 void lin_fwd(float* y, const float* x, const float* W, const float* b, int m, int n, int l) {
-    if (use_x3(m) && x3v2() && phip_x3_supported(0, m, n, l)) phip_x3_fwd(y, x, NULL, NULL, W, b, m, n, l, 0, NULL);
-    else if (use_x3(m)) phip_linear_x3_fwd(opf(y), opf(x), NULL, NULL, opf(W), b, m, n, l, 0, NULL);
+    if (use_x3(m) && phip_x3_supported(0, m, n, l)) phip_x3_fwd(y, x, NULL, NULL, W, b, m, n, l, 0, NULL);
     else phip_linear_fwd(y, x, W, b, m, n, l, 0);
 }
 void lin_bwd_x(float* gx, const float* g, const float* W, int m, int n, int l) {
-    if (use_x3(m) && x3v2() && phip_x3_supported(1, m, n, l)) phip_x3_bwd_x(gx, g, W, NULL, m, n, l);
-    else if (use_x3(m)) phip_linear_x3_bwd_x(opf(gx), opf(g), opf(W), NULL, NULL, m, n, l);
+    if (use_x3(m) && phip_x3_supported(1, m, n, l)) phip_x3_bwd_x(gx, g, W, NULL, m, n, l);
     else phip_linear_bwd_x(gx, g, W, NULL, m, n, l);
 }
 void lin_bwd_w(float* gW, const float* g, const float* x, int m, int n, int l) {
-    if (use_x3(m) && x3v2() && phip_x3_supported(2, m, n, l)) phip_x3_bwd_w(gW, NULL, g, x, m, n, l, 0);
-    else if (use_x3(m)) phip_linear_x3_bwd_w(gW, NULL, opf(g), opf(x), m, n, l, 0);
+    if (use_x3(m) && phip_x3_supported(2, m, n, l)) phip_x3_bwd_w(gW, NULL, g, x, m, n, l, 0);
     else phip_linear_bwd_w(gW, NULL, g, x, m, n, l);
 }
-
-/* set by nn_out_fused_step: the forward stops before the output layer (run fused with the head) */
-static int g_skip_out = 0;
 
 void nn_forward_dev_rows(NeuralNetwork* nn, const float* d_x, const int* d_rows, float* d_xcopy, int m) {
     nn_ensure_act(nn, m);
@@ -308,43 +272,22 @@ void nn_forward_dev_rows(NeuralNetwork* nn, const float* d_x, const int* d_rows,
     }
     nn->d_x0 = d_rows ? d_xcopy : d_x;
     nn->x0_dtype = 0;
-    const int planar = g_x3_planar && nn->d_w3;
-    const int pl_act = planar && g_x3_planar != 2;        /* 2: weight planes only (experiment) */
-    unsigned pl_in = 0;                                   /* bit i: layer i's input is pre-split */
-    const void* in = d_x;
-    if (pl_act && d_rows && d_xcopy && use_x3_layer(m, nn->layers[0].input_size, nn->layers[0].output_size)) {
-        /* gather + split the minibatch rows once; layer 0's forward and grad_W read the planes */
-        phip_gather_rows_x3((unsigned short*)d_xcopy, d_x, d_rows, m, nn->layers[0].input_size);
-        in = d_xcopy;
-        d_rows = NULL;
-        pl_in = 1u;
-    }
-    for (int i = 0; i < L - g_skip_out; i++) {
+    const float* in = d_x;
+    for (int i = 0; i < L; i++) {
         Layer* ly = &nn->layers[i];
         float* out = nn->layers[i + 1].d_input;
         const int n = ly->input_size, l = ly->output_size;
-        if (use_x3_layer(m, n, l) && x3v2() && !planar && phip_x3_supported(0, m, n, l)) {
-            phip_x3_fwd(out, (const float*)in, i == 0 ? d_rows : NULL, i == 0 ? d_xcopy : NULL, ly->d_weights,
-                        ly->d_biases, m, n, l, nn_is_relu(nn, i), act_bits(nn, i + 1));
-        } else if (use_x3_layer(m, n, l)) {
-            /* the output is written pre-split when the next layer reads it through the x3 engine */
-            const int out_pl = pl_act && i + 1 < L && use_x3_layer(m, l, nn->layers[i + 1].output_size);
-            const phip_opnd x = (pl_in >> i) & 1u ? oppl(in, (long)m * n) : opf(in);
-            const phip_opnd W = planar ? oppl(nn->d_w3 + nn->param_offset[i], w3_stride(nn)) : opf(ly->d_weights);
-            phip_linear_x3_fwd(out_pl ? oppl(out, (long)m * l) : opf(out), x, i == 0 ? d_rows : NULL,
-                               i == 0 ? d_xcopy : NULL, W, ly->d_biases, m, n, l, nn_is_relu(nn, i),
-                               act_bits(nn, i + 1));
-            if (out_pl) pl_in |= 1u << (i + 1);
+        if (use_x3_layer(m, n, l) && phip_x3_supported(0, m, n, l)) {
+            phip_x3_fwd(out, in, i == 0 ? d_rows : NULL, i == 0 ? d_xcopy : NULL, ly->d_weights, ly->d_biases, m, n,
+                        l, nn_is_relu(nn, i), act_bits(nn, i + 1));
         } else if (i == 0 && d_rows) {
-            phip_linear_fwd_gather(out, (const float*)in, d_rows, d_xcopy, ly->d_weights, ly->d_biases, m, n, l,
-                                   nn_is_relu(nn, i), act_bits(nn, i + 1));
+            phip_linear_fwd_gather(out, in, d_rows, d_xcopy, ly->d_weights, ly->d_biases, m, n, l, nn_is_relu(nn, i),
+                                   act_bits(nn, i + 1));
         } else {
-            phip_linear_fwd_bits(out, (const float*)in, ly->d_weights, ly->d_biases, m, n, l, nn_is_relu(nn, i),
-                                 act_bits(nn, i + 1));
+            phip_linear_fwd_bits(out, in, ly->d_weights, ly->d_biases, m, n, l, nn_is_relu(nn, i), act_bits(nn, i + 1));
         }
         in = out;
     }
-    nn->x3_in_planes = (int)pl_in;
     nn->bits_m = m;
     nn->cache_m_forward = m;
     nn->d_output = nn->layers[L].d_input;
@@ -352,46 +295,11 @@ void nn_forward_dev_rows(NeuralNetwork* nn, const float* d_x, const int* d_rows,
 
 void nn_forward_dev(NeuralNetwork* nn, const float* d_x, int m) { nn_forward_dev_rows(nn, d_x, NULL, NULL, m); }
 
-/* The output layer runs fused with the loss head (out_head.hip) when: fp32 storage (no bf16 mode,
- * no pre-split planes), at least one hidden layer, identity output activation, a supported
- * (width, A), a minibatch past the small-M regime, and PPO_OUT_FUSED=1. */
-int nn_out_fusable(const NeuralNetwork* nn, int m) {
-    /* opt-in (PPO_OUT_FUSED=1, read per update): measured slower than the separate launches at C4 —
-     * the A = 17 kernel spills its 136 grad_W accumulators (profiles/r01_out_fused.txt) */
-    const char* e = getenv("PPO_OUT_FUSED");
-    const int env = e && e[0] == '1';
-    const int L = nn->num_layers - 1;
-    if (!env || nn->dtype != 0 || g_x3_planar || L < 2 || m <= 1024) return 0;
-    if (nn_is_relu(nn, L - 1) || !nn_is_relu(nn, L - 2)) return 0;
-    return phip_out_fused_supported(nn->layers[L - 1].input_size, nn->layers[L - 1].output_size);
-}
-
-/* One minibatch step's forward + head + backward with the output layer fused (nn_out_fusable):
- * hidden forward, one memset of the gradients (plus `extra` trailing floats: the policy's logσ
- * gradient), the fused output layer + head, then the hidden layers' backward.  Same results as
- * nn_forward_dev_rows → head kernel → nn_backward_dev up to fp32 re-association of the output
- * layer's dot products. */
-void nn_out_fused_step(NeuralNetwork* nn, int head, const float* d_x, const int* d_rows, float* d_xcopy, int m,
-                       int extra, const float* tgt, const float* log_std, const float* action, const float* adv,
-                       const float* old_lp, float eps, float ent_coeff, float* grad_log_std, float* loss_accum) {
-    const int L = nn->num_layers - 1;
-    g_skip_out = 1;
-    nn_forward_dev_rows(nn, d_x, d_rows, d_xcopy, m);
-    g_skip_out = 0;
-    nn_ensure_grad(nn, m);
-    phip_memset(nn->d_grads, 0, sizeof(float) * (size_t)(nn->num_params + extra));
-    Layer* ly = &nn->layers[L - 1];
-    const int n = ly->input_size, A = ly->output_size;
-    phip_out_fused(head, ly->d_input, act_bits(nn, L - 1), ly->d_weights, ly->d_biases, m, n, A, tgt, log_std, action,
-                   adv, old_lp, eps, ent_coeff, nn->layers[L].d_input, ly->d_grad_x, ly->d_grad_weights,
-                   ly->d_grad_biases, grad_log_std, loss_accum);
-    nn->d_output = nn->layers[L].d_input;
-    g_skip_out = 1;
-    nn_backward_dev(nn, NULL, m, 0);
-    g_skip_out = 0;
-}
-
 void nn_backward_dev(NeuralNetwork* nn, const float* d_grad_out, int m, int want_grad_x0) {
+    nn_backward_dev_z(nn, d_grad_out, m, want_grad_x0, 0);
+}
+
+void nn_backward_dev_z(NeuralNetwork* nn, const float* d_grad_out, int m, int want_grad_x0, int grads_zero) {
     nn_ensure_grad(nn, m);
     const int L = nn->num_layers - 1;
     const float* g = d_grad_out;
@@ -402,10 +310,8 @@ void nn_backward_dev(NeuralNetwork* nn, const float* d_grad_out, int m, int want
         g = top;
     }
     /* one memset for every layer's gradient (split-K grad_W accumulates atomically);
-     * the trailing extra_floats (policy log_std grad) are owned by the caller and left alone.
-     * nn_out_fused_step: the output layer's gradients and grad_x are already written, the memset
-     * came before them */
-    if (!g_skip_out) phip_memset(nn->d_grads, 0, sizeof(float) * (size_t)nn->num_params);
+     * the trailing extra_floats (policy log_std grad) are owned by the caller and left alone */
+    if (!grads_zero) phip_memset(nn->d_grads, 0, sizeof(float) * (size_t)nn->num_params);
     if (nn->dtype == 1) {      /* bf16 mode: hidden gradients stored bf16, the top one (heads) fp32 */
         if (nn->bits_m != m) die("nn_backward_dev (bf16): backward must follow a forward over the same rows");
         int tg = 0;
@@ -430,34 +336,17 @@ void nn_backward_dev(NeuralNetwork* nn, const float* d_grad_out, int m, int want
     /* grad_W and grad_x of a layer are independent: with the ReLU′ bits of this forward they go
      * out as one launch (phip_linear_bwd_pair: grad_x tiles fill the CUs grad_W tiles leave).
      * (measured: grad_W on a second queue beside grad_x was slower than back to back) */
-    const int planar = g_x3_planar && nn->d_w3;
-    int g_pl = 0;                                         /* g (gradient at layer i's output) pre-split */
-    if (g_skip_out) g = nn->layers[L - 1].d_grad_x;
-    for (int i = L - 1 - g_skip_out; i >= 0; i--) {
+    for (int i = L - 1; i >= 0; i--) {
         Layer* ly = &nn->layers[i];
         const float* x = i == 0 ? nn->d_x0 : ly->d_input;
         const int n = ly->input_size, l = ly->output_size;
         const int want_gx = i > 0 || want_grad_x0;
         const int relu_in = i > 0 && nn_is_relu(nn, i - 1);
         const unsigned* bits = relu_in && nn->bits_m == m ? act_bits(nn, i) : NULL;   /* this forward's bits */
-        int gx_pl = 0;
-        if (use_x3_layer(m, n, l) && x3v2() && !planar && !g_pl && phip_x3_supported(2, m, n, l) &&
-            !(nn->bits_m == m && ((nn->x3_in_planes >> i) & 1))) {
+        if (use_x3_layer(m, n, l) && phip_x3_supported(2, m, n, l)) {
             phip_x3_bwd_w(ly->d_grad_weights, ly->d_grad_biases, g, x, m, n, l, 1);
             if (want_gx && (!relu_in || bits)) phip_x3_bwd_x(ly->d_grad_x, g, ly->d_weights, bits, m, n, l);
             else if (want_gx) phip_linear_bwd_x_bits(ly->d_grad_x, g, ly->d_weights, ly->d_input, NULL, m, n, l);
-        } else if (use_x3_layer(m, n, l)) {
-            const phip_opnd go = g_pl ? oppl(g, (long)m * l) : opf(g);
-            const phip_opnd xo = nn->bits_m == m && ((nn->x3_in_planes >> i) & 1) ? oppl(x, (long)m * n) : opf(x);
-            phip_linear_x3_bwd_w(ly->d_grad_weights, ly->d_grad_biases, go, xo, m, n, l, 1);
-            if (want_gx && (!relu_in || bits)) {
-                gx_pl = planar && g_x3_planar != 2 && i > 0 && use_x3_layer(m, nn->layers[i - 1].input_size, n);
-                const phip_opnd W = planar ? oppl(nn->d_w3 + nn->param_offset[i], w3_stride(nn)) : opf(ly->d_weights);
-                phip_linear_x3_bwd_x(gx_pl ? oppl(ly->d_grad_x, (long)m * n) : opf(ly->d_grad_x), go, W, NULL, bits, m, n, l);
-            } else if (want_gx) {
-                if (g_pl || xo.planes) die("nn_backward_dev: pre-split operands without this forward's ReLU bits");
-                phip_linear_bwd_x_bits(ly->d_grad_x, g, ly->d_weights, ly->d_input, NULL, m, n, l);
-            }
         } else if (want_gx && (!relu_in || bits)) {
             phip_linear_bwd_pair(ly->d_grad_weights, ly->d_grad_biases, ly->d_grad_x, g, x, ly->d_weights, bits, m, n,
                                  l, 1);
@@ -467,7 +356,6 @@ void nn_backward_dev(NeuralNetwork* nn, const float* d_grad_out, int m, int want
                 phip_linear_bwd_x_bits(ly->d_grad_x, g, ly->d_weights, relu_in ? ly->d_input : NULL, NULL, m, n, l);
         }
         g = ly->d_grad_x;
-        g_pl = gx_pl;
     }
     nn->cache_m_backward = m;
 }
@@ -579,7 +467,6 @@ void free_neural_network(NeuralNetwork* nn) {
     }
     phip_free(nn->d_act_bits);
     phip_free(nn->d_w16);
-    phip_free(nn->d_w3);
     phip_free(nn->d_tiny_wt);
     phip_free(nn->d_params);
     phip_free(nn->d_grads);

@@ -95,8 +95,8 @@ static PPODev* dev_ws(PPO* ppo, int B) {
         phip_free(d->rows_p); phip_free(d->states_p);
         d->rows = (int*)phip_malloc(sizeof(int) * (size_t)B);
         d->rows_p = (int*)phip_malloc(sizeof(int) * (size_t)B);
-        d->states = (float*)phip_malloc(X3_BYTES * (size_t)B * S);
-        d->states_p = (float*)phip_malloc(X3_BYTES * (size_t)B * S);
+        d->states = (float*)phip_malloc(sizeof(float) * (size_t)B * S);
+        d->states_p = (float*)phip_malloc(sizeof(float) * (size_t)B * S);
         d->actions = (float*)phip_malloc(sizeof(float) * (size_t)B * A);
         d->old_lp = (float*)phip_malloc(sizeof(float) * (size_t)B);
         d->adv = (float*)phip_malloc(sizeof(float) * (size_t)B);
@@ -315,12 +315,14 @@ static int tiny_net(NeuralNetwork* nn, Adam* adam, PhipTinyNet* t) {
 }
 
 /* Adam step of a network's flat span; in bf16 mode the same pass refreshes the bf16 parameter
- * shadow when the span starts at the network's parameters, else a separate conversion does */
-static void adam_update_net(Adam* adam, float lr, NeuralNetwork* nn) {
-    const int fused = nn->dtype == 1 && adam->flat && adam->weights[0] == nn->d_params;
-    if (!adam_update_cuda_w16(adam, lr, fused ? nn->d_w16 : NULL, nn->num_params) && nn->dtype == 1)
-        nn_sync_w16(nn);
-    if (nn->dtype == 0 && nn->d_w3 && nn_x3_planar()) nn_sync_w3(nn);     /* x3 weight planes */
+ * shadow when the span starts at the network's parameters, else a separate conversion does.
+ * zero_grads: the same pass clears the gradients it read (the next backward skips its memset) */
+static int adam_update_net(Adam* adam, float lr, NeuralNetwork* nn, int zero_grads) {
+    const int own = adam->flat && adam->weights[0] == nn->d_params && adam->grad_weights[0] == nn->d_grads;
+    const int fused = nn->dtype == 1 && own;
+    const int r = adam_update_cuda_w16(adam, lr, fused ? nn->d_w16 : NULL, nn->num_params, zero_grads && own);
+    if (!(r & 1) && nn->dtype == 1) nn_sync_w16(nn);
+    return (r & 2) != 0;                 /* the network's gradients are zero again */
 }
 
 static float* tiny_steps(PPODev* d, int slot, Adam* adam, float lr, int n) {
@@ -399,53 +401,55 @@ static int ppo_update_tiny(PPO* ppo, PPODev* d, int B, int n_epochs_policy, int 
         pp.policy = 1;
         if (phip_tiny_update(&probe, &pp) != 0) return -1;
     }
-    if (n_epochs_value > 0 && num_batches > 0) {
-        ph.policy = 0;
-        ph.n_epochs = n_epochs_value;
-        ph.perms = tiny_perms(ppo, d, shuffle_mode, n_epochs_value, limit, &ph);
-        ph.steps = tiny_steps(d, 0, ppo->adam_V, ppo->lr_V, n_epochs_value * num_batches);
-        if (phip_tiny_update(&nv, &ph) != 0) die("ppo_update: tiny value phase failed to launch");
-        d->n_v += (long)n_epochs_value * num_batches;
+    /* both phases' permutations and Adam step tables first, in the reference's order (value
+     * epochs' shuffles, then the policy's); then the two single-workgroup phases run concurrently
+     * (value on libppo's stream, policy on the side stream: they share only read-only buffer
+     * arrays), each on its own CU.  PPO_SERIAL=1 runs them one after the other. */
+    PhipTinyPhase pv = ph, pp = ph;
+    const int run_v = n_epochs_value > 0 && num_batches > 0, run_p = n_epochs_policy > 0 && num_batches > 0;
+    if (run_v) {
+        pv.policy = 0;
+        pv.n_epochs = n_epochs_value;
+        pv.perms = tiny_perms(ppo, d, shuffle_mode, n_epochs_value, limit, &pv);
+        pv.steps = tiny_steps(d, 0, ppo->adam_V, ppo->lr_V, n_epochs_value * num_batches);
     } else if (n_epochs_value > 0) {
         for (int j = 0; j < n_epochs_value; j++) { uint64_t key; next_perm(ppo, d, shuffle_mode, &key); }
     }
-    if (n_epochs_policy > 0 && num_batches > 0) {
-        ph.policy = 1;
-        ph.n_epochs = n_epochs_policy;
-        ph.perms = tiny_perms(ppo, d, shuffle_mode, n_epochs_policy, limit, &ph);
+    if (run_p) {
+        pp.policy = 1;
+        pp.n_epochs = n_epochs_policy;
+        pp.perms = tiny_perms(ppo, d, shuffle_mode, n_epochs_policy, limit, &pp);
         /* per step the entropy Adam steps before the policy Adam (ppo.cu:440-442); their step
          * counters are independent, so the two sequences can be generated one after the other */
-        ph.steps_ls = tiny_steps(d, 1, ppo->adam_entropy, ppo->lr_policy, n_epochs_policy * num_batches);
-        ph.steps = tiny_steps(d, 2, ppo->adam_policy, ppo->lr_policy, n_epochs_policy * num_batches);
-        if (phip_tiny_update(&np, &ph) != 0) die("ppo_update: tiny policy phase failed to launch");
-        d->n_p += (long)n_epochs_policy * num_batches;
+        pp.steps_ls = tiny_steps(d, 1, ppo->adam_entropy, ppo->lr_policy, n_epochs_policy * num_batches);
+        pp.steps = tiny_steps(d, 2, ppo->adam_policy, ppo->lr_policy, n_epochs_policy * num_batches);
     } else if (n_epochs_policy > 0) {
         for (int j = 0; j < n_epochs_policy; j++) { uint64_t key; next_perm(ppo, d, shuffle_mode, &key); }
     }
+    const char* serial_env = getenv("PPO_SERIAL");
+    const int concurrent = run_v && run_p && !(serial_env && *serial_env && *serial_env != '0');
+    if (concurrent) phip_side_fork();
+    if (run_v) {
+        if (phip_tiny_update(&nv, &pv) != 0) die("ppo_update: tiny value phase failed to launch");
+        d->n_v += (long)n_epochs_value * num_batches;
+    }
+    if (run_p) {
+        if (concurrent) phip_side_use(1);
+        if (phip_tiny_update(&np, &pp) != 0) die("ppo_update: tiny policy phase failed to launch");
+        if (concurrent) phip_side_use(0);
+        d->n_p += (long)n_epochs_policy * num_batches;
+    }
+    if (concurrent) phip_side_join();
     return 0;
 }
 
 static void ppo_update_body(PPO* ppo, float gamma, int batch_size, int n_epochs_policy, int n_epochs_value,
                             int shuffle_mode, unsigned long long seed);
 
-/* The x3 engine's pre-split storage (neural_network.c) applies for the duration of an update when
- * PPO_X3_PLANAR=1 (weights, activations, gradients and gathered rows as three bf16 planes) or 2
- * (weight planes only): weight planes refreshed here and after every Adam step.  Off by default:
- * measured slower at C4 (update 409 -> 442 ms with 1, -> 414 ms with 2; the planes are 1.5x the
- * fp32 bytes and the split it saves is not what bounds the x3 GEMM — DESIGN.md §4). */
 void ppo_update(void* vppo, float gamma, int batch_size, int n_epochs_policy, int n_epochs_value, int shuffle_mode,
                 unsigned long long seed) {
     PPO* ppo = (PPO*)vppo;
-    const char* e = getenv("PPO_X3_PLANAR");
-    const int mode = e && (*e == '1' || *e == '2') ? *e - '0' : 0;
-    const int planar = mode && ppo->V->dtype == 0 && ppo_gemm_f32_engine(-1) == 1;
-    if (planar) {
-        nn_sync_w3(ppo->V);
-        nn_sync_w3(ppo->policy->mu);
-    }
-    nn_set_x3_planar(planar ? mode : 0);
     ppo_update_body(ppo, gamma, batch_size, n_epochs_policy, n_epochs_value, shuffle_mode, seed);
-    nn_set_x3_planar(0);
     ppo->V->dev_version++;               /* HBM parameters moved (also by the single-workgroup path) */
     ppo->policy->mu->dev_version++;
 }
@@ -501,8 +505,10 @@ static void ppo_update_body(PPO* ppo, float gamma, int batch_size, int n_epochs_
     const char* serial_env = getenv("PPO_SERIAL");
     const int concurrent = nv > 0 && np > 0 && !(serial_env && *serial_env && *serial_env != '0');
     if (concurrent) phip_side_fork();
-    const int fuse_v = nn_out_fusable(V, B), fuse_p = nn_out_fusable(mu, B);
     long iv = 0, ip = 0;
+    /* gradients cleared by the previous Adam step (not after a loop's last step: a caller may read
+     * the last minibatch's gradients after the update) */
+    int v_zero = 0, p_zero = 0;
     while (iv < nv || ip < np) {
         /* serial: every value step first (the reference's order); concurrent: issue in proportion */
         const int take_v = iv < nv && (ip >= np || !concurrent || iv * np <= ip * nv);
@@ -513,16 +519,11 @@ static void ppo_update_body(PPO* ppo, float gamma, int batch_size, int n_epochs_
              * reads the buffer rows through them and leaves the gathered copy for its grad_W */
             phip_gather_rows(perm, keys_v[j], k * B, limit, B, S, A, buf->state_p, buf->action_p, buf->logprob_p,
                              buf->advantage_p, buf->adv_target_p, NULL, NULL, NULL, NULL, d->tgt, d->rows);
-            if (fuse_v) {       /* output layer + MSE head in one pass (out_head.hip) */
-                nn_out_fused_step(V, 0, buf->state_p, d->rows, d->states, B, 0, d->tgt, NULL, NULL, NULL, NULL, 0.f,
-                                  0.f, NULL, d->stats + 0);
-            } else {
-                nn_forward_dev_rows(V, buf->state_p, d->rows, d->states, B);
-                phip_mse(V->d_output, d->tgt, B, d->gv, NULL, d->stats + 0);
-                nn_backward_dev(V, d->gv, B, 0);
-            }
+            nn_forward_dev_rows(V, buf->state_p, d->rows, d->states, B);
+            phip_mse(V->d_output, d->tgt, B, d->gv, NULL, d->stats + 0);
+            nn_backward_dev_z(V, d->gv, B, 0, v_zero);
             phip_allreduce_sum_f32(V->d_grads, V->num_params);
-            adam_update_net(ppo->adam_V, ppo->lr_V, V);
+            v_zero = adam_update_net(ppo->adam_V, ppo->lr_V, V, iv + 1 < nv);
             d->n_v++;
             iv++;
         } else {
@@ -532,19 +533,13 @@ static void ppo_update_body(PPO* ppo, float gamma, int batch_size, int n_epochs_
             phip_gather_rows(perm, keys_p[j], k * B, limit, B, S, A, buf->state_p, buf->action_p, buf->logprob_p,
                              buf->advantage_p, buf->adv_target_p, NULL, d->actions, d->old_lp, d->adv, NULL,
                              d->rows_p);
-            if (fuse_p) {       /* output layer + clipped-surrogate head in one pass (out_head.hip) */
-                nn_out_fused_step(mu, 1, buf->state_p, d->rows_p, d->states_p, B, A, NULL, pol->d_log_std,
-                                  d->actions, d->adv, d->old_lp, ppo->epsilon, ppo->ent_coeff, pol->d_log_std_grad,
-                                  d->stats + 1);
-            } else {
-                nn_forward_dev_rows(mu, buf->state_p, d->rows_p, d->states_p, B);
-                phip_policy_head(mu->d_output, pol->d_log_std, d->actions, d->adv, d->old_lp, B, A, ppo->epsilon,
-                                 ppo->ent_coeff, d->gmu, pol->d_log_std_grad, d->stats + 1);
-                nn_backward_dev(mu, d->gmu, B, 0);
-            }
+            nn_forward_dev_rows(mu, buf->state_p, d->rows_p, d->states_p, B);
+            phip_policy_head(mu->d_output, pol->d_log_std, d->actions, d->adv, d->old_lp, B, A, ppo->epsilon,
+                             ppo->ent_coeff, d->gmu, pol->d_log_std_grad, d->stats + 1);
+            nn_backward_dev_z(mu, d->gmu, B, 0, p_zero);
             phip_allreduce_sum_f32(mu->d_grads, mu->num_params + align4(A));   /* μ grads + log_std grad */
             adam_update_cuda(ppo->adam_entropy, ppo->lr_policy);               /* ppo.cu:440-442 order */
-            adam_update_net(ppo->adam_policy, ppo->lr_policy, mu);
+            p_zero = adam_update_net(ppo->adam_policy, ppo->lr_policy, mu, ip + 1 < np);
             if (concurrent) phip_side_use(0);
             d->n_p++;
             ip++;

@@ -41,8 +41,8 @@ class NeuralNetwork(C.Structure):
                 ("act_cap_m", C.c_int), ("grad_cap_m", C.c_int), ("host_cap_m", C.c_int),
                 ("extra_floats", C.c_long), ("d_x0", c_float_p), ("d_act_bits", C.POINTER(C.c_uint)),
                 ("bits_m", C.c_int), ("dtype", C.c_int), ("x0_dtype", C.c_int), ("d_w16", C.c_void_p),
-                ("d_tiny_wt", c_float_p), ("tiny_wt_cap", C.c_long), ("d_w3", C.c_void_p),
-                ("x3_in_planes", C.c_int), ("h_sync", c_float_p), ("dev_version", C.c_long),
+                ("d_tiny_wt", c_float_p), ("tiny_wt_cap", C.c_long),
+                ("h_sync", c_float_p), ("dev_version", C.c_long),
                 ("host_version", C.c_long)]
 
 

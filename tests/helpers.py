@@ -39,11 +39,7 @@ def gpu_relu_masks(lib, nn_ptr, x_rows):
     m, cap = nn.bits_m, nn.act_cap_m
     if m != x_rows.shape[0] or not nn.d_x0 or not nn.d_act_bits:
         return None          # the last forward was not this one (e.g. the single-workgroup path)
-    if nn.x3_in_planes & 1:           # x3 engine: the gathered rows as three bf16 planes (exact sum)
-        pl = ppo_ffi.d2h(lib, nn.d_x0, np.uint16, 3 * m * sizes[0]).astype(np.uint32) << 16
-        x0 = pl.view(np.float32).reshape(3, m, sizes[0]).astype(np.float64).sum(0).astype(F32)
-    else:
-        x0 = ppo_ffi.d2h(lib, nn.d_x0, F32, m * sizes[0]).reshape(m, sizes[0])
+    x0 = ppo_ffi.d2h(lib, nn.d_x0, F32, m * sizes[0]).reshape(m, sizes[0])
     where = {r.tobytes(): i for i, r in enumerate(np.ascontiguousarray(x_rows, F32))}
     order = np.array([where[r.tobytes()] for r in x0])      # forward row j = reference row order[j]
     total = sum(cap * ((s + 31) // 32) for s in sizes)

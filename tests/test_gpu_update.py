@@ -28,7 +28,7 @@ CONFIGS = {
     "halfcheetah": dict(sizes=[17, 256, 256, 6], N=1024),
     "humanoid": dict(sizes=[376, 512, 512, 512, 17], N=2048),
     # B = N > 1024: x3 GEMM engine at width 256, A = 6 (and the opt-in fused output layer below)
-    "halfcheetah_fused": dict(sizes=[17, 256, 256, 6], N=2048),
+    "halfcheetah_2k": dict(sizes=[17, 256, 256, 6], N=2048),
 }
 
 
@@ -429,34 +429,3 @@ def test_degenerate_updates(lib, oracle):
     oracle.srand(8)
     assert r == oracle.libc().rand()
     lib.free_ppo(ppo)
-
-
-@pytest.mark.parametrize("cfg", ["humanoid", "halfcheetah_fused"])
-def test_out_fused_matches_unfused(lib, oracle, cfg, monkeypatch):
-    """The fused output layer + loss head (out_head.hip) against the separate launches
-    (PPO_OUT_FUSED=0) from identical state: one value and one policy minibatch, every gradient within
-    the GEMM tolerance, the log σ-gradient and the loss sums within reduction rounding."""
-    sizes, N = CONFIGS[cfg]["sizes"], CONFIGS[cfg]["N"]
-    A = sizes[-1]
-    out = {}
-    for mode in ("0", "1"):
-        monkeypatch.setenv("PPO_OUT_FUSED", mode)
-        ppo = make_ppo(lib, oracle, sizes, N, init_std=0.7, ent_coeff=0.01)
-        mu0, ls0 = policy_state(lib, ppo)
-        buf = synthetic_buffer(oracle, sizes, mu0, ls0, N, seed=21)
-        buf["logprob"] = (buf["logprob"] + np.random.default_rng(5).normal(scale=0.4, size=N)).astype(F32)
-        load_buffer(lib, ppo, buf)
-        lib.ppo_reset_stats(ppo)
-        lib.ppo_update(ppo, 0.99, N, 1, 1, 1, 13)
-        lib.ppo_synchronize()
-        st = (C.c_double * 7)()
-        lib.ppo_read_stats(ppo, st, 7)
-        pol = ppo.contents.policy.contents
-        out[mode] = dict(gV=nn_grads_packed(lib, ppo.contents.V), gmu=nn_grads_packed(lib, pol.mu),
-                         gls=ppo_ffi.d2h(lib, pol.d_log_std_grad, F32, A), stats=np.array(st[:4]))
-        lib.free_ppo(ppo)
-    a, b = out["0"], out["1"]
-    assert_gemm_close(b["gV"], a["gV"], N, f"{cfg} value grads (fused vs separate)")
-    assert_gemm_close(b["gmu"], a["gmu"], N, f"{cfg} policy grads (fused vs separate)")
-    assert_rel_close(b["gls"], a["gls"], 1e-3, 1e-4 * max(1.0, np.abs(a["gls"]).max()), "log_std grad")
-    np.testing.assert_allclose(b["stats"], a["stats"], rtol=1e-3, atol=1e-6)
