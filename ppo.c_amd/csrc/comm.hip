@@ -139,6 +139,7 @@ void ppo_comm_finalize(void) {
 }
 
 int phip_comm_world(void) { return g_world; }
+int phip_comm_active(void) { return g_comm != nullptr || g_loopback > 1; }
 int phip_comm_rank(void) { return g_rank; }
 
 void phip_allreduce_sum_f32(float* d_buf, long n) {
@@ -160,6 +161,37 @@ void phip_allreduce_sum_f32(float* d_buf, long n) {
 }
 
 void ppo_comm_allreduce_f32(float* d_buf, long n) { phip_allreduce_sum_f32(d_buf, n); }
+
+// Gradient buckets: the collective is queued on the comm stream behind the issuing stream's work
+// so far (a layer's grad_W), but the issuing stream does not wait for it — the backward of the
+// layers below runs while it travels; phip_allreduce_join() makes the issuing stream wait for
+// every collective queued so far (the comm stream runs them in order: waiting for the last one
+// suffices).
+static int g_pending = -1;
+
+void phip_allreduce_sum_f32_async(float* d_buf, long n) {
+    if ((!g_comm && !g_loopback) || n <= 0) return;
+    ppo::ProfScope ps(PPO_K_COMM, 4.0 * n);
+    int slot;
+    hipStream_t cs = comm_enter(&slot);
+    if (g_loopback) {
+        int grid = ppo_divup(n, 256);
+        if (grid > 2048) grid = 2048;
+        hipLaunchKernelGGL(scale_kernel, dim3(grid), dim3(256), 0, cs, d_buf, n, (float)g_loopback);
+        PPO_LAUNCH_CHECK();
+    } else {
+        nccl_check(ncclAllReduce(d_buf, d_buf, (size_t)n, ncclFloat32, ncclSum, g_comm, cs), "ncclAllReduce",
+                   __LINE__);
+    }
+    PPO_CHECK(hipEventRecord(g_done[slot], g_comm_stream));
+    g_pending = slot;
+}
+
+void phip_allreduce_join(void) {
+    if (g_pending < 0) return;
+    PPO_CHECK(hipStreamWaitEvent(ppo::stream(), g_done[g_pending], 0));
+    g_pending = -1;
+}
 
 void phip_allgather_f64(const double* d_send, double* d_recv, long n_per_rank) {
     if (!g_comm && !g_loopback) {

@@ -570,9 +570,11 @@ void launch_x3(X3Args a) {
 
 // tile configurations: 0 = 256×256 over 8 waves of 64×128 (forward, grad_x; one workgroup per CU),
 // 1 = 128×128 over 4 waves of 64×64, two workgroups per CU (narrow products), 2 = 128×128 over 8
-// waves of 32×64, 3 = 128×128 over two k-groups of 4 waves of 64×64, one workgroup per CU (grad_W)
+// waves of 32×64, 3 = 128×128 over two k-groups of 4 waves of 64×64, one workgroup per CU (grad_W),
+// 4 = 64×64 over 4 waves of 32×32, four workgroups per CU (small outputs: C3's 8192×256 minibatch
+// products have 32 tiles of 256×256 — an eighth of the CUs — but 512 of 64×64)
 struct CfgX3 { int bm, bn, kg, slots_per_cu; };
-constexpr CfgX3 kCfgX3[] = {{256, 256, 1, 1}, {128, 128, 1, 2}, {128, 128, 1, 1}, {128, 128, 2, 1}};
+constexpr CfgX3 kCfgX3[] = {{256, 256, 1, 1}, {128, 128, 1, 2}, {128, 128, 1, 1}, {128, 128, 2, 1}, {64, 64, 1, 4}};
 int g_force_x3 = -1;
 int g_split_x3 = 0;
 
@@ -603,6 +605,7 @@ void launch_cfg_x3(int c, const X3Args& a) {
     switch (c) {
         case 0: launch_x3<OP, 256, 256, 4, 512, 2, 1>(a); break;
         case 2: launch_x3<OP, 128, 128, 4, 512, 2, 1>(a); break;
+        case 4: launch_x3<OP, 64, 64, 2, 256, 4, 1>(a); break;
         case 3:
             if constexpr (OP == OP_TN) { launch_x3<OP, 128, 128, 2, 512, 2, 2>(a); break; }
             [[fallthrough]];
@@ -610,11 +613,15 @@ void launch_cfg_x3(int c, const X3Args& a) {
     }
 }
 
+// forward / grad_x: the largest tile whose grid still gives every CU a workgroup (one round of
+// 256×256 tiles, else 128×128 at two per CU, else 64×64)
 int pick_x3(int M, int N, int op) {
     if (g_force_x3 >= 0) return g_force_x3;
     if (op == OP_TN) return 3;
-    if (M >= 4096 && N >= 256) return 0;
-    return 1;
+    auto tiles = [&](int c) { return (long)ppo_divup(M, kCfgX3[c].bm) * ppo_divup(N, kCfgX3[c].bn); };
+    if (tiles(0) >= 256) return 0;
+    if (tiles(1) >= 256) return 1;
+    return 4;
 }
 
 inline bool al16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
@@ -673,7 +680,9 @@ void phip_x3_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, 
     const int c = pick_x3(l, n, OP_TN);
     const long tiles = (long)ppo_divup(l, kCfgX3[c].bm) * ppo_divup(n, kCfgX3[c].bn);
     // split-K over the batch: the grid stays within one round of workgroup slots (256 CUs × the
-    // configuration's workgroups per CU), each split ≥ 8 k-tiles per k-group
+    // configuration's workgroups per CU), each split ≥ 8 k-tiles per k-group.  (64×64 tiles for
+    // C3's 256×256 gradient measured 23.5 -> 20.7 µs but sum each output over longer fp32 chains:
+    // not adopted)
     const int kq = BK * kCfgX3[c].kg;                       // a split's k range: whole k-tiles per group
     const int target = g_split_x3 > 0 ? g_split_x3 : 256 * kCfgX3[c].slots_per_cu;
     int splits = (int)(target / tiles);

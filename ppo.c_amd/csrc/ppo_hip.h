@@ -201,7 +201,13 @@ void phip_link_next_state(float* next_state, const float* state, const uint8_t* 
 int  phip_comm_world(void);
 int  phip_comm_rank(void);
 int  phip_comm_min_i32(int v);      /* min over ranks (synchronous); identity at world 1 */
+/* a communicator is up (world > 1, the PPO_COMM_SELF one-rank rehearsal, or the loopback) */
+int  phip_comm_active(void);
 void phip_allreduce_sum_f32(float* d_buf, long n);
+/* gradient bucket: queued behind the issuing stream's work, which does not wait for it;
+ * phip_allreduce_join() makes the issuing stream wait for every bucket queued so far */
+void phip_allreduce_sum_f32_async(float* d_buf, long n);
+void phip_allreduce_join(void);
 void phip_allgather_f64(const double* d_send, double* d_recv, long n_per_rank);
 
 /* ---------------- profiling ---------------- */

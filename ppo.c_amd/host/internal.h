@@ -49,8 +49,12 @@ void nn_forward_dev(NeuralNetwork* nn, const float* d_x, int m);
 void nn_forward_dev_rows(NeuralNetwork* nn, const float* d_x, const int* d_rows, float* d_xcopy, int m);
 /* device backward from d_grad_out (no copy unless the output activation needs masking) */
 void nn_backward_dev(NeuralNetwork* nn, const float* d_grad_out, int m, int want_grad_x0);
-/* the same; grads_zero: d_grads already hold zeros (cleared by the previous Adam step), no memset */
-void nn_backward_dev_z(NeuralNetwork* nn, const float* d_grad_out, int m, int want_grad_x0, int grads_zero);
+/* the same; grads_zero: d_grads already hold zeros (cleared by the previous Adam step), no memset;
+ * reduce_extra ≥ 0 (data parallelism): the gradients are all-reduced in buckets of consecutive
+ * layers as the backward finishes them (top bucket: also the reduce_extra floats after the
+ * network's parameters — the policy's log σ gradient); the caller joins before Adam */
+void nn_backward_dev_z(NeuralNetwork* nn, const float* d_grad_out, int m, int want_grad_x0, int grads_zero,
+                       long reduce_extra);
 
 NeuralNetwork* nn_load_ex(FILE* file, long extra_floats);
 /* host mirror <-> HBM reconciliation (neural_network.c) */

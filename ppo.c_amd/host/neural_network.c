@@ -295,11 +295,24 @@ void nn_forward_dev_rows(NeuralNetwork* nn, const float* d_x, const int* d_rows,
 
 void nn_forward_dev(NeuralNetwork* nn, const float* d_x, int m) { nn_forward_dev_rows(nn, d_x, NULL, NULL, m); }
 
-void nn_backward_dev(NeuralNetwork* nn, const float* d_grad_out, int m, int want_grad_x0) {
-    nn_backward_dev_z(nn, d_grad_out, m, want_grad_x0, 0);
+/* gradient buckets (nn_backward_dev_z): ≥ 1 MiB of consecutive layers per all-reduce */
+#define GRAD_BUCKET_FLOATS (256L * 1024)
+
+/* layer i's gradients are queued: all-reduce [param_offset[i], *hi) once it holds a bucket's worth,
+ * or at the bottom layer (the flat layout [W0, b0, W1, b1, …] makes every bucket one span) */
+static void bucket_flush(NeuralNetwork* nn, int i, long* hi) {
+    const long lo = nn->param_offset[i];
+    if (i > 0 && *hi - lo < GRAD_BUCKET_FLOATS) return;
+    phip_allreduce_sum_f32_async(nn->d_grads + lo, *hi - lo);
+    *hi = lo;
 }
 
-void nn_backward_dev_z(NeuralNetwork* nn, const float* d_grad_out, int m, int want_grad_x0, int grads_zero) {
+void nn_backward_dev(NeuralNetwork* nn, const float* d_grad_out, int m, int want_grad_x0) {
+    nn_backward_dev_z(nn, d_grad_out, m, want_grad_x0, 0, -1);
+}
+
+void nn_backward_dev_z(NeuralNetwork* nn, const float* d_grad_out, int m, int want_grad_x0, int grads_zero,
+                       long reduce_extra) {
     nn_ensure_grad(nn, m);
     const int L = nn->num_layers - 1;
     const float* g = d_grad_out;
@@ -315,6 +328,7 @@ void nn_backward_dev_z(NeuralNetwork* nn, const float* d_grad_out, int m, int wa
     if (nn->dtype == 1) {      /* bf16 mode: hidden gradients stored bf16, the top one (heads) fp32 */
         if (nn->bits_m != m) die("nn_backward_dev (bf16): backward must follow a forward over the same rows");
         int tg = 0;
+        long hi = nn->num_params + (reduce_extra > 0 ? reduce_extra : 0);
         for (int i = L - 1; i >= 0; i--) {
             Layer* ly = &nn->layers[i];
             const void* x = i == 0 ? (const void*)nn->d_x0 : (const void*)ly->d_input;
@@ -329,6 +343,7 @@ void nn_backward_dev_z(NeuralNetwork* nn, const float* d_grad_out, int m, int wa
             }
             g = ly->d_grad_x;
             tg = tgx;
+            if (reduce_extra >= 0) bucket_flush(nn, i, &hi);
         }
         nn->cache_m_backward = m;
         return;
@@ -336,6 +351,7 @@ void nn_backward_dev_z(NeuralNetwork* nn, const float* d_grad_out, int m, int wa
     /* grad_W and grad_x of a layer are independent: with the ReLU′ bits of this forward they go
      * out as one launch (phip_linear_bwd_pair: grad_x tiles fill the CUs grad_W tiles leave).
      * (measured: grad_W on a second queue beside grad_x was slower than back to back) */
+    long hi = nn->num_params + (reduce_extra > 0 ? reduce_extra : 0);
     for (int i = L - 1; i >= 0; i--) {
         Layer* ly = &nn->layers[i];
         const float* x = i == 0 ? nn->d_x0 : ly->d_input;
@@ -356,6 +372,7 @@ void nn_backward_dev_z(NeuralNetwork* nn, const float* d_grad_out, int m, int wa
                 phip_linear_bwd_x_bits(ly->d_grad_x, g, ly->d_weights, relu_in ? ly->d_input : NULL, NULL, m, n, l);
         }
         g = ly->d_grad_x;
+        if (reduce_extra >= 0) bucket_flush(nn, i, &hi);
     }
     nn->cache_m_backward = m;
 }

@@ -470,6 +470,7 @@ static void ppo_update_body(PPO* ppo, float gamma, int batch_size, int n_epochs_
     const int num_batches = buf->capacity / B;                           /* D13 */
     const int world = phip_comm_world();
     const float gscale = 1.0f / (float)world;
+    const int comm = phip_comm_active();
     ppo->adam_V->grad_scale = gscale;
     ppo->adam_policy->grad_scale = gscale;
     ppo->adam_entropy->grad_scale = gscale;
@@ -521,8 +522,10 @@ static void ppo_update_body(PPO* ppo, float gamma, int batch_size, int n_epochs_
                              buf->advantage_p, buf->adv_target_p, NULL, NULL, NULL, NULL, d->tgt, d->rows);
             nn_forward_dev_rows(V, buf->state_p, d->rows, d->states, B);
             phip_mse(V->d_output, d->tgt, B, d->gv, NULL, d->stats + 0);
-            nn_backward_dev_z(V, d->gv, B, 0, v_zero);
-            phip_allreduce_sum_f32(V->d_grads, V->num_params);
+            /* with a communicator: gradients all-reduced in per-layer buckets as the backward
+             * produces them (comm.hip's comm stream), joined before Adam */
+            nn_backward_dev_z(V, d->gv, B, 0, v_zero, comm ? 0 : -1);
+            phip_allreduce_join();
             v_zero = adam_update_net(ppo->adam_V, ppo->lr_V, V, iv + 1 < nv);
             d->n_v++;
             iv++;
@@ -536,8 +539,9 @@ static void ppo_update_body(PPO* ppo, float gamma, int batch_size, int n_epochs_
             nn_forward_dev_rows(mu, buf->state_p, d->rows_p, d->states_p, B);
             phip_policy_head(mu->d_output, pol->d_log_std, d->actions, d->adv, d->old_lp, B, A, ppo->epsilon,
                              ppo->ent_coeff, d->gmu, pol->d_log_std_grad, d->stats + 1);
-            nn_backward_dev_z(mu, d->gmu, B, 0, p_zero);
-            phip_allreduce_sum_f32(mu->d_grads, mu->num_params + align4(A));   /* μ grads + log_std grad */
+            /* μ grads + (top bucket) the log σ gradient behind them */
+            nn_backward_dev_z(mu, d->gmu, B, 0, p_zero, comm ? align4(A) : -1);
+            phip_allreduce_join();
             adam_update_cuda(ppo->adam_entropy, ppo->lr_policy);               /* ppo.cu:440-442 order */
             p_zero = adam_update_net(ppo->adam_policy, ppo->lr_policy, mu, ip + 1 < np);
             if (concurrent) phip_side_use(0);

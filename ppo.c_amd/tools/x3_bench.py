@@ -21,13 +21,17 @@ def main():
     ap.add_argument("--cfgs", default="-1")
     ap.add_argument("--splits", default="0")
     ap.add_argument("--iters", type=int, default=30)
+    ap.add_argument("--shapes", default="", help="op,m,n,l;... (default: the C4/C3 list)")
     args = ap.parse_args()
+    shapes = [tuple(map(int, t.split(","))) for t in args.shapes.split(";")] if args.shapes else SHAPES
     lib = ppo_ffi.load()
     lib.ppo_set_device(0)
-    for op, m, n, l in SHAPES:
+    for op, m, n, l in shapes:
         for c in map(int, args.cfgs.split(",")):
             for s in map(int, args.splits.split(",")):
                 if op != 2 and s:
+                    continue
+                if c >= 0 and op == 2 and c not in (1, 3, 4):
                     continue
                 us = lib.ppo_bench_gemm_x3(op, m, n, l, args.iters if m < 1 << 20 else 5, c, s)
                 tf = 2.0 * m * n * l / (us * 1e-6) / 1e12

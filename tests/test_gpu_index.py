@@ -232,13 +232,15 @@ def test_c4_timed_policy_step(lib, oracle, c4):
 
 
 # ----------------------------------------------------------------------------- world > 1 on one GPU
-@pytest.mark.parametrize("k", [2, 4])
-def test_loopback_ranks_reproduce_one_gpu(lib, oracle, monkeypatch, k):
+@pytest.mark.parametrize("k,net", [(2, "c3"), (4, "c3"), (2, "c4")])
+def test_loopback_ranks_reproduce_one_gpu(lib, oracle, monkeypatch, k, net):
     """PPO_COMM_LOOPBACK=k: every world > 1 branch (grad_scale = 1/k, all-gather of Welford triples +
-    Chan combine, empty-shard agreement, comm stream) over k identical shards.  k = 2: the value
-    network and advantage statistics equal the one-GPU update bit for bit (split-K off); k = 4 within
-    the rounding of the 3-fold M2 sum; the policy within the log σ-gradient atomics bound."""
-    sizes, N, B = [17, 256, 256, 6], 4096, 512
+    Chan combine, empty-shard agreement, comm stream, per-layer gradient buckets) over k identical
+    shards.  k = 2: the value network and advantage statistics equal the one-GPU update bit for bit
+    (split-K off); k = 4 within the rounding of the 3-fold M2 sum; the policy within the log
+    σ-gradient atomics bound.  The C4-shaped networks (≈ 718 k parameters) are all-reduced in three
+    buckets per step (top two layers, layer 1, layer 0), the C3 ones in one."""
+    sizes, N, B = {"c3": ([17, 256, 256, 6], 4096, 512), "c4": ([376, 512, 512, 512, 17], 2048, 1024)}[net]
     lib.ppo_gemm_tune(-1, 1)
     out = {}
     try:
