@@ -100,9 +100,9 @@ def pmc_traffic():
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_gemm.json")))
     if not files:
-        return None, None
+        return {}, None
     d = json.load(open(files[-1]))
-    return d.get("hbm_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
+    return d, os.path.relpath(files[-1], ROOT)
 
 
 def cpu_baseline(lib, ppo, S, H, A, N, B, sample_envs=16, steps=2):
@@ -185,6 +185,8 @@ def main():
     ap.add_argument("--no-kernel-events", action="store_true")
     ap.add_argument("--gemm-flags", type=int, default=0, help="ppo_gemm_flags experiment bits (A/B runs)")
     ap.add_argument("--no-rollout", action="store_true", help="skip the rollout env-steps/s measurement")
+    ap.add_argument("--step-limit", default="", help="V,P: cap each update at V value and P policy minibatch steps "
+                    "(profiling passes only: a bounded sample of the same launches; the line is then not the metric)")
     ap.add_argument("--event-stride", type=int, default=7,
                     help="HIP events around every k-th launch of each kernel class (1 = all; each event pair "
                          "costs a few µs of stream time, so the throughput run samples)")
@@ -242,6 +244,9 @@ def main():
     if LIB.ppo_set_compute_dtype(ppo, 1 if dtype == "bf16" else 0) != 0:
         raise SystemExit("ppo_set_compute_dtype failed")
     LIB.ppo_fill_synthetic(ppo, E, T, args.seed * 1000 + rank, 1.0 / 500)
+    if args.step_limit:
+        lv, lp = (int(v) for v in args.step_limit.split(","))
+        LIB.ppo_set_step_limit(ppo, lv, lp)
     LIB.ppo_synchronize()
 
     def barrier():
@@ -374,22 +379,34 @@ def main():
     if serial and serial[2][0] and serial[0][0] > 0:
         s_ms, s_work, s_launches = serial[0][0], serial[1][0], serial[2][0]
         achieved = s_work / (s_ms * 1e-3) / 1e12
-        traffic, traffic_src = pmc_traffic() if args.config == "c4" else (None, None)   # PMC pass is of c4
+        pmc, traffic_src = pmc_traffic() if args.config == "c4" else ({}, None)   # PMC passes are of c4
+        traffic = pmc.get("hbm_bytes_per_launch")
+        dom = dict(shapes[0]) if shapes else None
+        if dom:
+            dom["frac"] = dom["tflops"] / peak
+            m_, n_, l_ = dom["m"], dom["n"], dom["l"]
+            # operands read once, output written once (fp32; grad_W: + its bias-gradient vector)
+            dom["algorithmic_bytes"] = 4 * (m_ * n_ + n_ * l_ + m_ * l_ + (l_ if dom["op"] == "grad_W" else 0))
+            pd = pmc.get("dominant") or {}
+            code = {"forward": "0", "grad_x": "1", "grad_W": "2"}.get(dom["op"])
+            if pd.get("kernel", "").startswith(f"gemm<{code},") and dom.get("engine") == "x3":
+                dom["traffic"] = pd.get("hbm_bytes_per_launch")
+                dom["traffic_kernel"] = pd.get("kernel")
         # lower bound of the GEMM class rate in the timed (concurrent) region: every GEMM launch's
         # algorithmic FLOPs over the whole wall time (non-GEMM time counted as GEMM-idle)
         conc = issued_work[0] / elapsed / 1e12
         result["roofline"] = {"bound": "mfma", "achieved": achieved, "peak": peak,
                               "unit": "TFLOP/s", "frac": achieved / peak, "traffic": traffic,
                               "traffic_source": traffic_src,
-                              "kernel": {"bf16": "gemm_bf16_kernel",
-                                         "x3": "gemm_bf16_kernel<P=3> (x3 engine: hidden and input layers) + "
+                              "kernel": {"bf16": "gemm_bf16_kernel / gemm_bf16_db_kernel",
+                                         "x3": "gemm_x3_kernel (x3 engine: hidden and input layers) + "
                                                "gemm_f32_kernel / gemm_pair_kernel (1- and A-wide output layers)",
                                          "exact": "gemm_f32_kernel"}[engine] +
                                         " (every linear-layer launch of one serialised update after the timed "
                                         "region; Σ 2MNK / Σ kernel duration, each duration stamped by the "
                                         "kernel's own dispatch (hipExtLaunchKernel events), as rocprofv3 "
                                         "--kernel-trace measures it)",
-                              "dominant": ({**shapes[0], "frac": shapes[0]["tflops"] / peak} if shapes else None),
+                              "dominant": dom,
                               "by_shape": shapes[:12],
                               "gemm_engine": engine,
                               "peak_basis": {"bf16": "dense bf16 MFMA spec",

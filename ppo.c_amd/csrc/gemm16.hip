@@ -62,7 +62,7 @@ __device__ __forceinline__ float bf_lo(unsigned u) { return __builtin_bit_cast(f
 // Staging of one operand tile (R rows × BK k) into a bf16 LDS image.  T = float or unsigned short
 // (bf16 bits).  One 16-B global load per slot: 4 fp32 or 8 bf16 elements.
 // ---------------------------------------------------------------------------
-template <int R, int BK, bool MN, typename T>
+template <int R, int BK, bool MN, typename T, int NTS = NT_>
 struct Stage16 {
     static constexpr bool F32 = sizeof(T) == 4;
     static constexpr int EPL = F32 ? 4 : 8;                 // elements per 16-B load
@@ -71,7 +71,7 @@ struct Stage16 {
     static constexpr int IMG = MN ? BK * PR : R * PK;       // bf16 elements
     static constexpr int PER_ROW = MN ? R / EPL : BK / EPL; // loads along the contiguous dimension
     static constexpr int TOTAL = MN ? BK * PER_ROW : R * PER_ROW;
-    static constexpr int ITERS = (TOTAL + NT_ - 1) / NT_;
+    static constexpr int ITERS = (TOTAL + NTS - 1) / NTS;
     static_assert(R % EPL == 0 && R >= 32, "tile rows");
     u32x4 v[ITERS];
     bool kok[ITERS];
@@ -86,7 +86,7 @@ struct Stage16 {
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) {
             int row, k;
-            coords(tid + it * NT_, row, k);
+            coords(tid + it * NTS, row, k);
             const int gr = min(r0 + row, Rmax - 1);
             src[it] = ridx ? ridx[gr] : gr;
         }
@@ -97,10 +97,10 @@ struct Stage16 {
                                          bool vec, int tid) {
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) {
-            const int idx = tid + it * NT_;
+            const int idx = tid + it * NTS;
             u32x4 x = u32x4{0u, 0u, 0u, 0u};
             kok[it] = true;
-            if (TOTAL % NT_ == 0 || idx < TOTAL) {
+            if (TOTAL % NTS == 0 || idx < TOTAL) {
                 int row, k;
                 coords(idx, row, k);
                 const int gr = r0 + row, gk = k0 + k;
@@ -136,8 +136,8 @@ struct Stage16 {
     __device__ __forceinline__ void store(unsigned short* img, int tid) const {
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) {
-            const int idx = tid + it * NT_;
-            if (TOTAL % NT_ == 0 || idx < TOTAL) {
+            const int idx = tid + it * NTS;
+            if (TOTAL % NTS == 0 || idx < TOTAL) {
                 int row, k;
                 coords(idx, row, k);
                 unsigned short* d = img + (MN ? k * PR + row : row * PK + k);
@@ -160,8 +160,8 @@ struct Stage16 {
         unsigned short* __restrict__ dst = static_cast<unsigned short*>(dstv);
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) {
-            const int idx = tid + it * NT_;
-            if (TOTAL % NT_ == 0 || idx < TOTAL) {
+            const int idx = tid + it * NTS;
+            if (TOTAL % NTS == 0 || idx < TOTAL) {
                 int row, k;
                 coords(idx, row, k);
                 const int gr = r0 + row, gk = k0 + k;
@@ -383,6 +383,174 @@ __global__ __launch_bounds__(NT_, 2) void gemm_bf16_kernel(Args a) {
         }
 }
 
+// ---------------------------------------------------------------------------
+// Double-buffered 256×256 tile for forward and grad_x at wide shapes (C5: 16384 × 1024 × 1024):
+// 512 threads = 8 waves of 64×128, BK = 64 (four MFMA k-steps of 32 products per wave), two LDS
+// images (2 × 72 KiB, one workgroup per CU) so each k-tile costs ONE barrier, and the LDS stores
+// of tile j+1 and the global loads of tile j+2 are issued between tile j's k-steps (the gemm_x3
+// pipeline with a single bf16 plane).  The classic kernel above (one image, two barriers per
+// k-tile, 4 waves) stays for grad_W and narrow products.
+// ---------------------------------------------------------------------------
+template <int OP, int BM, int BN, int WARPS_M, int BK, int NTH, typename TA, typename TB, typename TC>
+__global__ __launch_bounds__(NTH, 1) void gemm_bf16_db_kernel(Args a) {
+    static_assert(OP != OP_TN, "forward / grad_x only");
+    static_assert(BK == 64, "four k-steps per k-tile");
+    constexpr int NW = NTH / 64, WARPS_N = NW / WARPS_M;
+    constexpr int WM = BM / WARPS_M, WN = BN / WARPS_N;
+    constexpr int TM = WM / 32, TN = WN / 32;
+    static_assert(TM >= 1 && TN >= 1 && WARPS_M * WARPS_N == NW, "wave tiling");
+    constexpr bool B_MN = OP == OP_NN;
+    using SA = Stage16<BM, BK, false, TA, NTH>;
+    using SB = Stage16<BN, BK, B_MN, TB, NTH>;
+    constexpr int BUF = SA::IMG + SB::IMG;
+
+    extern __shared__ __attribute__((aligned(16))) unsigned short lds[];     // 2 × BUF
+
+    const int nwg = gridDim.x, b = blockIdx.x;
+    const int xcd = b & 7, qq = nwg >> 3, rr = nwg & 7;
+    const int t = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (b >> 3);
+    const int tn = t % a.tiles_n;
+    const int tm = (t / a.tiles_n) % a.tiles_m;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int K = a.K;
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = w / WARPS_N, wn = w % WARPS_N;
+    const int r = lane & 31, h = lane >> 5;
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+    SA sa;
+    SB sb;
+    sa.prep(OP == OP_NT ? a.ridx : nullptr, m0, a.M, tid);
+    if (!B_MN) sb.prep(nullptr, n0, a.N, tid);
+    const bool vec = a.vec != 0;
+    const TA* __restrict__ PA = static_cast<const TA*>(a.A);
+    const TB* __restrict__ PB = static_cast<const TB*>(a.B);
+    unsigned short* const buf0 = lds;
+    unsigned short* const buf1 = lds + BUF;
+
+    auto load = [&](int j) {
+        sa.load(PA, a.lda, m0, a.M, j * BK, K, vec, tid);
+        sb.load(PB, a.ldb, n0, a.N, j * BK, K, vec, tid);
+    };
+    auto kstep = [&](const unsigned short* img, int ks) {
+        bf16x8 fa[TM], fb[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) fa[i] = SA::frag(img, wm * WM + i * 32 + r, ks, lane);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) fb[j] = SB::frag(img + SA::IMG, wn * WN + j * 32 + r, ks, lane);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    };
+
+    const int nk = (K + BK - 1) / BK;
+    if (nk > 0) {
+        load(0);
+        sa.store(buf0, tid);
+        sb.store(buf0 + SA::IMG, tid);
+    }
+    if (nk > 1) load(1);
+    __syncthreads();
+    int j = 0;
+    // steady state: tile j's k-steps from one image; tile j+1's LDS stores into the other between
+    // them; tile j+2's loads behind; one barrier
+    for (; j < nk - 2; ++j) {
+        const unsigned short* cur = (j & 1) ? buf1 : buf0;
+        unsigned short* nxt = (j & 1) ? buf0 : buf1;
+        kstep(cur, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        kstep(cur, 1);
+        sa.store(nxt, tid);
+        __builtin_amdgcn_sched_barrier(0);
+        kstep(cur, 2);
+        sb.store(nxt + SA::IMG, tid);
+        __builtin_amdgcn_sched_barrier(0);
+        load(j + 2);
+        kstep(cur, 3);
+        __syncthreads();
+    }
+    for (; j < nk; ++j) {                                     // the last one or two tiles
+        const unsigned short* cur = (j & 1) ? buf1 : buf0;
+        unsigned short* nxt = (j & 1) ? buf0 : buf1;
+#pragma unroll
+        for (int ks = 0; ks < BK / 16; ++ks) kstep(cur, ks);
+        if (j + 1 < nk) {
+            sa.store(nxt, tid);
+            sb.store(nxt + SA::IMG, tid);
+        }
+        __syncthreads();
+    }
+
+    // epilogue (as gemm_bf16_kernel): every load a block needs is issued before its stores
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int jj = 0; jj < TN; ++jj) {
+            const int c0 = n0 + wn * WN + jj * 32;
+            const int col = c0 + r;
+            const int r0 = m0 + wm * WM + i * 32 + 4 * h;
+            const bool col_ok = col < a.N;
+            float bcol = 0.f;
+            if (OP == OP_NT && a.bias) bcol = a.bias[col_ok ? col : a.N - 1];
+            bool keep[16];
+            if (OP == OP_NN) {
+                if (a.bits_in) {
+                    unsigned wv[16];
+#pragma unroll
+                    for (int e = 0; e < 16; ++e)
+                        wv[e] = a.bits_in[(long)min(r0 + (e & 3) + 8 * (e >> 2), a.M - 1) * a.wpr + (c0 >> 5)];
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) keep[e] = (wv[e] >> r) & 1u;
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) keep[e] = true;
+                }
+            }
+            unsigned word = 0;
+#pragma unroll
+            for (int e = 0; e < 16; ++e) {
+                const int row = r0 + (e & 3) + 8 * (e >> 2);
+                const bool ok = col_ok && row < a.M;
+                float v = acc[i][jj][e];
+                const long off = (long)row * a.ldc + col;
+                if (OP == OP_NT) {
+                    v += bcol;
+                    if (a.relu) v = v > 0.f ? v : 0.f;
+                    if (Bits<TC>::code == 1) {
+                        const unsigned short hv = (unsigned short)(pack2(v, 0.f) & 0xffffu);
+                        v = bf_lo(hv);                  // bits describe the stored (rounded) value
+                        if (ok) static_cast<unsigned short*>(a.C)[off] = hv;
+                    } else if (ok) {
+                        static_cast<float*>(a.C)[off] = v;
+                    }
+                    if (a.bits_out) {
+                        const unsigned long long bb = __ballot(ok && v > 0.f);
+                        if (r == e) word = h ? (unsigned)(bb >> 32) : (unsigned)bb;
+                    }
+                } else if (ok) {
+                    v = keep[e] ? v : 0.f;
+                    if (Bits<TC>::code == 1) static_cast<unsigned short*>(a.C)[off] =
+                        (unsigned short)(pack2(v, 0.f) & 0xffffu);
+                    else static_cast<float*>(a.C)[off] = v;
+                }
+            }
+            if (OP == OP_NT && a.bits_out && r < 16) {
+                const int row = r0 + (r & 3) + 8 * (r >> 2);
+                if (row < a.M && c0 < a.N) a.bits_out[(long)row * a.wpr + (c0 >> 5)] = word;
+            }
+        }
+}
+
 using f32 = float;
 using b16 = unsigned short;
 
@@ -408,12 +576,37 @@ void launch(Args a) {
     PPO_LAUNCH_CHECK();
 }
 
+template <int OP, typename TA, typename TB, typename TC, int NTH = 512, int WM_ = 4>
+void launch_db(Args a) {
+    constexpr int BM = 256, BN = 256, BK = 64;
+    a.tiles_m = ppo_divup(a.M, BM);
+    a.tiles_n = ppo_divup(a.N, BN);
+    a.splits = 1;
+    const long grid = (long)a.tiles_m * a.tiles_n;
+    PPO_REQUIRE(grid > 0 && grid < (1L << 31), "gemm16 (db): grid out of range");
+    PPO_REQUIRE(a.acopy == nullptr, "gemm16 (db): no gathered copy");
+    constexpr size_t lds = 2 * sizeof(unsigned short) *
+                           (Stage16<BM, BK, false, TA, NTH>::IMG + Stage16<BN, BK, OP == OP_NN, TB, NTH>::IMG);
+    static_assert(lds <= 160 * 1024, "gemm16 (db): LDS images exceed 160 KiB");
+    auto kern = gemm_bf16_db_kernel<OP, BM, BN, WM_, BK, NTH, TA, TB, TC>;
+    static bool attr = false;                          // once per instantiation
+    if (!attr) {
+        PPO_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        attr = true;
+    }
+    PPO_TIMED_LAUNCH(kern, dim3((unsigned)grid), dim3(NTH), lds, ppo::stream(), a);
+    PPO_LAUNCH_CHECK();
+}
+
 // tile configurations {BM, BN, BK}: 0 = 128x128 (4 waves of 64x64), 1 = 128x32 (skinny N),
 // 2 = 32x128 (skinny M), 3 = 64x64, 4 = 128x128 with BK = 64, 5 = 256x128/64, 6 = 128x256/64,
-// 7 = 256x128/32, 8 = 128x32 with BK = 64 (output-layer forward)
+// 7 = 256x128/32, 8 = 128x32 with BK = 64 (output-layer forward), 9 = 256x256/64 double-buffered
+// over 8 waves of 64x128 (forward / grad_x; grad_W takes cfg 6).  Measured at C5 16384x1024x1024
+// (profiles/r02_gemm16_db.txt): forward 54.1 -> 52.8 µs, grad_x 49.9 -> 46.4 µs against cfg 6; the
+// same tile over 4 waves of 128x128 (one wave per SIMD) 73.6 / 59.7 µs (not adopted)
 struct Cfg { int bm, bn, bk; };
 constexpr Cfg kCfgs[] = {{128, 128, 32}, {128, 32, 32}, {32, 128, 32}, {64, 64, 32}, {128, 128, 64},
-                         {256, 128, 64}, {128, 256, 64}, {256, 128, 32}, {128, 32, 64}};
+                         {256, 128, 64}, {128, 256, 64}, {256, 128, 32}, {128, 32, 64}, {128, 256, 64}};
 int g_force16 = -1;
 int g_split16 = 0;          // split-K workgroup target override for grad_W (0 = automatic)
 
@@ -428,6 +621,12 @@ void launch_cfg(int c, const Args& a) {
         case 5: launch<OP, 256, 128, 2, 64, TA, TB, TC>(a); break;       // waves of 128x64
         case 6: launch<OP, 128, 256, 2, 64, TA, TB, TC>(a); break;       // waves of 64x128
         case 7: launch<OP, 256, 128, 2, 32, TA, TB, TC>(a); break;
+        case 9:
+            if constexpr (OP != OP_TN) {
+                if (a.vec && a.acopy == nullptr) { launch_db<OP, TA, TB, TC>(a); break; }
+            }
+            launch<OP, 128, 256, 2, 64, TA, TB, TC>(a);
+            break;
         default: launch<OP, 128, 32, 4, 64, TA, TB, TC>(a); break;      // skinny N, BK64
     }
 }
@@ -440,6 +639,8 @@ int pick16(int M, int N, int op = OP_NT) {
     if (N <= 32 && M > 32) return op == OP_NT ? 8 : 1;   // output-layer forward: BK64 (13.8 vs 17.0 µs at C5)
     if (M <= 32 && N > 32) return 2;
     if (M <= 64 || N <= 64) return 3;
+    // forward / grad_x with a grid of ≥ 256 double-buffered 256×256 tiles (one per CU)
+    if (op != OP_TN && (long)ppo_divup(M, 256) * ppo_divup(N, 256) >= 256) return 9;
     if (N % 256 == 0 && M >= 256) return 6;
     return op == OP_NN ? 4 : 0;
 }

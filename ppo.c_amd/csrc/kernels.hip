@@ -314,8 +314,8 @@ void phip_policy_loss(const float* adv, const float* lp, const float* old_lp, fl
 
 void phip_policy_head(const float* mu, const float* log_std, const float* action, const float* adv,
                       const float* old_lp, int m, int A, float epsilon, float ent_coeff, float* grad_mu,
-                      float* grad_log_std, float* d_loss_accum) {
-    phip_memset(grad_log_std, 0, sizeof(float) * (size_t)A);
+                      float* grad_log_std, float* d_loss_accum, int ls_zeroed) {
+    if (!ls_zeroed) phip_memset(grad_log_std, 0, sizeof(float) * (size_t)A);
     if (m <= 0) return;
     PPO_REQUIRE(A > 0 && A <= 4096, "phip_policy_head: action size out of range");
     ppo::ProfScope ps(PPO_K_HEAD, 4.0 * m * (3 * A + 2));

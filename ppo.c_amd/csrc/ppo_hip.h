@@ -134,10 +134,12 @@ void phip_entropy(const float* log_std, int A, float* d_out);
 void phip_policy_loss(const float* adv, const float* lp, const float* old_lp, float* grad_lp, int m,
                       float epsilon, float ent_coeff, const float* d_entropy, float* d_loss, float* d_loss_accum);
 /* fused policy head for the update: log-prob, ratio/clip, grad_lp, grad_mu, grad_log_std
- * (+ −ent_coeff, ppo.cu:436-438); loss accumulated into d_loss_accum. */
+ * (+ −ent_coeff, ppo.cu:436-438); loss accumulated into d_loss_accum; ls_zeroed: grad_log_std
+ * already holds zeros (cleared by the previous entropy Adam step), else it is cleared first. */
 void phip_policy_head(const float* mu, const float* log_std, const float* action, const float* adv,
                       const float* old_lp, int m, int A, float epsilon, float ent_coeff,
-                      float* grad_mu, float* grad_log_std, float* d_loss_accum);
+                      float* grad_mu, float* grad_log_std, float* d_loss_accum,
+                      int ls_zeroed);
 
 /* ---------------- GAE + normalisation (gae.hip) ---------------- */
 /* advantages and targets by an exact segmented reverse scan; d_welford[0..2] =

@@ -173,6 +173,10 @@ int adam_update_cuda_w16(Adam* adam, float lr, unsigned short* w16, long n16, in
     bias_corrections(adam, &bc1, &bc2);
     nn_note_device_update(adam->weights[0]);          /* the network's host mirrors are now stale */
     if (adam->flat) {
+        /* the clearing pass is the vectorised kernel's: 16-B aligned spans only */
+        const uintptr_t al = (uintptr_t)adam->weights[0] | (uintptr_t)adam->grad_weights[0] | (uintptr_t)adam->m |
+                             (uintptr_t)adam->v;
+        if (al & 15u) zero_g = 0;
         phip_adam_flat_w16(adam->weights[0], adam->grad_weights[0], adam->m, adam->v, adam->span, lr, adam->beta1,
                            adam->beta2, bc1, bc2, adam->grad_scale, w16, w16 ? n16 : 0, zero_g);
         return (w16 != NULL) | (zero_g ? 2 : 0);

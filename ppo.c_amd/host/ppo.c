@@ -509,7 +509,7 @@ static void ppo_update_body(PPO* ppo, float gamma, int batch_size, int n_epochs_
     long iv = 0, ip = 0;
     /* gradients cleared by the previous Adam step (not after a loop's last step: a caller may read
      * the last minibatch's gradients after the update) */
-    int v_zero = 0, p_zero = 0;
+    int v_zero = 0, p_zero = 0, ls_zero = 0;
     while (iv < nv || ip < np) {
         /* serial: every value step first (the reference's order); concurrent: issue in proportion */
         const int take_v = iv < nv && (ip >= np || !concurrent || iv * np <= ip * nv);
@@ -538,11 +538,14 @@ static void ppo_update_body(PPO* ppo, float gamma, int batch_size, int n_epochs_
                              d->rows_p);
             nn_forward_dev_rows(mu, buf->state_p, d->rows_p, d->states_p, B);
             phip_policy_head(mu->d_output, pol->d_log_std, d->actions, d->adv, d->old_lp, B, A, ppo->epsilon,
-                             ppo->ent_coeff, d->gmu, pol->d_log_std_grad, d->stats + 1);
+                             ppo->ent_coeff, d->gmu, pol->d_log_std_grad, d->stats + 1, ls_zero);
             /* μ grads + (top bucket) the log σ gradient behind them */
             nn_backward_dev_z(mu, d->gmu, B, 0, p_zero, comm ? align4(A) : -1);
             phip_allreduce_join();
-            adam_update_cuda(ppo->adam_entropy, ppo->lr_policy);               /* ppo.cu:440-442 order */
+            /* ppo.cu:440-442 order; the entropy Adam clears the log σ gradient it read (the next
+             * policy head accumulates into zeros) */
+            ls_zero = ppo->adam_entropy->flat && ppo->adam_entropy->grad_weights[0] == pol->d_log_std_grad &&
+                      (adam_update_cuda_w16(ppo->adam_entropy, ppo->lr_policy, NULL, 0, ip + 1 < np) & 2);
             p_zero = adam_update_net(ppo->adam_policy, ppo->lr_policy, mu, ip + 1 < np);
             if (concurrent) phip_side_use(0);
             d->n_p++;

@@ -12,7 +12,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import ppo_ffi  # noqa: E402
 
 NAMES = {0: "128x128/bk32", 1: "128x32/bk32", 2: "32x128/bk32", 3: "64x64/bk32", 4: "128x128/bk64",
-         5: "256x128/bk64", 6: "128x256/bk64", 7: "256x128/bk32"}
+         5: "256x128/bk64", 6: "128x256/bk64", 7: "256x128/bk32", 8: "128x32/bk64", 9: "256x256/bk64 db", 10: "256x256 db 4w"}
 
 
 def main():
@@ -23,7 +23,7 @@ def main():
     lib = ppo_ffi.load()
     lib.ppo_set_device(0)
     m, n, l = (int(v) for v in args.shape.split(","))
-    for op in (0, 1, 2):
+    for op in (0, 1) if os.environ.get("NO_GRADW") else (0, 1, 2):
         for cfg in (int(c) for c in args.cfgs.split(",")):
             for tgt in ([128, 256, 512, 1024] if op == 2 else [0]):
                 us = lib.ppo_bench_gemm16(op, m, n, l, 20, cfg, tgt)

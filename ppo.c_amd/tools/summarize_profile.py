@@ -56,21 +56,33 @@ def main():
 
     if args.fetch and args.write:
         def load(fn, ctr):
-            vals = []
+            vals = collections.defaultdict(list)
             for r in csv.DictReader(open(fn)):
                 if r["Counter_Name"] == ctr and "gemm_" in r["Kernel_Name"] and "_kernel" in r["Kernel_Name"]:
-                    vals.append(float(r["Counter_Value"]))
+                    vals[gemm_key(r["Kernel_Name"], r["Grid_Size"])].append(float(r["Counter_Value"]))
             return vals
         f, w = load(args.fetch, "FETCH_SIZE"), load(args.write, "WRITE_SIZE")
-        n = len(f)
-        res = {"launches": n,
-               "fetch_size_kb_sum": sum(f), "write_size_kb_sum": sum(w),
-               "hbm_bytes_per_launch": (2 * sum(f) + sum(w)) * 1024 / max(1, n),
-               "note": "(2*FETCH_SIZE + WRITE_SIZE)*1024 per GEMM launch (gemm_f32_kernel / gemm_pair_kernel / gemm_bf16_kernel, a pair "
-                       "launch counting once as in bench.py's roofline), averaged over one "
-                       "bench.py update (+ synthetic fill); separate --pmc passes for each counter"}
+        # per kernel (template + grid): HBM bytes per launch from the counter passes; the class
+        # average weights each kernel by its launch count in the TRACED update (the counter passes
+        # may sample fewer minibatch steps), so it has the mix of bench.py's roofline
+        per = {}
+        for k in f:
+            if k in w and f[k] and w[k]:
+                per[k] = (2 * sum(f[k]) / len(f[k]) + sum(w[k]) / len(w[k])) * 1024
+        cnt = {k: len(v) for k, v in by.items() if k in per}
+        tot = sum(cnt.values())
+        dom = max(by, key=lambda k: sum(by[k]))
+        res = {"launches_traced": tot,
+               "hbm_bytes_per_launch": sum(per[k] * c for k, c in cnt.items()) / max(1, tot),
+               "dominant": {"kernel": dom, "hbm_bytes_per_launch": per.get(dom),
+                            "avg_us": sum(by[dom]) / len(by[dom]) / 1e3, "launches": len(by[dom])},
+               "by_kernel": {k: {"hbm_bytes_per_launch": per[k], "launches_in_update": cnt[k],
+                                 "pmc_samples": len(f[k])} for k in sorted(cnt, key=lambda k: -cnt[k])},
+               "note": "(2*FETCH_SIZE + WRITE_SIZE)*1024 per GEMM launch (gfx950: FETCH_SIZE reports half of a "
+                       "wide coalesced read), separate --pmc passes per counter; class average weighted by the "
+                       "traced serial update's launch counts (a pair launch counts once, as in bench.py)"}
         json.dump(res, open(os.path.join(out, f"{args.tag}_pmc_gemm.json"), "w"), indent=1)
-        print(json.dumps(res))
+        print(json.dumps(res, indent=1))
 
 
 if __name__ == "__main__":
