@@ -412,19 +412,25 @@ __global__ __launch_bounds__(NT_, 4) void gemm_pair_kernel(Args aw, Args ax, int
 }
 
 // ---------------------------------------------------------------------------
-// Small-M forward (rollout steps over E environments, Pendulum-sized minibatches): y = x·Wᵀ + b
-// for M ≤ a few hundred rows.  The 128-row tiles of gemm_f32_kernel would put a 256 × 512 layer on
-// 16 workgroups that each walk the whole K serially (25 µs).  Here a 512-thread workgroup owns a
-// 32 × 32 output block and splits K over its 8 waves; each wave streams its K-slice straight from
-// global memory into MFMA operands (lane half h takes 32 consecutive k of each 64-deep chunk: 8
-// float4 loads per operand, no LDS staging), and the 8 partial 32×32 accumulators are summed
-// through LDS before the fused bias / ReLU / ReLU′-bit epilogue.  Same fp32 MFMA numerics.
+// Small-M products (rollout steps over E environments, the reference's B = 64 minibatches).  The
+// 128-row tiles of gemm_f32_kernel would put a 64 × 512 product on 8–16 workgroups that each walk
+// the whole K serially (17 µs for a 64×512×512 grad_x).  Here a 512-thread workgroup owns a 32 × 32
+// output block and splits K over its 8 waves; each wave streams its K-slice straight from global
+// memory into MFMA operands (lane half h takes 32 consecutive k of each 64-deep chunk: float4 loads
+// along a k-contiguous operand, one coalesced scalar per k across the 32 lanes of a row-contiguous
+// one; no LDS staging), and the 8 partial 32×32 accumulators are summed through LDS before the
+// fused epilogue.  Same fp32 MFMA numerics.
+//   NT forward  A(r, k) = x[ridx(r)·lda + k]   B(c, k) = W[c·ldb + k]   + bias, ReLU, bits, gathered copy
+//   NN grad_x   A(r, k) = g[r·lda + k]         B(c, k) = W[k·ldb + c]   ⊙ ReLU′ (bits or mask)
+//   TN grad_W   A(r, k) = g[k·lda + r]         B(c, k) = x[k·ldb + c]   whole K per workgroup (plain
+//               stores, no split-K) + the bias gradient Σ_k A(r, k) from the tn == 0 column of blocks
 // ---------------------------------------------------------------------------
 constexpr int SM_WAVES = 8;
 
-template <bool VEC>
+template <int OP, bool VEC>
 __global__ __launch_bounds__(64 * SM_WAVES) void gemm_smallm_kernel(Args a) {
     __shared__ float red[SM_WAVES][32 * 33];
+    __shared__ float bred[SM_WAVES][64];
     const int tiles_n = a.tiles_n;
     const int tm = blockIdx.x / tiles_n, tn = blockIdx.x % tiles_n;
     const int m0 = tm * 32, n0 = tn * 32;
@@ -433,11 +439,14 @@ __global__ __launch_bounds__(64 * SM_WAVES) void gemm_smallm_kernel(Args a) {
     const int K = a.K;
     const int kslice = ((K + SM_WAVES - 1) / SM_WAVES + 63) / 64 * 64;   // per-wave K range, 64-aligned
     const int kb = w * kslice, ke = min(K, kb + kslice);
-    const float* __restrict__ X = static_cast<const float*>(a.A);
-    const float* __restrict__ W = static_cast<const float*>(a.B);
-    const int arow = min(m0 + r, a.M - 1);
-    const long abase = (long)(a.ridx ? a.ridx[arow] : arow) * a.lda;
-    const long bbase = (long)min(n0 + r, a.N - 1) * a.ldb;
+    const float* __restrict__ PA = a.A;
+    const float* __restrict__ PB = a.B;
+    const int arow = min(m0 + r, a.M - 1), bcol = min(n0 + r, a.N - 1);
+    const long abase = OP == OP_TN ? (long)arow : (long)(OP == OP_NT && a.ridx ? a.ridx[arow] : arow) * a.lda;
+    const long bbase = OP == OP_NT ? (long)bcol * a.ldb : (long)bcol;
+    const bool copy = OP == OP_NT && a.acopy != nullptr && tn == 0 && m0 + r < a.M;
+    const bool bsum = OP == OP_TN && a.gbias != nullptr && tn == 0;
+    float bpart = 0.f;
 
     f32x16 acc;
 #pragma unroll
@@ -445,27 +454,52 @@ __global__ __launch_bounds__(64 * SM_WAVES) void gemm_smallm_kernel(Args a) {
     for (int k0 = kb; k0 < ke; k0 += 64) {
         const int kl = k0 + 32 * h;                      // this lane's 32 k values
         float av[32], bv[32];
-        if (VEC) {
+        if (OP != OP_TN && VEC) {                        // A k-contiguous: float4 loads
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
                 const int kq = kl + 4 * q;
                 const bool ok = kq < ke;
-                const int kc = ok ? kq : 0;
-                const f32x4 ta = *reinterpret_cast<const f32x4*>(X + abase + kc);
-                const f32x4 tb = *reinterpret_cast<const f32x4*>(W + bbase + kc);
+                const f32x4 ta = *reinterpret_cast<const f32x4*>(PA + abase + (ok ? kq : 0));
+                if (copy && ok) *reinterpret_cast<f32x4*>(a.acopy + (long)(m0 + r) * K + kq) = ta;
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    av[4 * q + e] = ok ? ta[e] : 0.f;
-                    bv[4 * q + e] = ok ? tb[e] : 0.f;
-                }
+                for (int e = 0; e < 4; ++e) av[4 * q + e] = ok ? ta[e] : 0.f;
             }
-        } else {
+        } else if (OP != OP_TN) {
 #pragma unroll
             for (int q = 0; q < 32; ++q) {
                 const bool ok = kl + q < ke;
-                av[q] = ok ? X[abase + kl + q] : 0.f;
-                bv[q] = ok ? W[bbase + kl + q] : 0.f;
+                av[q] = ok ? PA[abase + kl + q] : 0.f;
+                if (copy && ok) a.acopy[(long)(m0 + r) * K + kl + q] = av[q];
             }
+        } else {                                         // A row-contiguous: one scalar per k
+#pragma unroll
+            for (int q = 0; q < 32; ++q) {
+                const bool ok = kl + q < ke;
+                av[q] = ok ? PA[abase + (long)(ok ? kl + q : 0) * a.lda] : 0.f;
+            }
+        }
+        if (OP == OP_NT && VEC) {                        // B k-contiguous
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int kq = kl + 4 * q;
+                const bool ok = kq < ke;
+                const f32x4 tb = *reinterpret_cast<const f32x4*>(PB + bbase + (ok ? kq : 0));
+#pragma unroll
+                for (int e = 0; e < 4; ++e) bv[4 * q + e] = ok ? tb[e] : 0.f;
+            }
+        } else if (OP == OP_NT) {
+#pragma unroll
+            for (int q = 0; q < 32; ++q) bv[q] = kl + q < ke ? PB[bbase + kl + q] : 0.f;
+        } else {                                         // B row-contiguous
+#pragma unroll
+            for (int q = 0; q < 32; ++q) {
+                const bool ok = kl + q < ke;
+                bv[q] = ok ? PB[bbase + (long)(ok ? kl + q : 0) * a.ldb] : 0.f;
+            }
+        }
+        if (bsum) {
+#pragma unroll
+            for (int q = 0; q < 32; ++q) bpart += av[q];
         }
 #pragma unroll
         for (int q = 0; q < 32; ++q) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[q], bv[q], acc, 0, 0, 0);
@@ -473,11 +507,17 @@ __global__ __launch_bounds__(64 * SM_WAVES) void gemm_smallm_kernel(Args a) {
     // C/D map: col = r, row = (e&3) + 8(e>>2) + 4h
 #pragma unroll
     for (int e = 0; e < 16; ++e) red[w][((e & 3) + 8 * (e >> 2) + 4 * h) * 33 + r] = acc[e];
+    if (bsum) bred[w][h * 32 + r] = bpart;
     __syncthreads();
+    if (bsum && threadIdx.x < 32) {                      // bias gradient of row m0 + r: Σ over all k
+        float t = 0.f;
+        for (int q = 0; q < SM_WAVES; ++q) t += bred[q][threadIdx.x] + bred[q][32 + threadIdx.x];
+        if (m0 + (int)threadIdx.x < a.M) a.gbias[m0 + threadIdx.x] = t;
+    }
     if (w == 0) {
         const int col = n0 + r;
         const bool col_ok = col < a.N;
-        const float bcol = (a.bias && col_ok) ? a.bias[col] : 0.f;
+        const float bc = (OP == OP_NT && a.bias && col_ok) ? a.bias[col] : 0.f;
         unsigned word = 0;
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
@@ -485,21 +525,42 @@ __global__ __launch_bounds__(64 * SM_WAVES) void gemm_smallm_kernel(Args a) {
             float v = 0.f;
 #pragma unroll
             for (int q = 0; q < SM_WAVES; ++q) v += red[q][rr * 33 + r];
-            v += bcol;
-            if (a.relu) v = v > 0.f ? v : 0.f;
             const int row = m0 + rr;
             const bool ok = col_ok && row < a.M;
-            if (ok) static_cast<float*>(a.C)[(long)row * a.ldc + col] = v;
-            if (a.bits_out) {
-                const unsigned long long bb = __ballot(ok && v > 0.f);
-                if (r == e) word = h ? (unsigned)(bb >> 32) : (unsigned)bb;
+            if (OP == OP_NT) {
+                v += bc;
+                if (a.relu) v = v > 0.f ? v : 0.f;
+                if (ok) a.C[(long)row * a.ldc + col] = v;
+                if (a.bits_out) {
+                    const unsigned long long bb = __ballot(ok && v > 0.f);
+                    if (r == e) word = h ? (unsigned)(bb >> 32) : (unsigned)bb;
+                }
+            } else if (OP == OP_NN) {
+                if (ok) {
+                    bool keep = true;
+                    if (a.bits_in) keep = (a.bits_in[(long)row * a.wpr + (n0 >> 5)] >> r) & 1u;
+                    else if (a.mask) keep = a.mask[(long)row * a.ldmask + col] > 0.f;
+                    a.C[(long)row * a.ldc + col] = keep ? v : 0.f;
+                }
+            } else if (ok) {
+                a.C[(long)row * a.ldc + col] = v;
             }
         }
-        if (a.bits_out && r < 16) {
+        if (OP == OP_NT && a.bits_out && r < 16) {
             const int row = m0 + (r & 3) + 8 * (r >> 2) + 4 * h;
             if (row < a.M && n0 < a.N) a.bits_out[(long)row * a.wpr + (n0 >> 5)] = word;
         }
     }
+}
+
+template <int OP>
+void launch_smallm(Args a, bool vec) {
+    a.tiles_n = ppo_divup(a.N, 32);
+    const long grid = (long)ppo_divup(a.M, 32) * a.tiles_n;
+    PPO_REQUIRE(grid > 0 && grid < (1L << 31), "gemm (small M): grid out of range");
+    if (vec) PPO_TIMED_LAUNCH((gemm_smallm_kernel<OP, true>), dim3((unsigned)grid), dim3(64 * SM_WAVES), 0, ppo::stream(), a);
+    else PPO_TIMED_LAUNCH((gemm_smallm_kernel<OP, false>), dim3((unsigned)grid), dim3(64 * SM_WAVES), 0, ppo::stream(), a);
+    PPO_LAUNCH_CHECK();
 }
 
 inline bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
@@ -581,9 +642,11 @@ int pick_cfg(int op, int M, int N, int* splitk_target = nullptr) {
 }
 
 // the tiled kernel leaves most CUs idle when its grid is small and each workgroup walks all of K
+// (n = K): below 64 the K split leaves most of the workgroup idle and 64×64 tiles are faster
+// (tools/smallm_sweep.py, profiles/r02_smallm_sweep.txt)
 bool use_smallm(int m, int n, int l) {
     const long tiled_wgs = (long)ppo_divup(m, 128) * ppo_divup(l, 64);
-    return m <= 1024 && tiled_wgs < 64;
+    return m <= 1024 && n >= 64 && tiled_wgs < 64;
 }
 
 void fwd(float* y, const float* x, const float* W, const float* b, int m, int n, int l, int relu, unsigned* bits,
@@ -596,16 +659,10 @@ void fwd(float* y, const float* x, const float* W, const float* b, int m, int n,
     a.bits_out = bits; a.wpr = ppo_divup(l, 32);
     a.vec_a = (n % 4 == 0) && aligned16(x);             // kcont, extent K = n
     a.vec_b = (n % 4 == 0) && aligned16(W);
-    // small M (rollout over E envs, Pendulum-sized minibatches): split-K inside a workgroup —
-    // only when no gathered copy is wanted (that path keeps the tiled kernel's copy-out)
-    if (cfg < 0 && g_force_cfg < 0 && !acopy && use_smallm(m, n, l)) {
-        a.tiles_n = ppo_divup(l, 32);
-        const int grid = ppo_divup(m, 32) * a.tiles_n;
-        if (a.vec_a && a.vec_b)
-            PPO_TIMED_LAUNCH(gemm_smallm_kernel<true>, dim3(grid), dim3(64 * SM_WAVES), 0, ppo::stream(), a);
-        else
-            PPO_TIMED_LAUNCH(gemm_smallm_kernel<false>, dim3(grid), dim3(64 * SM_WAVES), 0, ppo::stream(), a);
-        PPO_LAUNCH_CHECK();
+    // small M (rollout over E envs, B = 64 minibatches): split-K inside a workgroup (the fused
+    // gather's copy of the rows is written by the first column of blocks)
+    if (cfg < 0 && g_force_cfg < 0 && use_smallm(m, n, l)) {
+        launch_smallm<OP_NT>(a, a.vec_a && a.vec_b);
         return;
     }
     launch_cfg<OP_NT>(cfg < 0 ? pick_cfg(OP_NT, m, l) : cfg, a);
@@ -625,8 +682,18 @@ Args bwd_x_args(float* gx, const float* g, const float* W, const float* mask, co
 
 void bwd_x(float* gx, const float* g, const float* W, const float* mask, const unsigned* bits, int m, int n, int l,
            int cfg) {
-    launch_cfg<OP_NN>(cfg < 0 ? pick_cfg(OP_NN, m, n) : cfg, bwd_x_args(gx, g, W, mask, bits, m, n, l));
+    const Args a = bwd_x_args(gx, g, W, mask, bits, m, n, l);
+    if (cfg < 0 && g_force_cfg < 0 && use_smallm(m, l, n)) {
+        launch_smallm<OP_NN>(a, a.vec_a);
+        return;
+    }
+    launch_cfg<OP_NN>(cfg < 0 ? pick_cfg(OP_NN, m, n) : cfg, a);
 }
+
+// grad_W over a small batch (K = m): one 32×32 block per workgroup with the whole K split over its
+// waves beats split-K tiles at 128 < m ≤ 256 (512×512 at m = 256: 6.1 vs 10.5 µs); below that, 64×64
+// tiles (no split) are faster than both (5.1 vs 5.9 µs at m = 64) and than 128×128 (10.3 µs)
+bool use_smallm_w(int m, int n, int l) { return m > 128 && m <= 256 && (long)ppo_divup(l, 32) * ppo_divup(n, 32) >= 16; }
 
 // grad_W reduces over the minibatch (K = m): split-K so the grid fills the chip; f32 atomics
 // into an output that is zero on entry (zeroed != 0) or zeroed here.  Returns the arguments and
@@ -671,8 +738,17 @@ void bwd_w(float* gW, float* gb, const float* g, const float* x, int m, int n, i
         }
         return;
     }
+    if (cfg < 0 && g_force_cfg < 0 && use_smallm_w(m, n, l)) {       // plain stores: zeroed or not
+        Args a{};
+        a.A = g; a.lda = l; a.B = x; a.ldb = n; a.C = gW; a.ldc = n;
+        a.M = l; a.N = n; a.K = m;
+        a.gbias = gb;
+        launch_smallm<OP_TN>(a, false);
+        return;
+    }
     int c = 0;
-    const Args a = bwd_w_args(gW, gb, g, x, m, n, l, zeroed, cfg, &c);
+    const Args a = bwd_w_args(gW, gb, g, x, m, n, l, zeroed, cfg < 0 && g_force_cfg < 0 && m <= 128 && l > 32 && n > 32 ? 4 : cfg,
+                              &c);
     launch_cfg<OP_TN>(c, a);
 }
 

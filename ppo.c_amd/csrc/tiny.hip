@@ -482,17 +482,22 @@ int phip_tiny_update(const PhipTinyNet* net, const PhipTinyPhase* ph) {
     if (a.stamps) {                      // diagnostics: mean µs per phase over steps 1..63
         unsigned long long h[64 * 12];
         phip_d2h(h, a.stamps, sizeof(h));
+        int dev = 0, khz = 0;
+        PPO_CHECK(hipGetDevice(&dev));
+        PPO_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+        const double mhz = khz > 0 ? khz / 1000.0 : 100.0;     // wall_clock64() ticks per µs
+        fprintf(stderr, "tiny: wall clock %.1f MHz\n", mhz);
         double acc[5] = {0, 0, 0, 0, 0};
         int n = 0;
         for (int st = 1; st < 64 && st < ph->n_epochs * ph->num_batches; ++st, ++n)
-            for (int k = 0; k < 5; ++k) acc[k] += (double)(h[st * 8 + k + 1] - h[st * 8 + k]) / 100.0;
-        const double clk = (double)(h[63 * 8 + 6] - h[1 * 8 + 6]) / ((double)(h[63 * 8] - h[1 * 8]) / 100.0);
+            for (int k = 0; k < 5; ++k) acc[k] += (double)(h[st * 8 + k + 1] - h[st * 8 + k]) / mhz;
+        const double clk = (double)(h[63 * 8 + 6] - h[1 * 8 + 6]) / ((double)(h[63 * 8] - h[1 * 8]) / mhz);
         if (n) fprintf(stderr, "tiny: shader clock %.0f MHz\n", clk);
         double fl[3] = {0, 0, 0};
         for (int st = 1; st < 64 && st < ph->n_epochs * ph->num_batches; ++st) {
-            fl[0] += (double)(h[512 + st * 4 + 0] - h[st * 8 + 1]) / 100.0;
-            fl[1] += (double)(h[512 + st * 4 + 1] - h[512 + st * 4 + 0]) / 100.0;
-            fl[2] += (double)(h[512 + st * 4 + 2] - h[512 + st * 4 + 1]) / 100.0;
+            fl[0] += (double)(h[512 + st * 4 + 0] - h[st * 8 + 1]) / mhz;
+            fl[1] += (double)(h[512 + st * 4 + 1] - h[512 + st * 4 + 0]) / mhz;
+            fl[2] += (double)(h[512 + st * 4 + 2] - h[512 + st * 4 + 1]) / mhz;
         }
         if (n) fprintf(stderr, "tiny: forward layers (us): %.2f %.2f %.2f\n", fl[0] / n, fl[1] / n, fl[2] / n);
         if (n)

@@ -137,3 +137,32 @@ def test_mlp_paired_backward(lib, ncfg, sizes, m):
     for a, b in zip(out[0][1], out[4][1]):          # every hidden layer's grad_x, output layer's included
         np.testing.assert_array_equal(a, b)
     np.testing.assert_allclose(out[0][0], out[4][0], rtol=1e-5, atol=1e-5 * np.abs(out[4][0]).max())
+
+
+@pytest.mark.parametrize("sizes,m", [([376, 512, 512, 17], 64), ([376, 512, 512, 1], 200), ([17, 256, 256, 6], 64),
+                                     ([1024, 1024, 17], 33)])
+def test_mlp_small_batch_auto(lib, oracle, sizes, m):
+    """The reference's minibatch size (B = 64) through the automatic kernel choice: the small-M
+    kernels (32×32 blocks, K split over 8 waves) for the forward with its ReLU′ bits, grad_x with the
+    mask, and grad_W over the whole batch with its bias-gradient sums — whole MLP against the oracle,
+    both fp32 engines' automatic routes (x3 only serves m > 1024, so both run the exact kernels)."""
+    rng = np.random.default_rng(sum(sizes) + m)
+    relu = [1] * (len(sizes) - 2) + [0]
+    names = ["relu"] * (len(sizes) - 2) + ["none"]
+    nn = lib.create_neural_network(ppo_ffi.c_ints(sizes), ppo_ffi.c_strings(names), len(sizes))
+    params = (rng.uniform(-1, 1, oracle.mlp_num_params(sizes)) * 0.1).astype(F32)
+    nn_set_params_packed(lib, nn, params)
+    x, gout = _rand(rng, (m, sizes[0])), _rand(rng, (m, sizes[-1]))
+    acts = oracle.mlp_forward(sizes, relu, params, x)
+    y_ref = oracle.mlp_layer_outputs(sizes, acts, m)[-1]
+    g_ref = oracle.mlp_backward(sizes, relu, params, x, acts, gout)
+    dx, dgo = dev(lib, x), dev(lib, gout)
+    lib.ppo_gemm_tune(-1, 0)
+    try:
+        lib.forward_propagation_cuda(nn, dx.ptr, m)
+        y = ppo_ffi.d2h(lib, nn.contents.d_output, F32, m * sizes[-1]).reshape(m, sizes[-1])
+        assert_gemm_close(y, y_ref, max(sizes), "small-batch MLP forward")
+        lib.backward_propagation_cuda(nn, dgo.ptr, m)
+        assert_gemm_close(nn_grads_packed(lib, nn), g_ref, m, "small-batch MLP grads")
+    finally:
+        lib.free_neural_network(nn)

@@ -20,6 +20,7 @@ LINEAR_SHAPES = [
     (4096, 376, 512), (4096, 512, 512), (4096, 512, 17), (4096, 512, 1),   # C4 layers
     (2048, 1024, 1024),                                # C5 hidden (fp32 path)
     (1, 3, 64), (1, 376, 512), (33, 5, 7), (130, 129, 131),               # m = 1 rollout, odd sizes
+    (64, 376, 512), (64, 512, 512), (64, 512, 17), (200, 256, 256), (256, 1024, 1024),   # B = 64 / small M
 ]
 
 
