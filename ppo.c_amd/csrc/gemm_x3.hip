@@ -384,6 +384,9 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
             unsigned short* nxt = (j & 1) ? buf0 : buf1;
             const int k1 = k0_of(j + 1);
             read_frags(cur);
+#ifdef PPO_X3_PRIO
+            __builtin_amdgcn_s_setprio(1);
+#endif
             mfma_group(0);
             __builtin_amdgcn_sched_barrier(0);
             mfma_group(1);
@@ -397,6 +400,9 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
             __builtin_amdgcn_sched_barrier(0);
             mfma_group(4);
             mfma_group(5);
+#ifdef PPO_X3_PRIO
+            __builtin_amdgcn_s_setprio(0);
+#endif
             __syncthreads();
         }
         for (; j < NK; ++j) {                                 // the last one or two tiles
@@ -520,13 +526,21 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
                 if (OP == OP_NT) {
                     v += bcol;
                     if (a.relu) v = v > 0.f ? v : 0.f;
+#ifdef PPO_X3_NTSTORE
+                    if (ok) __builtin_nontemporal_store(v, dst);
+#else
                     if (ok) *dst = v;
+#endif
                     if (a.bits_out) {
                         const unsigned long long bb = __ballot(ok && v > 0.f);
                         if (r == e) word = h ? (unsigned)(bb >> 32) : (unsigned)bb;
                     }
                 } else if (OP == OP_NN) {
+#ifdef PPO_X3_NTSTORE
+                    if (ok) __builtin_nontemporal_store(keep[e] ? v : 0.f, dst);
+#else
                     if (ok) *dst = keep[e] ? v : 0.f;
+#endif
                 } else if (ok) {
                     if (a.splits > 1) atomicAdd(dst, v);
                     else *dst = v;
