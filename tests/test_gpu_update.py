@@ -429,3 +429,46 @@ def test_degenerate_updates(lib, oracle):
     oracle.srand(8)
     assert r == oracle.libc().rand()
     lib.free_ppo(ppo)
+
+
+@pytest.mark.parametrize("net", ["c3_exact", "c4_x3", "c4_exact"])
+def test_short_update_elementwise(lib, oracle, net):
+    """A short whole update (GAE, 2 value epochs and 1 policy epoch of 4 minibatches: up to 12 Adam
+    steps per network, device Feistel shuffle on both sides) against the oracle's update of the same
+    buffer, element by element (diagnostic quantiles printed; bounds below)."""
+    sizes, N, B = {"c3_exact": ([17, 256, 256, 6], 2048, 512), "c4_x3": ([376, 512, 512, 512, 17], 8192, 2048),
+                   "c4_exact": ([376, 512, 512, 512, 17], 8192, 2048)}[net]
+    old = lib.ppo_gemm_f32_engine(0 if net.endswith("exact") else 1)
+    try:
+        ppo = make_ppo(lib, oracle, sizes, N, init_std=0.7)
+        mu0, ls0 = policy_state(lib, ppo)
+        v0 = nn_params_packed(lib, ppo.contents.V)
+        buf = synthetic_buffer(oracle, sizes, mu0, ls0, N, seed=33, n_envs=8)
+        load_buffer(lib, ppo, buf)
+        lib.ppo_reset_stats(ppo)
+        lib.ppo_update(ppo, 0.99, B, 1, 2, 1, 4242)
+        lib.ppo_synchronize()
+    finally:
+        lib.ppo_gemm_f32_engine(old)
+    st = (C.c_double * 7)()
+    lib.ppo_read_stats(ppo, st, 7)
+    mu1, ls1 = policy_state(lib, ppo)
+    v1 = nn_params_packed(lib, ppo.contents.V)
+    ref = oracle.ppo_update(sizes, RELU(sizes), mu0, ls0, v0, buf, batch_size=B, n_epochs_policy=1,
+                            n_epochs_value=2, shuffle_mode=1, seed=4242)
+    steps_v, steps_p = 2 * (N // B), N // B
+    assert st[1] == ref["n_v"] == steps_v and st[3] == ref["n_p"] == steps_p
+    lr = 3e-4
+    for got, want, start, n_steps, what in ((v1, ref["v"], v0, steps_v, "V"), (mu1, ref["mu"], mu0, steps_p, "mu"),
+                                            (ls1, ref["log_std"], ls0, steps_p, "log_std")):
+        err = np.abs(got.astype(np.float64) - want)
+        moved = np.abs(want.astype(np.float64) - start)
+        q = {f: float((err <= f * lr).mean()) for f in (1e-3, 1e-2, 1e-1)}
+        print(f"{net} {what}: n={err.size} within lr x 1e-3 / 1e-2 / 1e-1: " +
+              " / ".join(f"{100 * v:.3f} %" for v in q.values()) +
+              f"; max err {err.max():.3g} (= {err.max() / lr:.3f} lr); median movement {np.median(moved) / lr:.2f} lr")
+        assert err.max() <= 2 * lr * n_steps, f"{what}: max err {err.max()}"
+        assert q[1e-1] >= 0.99, f"{what}: only {q[1e-1] * 100:.2f} % within 0.1·lr"
+    np.testing.assert_allclose(st[0], ref["sum_v_loss"], rtol=1e-3)
+    np.testing.assert_allclose(st[2], ref["sum_policy_loss"], rtol=1e-3, atol=1e-5)
+    lib.free_ppo(ppo)
