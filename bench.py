@@ -387,11 +387,16 @@ def main():
             m_, n_, l_ = dom["m"], dom["n"], dom["l"]
             # operands read once, output written once (fp32; grad_W: + its bias-gradient vector)
             dom["algorithmic_bytes"] = 4 * (m_ * n_ + n_ * l_ + m_ * l_ + (l_ if dom["op"] == "grad_W" else 0))
-            pd = pmc.get("dominant") or {}
+            # the PMC pass's kernel of this op (template's first parameter) with the most launches
+            # in the traced update: for C4 the 512-wide hidden-layer instance of the dominant shape
             code = {"forward": "0", "grad_x": "1", "grad_W": "2"}.get(dom["op"])
-            if pd.get("kernel", "").startswith(f"gemm<{code},") and dom.get("engine") == "x3":
-                dom["traffic"] = pd.get("hbm_bytes_per_launch")
-                dom["traffic_kernel"] = pd.get("kernel")
+            cand = [(v.get("launches_in_update", 0), k, v) for k, v in (pmc.get("by_kernel") or {}).items()
+                    if k.startswith(f"gemm<{code}, ") and "true" not in k and "false" not in k   # x3 template
+                    and dom.get("engine") == "x3"]
+            if cand:
+                _, k, v = max(cand)
+                dom["traffic"] = v.get("hbm_bytes_per_launch")
+                dom["traffic_kernel"] = k
         # lower bound of the GEMM class rate in the timed (concurrent) region: every GEMM launch's
         # algorithmic FLOPs over the whole wall time (non-GEMM time counted as GEMM-idle)
         conc = issued_work[0] / elapsed / 1e12
