@@ -856,6 +856,9 @@ int ppo_gemm_flags(int flags) {
     return old;
 }
 
+// ppo_gemm_tune(·, 1): split-K off — deterministic (atomic-free) parameter gradients requested
+int phip_gemm_deterministic(void) { return g_splitk_override == 1; }
+
 int ppo_gemm_tune(int force_cfg, int splitk_target) {
     g_force_cfg = force_cfg;
     if (splitk_target >= 0) g_splitk_override = splitk_target;

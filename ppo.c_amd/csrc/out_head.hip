@@ -1,0 +1,285 @@
+// out_head.hip — a minibatch step's output layer fused with its loss head, for narrow outputs
+// (value networks A = 1, small action spaces), fp32 storage.
+//
+// Replaces four launches per step inside ppo_update:
+//   output-layer forward    y = x·Wᵀ + b                         mat_mul.cu:122-163 (K1+K2)
+//   loss head               value: MSE + derivative                 loss.cu:5-83 (K8+K9)
+//                           policy: log-prob, ratio/clip, ∂/∂μ, ∂/∂logσ (+ −c_ent)
+//                                                                  ppo.cu:82-107,436-438, policy.cu:67-111
+//   output-layer backward   gx = (g·W) ⊙ 1[x > 0], gW += gᵀ·x, gb += Σ g
+//                                                                  mat_mul.cu:165-217, neural_network.cu:108-118
+// The last hidden activation x [m, n] is read once and gx written once: ≈ 8·m·n bytes per step (the
+// separate launches read x twice and round-trip y and g through HBM, and their GEMM grids were
+// latency-bound at these shapes).
+//
+// One wave per row (rows strided over every wave of the grid); lane l owns the NPL = n/64 columns
+// [l·NPL, l·NPL + NPL): its slice of W (A·NPL values) and its gW accumulators sit in registers.
+// y_a is a wave sum of the lanes' partial dots; every lane then evaluates the head on the full row
+// (the same arithmetic as kernels.hip's mse_kernel / policy_head_kernel given y), and g·W, gᵀ·x use
+// the lane's columns.  gW / gb / grad_logσ / loss: summed over the workgroup's waves through LDS,
+// then one f32 atomic per element per workgroup into outputs that are zero on entry (as the split-K
+// grad_W GEMMs).  The wide policy output (A = 17) keeps the GEMM path: its A·NPL weights and
+// accumulators do not fit the registers of one lane (measured in round 1: spills, 10× slower).
+#include "dev.h"
+
+#include <cmath>
+
+namespace {
+
+constexpr int NTH = 256;                   // 4 waves
+constexpr int NW = NTH / 64;
+
+__device__ __forceinline__ float wsum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// policy.cu:67-74 with the reference's double temporaries (kernels.hip log_prob_row)
+template <int A>
+__device__ __forceinline__ float log_prob_row(const float (&mu)[A], const float* log_std, const float (&a)[A]) {
+    const float c = (float)(-0.5 * A * (double)logf((float)(2 * M_PI)));
+    float lp = c;
+#pragma unroll
+    for (int j = 0; j < A; ++j) {
+        const float z = (a[j] - mu[j]) / expf(log_std[j]);
+        lp = (float)((double)lp - ((double)log_std[j] + 0.5 * (double)(z * z)));
+    }
+    return lp;
+}
+
+// ppo.cu:82-107 per sample (kernels.hip surrogate)
+__device__ __forceinline__ float surrogate(float adv, float lp, float old_lp, float eps, int m, float* grad) {
+    const float ratio = (float)exp((double)(lp - old_lp));
+    const int adv_pos = adv > 0;
+    const int ratio_pos = ratio > 1 + eps;
+    const int ratio_neg = ratio < 1 - eps;
+    *grad = -(adv_pos * !ratio_pos + !adv_pos * !ratio_neg) * adv * ratio / m;
+    return adv * (adv_pos * (ratio_pos * (1 + eps) + !ratio_pos * ratio) +
+                  !adv_pos * (ratio_neg * (1 - eps) + !ratio_neg * ratio));
+}
+
+struct OutArgs {
+    const float* x; const float* W; const float* b;   // x [m, n] (the last hidden activation), W [A, n], b [A]
+    int m, n, relu_in;                                // relu_in: gx masked by x > 0
+    const float* tgt;                                 // value head: targets [m]
+    const float* log_std; const float* action; const float* adv; const float* old_lp;   // policy head
+    float eps, ent_coeff;
+    float* y; float* gx; float* gW; float* gb; float* grad_log_std; float* loss_accum;
+};
+
+template <int NPL>
+__device__ __forceinline__ void load_cols(const float* __restrict__ p, float (&v)[NPL]) {
+    if constexpr (NPL == 8) {
+        const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    } else if constexpr (NPL == 4) {
+        const float4 a = *reinterpret_cast<const float4*>(p);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    } else if constexpr (NPL == 2) {
+        const float2 a = *reinterpret_cast<const float2*>(p);
+        v[0] = a.x; v[1] = a.y;
+    } else {
+        v[0] = p[0];
+    }
+}
+
+template <int NPL>
+__device__ __forceinline__ void store_cols(float* __restrict__ p, const float (&v)[NPL]) {
+    if constexpr (NPL == 8) {
+        *reinterpret_cast<float4*>(p) = float4{v[0], v[1], v[2], v[3]};
+        *reinterpret_cast<float4*>(p + 4) = float4{v[4], v[5], v[6], v[7]};
+    } else if constexpr (NPL == 4) {
+        *reinterpret_cast<float4*>(p) = float4{v[0], v[1], v[2], v[3]};
+    } else if constexpr (NPL == 2) {
+        *reinterpret_cast<float2*>(p) = float2{v[0], v[1]};
+    } else {
+        p[0] = v[0];
+    }
+}
+
+// HEAD 0: value (A = 1, MSE against tgt); HEAD 1: policy (clipped surrogate + Gaussian log-prob)
+template <int NPL, int A, int HEAD>
+__global__ __launch_bounds__(NTH) void out_head_kernel(OutArgs p) {
+    static_assert(HEAD == 1 || A == 1, "value head: one output");
+    constexpr int N = 64 * NPL;
+    __shared__ float red[NW][A * N];
+    __shared__ float redb[NW][2 * A + 1];              // gb, grad_logσ partials, loss
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c0 = lane * NPL;
+    const int m = p.m;
+
+    float Wr[A][NPL], bias[A], e2[A], ls[A];
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+        load_cols<NPL>(p.W + (long)a * N + c0, Wr[a]);
+        bias[a] = p.b[a];
+        if (HEAD == 1) {
+            ls[a] = p.log_std[a];
+            e2[a] = expf(-2 * ls[a]);
+        }
+    }
+    float gWacc[A][NPL], gbacc[A], glsacc[A];
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+        gbacc[a] = glsacc[a] = 0.f;
+#pragma unroll
+        for (int q = 0; q < NPL; ++q) gWacc[a][q] = 0.f;
+    }
+    float loss = 0.f;
+
+    const int gw = blockIdx.x * NW + w, nwaves = gridDim.x * NW;
+    for (int row = gw; row < m; row += nwaves) {
+        float xv[NPL];
+        load_cols<NPL>(p.x + (long)row * N + c0, xv);
+        float yv[A];
+#pragma unroll
+        for (int a = 0; a < A; ++a) {
+            float part = 0.f;
+#pragma unroll
+            for (int q = 0; q < NPL; ++q) part += xv[q] * Wr[a][q];
+            yv[a] = wsum(part) + bias[a];
+        }
+        float g[A];
+        if (HEAD == 0) {                                   // loss.cu:5-23 (kernels.hip mse_kernel)
+            const float t = p.tgt[row];
+            const float d = t - yv[0];
+            loss += d * d;
+            g[0] = 2 * (yv[0] - t) / (float)m;
+        } else {                                           // kernels.hip policy_head_kernel, per row
+            float act[A];
+#pragma unroll
+            for (int a = 0; a < A; ++a) act[a] = p.action[(long)row * A + a];
+            const float lp = log_prob_row<A>(yv, p.log_std, act);
+            float glp;
+            loss += surrogate(p.adv[row], lp, p.old_lp[row], p.eps, m, &glp);
+#pragma unroll
+            for (int a = 0; a < A; ++a) {
+                const float d = act[a] - yv[a];
+                g[a] = d * e2[a] * glp;
+                glsacc[a] += (-1 + d * d * e2[a]) * glp;
+            }
+        }
+        if (lane == 0) {
+#pragma unroll
+            for (int a = 0; a < A; ++a) p.y[(long)row * A + a] = yv[a];
+        }
+        float gxv[NPL];
+#pragma unroll
+        for (int q = 0; q < NPL; ++q) {
+            float s = 0.f;
+#pragma unroll
+            for (int a = 0; a < A; ++a) s += g[a] * Wr[a][q];
+            gxv[q] = (!p.relu_in || xv[q] > 0.f) ? s : 0.f;
+        }
+        store_cols<NPL>(p.gx + (long)row * N + c0, gxv);
+#pragma unroll
+        for (int a = 0; a < A; ++a) {
+            gbacc[a] += g[a];
+#pragma unroll
+            for (int q = 0; q < NPL; ++q) gWacc[a][q] += g[a] * xv[q];
+        }
+    }
+
+    // workgroup sums in wave order, then one atomic per element
+#pragma unroll
+    for (int a = 0; a < A; ++a)
+#pragma unroll
+        for (int q = 0; q < NPL; ++q) red[w][a * N + c0 + q] = gWacc[a][q];
+    if (lane == 0) {
+#pragma unroll
+        for (int a = 0; a < A; ++a) {
+            redb[w][a] = gbacc[a];
+            redb[w][A + a] = glsacc[a];
+        }
+        redb[w][2 * A] = loss;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < A * N; i += NTH) {
+        float s = 0.f;
+#pragma unroll
+        for (int v = 0; v < NW; ++v) s += red[v][i];
+        atomicAdd(p.gW + i, s);
+    }
+    if (threadIdx.x < A) {
+        float s = 0.f, l = 0.f;
+#pragma unroll
+        for (int v = 0; v < NW; ++v) { s += redb[v][threadIdx.x]; l += redb[v][A + threadIdx.x]; }
+        atomicAdd(p.gb + threadIdx.x, s);
+        if (HEAD == 1) {
+            if (blockIdx.x == 0) l += -p.ent_coeff;                        // ppo.cu:436-438 (D4)
+            atomicAdd(p.grad_log_std + threadIdx.x, l);
+        }
+    }
+    if (threadIdx.x == 0 && p.loss_accum) {
+        float s = 0.f;
+#pragma unroll
+        for (int v = 0; v < NW; ++v) s += redb[v][2 * A];
+        if (HEAD == 0) {
+            atomicAdd(p.loss_accum, s * (1.0f / (float)m));
+        } else {
+            float contrib = -s / m;
+            if (blockIdx.x == 0) {
+                float ent = (float)(A * 0.5 * (1 + log(2 * M_PI)));
+                for (int j = 0; j < A; ++j) ent += ls[j];
+                contrib -= p.ent_coeff * ent;
+            }
+            atomicAdd(p.loss_accum, contrib);
+        }
+    }
+}
+
+template <int NPL, int A, int HEAD>
+void launch(const OutArgs& a) {
+    // about 16 rows per wave, at most 1024 workgroups (4 per CU)
+    int grid = ppo_divup(a.m, NW * 16);
+    if (grid > 1024) grid = 1024;
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL((out_head_kernel<NPL, A, HEAD>), dim3(grid), dim3(NTH), 0, ppo::stream(), a);
+    PPO_LAUNCH_CHECK();
+}
+
+template <int A, int HEAD>
+bool launch_npl(const OutArgs& a) {
+    switch (a.n) {
+        case 64: launch<1, A, HEAD>(a); return true;
+        case 128: launch<2, A, HEAD>(a); return true;
+        case 256: launch<4, A, HEAD>(a); return true;
+        case 512: launch<8, A, HEAD>(a); return true;
+        default: return false;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int phip_out_head_supported(int head, int n, int A) {
+    if (n != 64 && n != 128 && n != 256 && n != 512) return 0;
+    return head == 0 ? A == 1 : (A == 1 || A == 6);
+}
+
+void phip_out_head(int head, const float* x, int relu_in, const float* W, const float* b, int m, int n, int A,
+                   const float* tgt, const float* log_std, const float* action, const float* adv,
+                   const float* old_lp, float eps, float ent_coeff, float* y, float* gx, float* gW, float* gb,
+                   float* grad_log_std, float* loss_accum) {
+    if (m <= 0) return;
+    PPO_REQUIRE(phip_out_head_supported(head, n, A), "phip_out_head: unsupported shape");
+    PPO_REQUIRE(x && W && b && y && gx && gW && gb, "phip_out_head: null operand");
+    PPO_REQUIRE(head == 0 ? tgt != nullptr : (log_std && action && adv && old_lp && grad_log_std),
+                "phip_out_head: missing head inputs");
+    PPO_REQUIRE((((uintptr_t)x | (uintptr_t)gx | (uintptr_t)W) & 15u) == 0, "phip_out_head: unaligned operands");
+    ppo::ProfScope ps(PPO_K_HEAD, 8.0 * m * n);
+    OutArgs a{};
+    a.x = x; a.W = W; a.b = b; a.m = m; a.n = n; a.relu_in = relu_in;
+    a.tgt = tgt; a.log_std = log_std; a.action = action; a.adv = adv; a.old_lp = old_lp;
+    a.eps = eps; a.ent_coeff = ent_coeff;
+    a.y = y; a.gx = gx; a.gW = gW; a.gb = gb; a.grad_log_std = grad_log_std; a.loss_accum = loss_accum;
+    bool ok = false;
+    if (head == 0) ok = launch_npl<1, 0>(a);
+    else if (A == 1) ok = launch_npl<1, 1>(a);
+    else ok = launch_npl<6, 1>(a);
+    PPO_REQUIRE(ok, "phip_out_head: no instantiation");
+}
+
+}  // extern "C"

@@ -260,7 +260,16 @@ void lin_bwd_w(float* gW, const float* g, const float* x, int m, int n, int l) {
     else phip_linear_bwd_w(gW, NULL, g, x, m, n, l);
 }
 
+/* forward through the first `upto` linear layers (fp32 storage; upto = L: the whole network) */
+static void nn_forward_dev_upto(NeuralNetwork* nn, const float* d_x, const int* d_rows, float* d_xcopy, int m,
+                                int upto);
+
 void nn_forward_dev_rows(NeuralNetwork* nn, const float* d_x, const int* d_rows, float* d_xcopy, int m) {
+    nn_forward_dev_upto(nn, d_x, d_rows, d_xcopy, m, nn->num_layers - 1);
+}
+
+static void nn_forward_dev_upto(NeuralNetwork* nn, const float* d_x, const int* d_rows, float* d_xcopy, int m,
+                                int upto) {
     nn_ensure_act(nn, m);
     const int L = nn->num_layers - 1;
     if (nn->dtype == 1) {
@@ -273,7 +282,7 @@ void nn_forward_dev_rows(NeuralNetwork* nn, const float* d_x, const int* d_rows,
     nn->d_x0 = d_rows ? d_xcopy : d_x;
     nn->x0_dtype = 0;
     const float* in = d_x;
-    for (int i = 0; i < L; i++) {
+    for (int i = 0; i < upto; i++) {
         Layer* ly = &nn->layers[i];
         float* out = nn->layers[i + 1].d_input;
         const int n = ly->input_size, l = ly->output_size;
@@ -311,12 +320,22 @@ void nn_backward_dev(NeuralNetwork* nn, const float* d_grad_out, int m, int want
     nn_backward_dev_z(nn, d_grad_out, m, want_grad_x0, 0, -1);
 }
 
+static void nn_backward_dev_top(NeuralNetwork* nn, const float* d_grad_out, int m, int want_grad_x0,
+                                int grads_zero, long reduce_extra, int top);
+
 void nn_backward_dev_z(NeuralNetwork* nn, const float* d_grad_out, int m, int want_grad_x0, int grads_zero,
                        long reduce_extra) {
+    nn_backward_dev_top(nn, d_grad_out, m, want_grad_x0, grads_zero, reduce_extra, nn->num_layers - 1);
+}
+
+/* backward through layers top-1 … 0, starting from the gradient at layer top's input (top = L: the
+ * whole network, from the output gradient; top = L-1: the output layer's backward already ran) */
+static void nn_backward_dev_top(NeuralNetwork* nn, const float* d_grad_out, int m, int want_grad_x0,
+                                int grads_zero, long reduce_extra, int top) {
     nn_ensure_grad(nn, m);
     const int L = nn->num_layers - 1;
     const float* g = d_grad_out;
-    if (nn_is_relu(nn, L - 1)) {      /* output activation: mask a copy (rare; the reference uses "none") */
+    if (top == L && nn_is_relu(nn, L - 1)) {      /* output activation: mask a copy (rare; the reference uses "none") */
         float* top = nn->layers[L].d_grad_x;
         if (top != d_grad_out) phip_d2d(top, d_grad_out, sizeof(float) * (size_t)m * nn->output_size);
         phip_relu_bwd(nn->layers[L].d_input, top, (long)m * nn->output_size);
@@ -329,7 +348,7 @@ void nn_backward_dev_z(NeuralNetwork* nn, const float* d_grad_out, int m, int wa
         if (nn->bits_m != m) die("nn_backward_dev (bf16): backward must follow a forward over the same rows");
         int tg = 0;
         long hi = nn->num_params + (reduce_extra > 0 ? reduce_extra : 0);
-        for (int i = L - 1; i >= 0; i--) {
+        for (int i = top - 1; i >= 0; i--) {
             Layer* ly = &nn->layers[i];
             const void* x = i == 0 ? (const void*)nn->d_x0 : (const void*)ly->d_input;
             phip_linear16_bwd_w(ly->d_grad_weights, ly->d_grad_biases, g, tg, x, i == 0 ? nn->x0_dtype : 1, m,
@@ -352,7 +371,7 @@ void nn_backward_dev_z(NeuralNetwork* nn, const float* d_grad_out, int m, int wa
      * out as one launch (phip_linear_bwd_pair: grad_x tiles fill the CUs grad_W tiles leave).
      * (measured: grad_W on a second queue beside grad_x was slower than back to back) */
     long hi = nn->num_params + (reduce_extra > 0 ? reduce_extra : 0);
-    for (int i = L - 1; i >= 0; i--) {
+    for (int i = top - 1; i >= 0; i--) {
         Layer* ly = &nn->layers[i];
         const float* x = i == 0 ? nn->d_x0 : ly->d_input;
         const int n = ly->input_size, l = ly->output_size;
@@ -375,6 +394,36 @@ void nn_backward_dev_z(NeuralNetwork* nn, const float* d_grad_out, int m, int wa
         if (reduce_extra >= 0) bucket_flush(nn, i, &hi);
     }
     nn->cache_m_backward = m;
+}
+
+/* The output layer fused with the loss head (out_head.hip) for one minibatch step: fp32 storage, at
+ * least one hidden layer, identity output, a supported (width, A), and no deterministic-GEMM request
+ * (ppo_gemm_tune(·, 1)); PPO_OUT_HEAD=0 disables it (read per call). */
+int nn_out_head_ok(const NeuralNetwork* nn, int head) {
+    const char* e = getenv("PPO_OUT_HEAD");
+    if ((e && e[0] == '0') || phip_gemm_deterministic()) return 0;     /* its gW sums use f32 atomics */
+    const int L = nn->num_layers - 1;
+    if (nn->dtype != 0 || L < 2 || nn_is_relu(nn, L - 1)) return 0;
+    return phip_out_head_supported(head, nn->layers[L - 1].input_size, nn->layers[L - 1].output_size);
+}
+
+/* forward (all but the output layer), then the fused output layer + head + output-layer backward,
+ * then the hidden layers' backward — the same results as nn_forward_dev_rows → head kernel →
+ * nn_backward_dev_z up to fp32 re-association of the output layer's sums */
+void nn_out_head_step(NeuralNetwork* nn, int head, const float* d_x, const int* d_rows, float* d_xcopy, int m,
+                      int grads_zero, long reduce_extra, const float* tgt, const float* log_std, const float* action,
+                      const float* adv, const float* old_lp, float eps, float ent_coeff, float* grad_log_std,
+                      float* loss_accum) {
+    const int L = nn->num_layers - 1;
+    nn_forward_dev_upto(nn, d_x, d_rows, d_xcopy, m, L - 1);
+    nn_ensure_grad(nn, m);
+    if (!grads_zero) phip_memset(nn->d_grads, 0, sizeof(float) * (size_t)nn->num_params);
+    Layer* ly = &nn->layers[L - 1];
+    phip_out_head(head, ly->d_input, nn_is_relu(nn, L - 2), ly->d_weights, ly->d_biases, m, ly->input_size,
+                  ly->output_size, tgt, log_std, action, adv, old_lp, eps, ent_coeff, nn->layers[L].d_input,
+                  ly->d_grad_x, ly->d_grad_weights, ly->d_grad_biases, grad_log_std, loss_accum);
+    nn->d_output = nn->layers[L].d_input;
+    nn_backward_dev_top(nn, ly->d_grad_x, m, 0, 1, reduce_extra, L - 1);
 }
 
 /* neural_network.cu:74-105: copies the input into layers[0].d_input first. */

@@ -510,6 +510,7 @@ static void ppo_update_body(PPO* ppo, float gamma, int batch_size, int n_epochs_
     /* gradients cleared by the previous Adam step (not after a loop's last step: a caller may read
      * the last minibatch's gradients after the update) */
     int v_zero = 0, p_zero = 0, ls_zero = 0;
+    const int fuse_v = nn_out_head_ok(V, 0), fuse_p = nn_out_head_ok(mu, 1);
     while (iv < nv || ip < np) {
         /* serial: every value step first (the reference's order); concurrent: issue in proportion */
         const int take_v = iv < nv && (ip >= np || !concurrent || iv * np <= ip * nv);
@@ -520,11 +521,16 @@ static void ppo_update_body(PPO* ppo, float gamma, int batch_size, int n_epochs_
              * reads the buffer rows through them and leaves the gathered copy for its grad_W */
             phip_gather_rows(perm, keys_v[j], k * B, limit, B, S, A, buf->state_p, buf->action_p, buf->logprob_p,
                              buf->advantage_p, buf->adv_target_p, NULL, NULL, NULL, NULL, d->tgt, d->rows);
-            nn_forward_dev_rows(V, buf->state_p, d->rows, d->states, B);
-            phip_mse(V->d_output, d->tgt, B, d->gv, NULL, d->stats + 0);
             /* with a communicator: gradients all-reduced in per-layer buckets as the backward
              * produces them (comm.hip's comm stream), joined before Adam */
-            nn_backward_dev_z(V, d->gv, B, 0, v_zero, comm ? 0 : -1);
+            if (fuse_v) {       /* output layer + MSE + output-layer backward in one pass (out_head.hip) */
+                nn_out_head_step(V, 0, buf->state_p, d->rows, d->states, B, v_zero, comm ? 0 : -1, d->tgt, NULL,
+                                 NULL, NULL, NULL, 0.f, 0.f, NULL, d->stats + 0);
+            } else {
+                nn_forward_dev_rows(V, buf->state_p, d->rows, d->states, B);
+                phip_mse(V->d_output, d->tgt, B, d->gv, NULL, d->stats + 0);
+                nn_backward_dev_z(V, d->gv, B, 0, v_zero, comm ? 0 : -1);
+            }
             phip_allreduce_join();
             v_zero = adam_update_net(ppo->adam_V, ppo->lr_V, V, iv + 1 < nv);
             d->n_v++;
@@ -536,11 +542,18 @@ static void ppo_update_body(PPO* ppo, float gamma, int batch_size, int n_epochs_
             phip_gather_rows(perm, keys_p[j], k * B, limit, B, S, A, buf->state_p, buf->action_p, buf->logprob_p,
                              buf->advantage_p, buf->adv_target_p, NULL, d->actions, d->old_lp, d->adv, NULL,
                              d->rows_p);
-            nn_forward_dev_rows(mu, buf->state_p, d->rows_p, d->states_p, B);
-            phip_policy_head(mu->d_output, pol->d_log_std, d->actions, d->adv, d->old_lp, B, A, ppo->epsilon,
-                             ppo->ent_coeff, d->gmu, pol->d_log_std_grad, d->stats + 1, ls_zero);
             /* μ grads + (top bucket) the log σ gradient behind them */
-            nn_backward_dev_z(mu, d->gmu, B, 0, p_zero, comm ? align4(A) : -1);
+            if (fuse_p) {       /* output layer + clipped surrogate + output-layer backward (out_head.hip) */
+                if (!ls_zero) phip_memset(pol->d_log_std_grad, 0, sizeof(float) * (size_t)A);
+                nn_out_head_step(mu, 1, buf->state_p, d->rows_p, d->states_p, B, p_zero, comm ? align4(A) : -1, NULL,
+                                 pol->d_log_std, d->actions, d->adv, d->old_lp, ppo->epsilon, ppo->ent_coeff,
+                                 pol->d_log_std_grad, d->stats + 1);
+            } else {
+                nn_forward_dev_rows(mu, buf->state_p, d->rows_p, d->states_p, B);
+                phip_policy_head(mu->d_output, pol->d_log_std, d->actions, d->adv, d->old_lp, B, A, ppo->epsilon,
+                                 ppo->ent_coeff, d->gmu, pol->d_log_std_grad, d->stats + 1, ls_zero);
+                nn_backward_dev_z(mu, d->gmu, B, 0, p_zero, comm ? align4(A) : -1);
+            }
             phip_allreduce_join();
             /* ppo.cu:440-442 order; the entropy Adam clears the log σ gradient it read (the next
              * policy head accumulates into zeros) */

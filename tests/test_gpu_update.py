@@ -472,3 +472,37 @@ def test_short_update_elementwise(lib, oracle, net):
     np.testing.assert_allclose(st[0], ref["sum_v_loss"], rtol=1e-3)
     np.testing.assert_allclose(st[2], ref["sum_policy_loss"], rtol=1e-3, atol=1e-5)
     lib.free_ppo(ppo)
+
+
+@pytest.mark.parametrize("cfg", ["humanoid", "halfcheetah_2k"])
+def test_out_head_matches_separate(lib, oracle, cfg, monkeypatch):
+    """The fused output layer + loss head + output-layer backward (out_head.hip; value A = 1 and,
+    for halfcheetah, the A = 6 policy) against the separate launches (PPO_OUT_HEAD=0) from identical
+    state: one value and one policy minibatch, every gradient within the GEMM tolerance, the log
+    σ-gradient and the loss sums within reduction rounding."""
+    sizes, N = CONFIGS[cfg]["sizes"], CONFIGS[cfg]["N"]
+    A = sizes[-1]
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("PPO_OUT_HEAD", mode)
+        ppo = make_ppo(lib, oracle, sizes, N, init_std=0.7, ent_coeff=0.01)
+        mu0, ls0 = policy_state(lib, ppo)
+        buf = synthetic_buffer(oracle, sizes, mu0, ls0, N, seed=21)
+        buf["logprob"] = (buf["logprob"] + np.random.default_rng(5).normal(scale=0.4, size=N)).astype(F32)
+        load_buffer(lib, ppo, buf)
+        lib.ppo_reset_stats(ppo)
+        lib.ppo_update(ppo, 0.99, N, 1, 1, 1, 13)
+        lib.ppo_synchronize()
+        st = (C.c_double * 7)()
+        lib.ppo_read_stats(ppo, st, 7)
+        pol = ppo.contents.policy.contents
+        out[mode] = dict(gV=nn_grads_packed(lib, ppo.contents.V), gmu=nn_grads_packed(lib, pol.mu),
+                         gls=ppo_ffi.d2h(lib, pol.d_log_std_grad, F32, A), stats=np.array(st[:4]),
+                         yV=ppo_ffi.d2h(lib, ppo.contents.V.contents.d_output, F32, N))
+        lib.free_ppo(ppo)
+    a, b = out["0"], out["1"]
+    assert_gemm_close(b["gV"], a["gV"], N, f"{cfg} value grads (fused vs separate)")
+    assert_gemm_close(b["gmu"], a["gmu"], N, f"{cfg} policy grads (fused vs separate)")
+    assert_gemm_close(b["yV"], a["yV"], sizes[-2], f"{cfg} value output (fused vs separate)")
+    assert_rel_close(b["gls"], a["gls"], 1e-3, 1e-4 * max(1.0, np.abs(a["gls"]).max()), "log_std grad")
+    np.testing.assert_allclose(b["stats"], a["stats"], rtol=1e-3, atol=1e-6)
