@@ -18,10 +18,14 @@
 // (the same arithmetic as kernels.hip's mse_kernel / policy_head_kernel given y), and g·W, gᵀ·x use
 // the lane's columns.  gW / gb / grad_logσ / loss: summed over the workgroup's waves through LDS,
 // then one f32 atomic per element per workgroup into outputs that are zero on entry (as the split-K
-// grad_W GEMMs).  The wide policy output (A = 17) keeps the GEMM path: its A·NPL weights and
-// accumulators do not fit the registers of one lane (measured in round 1: spills, 10× slower).
+// grad_W GEMMs).  The wide policy output (A = 17) keeps the separate launches: one wave per row
+// would need 2·17·8 registers for its weights and accumulators alone (the round-1 fused kernel
+// spilled, 10× slower), and splitting each row over two waves (4 columns per lane, 256 VGPRs, one
+// wave per SIMD) measured slower than the separate launches (C4 update 330 -> 347 ms,
+// profiles/r02_out_head_ab.txt).
 #include "dev.h"
 
+#include <algorithm>
 #include <cmath>
 
 namespace {
@@ -98,15 +102,21 @@ __device__ __forceinline__ void store_cols(float* __restrict__ p, const float (&
     }
 }
 
-// HEAD 0: value (A = 1, MSE against tgt); HEAD 1: policy (clipped surrogate + Gaussian log-prob)
-template <int NPL, int A, int HEAD>
+// HEAD 0: value (A = 1, MSE against tgt); HEAD 1: policy (clipped surrogate + Gaussian log-prob).
+// WPR waves share a row (WPR = 2 for wide outputs: each lane then holds half the weights and
+// accumulators); their partial dot products meet in LDS, one barrier per row step.
+template <int NPL, int A, int HEAD, int WPR>
 __global__ __launch_bounds__(NTH) void out_head_kernel(OutArgs p) {
     static_assert(HEAD == 1 || A == 1, "value head: one output");
-    constexpr int N = 64 * NPL;
-    __shared__ float red[NW][A * N];
+    constexpr int N = 64 * NPL * WPR;                  // the layer's input width
+    constexpr int SLOTS = NW / WPR;                    // rows in flight per workgroup
+    extern __shared__ float sm[];
+    float* red = sm;                                   // [SLOTS][A·N] gW partials (after the row loop)
+    float* xch = sm;                                   // [2][SLOTS][WPR][A] partial dots (row loop)
     __shared__ float redb[NW][2 * A + 1];              // gb, grad_logσ partials, loss
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int c0 = lane * NPL;
+    const int slot = w / WPR, part = w % WPR;
+    const int c0 = (part * 64 + lane) * NPL;
     const int m = p.m;
 
     float Wr[A][NPL], bias[A], e2[A], ls[A];
@@ -128,23 +138,46 @@ __global__ __launch_bounds__(NTH) void out_head_kernel(OutArgs p) {
     }
     float loss = 0.f;
 
-    const int gw = blockIdx.x * NW + w, nwaves = gridDim.x * NW;
-    for (int row = gw; row < m; row += nwaves) {
+    int it = 0;
+    for (int base = blockIdx.x * SLOTS; base < m; base += gridDim.x * SLOTS, ++it) {
+        const int row = base + slot;
+        const bool valid = row < m;                    // every wave reaches the barrier
         float xv[NPL];
-        load_cols<NPL>(p.x + (long)row * N + c0, xv);
+        if (valid) load_cols<NPL>(p.x + (long)row * N + c0, xv);
+        else
+#pragma unroll
+            for (int q = 0; q < NPL; ++q) xv[q] = 0.f;
         float yv[A];
 #pragma unroll
         for (int a = 0; a < A; ++a) {
-            float part = 0.f;
+            float part_s = 0.f;
 #pragma unroll
-            for (int q = 0; q < NPL; ++q) part += xv[q] * Wr[a][q];
-            yv[a] = wsum(part) + bias[a];
+            for (int q = 0; q < NPL; ++q) part_s += xv[q] * Wr[a][q];
+            yv[a] = wsum(part_s);
         }
+        if constexpr (WPR > 1) {
+            float* x2 = xch + (it & 1) * (SLOTS * WPR * A);
+            if (lane == 0)
+#pragma unroll
+                for (int a = 0; a < A; ++a) x2[(slot * WPR + part) * A + a] = yv[a];
+            __syncthreads();
+#pragma unroll
+            for (int a = 0; a < A; ++a) {
+                float t = 0.f;
+#pragma unroll
+                for (int q = 0; q < WPR; ++q) t += x2[(slot * WPR + q) * A + a];
+                yv[a] = t;
+            }
+        }
+#pragma unroll
+        for (int a = 0; a < A; ++a) yv[a] += bias[a];
+        if (!valid) continue;
+        const bool owner = part == 0;                  // one wave per row counts the row-wide sums
         float g[A];
         if (HEAD == 0) {                                   // loss.cu:5-23 (kernels.hip mse_kernel)
             const float t = p.tgt[row];
             const float d = t - yv[0];
-            loss += d * d;
+            if (owner) loss += d * d;
             g[0] = 2 * (yv[0] - t) / (float)m;
         } else {                                           // kernels.hip policy_head_kernel, per row
             float act[A];
@@ -152,15 +185,16 @@ __global__ __launch_bounds__(NTH) void out_head_kernel(OutArgs p) {
             for (int a = 0; a < A; ++a) act[a] = p.action[(long)row * A + a];
             const float lp = log_prob_row<A>(yv, p.log_std, act);
             float glp;
-            loss += surrogate(p.adv[row], lp, p.old_lp[row], p.eps, m, &glp);
+            const float sv = surrogate(p.adv[row], lp, p.old_lp[row], p.eps, m, &glp);
+            if (owner) loss += sv;
 #pragma unroll
             for (int a = 0; a < A; ++a) {
                 const float d = act[a] - yv[a];
                 g[a] = d * e2[a] * glp;
-                glsacc[a] += (-1 + d * d * e2[a]) * glp;
+                if (owner) glsacc[a] += (-1 + d * d * e2[a]) * glp;
             }
         }
-        if (lane == 0) {
+        if (owner && lane == 0) {
 #pragma unroll
             for (int a = 0; a < A; ++a) p.y[(long)row * A + a] = yv[a];
         }
@@ -175,17 +209,18 @@ __global__ __launch_bounds__(NTH) void out_head_kernel(OutArgs p) {
         store_cols<NPL>(p.gx + (long)row * N + c0, gxv);
 #pragma unroll
         for (int a = 0; a < A; ++a) {
-            gbacc[a] += g[a];
+            if (owner) gbacc[a] += g[a];
 #pragma unroll
             for (int q = 0; q < NPL; ++q) gWacc[a][q] += g[a] * xv[q];
         }
     }
 
-    // workgroup sums in wave order, then one atomic per element
+    // workgroup sums (row slots in order), then one atomic per element
+    __syncthreads();                                   // the exchange buffer is reused below
 #pragma unroll
     for (int a = 0; a < A; ++a)
 #pragma unroll
-        for (int q = 0; q < NPL; ++q) red[w][a * N + c0 + q] = gWacc[a][q];
+        for (int q = 0; q < NPL; ++q) red[slot * (A * N) + a * N + c0 + q] = gWacc[a][q];
     if (lane == 0) {
 #pragma unroll
         for (int a = 0; a < A; ++a) {
@@ -198,7 +233,7 @@ __global__ __launch_bounds__(NTH) void out_head_kernel(OutArgs p) {
     for (int i = threadIdx.x; i < A * N; i += NTH) {
         float s = 0.f;
 #pragma unroll
-        for (int v = 0; v < NW; ++v) s += red[v][i];
+        for (int v = 0; v < SLOTS; ++v) s += red[v * (A * N) + i];
         atomicAdd(p.gW + i, s);
     }
     if (threadIdx.x < A) {
@@ -229,23 +264,36 @@ __global__ __launch_bounds__(NTH) void out_head_kernel(OutArgs p) {
     }
 }
 
-template <int NPL, int A, int HEAD>
+template <int NPL, int A, int HEAD, int WPR>
 void launch(const OutArgs& a) {
-    // about 16 rows per wave, at most 1024 workgroups (4 per CU)
-    int grid = ppo_divup(a.m, NW * 16);
+    constexpr int N = 64 * NPL * WPR, SLOTS = NW / WPR;
+    const size_t lds = sizeof(float) * (size_t)std::max(SLOTS * A * N, 2 * SLOTS * WPR * A);
+    static_assert(sizeof(float) * SLOTS * A * N <= 150 * 1024, "out_head: LDS");
+    auto kern = out_head_kernel<NPL, A, HEAD, WPR>;
+    if (lds > 64 * 1024) {
+        static bool attr = false;
+        if (!attr) {
+            PPO_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            attr = true;
+        }
+    }
+    // about 16 rows per wave slot, at most 1024 workgroups
+    int grid = ppo_divup(a.m, SLOTS * 16);
     if (grid > 1024) grid = 1024;
     if (grid < 1) grid = 1;
-    hipLaunchKernelGGL((out_head_kernel<NPL, A, HEAD>), dim3(grid), dim3(NTH), 0, ppo::stream(), a);
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(NTH), lds, ppo::stream(), a);
     PPO_LAUNCH_CHECK();
 }
 
+// one wave per row up to width 512; two waves per row at width 1024 (value networks)
 template <int A, int HEAD>
-bool launch_npl(const OutArgs& a) {
+bool launch_n(const OutArgs& a) {
     switch (a.n) {
-        case 64: launch<1, A, HEAD>(a); return true;
-        case 128: launch<2, A, HEAD>(a); return true;
-        case 256: launch<4, A, HEAD>(a); return true;
-        case 512: launch<8, A, HEAD>(a); return true;
+        case 64: launch<1, A, HEAD, 1>(a); return true;
+        case 128: launch<2, A, HEAD, 1>(a); return true;
+        case 256: launch<4, A, HEAD, 1>(a); return true;
+        case 512: launch<8, A, HEAD, 1>(a); return true;
+        case 1024: if constexpr (A == 1) { launch<8, A, HEAD, 2>(a); return true; } return false;
         default: return false;
     }
 }
@@ -255,7 +303,7 @@ bool launch_npl(const OutArgs& a) {
 extern "C" {
 
 int phip_out_head_supported(int head, int n, int A) {
-    if (n != 64 && n != 128 && n != 256 && n != 512) return 0;
+    if (n != 64 && n != 128 && n != 256 && n != 512 && !(n == 1024 && A == 1)) return 0;
     return head == 0 ? A == 1 : (A == 1 || A == 6);
 }
 
@@ -276,9 +324,9 @@ void phip_out_head(int head, const float* x, int relu_in, const float* W, const 
     a.eps = eps; a.ent_coeff = ent_coeff;
     a.y = y; a.gx = gx; a.gW = gW; a.gb = gb; a.grad_log_std = grad_log_std; a.loss_accum = loss_accum;
     bool ok = false;
-    if (head == 0) ok = launch_npl<1, 0>(a);
-    else if (A == 1) ok = launch_npl<1, 1>(a);
-    else ok = launch_npl<6, 1>(a);
+    if (head == 0) ok = launch_n<1, 0>(a);
+    else if (A == 1) ok = launch_n<1, 1>(a);
+    else ok = launch_n<6, 1>(a);
     PPO_REQUIRE(ok, "phip_out_head: no instantiation");
 }
 
