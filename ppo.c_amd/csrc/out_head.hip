@@ -139,14 +139,20 @@ __global__ __launch_bounds__(NTH) void out_head_kernel(OutArgs p) {
     float loss = 0.f;
 
     int it = 0;
-    for (int base = blockIdx.x * SLOTS; base < m; base += gridDim.x * SLOTS, ++it) {
+    const int stride = gridDim.x * SLOTS;
+    // the next row's slice is loaded while this row is processed (one row of latency hidden)
+    float xn[NPL];
+    {
+        const int r0 = blockIdx.x * SLOTS + slot;
+        if (r0 < m) load_cols<NPL>(p.x + (long)r0 * N + c0, xn);
+    }
+    for (int base = blockIdx.x * SLOTS; base < m; base += stride, ++it) {
         const int row = base + slot;
         const bool valid = row < m;                    // every wave reaches the barrier
         float xv[NPL];
-        if (valid) load_cols<NPL>(p.x + (long)row * N + c0, xv);
-        else
 #pragma unroll
-            for (int q = 0; q < NPL; ++q) xv[q] = 0.f;
+        for (int q = 0; q < NPL; ++q) xv[q] = valid ? xn[q] : 0.f;
+        if (row + stride < m) load_cols<NPL>(p.x + (long)(row + stride) * N + c0, xn);
         float yv[A];
 #pragma unroll
         for (int a = 0; a < A; ++a) {
