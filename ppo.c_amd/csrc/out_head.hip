@@ -1,5 +1,5 @@
 // out_head.hip — a minibatch step's output layer fused with its loss head, for narrow outputs
-// (value networks A = 1, small action spaces), fp32 storage.
+// (value networks A = 1, small action spaces): fp32 storage, and bf16 storage for value networks.
 //
 // Replaces four launches per step inside ppo_update:
 //   output-layer forward    y = x·Wᵀ + b                         mat_mul.cu:122-163 (K1+K2)
@@ -64,13 +64,55 @@ __device__ __forceinline__ float surrogate(float adv, float lp, float old_lp, fl
 }
 
 struct OutArgs {
-    const float* x; const float* W; const float* b;   // x [m, n] (the last hidden activation), W [A, n], b [A]
+    const void* x; const void* W; const float* b;     // x [m, n] (the last hidden activation), W [A, n], b [A]
     int m, n, relu_in;                                // relu_in: gx masked by x > 0
     const float* tgt;                                 // value head: targets [m]
     const float* log_std; const float* action; const float* adv; const float* old_lp;   // policy head
     float eps, ent_coeff;
-    float* y; float* gx; float* gW; float* gb; float* grad_log_std; float* loss_accum;
+    float* y; void* gx; float* gW; float* gb; float* grad_log_std; float* loss_accum;
 };
+
+// bf16 storage (bf16 compute mode): NPL elements of 2 B, widened to fp32 exactly
+__device__ __forceinline__ float bf(unsigned short h) { return __builtin_bit_cast(float, (unsigned)h << 16); }
+__device__ __forceinline__ unsigned short to_bf(float f) {          // round to nearest even (as gemm16.hip)
+    typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+    bf16x2 p = {(__bf16)f, (__bf16)0.f};
+    return (unsigned short)(__builtin_bit_cast(unsigned, p) & 0xffffu);
+}
+
+template <int NPL>
+__device__ __forceinline__ void load_cols(const unsigned short* __restrict__ p, float (&v)[NPL]) {
+    if constexpr (NPL == 8) {
+        const uint4 a = *reinterpret_cast<const uint4*>(p);
+        const unsigned w[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) { v[2 * q] = bf((unsigned short)(w[q] & 0xffffu)); v[2 * q + 1] = bf((unsigned short)(w[q] >> 16)); }
+    } else if constexpr (NPL == 4) {
+        const uint2 a = *reinterpret_cast<const uint2*>(p);
+        v[0] = bf((unsigned short)(a.x & 0xffffu)); v[1] = bf((unsigned short)(a.x >> 16));
+        v[2] = bf((unsigned short)(a.y & 0xffffu)); v[3] = bf((unsigned short)(a.y >> 16));
+    } else {
+#pragma unroll
+        for (int q = 0; q < NPL; ++q) v[q] = bf(p[q]);
+    }
+}
+
+template <int NPL>
+__device__ __forceinline__ void store_cols(unsigned short* __restrict__ p, const float (&v)[NPL]) {
+    if constexpr (NPL == 8) {
+        unsigned w[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) w[q] = (unsigned)to_bf(v[2 * q]) | ((unsigned)to_bf(v[2 * q + 1]) << 16);
+        *reinterpret_cast<uint4*>(p) = uint4{w[0], w[1], w[2], w[3]};
+    } else if constexpr (NPL == 4) {
+        const unsigned a = (unsigned)to_bf(v[0]) | ((unsigned)to_bf(v[1]) << 16);
+        const unsigned b = (unsigned)to_bf(v[2]) | ((unsigned)to_bf(v[3]) << 16);
+        *reinterpret_cast<uint2*>(p) = uint2{a, b};
+    } else {
+#pragma unroll
+        for (int q = 0; q < NPL; ++q) p[q] = to_bf(v[q]);
+    }
+}
 
 template <int NPL>
 __device__ __forceinline__ void load_cols(const float* __restrict__ p, float (&v)[NPL]) {
@@ -105,8 +147,15 @@ __device__ __forceinline__ void store_cols(float* __restrict__ p, const float (&
 // HEAD 0: value (A = 1, MSE against tgt); HEAD 1: policy (clipped surrogate + Gaussian log-prob).
 // WPR waves share a row (WPR = 2 for wide outputs: each lane then holds half the weights and
 // accumulators); their partial dot products meet in LDS, one barrier per row step.
-template <int NPL, int A, int HEAD, int WPR>
+// T: storage of x, W and gx — float (fp32 mode) or unsigned short (bf16 mode: x and gx bf16, W the
+// bf16 parameter shadow, and the head gradient rounded to bf16 before its products, as the separate
+// bf16 GEMMs round the fp32 operand they stage)
+template <int NPL, int A, int HEAD, int WPR, typename T>
 __global__ __launch_bounds__(NTH) void out_head_kernel(OutArgs p) {
+    constexpr bool B16 = sizeof(T) == 2;
+    const T* __restrict__ X = static_cast<const T*>(p.x);
+    const T* __restrict__ Wp = static_cast<const T*>(p.W);
+    T* __restrict__ GX = static_cast<T*>(p.gx);
     static_assert(HEAD == 1 || A == 1, "value head: one output");
     constexpr int N = 64 * NPL * WPR;                  // the layer's input width
     constexpr int SLOTS = NW / WPR;                    // rows in flight per workgroup
@@ -122,7 +171,7 @@ __global__ __launch_bounds__(NTH) void out_head_kernel(OutArgs p) {
     float Wr[A][NPL], bias[A], e2[A], ls[A];
 #pragma unroll
     for (int a = 0; a < A; ++a) {
-        load_cols<NPL>(p.W + (long)a * N + c0, Wr[a]);
+        load_cols<NPL>(Wp + (long)a * N + c0, Wr[a]);
         bias[a] = p.b[a];
         if (HEAD == 1) {
             ls[a] = p.log_std[a];
@@ -144,7 +193,7 @@ __global__ __launch_bounds__(NTH) void out_head_kernel(OutArgs p) {
     float xn[NPL];
     {
         const int r0 = blockIdx.x * SLOTS + slot;
-        if (r0 < m) load_cols<NPL>(p.x + (long)r0 * N + c0, xn);
+        if (r0 < m) load_cols<NPL>(X + (long)r0 * N + c0, xn);
     }
     for (int base = blockIdx.x * SLOTS; base < m; base += stride, ++it) {
         const int row = base + slot;
@@ -152,7 +201,7 @@ __global__ __launch_bounds__(NTH) void out_head_kernel(OutArgs p) {
         float xv[NPL];
 #pragma unroll
         for (int q = 0; q < NPL; ++q) xv[q] = valid ? xn[q] : 0.f;
-        if (row + stride < m) load_cols<NPL>(p.x + (long)(row + stride) * N + c0, xn);
+        if (row + stride < m) load_cols<NPL>(X + (long)(row + stride) * N + c0, xn);
         float yv[A];
 #pragma unroll
         for (int a = 0; a < A; ++a) {
@@ -204,6 +253,10 @@ __global__ __launch_bounds__(NTH) void out_head_kernel(OutArgs p) {
 #pragma unroll
             for (int a = 0; a < A; ++a) p.y[(long)row * A + a] = yv[a];
         }
+        if constexpr (B16) {
+#pragma unroll
+            for (int a = 0; a < A; ++a) g[a] = bf(to_bf(g[a]));
+        }
         float gxv[NPL];
 #pragma unroll
         for (int q = 0; q < NPL; ++q) {
@@ -212,7 +265,7 @@ __global__ __launch_bounds__(NTH) void out_head_kernel(OutArgs p) {
             for (int a = 0; a < A; ++a) s += g[a] * Wr[a][q];
             gxv[q] = (!p.relu_in || xv[q] > 0.f) ? s : 0.f;
         }
-        store_cols<NPL>(p.gx + (long)row * N + c0, gxv);
+        store_cols<NPL>(GX + (long)row * N + c0, gxv);
 #pragma unroll
         for (int a = 0; a < A; ++a) {
             if (owner) gbacc[a] += g[a];
@@ -270,12 +323,12 @@ __global__ __launch_bounds__(NTH) void out_head_kernel(OutArgs p) {
     }
 }
 
-template <int NPL, int A, int HEAD, int WPR>
+template <int NPL, int A, int HEAD, int WPR, typename T>
 void launch(const OutArgs& a) {
     constexpr int N = 64 * NPL * WPR, SLOTS = NW / WPR;
     const size_t lds = sizeof(float) * (size_t)std::max(SLOTS * A * N, 2 * SLOTS * WPR * A);
     static_assert(sizeof(float) * SLOTS * A * N <= 150 * 1024, "out_head: LDS");
-    auto kern = out_head_kernel<NPL, A, HEAD, WPR>;
+    auto kern = out_head_kernel<NPL, A, HEAD, WPR, T>;
     if (lds > 64 * 1024) {
         static bool attr = false;
         if (!attr) {
@@ -292,14 +345,14 @@ void launch(const OutArgs& a) {
 }
 
 // one wave per row up to width 512; two waves per row at width 1024 (value networks)
-template <int A, int HEAD>
+template <int A, int HEAD, typename T>
 bool launch_n(const OutArgs& a) {
     switch (a.n) {
-        case 64: launch<1, A, HEAD, 1>(a); return true;
-        case 128: launch<2, A, HEAD, 1>(a); return true;
-        case 256: launch<4, A, HEAD, 1>(a); return true;
-        case 512: launch<8, A, HEAD, 1>(a); return true;
-        case 1024: if constexpr (A == 1) { launch<8, A, HEAD, 2>(a); return true; } return false;
+        case 64: launch<1, A, HEAD, 1, T>(a); return true;
+        case 128: launch<2, A, HEAD, 1, T>(a); return true;
+        case 256: launch<4, A, HEAD, 1, T>(a); return true;
+        case 512: launch<8, A, HEAD, 1, T>(a); return true;
+        case 1024: if constexpr (A == 1) { launch<8, A, HEAD, 2, T>(a); return true; } return false;
         default: return false;
     }
 }
@@ -313,9 +366,9 @@ int phip_out_head_supported(int head, int n, int A) {
     return head == 0 ? A == 1 : (A == 1 || A == 6);
 }
 
-void phip_out_head(int head, const float* x, int relu_in, const float* W, const float* b, int m, int n, int A,
-                   const float* tgt, const float* log_std, const float* action, const float* adv,
-                   const float* old_lp, float eps, float ent_coeff, float* y, float* gx, float* gW, float* gb,
+void phip_out_head(int head, int bf16, const void* x, int relu_in, const void* W, const float* b, int m, int n,
+                   int A, const float* tgt, const float* log_std, const float* action, const float* adv,
+                   const float* old_lp, float eps, float ent_coeff, float* y, void* gx, float* gW, float* gb,
                    float* grad_log_std, float* loss_accum) {
     if (m <= 0) return;
     PPO_REQUIRE(phip_out_head_supported(head, n, A), "phip_out_head: unsupported shape");
@@ -329,10 +382,14 @@ void phip_out_head(int head, const float* x, int relu_in, const float* W, const 
     a.tgt = tgt; a.log_std = log_std; a.action = action; a.adv = adv; a.old_lp = old_lp;
     a.eps = eps; a.ent_coeff = ent_coeff;
     a.y = y; a.gx = gx; a.gW = gW; a.gb = gb; a.grad_log_std = grad_log_std; a.loss_accum = loss_accum;
+    using b16 = unsigned short;
     bool ok = false;
-    if (head == 0) ok = launch_n<1, 0>(a);
-    else if (A == 1) ok = launch_n<1, 1>(a);
-    else ok = launch_n<6, 1>(a);
+    if (bf16) {
+        PPO_REQUIRE(head == 0, "phip_out_head: bf16 storage for the value head only");
+        ok = launch_n<1, 0, b16>(a);
+    } else if (head == 0) ok = launch_n<1, 0, float>(a);
+    else if (A == 1) ok = launch_n<1, 1, float>(a);
+    else ok = launch_n<6, 1, float>(a);
     PPO_REQUIRE(ok, "phip_out_head: no instantiation");
 }
 

@@ -127,13 +127,14 @@ void phip_axpy(float* y, const float* x, long count);
 void phip_mse(const float* y, const float* t, long count, float* grad, float* d_loss, float* d_loss_accum);
 /* out_head.hip: output layer forward + loss head + output-layer backward in one pass (ppo_update;
  * head 0 = value, A = 1, MSE against tgt; 1 = policy, clipped surrogate); gW / gb / grad_log_std
- * accumulated into zeroed outputs, loss into loss_accum; widths 64/128/256/512, A ∈ {1, 6} */
+ * accumulated into zeroed outputs, loss into loss_accum; widths 64…1024, A ∈ {1, 6}; bf16 != 0:
+ * x, W and gx stored bf16 (bf16 compute mode, value head) */
 int  phip_out_head_supported(int head, int n, int A);
 /* gemm.hip: 1 when ppo_gemm_tune(·, 1) asked for atomic-free (deterministic) gradient products */
 int  phip_gemm_deterministic(void);
-void phip_out_head(int head, const float* x, int relu_in, const float* W, const float* b, int m, int n, int A,
-                   const float* tgt, const float* log_std, const float* action, const float* adv,
-                   const float* old_lp, float eps, float ent_coeff, float* y, float* gx, float* gW, float* gb,
+void phip_out_head(int head, int bf16, const void* x, int relu_in, const void* W, const float* b, int m, int n,
+                   int A, const float* tgt, const float* log_std, const float* action, const float* adv,
+                   const float* old_lp, float eps, float ent_coeff, float* y, void* gx, float* gW, float* gb,
                    float* grad_log_std, float* loss_accum);
 void phip_log_prob(const float* mu, const float* log_std, const float* action, float* out, int m, int A);
 void phip_log_prob_bwd(const float* mu, const float* log_std, const float* action, const float* grad_in,

@@ -201,7 +201,8 @@ void nn_ensure_grad(NeuralNetwork* nn, int m) {
 /* Forward over m rows.  With d_rows != NULL, input row r is d_x[d_rows[r]] (the minibatch gather
  * fused into layer 0), and the gathered rows are written to d_xcopy, which backward then uses as
  * layer 0's input. */
-static void nn_forward_dev_bf16(NeuralNetwork* nn, const float* d_x, const int* d_rows, float* d_xcopy, int m) {
+static void nn_forward_dev_bf16(NeuralNetwork* nn, const float* d_x, const int* d_rows, float* d_xcopy, int m,
+                                int upto) {
     const int L = nn->num_layers - 1;
     nn->d_x0 = d_rows ? d_xcopy : d_x;
     nn->x0_dtype = d_rows ? 1 : 0;                 /* the gathered copy is written as bf16 */
@@ -215,7 +216,7 @@ static void nn_forward_dev_bf16(NeuralNetwork* nn, const float* d_x, const int* 
         d_rows = NULL;
         d_xcopy = NULL;
     }
-    for (int i = 0; i < L; i++) {
+    for (int i = 0; i < upto; i++) {
         Layer* ly = &nn->layers[i];
         float* out = nn->layers[i + 1].d_input;    /* hidden: bf16 storage; network output: fp32 */
         const int tout = i == L - 1 ? 0 : 1;
@@ -273,7 +274,7 @@ static void nn_forward_dev_upto(NeuralNetwork* nn, const float* d_x, const int* 
     nn_ensure_act(nn, m);
     const int L = nn->num_layers - 1;
     if (nn->dtype == 1) {
-        nn_forward_dev_bf16(nn, d_x, d_rows, d_xcopy, m);
+        nn_forward_dev_bf16(nn, d_x, d_rows, d_xcopy, m, upto);
         nn->bits_m = m;
         nn->cache_m_forward = m;
         nn->d_output = nn->layers[L].d_input;
@@ -346,7 +347,7 @@ static void nn_backward_dev_top(NeuralNetwork* nn, const float* d_grad_out, int 
     if (!grads_zero) phip_memset(nn->d_grads, 0, sizeof(float) * (size_t)nn->num_params);
     if (nn->dtype == 1) {      /* bf16 mode: hidden gradients stored bf16, the top one (heads) fp32 */
         if (nn->bits_m != m) die("nn_backward_dev (bf16): backward must follow a forward over the same rows");
-        int tg = 0;
+        int tg = top == L ? 0 : 1;             /* below a fused output layer: its bf16 grad_x */
         long hi = nn->num_params + (reduce_extra > 0 ? reduce_extra : 0);
         for (int i = top - 1; i >= 0; i--) {
             Layer* ly = &nn->layers[i];
@@ -396,14 +397,16 @@ static void nn_backward_dev_top(NeuralNetwork* nn, const float* d_grad_out, int 
     nn->cache_m_backward = m;
 }
 
-/* The output layer fused with the loss head (out_head.hip) for one minibatch step: fp32 storage, at
- * least one hidden layer, identity output, a supported (width, A), and no deterministic-GEMM request
- * (ppo_gemm_tune(·, 1)); PPO_OUT_HEAD=0 disables it (read per call). */
+/* The output layer fused with the loss head (out_head.hip) for one minibatch step: at least one
+ * hidden layer, identity output, a supported (width, A) — fp32 storage, or bf16 storage for the value
+ * head — and no deterministic-GEMM request (ppo_gemm_tune(·, 1)); PPO_OUT_HEAD=0 disables it (read
+ * per call). */
 int nn_out_head_ok(const NeuralNetwork* nn, int head) {
     const char* e = getenv("PPO_OUT_HEAD");
     if ((e && e[0] == '0') || phip_gemm_deterministic()) return 0;     /* its gW sums use f32 atomics */
     const int L = nn->num_layers - 1;
-    if (nn->dtype != 0 || L < 2 || nn_is_relu(nn, L - 1)) return 0;
+    if (L < 2 || nn_is_relu(nn, L - 1)) return 0;
+    if (nn->dtype == 1 && (head != 0 || nn->param_offset[L - 1] % 8 != 0)) return 0;   /* W shadow: 16-B rows */
     return phip_out_head_supported(head, nn->layers[L - 1].input_size, nn->layers[L - 1].output_size);
 }
 
@@ -419,9 +422,12 @@ void nn_out_head_step(NeuralNetwork* nn, int head, const float* d_x, const int* 
     nn_ensure_grad(nn, m);
     if (!grads_zero) phip_memset(nn->d_grads, 0, sizeof(float) * (size_t)nn->num_params);
     Layer* ly = &nn->layers[L - 1];
-    phip_out_head(head, ly->d_input, nn_is_relu(nn, L - 2), ly->d_weights, ly->d_biases, m, ly->input_size,
-                  ly->output_size, tgt, log_std, action, adv, old_lp, eps, ent_coeff, nn->layers[L].d_input,
-                  ly->d_grad_x, ly->d_grad_weights, ly->d_grad_biases, grad_log_std, loss_accum);
+    const int b16 = nn->dtype == 1;            /* bf16 mode: bf16 activation / gradient, the W shadow */
+    phip_out_head(head, b16, ly->d_input, nn_is_relu(nn, L - 2), b16 ? (const void*)(nn->d_w16 + nn->param_offset[L - 1])
+                                                                     : (const void*)ly->d_weights,
+                  ly->d_biases, m, ly->input_size, ly->output_size, tgt, log_std, action, adv, old_lp, eps, ent_coeff,
+                  nn->layers[L].d_input, ly->d_grad_x, ly->d_grad_weights, ly->d_grad_biases, grad_log_std,
+                  loss_accum);
     nn->d_output = nn->layers[L].d_input;
     nn_backward_dev_top(nn, ly->d_grad_x, m, 0, 1, reduce_extra, L - 1);
 }

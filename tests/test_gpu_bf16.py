@@ -137,3 +137,32 @@ def test_bf16_update_tracks_fp32(lib):
     assert abs(s16[2] - s32[2]) <= 0.05 * abs(s32[2]) + 1e-3, (s16, s32)
     cos = float(d16 @ d32 / (np.linalg.norm(d16) * np.linalg.norm(d32) + 1e-30))
     assert cos > 0.9, cos
+
+
+def test_bf16_out_head_matches_separate(lib, monkeypatch):
+    """bf16 mode's fused value head (out_head.hip with bf16 x / gx and the bf16 weight shadow; C5's
+    1024-wide value network) against the separate bf16 launches (PPO_OUT_HEAD=0) from identical state:
+    one value minibatch, value output, every value gradient and the loss sums within bf16 tolerance
+    (the two paths round the same fp32 values to bf16; sums differ in order only)."""
+    sizes, T, E = [1024, 1024, 1024, 17], 512, 8
+    N = T * E
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("PPO_OUT_HEAD", mode)
+        ppo_ffi.C.CDLL("libc.so.6").srand(78)
+        ppo = lib.create_ppo(ppo_ffi.c_strings(["relu", "relu", "none"]), ppo_ffi.c_ints(sizes), 4, N, 3e-4, 3e-4,
+                             0.95, 0.2, 0.0, 1.0, True)
+        assert lib.ppo_set_compute_dtype(ppo, 1) == 0
+        lib.ppo_fill_synthetic(ppo, E, T, 98, 1.0 / 500)
+        lib.ppo_reset_stats(ppo)
+        lib.ppo_update(ppo, 0.99, N, 1, 1, 1, 13)
+        lib.ppo_synchronize()
+        st = (ppo_ffi.C.c_double * 7)()
+        lib.ppo_read_stats(ppo, st, 7)
+        V = ppo.contents.V
+        out[mode] = (nn_grads_packed(lib, V), ppo_ffi.d2h(lib, V.contents.d_output, F32, N), np.array(st[:4]))
+        lib.free_ppo(ppo)
+    (g0, y0, s0), (g1, y1, s1) = out["0"], out["1"]
+    close(y1, y0, 1e-4, "value output (fused vs separate)")
+    close(g1, g0, 2e-3, "value grads (fused vs separate)")
+    np.testing.assert_allclose(s1, s0, rtol=1e-3, atol=1e-6)
