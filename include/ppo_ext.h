@@ -135,6 +135,8 @@ int    ppo_gemm_x3_tune(int force_cfg, int splitk_target);
  * launched with PPO_X3_ABLATE=32 — s_memtime at start, after the prologue, after the mainloop, at
  * the end; s_memrealtime (100 MHz, one clock for every XCD) at start and end; returns the slots */
 int    ppo_x3_stamps(unsigned long long* out, int n);
+/* diagnostic: the same for the double-buffered bf16 GEMM (gemm16.hip, -DPPO_G16_ABLATE=32 builds; else 0) */
+int    ppo_g16_stamps(unsigned long long* out, int n);
 /* average device µs of one x3 launch (fp32 operands; op as ppo_bench_gemm) */
 double ppo_bench_gemm_x3(int op, int m, int n, int l, int iters, int cfg, int splitk_target);
 

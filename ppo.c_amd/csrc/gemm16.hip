@@ -37,6 +37,16 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int NT_ = 256;
 
+#ifndef PPO_G16_ABLATE
+#define PPO_G16_ABLATE 0          // diagnostic builds only (tools/build_variant.sh): 1 no MFMA, 2 no epilogue
+#endif                            // stores, 4 no steady-state global loads, 8 no steady-state LDS stores,
+                                  // 16 no fragment reads, 32 stamps, 64 no bias / mask loads
+#if PPO_G16_ABLATE & 32
+// s_memtime of wave 0 of each workgroup: start, after the mainloop, epilogue issued, stores drained;
+// s_memrealtime (100 MHz) at start and drained
+__device__ unsigned long long g_g16_stamps[8192 * 8];
+#endif
+
 enum Op { OP_NT = 0, OP_NN = 1, OP_TN = 2 };
 
 struct Args {
@@ -48,6 +58,7 @@ struct Args {
     float* gbias;
     int kchunk, splits, tiles_m, tiles_n;
     int vec;
+    int cvec;                             // bf16 C: N and ldc multiples of 8, C 16-B aligned (LDS-staged epilogue)
 };
 
 // fp32 → bf16, round to nearest even (NaN stays NaN: v_cvt_pk_bf16_f32)
@@ -440,17 +451,40 @@ __global__ __launch_bounds__(NTH, 1) void gemm_bf16_db_kernel(Args a) {
         sa.load(PA, a.lda, m0, a.M, j * BK, K, vec, tid);
         sb.load(PB, a.ldb, n0, a.N, j * BK, K, vec, tid);
     };
+    constexpr int AB = PPO_G16_ABLATE;
+    auto stamp = [&](int slot) {
+#if PPO_G16_ABLATE & 32
+        if (tid == 0 && b < 8192) {
+            g_g16_stamps[b * 8 + slot] = __builtin_amdgcn_s_memtime();
+            if (slot == 0 || slot == 3) g_g16_stamps[b * 8 + 4 + slot / 3] = __builtin_amdgcn_s_memrealtime();
+        }
+#endif
+        (void)slot;
+    };
+    stamp(0);
     auto kstep = [&](const unsigned short* img, int ks) {
         bf16x8 fa[TM], fb[TN];
+        if constexpr (AB & 16) {
 #pragma unroll
-        for (int i = 0; i < TM; ++i) fa[i] = SA::frag(img, wm * WM + i * 32 + r, ks, lane);
+            for (int i = 0; i < TM; ++i) fa[i] = __builtin_bit_cast(bf16x8, u32x4{(unsigned)ks, 1u, 2u, 3u});
 #pragma unroll
-        for (int j = 0; j < TN; ++j) fb[j] = SB::frag(img + SA::IMG, wn * WN + j * 32 + r, ks, lane);
+            for (int j = 0; j < TN; ++j) fb[j] = __builtin_bit_cast(bf16x8, u32x4{(unsigned)lane, 1u, 2u, 3u});
+        } else {
+#pragma unroll
+            for (int i = 0; i < TM; ++i) fa[i] = SA::frag(img, wm * WM + i * 32 + r, ks, lane);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) fb[j] = SB::frag(img + SA::IMG, wn * WN + j * 32 + r, ks, lane);
+        }
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int j = 0; j < TN; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+            for (int j = 0; j < TN; ++j) {
+                if constexpr (AB & 1) {
+                    acc[i][j][0] += __builtin_bit_cast(u32x4, fa[i])[0] ^ __builtin_bit_cast(u32x4, fb[j])[1];
+                } else {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+                }
+            }
     };
 
     const int nk = (K + BK - 1) / BK;
@@ -470,12 +504,12 @@ __global__ __launch_bounds__(NTH, 1) void gemm_bf16_db_kernel(Args a) {
         kstep(cur, 0);
         __builtin_amdgcn_sched_barrier(0);
         kstep(cur, 1);
-        sa.store(nxt, tid);
+        if constexpr (!(AB & 8)) sa.store(nxt, tid);
         __builtin_amdgcn_sched_barrier(0);
         kstep(cur, 2);
-        sb.store(nxt + SA::IMG, tid);
+        if constexpr (!(AB & 8)) sb.store(nxt + SA::IMG, tid);
         __builtin_amdgcn_sched_barrier(0);
-        load(j + 2);
+        if constexpr (!(AB & 4)) load(j + 2);
         kstep(cur, 3);
         __syncthreads();
     }
@@ -491,6 +525,116 @@ __global__ __launch_bounds__(NTH, 1) void gemm_bf16_db_kernel(Args a) {
         __syncthreads();
     }
 
+    stamp(1);
+    if constexpr (AB & 2) {                                   // keep the accumulators live
+        float t = 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int jj = 0; jj < TN; ++jj)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) t += acc[i][jj][e];
+        if (t == 1234.5f) static_cast<float*>(a.C)[tid] = t;
+        return;
+    }
+    // bf16 output: the tile goes through LDS (free after the last barrier) as packed column pairs,
+    // then out as 16-B stores, 32 lanes per 512-B row segment; the ReLU′ bits (forward) and the
+    // incoming mask (grad_x) are applied on that row-major read-back, 8 columns per lane, so the
+    // register phase is branch-free (measured at C5: the per-element ballots, mask loads and 2-B
+    // stores of the generic epilogue took 14 of the forward's 53 µs and 8 of grad_x's 48 µs)
+    if constexpr (sizeof(TC) == 2) {
+        if (a.cvec) {
+            constexpr int CP = BN + 32;                       // pitch ≡ 16 dwords (mod 32): rows a, a+1 of
+            static_assert((size_t)BM * CP <= 2 * (size_t)BUF, "gemm16 (db): C image exceeds LDS");  // a write
+            unsigned short* const cimg = lds;                 // on disjoint banks
+            const bool odd = r & 1;
+            float bcol[TN];
+#pragma unroll
+            for (int jj = 0; jj < TN; ++jj) {
+                const int col = n0 + wn * WN + jj * 32 + r;
+                bcol[jj] = (OP == OP_NT && a.bias && !(AB & 64)) ? a.bias[col < a.N ? col : a.N - 1] : 0.f;
+            }
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int jj = 0; jj < TN; ++jj) {
+                    float vv[16];
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) {
+                        float v = acc[i][jj][e];
+                        if (OP == OP_NT) {
+                            v += bcol[jj];
+                            if (a.relu) v = v > 0.f ? v : 0.f;
+                        }
+                        vv[e] = v;
+                    }
+                    // lanes r, r^1 swap one value (DPP): the even lane writes row e's pair of columns
+                    // (r, r+1), the odd lane row e+1's
+#pragma unroll
+                    for (int e = 0; e < 16; e += 2) {
+                        const float send = odd ? vv[e] : vv[e + 1];
+                        const float recv = __builtin_bit_cast(
+                            float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), 0xB1, 0xF, 0xF, true));
+                        const float lo = odd ? recv : vv[e], hi = odd ? vv[e + 1] : recv;
+                        const int lrow = wm * WM + i * 32 + 4 * h + (e & 3) + 8 * (e >> 2) + (odd ? 1 : 0);
+                        *reinterpret_cast<unsigned*>(cimg + lrow * CP + wn * WN + jj * 32 + (r & ~1)) = pack2(lo, hi);
+                    }
+                }
+            __syncthreads();
+            constexpr int CH = BN / 8;                        // 16-B chunks per tile row (4 per 32-bit word)
+            constexpr int IT = BM * CH / NTH;
+            unsigned short* __restrict__ C = static_cast<unsigned short*>(a.C);
+            unsigned mword[IT];
+            if (OP == OP_NN) {                                // grad_x: the mask words, all loads first
+#pragma unroll
+                for (int it = 0; it < IT; ++it) {
+                    const int idx = tid + it * NTH;
+                    const int grow = min(m0 + idx / CH, a.M - 1), gcol = n0 + (idx % CH) * 8;
+                    mword[it] = (a.bits_in && !(AB & 64)) ? a.bits_in[(long)grow * a.wpr + (min(gcol, a.N - 1) >> 5)]
+                                                           : ~0u;
+                }
+            }
+#pragma unroll
+            for (int it = 0; it < IT; ++it) {
+                const int idx = tid + it * NTH;
+                const int row = idx / CH, ch = idx % CH;
+                const int grow = m0 + row, gcol = n0 + ch * 8;
+                u32x4 v = *reinterpret_cast<const u32x4*>(cimg + row * CP + ch * 8);
+                if (OP == OP_NN) {
+                    const unsigned byte = mword[it] >> (8 * (ch & 3));
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const unsigned keep = (0xffffu * ((byte >> (2 * q)) & 1u)) | (0xffff0000u * ((byte >> (2 * q + 1)) & 1u));
+                        v[q] &= keep;
+                    }
+                }
+                const bool ok = grow < a.M && gcol < a.N;
+                if (ok) *reinterpret_cast<u32x4*>(C + (long)grow * a.ldc + gcol) = v;
+                if (OP == OP_NT && a.bits_out) {
+                    // bit c of the byte: column gcol + c stored > 0 (post-ReLU values are ≥ +0)
+                    unsigned byte = 0;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        byte |= (unsigned)((short)(v[q] & 0xffffu) > 0) << (2 * q);
+                        byte |= (unsigned)((short)(v[q] >> 16) > 0) << (2 * q + 1);
+                    }
+                    if (!ok) byte = 0;                      // columns past N carry no bits
+                    // the 4 lanes of a quad hold the 4 bytes of one 32-column word (ch & 3 = lane & 3)
+                    const int b1 = __builtin_amdgcn_mov_dpp((int)byte, 0x55, 0xF, 0xF, true);   // quad lane 1
+                    const int b2 = __builtin_amdgcn_mov_dpp((int)byte, 0xAA, 0xF, 0xF, true);   // quad lane 2
+                    const int b3 = __builtin_amdgcn_mov_dpp((int)byte, 0xFF, 0xF, 0xF, true);   // quad lane 3
+                    const unsigned word = byte | ((unsigned)b1 << 8) | ((unsigned)b2 << 16) | ((unsigned)b3 << 24);
+                    if ((ch & 3) == 0 && ok) a.bits_out[(long)grow * a.wpr + (gcol >> 5)] = word;
+                }
+            }
+            if constexpr ((AB & 32) != 0) {
+                stamp(2);
+                __builtin_amdgcn_s_waitcnt(0);
+                stamp(3);
+            }
+            return;
+        }
+    }
     // epilogue (as gemm_bf16_kernel): every load a block needs is issued before its stores
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -588,6 +732,7 @@ void launch_db(Args a) {
     constexpr size_t lds = 2 * sizeof(unsigned short) *
                            (Stage16<BM, BK, false, TA, NTH>::IMG + Stage16<BN, BK, OP == OP_NN, TB, NTH>::IMG);
     static_assert(lds <= 160 * 1024, "gemm16 (db): LDS images exceed 160 KiB");
+    a.cvec = a.N % 8 == 0 && a.ldc % 8 == 0 && ((uintptr_t)a.C & 15u) == 0;
     auto kern = gemm_bf16_db_kernel<OP, BM, BN, WM_, BK, NTH, TA, TB, TC>;
     static bool attr = false;                          // once per instantiation
     if (!attr) {
@@ -776,6 +921,17 @@ double ppo_bench_gemm16(int op, int m, int n, int l, int iters, int cfg, int spl
     g_split16 = saved_split;
     phip_free(x); phip_free(W); phip_free(y); phip_free(tmp); phip_free(b); phip_free(gw); phip_free(bits);
     return 1000.0 * ms / (iters > 0 ? iters : 1);
+}
+
+int ppo_g16_stamps(unsigned long long* out, int n) {
+#if PPO_G16_ABLATE & 32
+    phip_sync();
+    PPO_CHECK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_g16_stamps), sizeof(unsigned long long) * (size_t)std::min(n, 8192 * 8)));
+    return 8192 * 8;
+#else
+    (void)out; (void)n;
+    return 0;
+#endif
 }
 
 }  // extern "C"

@@ -110,6 +110,7 @@ _SIGS = {
     "ppo_gemm_x3_tune": (C.c_int, [C.c_int, C.c_int]),
     "ppo_bench_gemm_x3": (C.c_double, [C.c_int] * 7),
     "ppo_x3_stamps": (C.c_int, [C.POINTER(C.c_ulonglong), C.c_int]),
+    "ppo_g16_stamps": (C.c_int, [C.POINTER(C.c_ulonglong), C.c_int]),
     "ppo_set_compute_dtype": (C.c_int, [_P, C.c_int]),
     "ppo_rollout_device": (None, [_P, C.c_int, C.c_int, C.c_int, C.c_ulonglong]),
     "nn_set_compute_dtype": (C.c_int, [_P, C.c_int]),
