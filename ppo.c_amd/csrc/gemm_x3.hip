@@ -486,8 +486,75 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
         if (t == 12345.678f) a.C[tid] = 1.f;
         return;
     }
-    // epilogue: 32×32 accumulator block (i, j): lane (r, h) holds column r, rows 4h + (e&3) + 8(e>>2);
-    // every load a block needs (bias, ReLU′ bit words) is issued before its stores
+    // forward / grad_x epilogue: 32×32 accumulator block (i, j): lane (r, h) holds column r, rows
+    // 4h + (e&3) + 8(e>>2).  Branch-free per element: the bias loads hoisted, the ReLU′-bit ballots
+    // in a loop version of their own, grad_x's mask words brought into LDS by one coalesced pass
+    // (they were 16 dependent loads per block).  Element stores in the accumulator layout (each wave
+    // store: two 128-B row segments).
+    if constexpr (OP != OP_TN) {
+        float bcol[TN];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int col = n0 + wn * WN + j * 32 + r;
+            bcol[j] = (OP == OP_NT && a.bias) ? a.bias[col < a.N ? col : a.N - 1] : 0.f;
+        }
+        constexpr int WPT = BN / 32;                            // mask words per tile row
+        static_assert(BM * WPT * 4 <= KG * 2 * BUF * 2, "x3 epilogue: mask words exceed LDS");
+        unsigned* const mk = reinterpret_cast<unsigned*>(lds);  // images no longer read (last barrier)
+        const bool masked = OP == OP_NN && a.bits_in != nullptr;
+        if (masked) {
+            for (int idx = tid; idx < BM * WPT; idx += NTH) {
+                const int grow = min(m0 + idx / WPT, a.M - 1);
+                const int gw = min((n0 >> 5) + idx % WPT, a.wpr - 1);
+                mk[idx] = a.bits_in[(long)grow * a.wpr + gw];
+            }
+            __syncthreads();
+        }
+        auto body = [&](auto BITSc) {
+            constexpr bool BITS = decltype(BITSc)::value;
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    const int c0 = n0 + wn * WN + j * 32;
+                    const int col = c0 + r;
+                    const int lr0 = wm * WM + i * 32 + 4 * h;      // tile row of element 0
+                    const int r0 = m0 + lr0;
+                    const bool col_ok = col < a.N;
+                    unsigned word = 0;
+#pragma unroll
+                    for (int e = 0; e < 16; ++e) {
+                        const int dr = (e & 3) + 8 * (e >> 2);
+                        const int row = r0 + dr;
+                        const bool ok = col_ok && row < a.M;
+                        float v = acc[i][j][e];
+                        float* dst = a.C + (long)row * a.ldc + col;
+                        if (OP == OP_NT) {
+                            v += bcol[j];
+                            if (a.relu) v = v > 0.f ? v : 0.f;
+                            if (ok) *dst = v;
+                            if constexpr (BITS) {
+                                const unsigned long long bb = __ballot(ok && v > 0.f);
+                                const unsigned half = h ? (unsigned)(bb >> 32) : (unsigned)bb;
+                                word = r == e ? half : word;
+                            }
+                        } else {
+                            if (masked && !((mk[(lr0 + dr) * WPT + ((c0 - n0) >> 5)] >> r) & 1u)) v = 0.f;
+                            if (ok) *dst = v;
+                        }
+                    }
+                    if (BITS && r < 16) {
+                        const int row = r0 + (r & 3) + 8 * (r >> 2);
+                        if (row < a.M && c0 < a.N) a.bits_out[(long)row * a.wpr + (c0 >> 5)] = word;
+                    }
+                }
+        };
+        if (OP == OP_NT && a.bits_out) body(T{});
+        else body(F{});
+        if (ABL & 32) stamp(3);
+        return;
+    }
+    // grad_W epilogue: every load a block needs is issued before its stores
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll

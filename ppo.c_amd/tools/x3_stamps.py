@@ -16,13 +16,14 @@ import ppo_ffi  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--lib", default=None)
+ap.add_argument("--op", type=int, default=0, help="0 forward, 1 grad_x")
 ap.add_argument("shape", nargs="*", type=int, default=[32768, 512, 512])
 args = ap.parse_args()
 lib = ppo_ffi.load(args.lib or os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "lib", "variants", "libppo_diag.so"))
 lib.ppo_set_device(0)
 m, n, l = args.shape
-lib.ppo_bench_gemm_x3(0, m, n, l, 400, 0, 0)          # ≥ 2 s of back-to-back launches: settled clock
-us = lib.ppo_bench_gemm_x3(0, m, n, l, 50, 0, 0)
+lib.ppo_bench_gemm_x3(args.op, m, n, l, 400, 0, 0)          # ≥ 2 s of back-to-back launches: settled clock
+us = lib.ppo_bench_gemm_x3(args.op, m, n, l, 50, 0, 0)
 buf = (C.c_ulonglong * (8192 * 8))()
 lib.ppo_x3_stamps(buf, 8192 * 8)
 nwg = ((m + 255) // 256) * ((l + 255) // 256)
@@ -32,7 +33,7 @@ life = st[:, 3] - st[:, 0]
 rt0, rt1 = st[:, 4], st[:, 5]
 span_us = (rt1.max() - rt0.min()) / 100.0
 clk = life / ((rt1 - rt0) / 100.0) / 1e3                 # GHz per workgroup
-print(f"forward m={m} n={n} l={l}: {us:.1f} us per launch (events), {nwg} workgroups")
+print(f"op{args.op} m={m} n={n} l={l}: {us:.1f} us per launch (events), {nwg} workgroups")
 for name, v in (("prologue", pro), ("mainloop", main), ("epilogue", epi), ("lifetime", life)):
     print(f"{name:13s} cycles: min {v.min():8d}  median {int(np.median(v)):8d}  max {v.max():8d}")
 print(f"start skew {(rt0.max() - rt0.min()) / 100.0:.2f} us, end skew {(rt1.max() - rt1.min()) / 100.0:.2f} us, "
