@@ -394,149 +394,15 @@ __global__ __launch_bounds__(NT_, 2) void gemm_bf16_kernel(Args a) {
         }
 }
 
-// ---------------------------------------------------------------------------
-// Double-buffered 256×256 tile for forward and grad_x at wide shapes (C5: 16384 × 1024 × 1024):
-// 512 threads = 8 waves of 64×128, BK = 64 (four MFMA k-steps of 32 products per wave), two LDS
-// images (2 × 72 KiB, one workgroup per CU) so each k-tile costs ONE barrier, and the LDS stores
-// of tile j+1 and the global loads of tile j+2 are issued between tile j's k-steps (the gemm_x3
-// pipeline with a single bf16 plane).  The classic kernel above (one image, two barriers per
-// k-tile, 4 waves) stays for grad_W and narrow products.
-// ---------------------------------------------------------------------------
-template <int OP, int BM, int BN, int WARPS_M, int BK, int NTH, typename TA, typename TB, typename TC>
-__global__ __launch_bounds__(NTH, 1) void gemm_bf16_db_kernel(Args a) {
-    static_assert(OP != OP_TN, "forward / grad_x only");
-    static_assert(BK == 64, "four k-steps per k-tile");
-    constexpr int NW = NTH / 64, WARPS_N = NW / WARPS_M;
-    constexpr int WM = BM / WARPS_M, WN = BN / WARPS_N;
-    constexpr int TM = WM / 32, TN = WN / 32;
-    static_assert(TM >= 1 && TN >= 1 && WARPS_M * WARPS_N == NW, "wave tiling");
-    constexpr bool B_MN = OP == OP_NN;
-    using SA = Stage16<BM, BK, false, TA, NTH>;
-    using SB = Stage16<BN, BK, B_MN, TB, NTH>;
-    constexpr int BUF = SA::IMG + SB::IMG;
-
-    extern __shared__ __attribute__((aligned(16))) unsigned short lds[];     // 2 × BUF
-
-    const int nwg = gridDim.x, b = blockIdx.x;
-    const int xcd = b & 7, qq = nwg >> 3, rr = nwg & 7;
-    const int t = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (b >> 3);
-    const int tn = t % a.tiles_n;
-    const int tm = (t / a.tiles_n) % a.tiles_m;
-    const int m0 = tm * BM, n0 = tn * BN;
-    const int K = a.K;
-
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int wm = w / WARPS_N, wn = w % WARPS_N;
-    const int r = lane & 31, h = lane >> 5;
-
-    f32x16 acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-
-    SA sa;
-    SB sb;
-    sa.prep(OP == OP_NT ? a.ridx : nullptr, m0, a.M, tid);
-    if (!B_MN) sb.prep(nullptr, n0, a.N, tid);
-    const bool vec = a.vec != 0;
-    const TA* __restrict__ PA = static_cast<const TA*>(a.A);
-    const TB* __restrict__ PB = static_cast<const TB*>(a.B);
-    unsigned short* const buf0 = lds;
-    unsigned short* const buf1 = lds + BUF;
-
-    auto load = [&](int j) {
-        sa.load(PA, a.lda, m0, a.M, j * BK, K, vec, tid);
-        sb.load(PB, a.ldb, n0, a.N, j * BK, K, vec, tid);
-    };
+// Epilogue of the 256×256 kernels (8 waves of (TM·32)×(TN·32), 32×32 accumulator blocks: lane (r, h)
+// holds column r, rows 4h + (e&3) + 8(e>>2)).  LDS (BM × (BN + 32) bf16) must be free on entry.
+template <int OP, int BM, int BN, int TM, int TN, int NTH, typename TC, typename S>
+__device__ __forceinline__ void epilogue256(const Args& a, f32x16 (&acc)[TM][TN], unsigned short* lds, int m0,
+                                            int n0, int wm, int wn, int tid, S&& stamp) {
+    constexpr int WM = TM * 32, WN = TN * 32;
     constexpr int AB = PPO_G16_ABLATE;
-    auto stamp = [&](int slot) {
-#if PPO_G16_ABLATE & 32
-        if (tid == 0 && b < 8192) {
-            g_g16_stamps[b * 8 + slot] = __builtin_amdgcn_s_memtime();
-            if (slot == 0 || slot == 3) g_g16_stamps[b * 8 + 4 + slot / 3] = __builtin_amdgcn_s_memrealtime();
-        }
-#endif
-        (void)slot;
-    };
-    stamp(0);
-    auto kstep = [&](const unsigned short* img, int ks) {
-        bf16x8 fa[TM], fb[TN];
-        if constexpr (AB & 16) {
-#pragma unroll
-            for (int i = 0; i < TM; ++i) fa[i] = __builtin_bit_cast(bf16x8, u32x4{(unsigned)ks, 1u, 2u, 3u});
-#pragma unroll
-            for (int j = 0; j < TN; ++j) fb[j] = __builtin_bit_cast(bf16x8, u32x4{(unsigned)lane, 1u, 2u, 3u});
-        } else {
-#pragma unroll
-            for (int i = 0; i < TM; ++i) fa[i] = SA::frag(img, wm * WM + i * 32 + r, ks, lane);
-#pragma unroll
-            for (int j = 0; j < TN; ++j) fb[j] = SB::frag(img + SA::IMG, wn * WN + j * 32 + r, ks, lane);
-        }
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                if constexpr (AB & 1) {
-                    acc[i][j][0] += __builtin_bit_cast(u32x4, fa[i])[0] ^ __builtin_bit_cast(u32x4, fb[j])[1];
-                } else {
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-                }
-            }
-    };
-
-    const int nk = (K + BK - 1) / BK;
-    if (nk > 0) {
-        load(0);
-        sa.store(buf0, tid);
-        sb.store(buf0 + SA::IMG, tid);
-    }
-    if (nk > 1) load(1);
-    __syncthreads();
-    int j = 0;
-    // steady state: tile j's k-steps from one image; tile j+1's LDS stores into the other between
-    // them; tile j+2's loads behind; one barrier
-    for (; j < nk - 2; ++j) {
-        const unsigned short* cur = (j & 1) ? buf1 : buf0;
-        unsigned short* nxt = (j & 1) ? buf0 : buf1;
-        kstep(cur, 0);
-        __builtin_amdgcn_sched_barrier(0);
-        kstep(cur, 1);
-        if constexpr (!(AB & 8)) sa.store(nxt, tid);
-        __builtin_amdgcn_sched_barrier(0);
-        kstep(cur, 2);
-        if constexpr (!(AB & 8)) sb.store(nxt + SA::IMG, tid);
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (!(AB & 4)) load(j + 2);
-        kstep(cur, 3);
-        __syncthreads();
-    }
-    for (; j < nk; ++j) {                                     // the last one or two tiles
-        const unsigned short* cur = (j & 1) ? buf1 : buf0;
-        unsigned short* nxt = (j & 1) ? buf0 : buf1;
-#pragma unroll
-        for (int ks = 0; ks < BK / 16; ++ks) kstep(cur, ks);
-        if (j + 1 < nk) {
-            sa.store(nxt, tid);
-            sb.store(nxt + SA::IMG, tid);
-        }
-        __syncthreads();
-    }
-
-    stamp(1);
-    if constexpr (AB & 2) {                                   // keep the accumulators live
-        float t = 0.f;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int jj = 0; jj < TN; ++jj)
-#pragma unroll
-                for (int e = 0; e < 16; ++e) t += acc[i][jj][e];
-        if (t == 1234.5f) static_cast<float*>(a.C)[tid] = t;
-        return;
-    }
+    const int lane = tid & 63, r = lane & 31, h = lane >> 5;
+    (void)stamp;
     // bf16 output: the tile goes through LDS (free after the last barrier) as packed column pairs,
     // then out as 16-B stores, 32 lanes per 512-B row segment; the ReLU′ bits (forward) and the
     // incoming mask (grad_x) are applied on that row-major read-back, 8 columns per lane, so the
@@ -545,8 +411,7 @@ __global__ __launch_bounds__(NTH, 1) void gemm_bf16_db_kernel(Args a) {
     if constexpr (sizeof(TC) == 2) {
         if (a.cvec) {
             constexpr int CP = BN + 32;                       // pitch ≡ 16 dwords (mod 32): rows a, a+1 of
-            static_assert((size_t)BM * CP <= 2 * (size_t)BUF, "gemm16 (db): C image exceeds LDS");  // a write
-            unsigned short* const cimg = lds;                 // on disjoint banks
+            unsigned short* const cimg = lds;                 // a write on disjoint banks (callers size LDS)
             const bool odd = r & 1;
             float bcol[TN];
 #pragma unroll
@@ -695,6 +560,313 @@ __global__ __launch_bounds__(NTH, 1) void gemm_bf16_db_kernel(Args a) {
         }
 }
 
+// ---------------------------------------------------------------------------
+// Double-buffered 256×256 tile for forward and grad_x at wide shapes (C5: 16384 × 1024 × 1024):
+// 512 threads = 8 waves of 64×128, BK = 64 (four MFMA k-steps of 32 products per wave), two LDS
+// images (2 × 72 KiB, one workgroup per CU) so each k-tile costs ONE barrier, and the LDS stores
+// of tile j+1 and the global loads of tile j+2 are issued between tile j's k-steps (the gemm_x3
+// pipeline with a single bf16 plane).  The classic kernel above (one image, two barriers per
+// k-tile, 4 waves) stays for grad_W and narrow products.
+// ---------------------------------------------------------------------------
+template <int OP, int BM, int BN, int WARPS_M, int BK, int NTH, typename TA, typename TB, typename TC>
+__global__ __launch_bounds__(NTH, 1) void gemm_bf16_db_kernel(Args a) {
+    static_assert(OP != OP_TN, "forward / grad_x only");
+    static_assert(BK == 64, "four k-steps per k-tile");
+    constexpr int NW = NTH / 64, WARPS_N = NW / WARPS_M;
+    constexpr int WM = BM / WARPS_M, WN = BN / WARPS_N;
+    constexpr int TM = WM / 32, TN = WN / 32;
+    static_assert(TM >= 1 && TN >= 1 && WARPS_M * WARPS_N == NW, "wave tiling");
+    constexpr bool B_MN = OP == OP_NN;
+    using SA = Stage16<BM, BK, false, TA, NTH>;
+    using SB = Stage16<BN, BK, B_MN, TB, NTH>;
+    constexpr int BUF = SA::IMG + SB::IMG;
+
+    extern __shared__ __attribute__((aligned(16))) unsigned short lds[];     // 2 × BUF
+
+    const int nwg = gridDim.x, b = blockIdx.x;
+    const int xcd = b & 7, qq = nwg >> 3, rr = nwg & 7;
+    const int t = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (b >> 3);
+    const int tn = t % a.tiles_n;
+    const int tm = (t / a.tiles_n) % a.tiles_m;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int K = a.K;
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = w / WARPS_N, wn = w % WARPS_N;
+    const int r = lane & 31;
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+    SA sa;
+    SB sb;
+    sa.prep(OP == OP_NT ? a.ridx : nullptr, m0, a.M, tid);
+    if (!B_MN) sb.prep(nullptr, n0, a.N, tid);
+    const bool vec = a.vec != 0;
+    const TA* __restrict__ PA = static_cast<const TA*>(a.A);
+    const TB* __restrict__ PB = static_cast<const TB*>(a.B);
+    unsigned short* const buf0 = lds;
+    unsigned short* const buf1 = lds + BUF;
+
+    auto load = [&](int j) {
+        sa.load(PA, a.lda, m0, a.M, j * BK, K, vec, tid);
+        sb.load(PB, a.ldb, n0, a.N, j * BK, K, vec, tid);
+    };
+    constexpr int AB = PPO_G16_ABLATE;
+    auto stamp = [&](int slot) {
+#if PPO_G16_ABLATE & 32
+        if (tid == 0 && b < 8192) {
+            g_g16_stamps[b * 8 + slot] = __builtin_amdgcn_s_memtime();
+            if (slot == 0 || slot == 3) g_g16_stamps[b * 8 + 4 + slot / 3] = __builtin_amdgcn_s_memrealtime();
+        }
+#endif
+        (void)slot;
+    };
+    stamp(0);
+    auto kstep = [&](const unsigned short* img, int ks) {
+        bf16x8 fa[TM], fb[TN];
+        if constexpr (AB & 16) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i) fa[i] = __builtin_bit_cast(bf16x8, u32x4{(unsigned)ks, 1u, 2u, 3u});
+#pragma unroll
+            for (int j = 0; j < TN; ++j) fb[j] = __builtin_bit_cast(bf16x8, u32x4{(unsigned)lane, 1u, 2u, 3u});
+        } else {
+#pragma unroll
+            for (int i = 0; i < TM; ++i) fa[i] = SA::frag(img, wm * WM + i * 32 + r, ks, lane);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) fb[j] = SB::frag(img + SA::IMG, wn * WN + j * 32 + r, ks, lane);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                if constexpr (AB & 1) {
+                    acc[i][j][0] += __builtin_bit_cast(u32x4, fa[i])[0] ^ __builtin_bit_cast(u32x4, fb[j])[1];
+                } else {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+                }
+            }
+    };
+
+    const int nk = (K + BK - 1) / BK;
+    if (nk > 0) {
+        load(0);
+        sa.store(buf0, tid);
+        sb.store(buf0 + SA::IMG, tid);
+    }
+    if (nk > 1) load(1);
+    __syncthreads();
+    int j = 0;
+    // steady state: tile j's k-steps from one image; tile j+1's LDS stores into the other between
+    // them; tile j+2's loads behind; one barrier
+    for (; j < nk - 2; ++j) {
+        const unsigned short* cur = (j & 1) ? buf1 : buf0;
+        unsigned short* nxt = (j & 1) ? buf0 : buf1;
+        kstep(cur, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        kstep(cur, 1);
+        if constexpr (!(AB & 8)) sa.store(nxt, tid);
+        __builtin_amdgcn_sched_barrier(0);
+        kstep(cur, 2);
+        if constexpr (!(AB & 8)) sb.store(nxt + SA::IMG, tid);
+        __builtin_amdgcn_sched_barrier(0);
+        if constexpr (!(AB & 4)) load(j + 2);
+        kstep(cur, 3);
+        __syncthreads();
+    }
+    for (; j < nk; ++j) {                                     // the last one or two tiles
+        const unsigned short* cur = (j & 1) ? buf1 : buf0;
+        unsigned short* nxt = (j & 1) ? buf0 : buf1;
+#pragma unroll
+        for (int ks = 0; ks < BK / 16; ++ks) kstep(cur, ks);
+        if (j + 1 < nk) {
+            sa.store(nxt, tid);
+            sb.store(nxt + SA::IMG, tid);
+        }
+        __syncthreads();
+    }
+
+    stamp(1);
+    if constexpr (AB & 2) {                                   // keep the accumulators live
+        float t = 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int jj = 0; jj < TN; ++jj)
+#pragma unroll
+                for (int e = 0; e < 16; ++e) t += acc[i][jj][e];
+        if (t == 1234.5f) static_cast<float*>(a.C)[tid] = t;
+        return;
+    }
+    static_assert((size_t)BM * (BN + 32) <= 2 * (size_t)BUF, "gemm16 (db): C image exceeds LDS");
+    epilogue256<OP, BM, BN, TM, TN, NTH, TC>(a, acc, lds, m0, n0, wm, wn, tid, stamp);
+}
+
+// ---------------------------------------------------------------------------
+// LDS-DMA 256×256 tile (forward and grad_x with bf16 operands, K a multiple of 64): each k-tile's A
+// and B images arrive by global_load_lds_dwordx4 (1 KiB per wave-instruction, no VGPR staging, no
+// ds_write pass), two images, one barrier per k-tile; the next k-step's fragments are read while
+// this k-step's MFMAs run.  Images are unpadded with XOR-swizzled 16-B chunks, the swizzle applied
+// on the per-lane global SOURCE address (the DMA destination is lane-linear):
+//   k-contiguous [R][64]:  row R's chunk c (k 8c..8c+7) at position c ^ ((R >> 1) & 7) — the 16
+//                          rows of a ds_read_b128 lane group land on 16 distinct 16-B bank slots
+//   n-contiguous [64][256] (grad_x's W): k-row q's chunk c (n 8c..8c+7) at c ^ ((q & 3) << 2) —
+//                          the 4 k-rows of a ds_read_b64_tr_b16 group on distinct 64-B bank ranges
+// Measured at C5 16384×1024×1024 (profiles/r02_gemm16_dma.txt): forward 47.5 -> 41.3 µs, grad_x
+// 44.8 -> 43.1 µs against the register-staged kernel above.  Not adopted: a ring of 4 or 5 stages
+// of 32 k (one barrier per stage; forward 42.4 / 43.2, grad_x 49.2 / 51.4 µs) and a tile-dependent
+// rotation of the k order (forward 44.4 µs: tiles sharing an A panel stop sharing its L2 lines).
+// The MFMA-free loop alone (DMA + fragment reads + barriers) takes 45k of the forward's 56k
+// mainloop cycles: the per-CU operand intake (≈ 50 GB/s per CU), not the MFMA, bounds it.
+// ---------------------------------------------------------------------------
+template <int OP, typename TC>
+__global__ __launch_bounds__(512, 1) void gemm_bf16_dma_kernel(Args a) {
+    static_assert(OP != OP_TN, "forward / grad_x only");
+    constexpr int BM = 256, BN = 256, BK = 64, NTH = 512, WARPS_N = 2;
+    constexpr int WM = 64, WN = 128, TM = 2, TN = 4;
+    constexpr bool B_MN = OP == OP_NN;
+    constexpr int IMG = BM * BK;                       // elements per operand image (32 KiB)
+    constexpr int BUF = 2 * IMG;
+    extern __shared__ __attribute__((aligned(16))) unsigned short lds[];     // max(2·BUF, C image)
+    typedef __attribute__((address_space(3))) void* lds_ptr;
+    typedef __attribute__((address_space(1))) void* g_ptr;
+
+    const int nwg = gridDim.x, b = blockIdx.x;
+    const int xcd = b & 7, qq = nwg >> 3, rr = nwg & 7;
+    const int t = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (b >> 3);
+    const int tn = t % a.tiles_n;
+    const int tm = (t / a.tiles_n) % a.tiles_m;
+    const int m0 = tm * BM, n0 = tn * BN;
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = w / WARPS_N, wn = w % WARPS_N;
+    const int r = lane & 31, h = lane >> 5;
+    constexpr int AB = PPO_G16_ABLATE;
+    auto stamp = [&](int slot) {
+#if PPO_G16_ABLATE & 32
+        if (tid == 0 && b < 8192) {
+            g_g16_stamps[b * 8 + slot] = __builtin_amdgcn_s_memtime();
+            if (slot == 0 || slot == 3) g_g16_stamps[b * 8 + 4 + slot / 3] = __builtin_amdgcn_s_memrealtime();
+        }
+#endif
+        (void)slot;
+    };
+    stamp(0);
+
+    // DMA sources: wave w fills the images' 1-KiB pieces 4w..4w+3 (piece q: rows 8q..8q+7 of a
+    // k-contiguous image, k-rows 2q, 2q+1 of the n-contiguous one); element offsets without k0
+    const unsigned short* __restrict__ PA = static_cast<const unsigned short*>(a.A);
+    const unsigned short* __restrict__ PB = static_cast<const unsigned short*>(a.B);
+    int offa[4], offb[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int q = 4 * w + i;
+        {
+            const int row = 8 * q + (lane >> 3), p = lane & 7, c = p ^ ((row >> 1) & 7);
+            const int gr = min(m0 + row, a.M - 1);
+            offa[i] = (a.ridx ? a.ridx[gr] : gr) * a.lda + 8 * c;
+        }
+        if (!B_MN) {
+            const int row = 8 * q + (lane >> 3), p = lane & 7, c = p ^ ((row >> 1) & 7);
+            offb[i] = min(n0 + row, a.N - 1) * a.ldb + 8 * c;
+        } else {
+            const int kr = 2 * q + (lane >> 5), p = lane & 31, c = p ^ ((kr & 3) << 2);
+            offb[i] = kr * a.ldb + n0 + 8 * c;
+        }
+    }
+    const int kstride_b = B_MN ? BK * a.ldb : BK;     // element step of B's source per k-tile
+    const int nk = a.K / BK;
+    auto dma = [&](int j, unsigned short* img) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            __builtin_amdgcn_global_load_lds((g_ptr)(PA + offa[i] + j * BK), (lds_ptr)(img + (4 * w + i) * 512), 16, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            __builtin_amdgcn_global_load_lds((g_ptr)(PB + offb[i] + (long)j * kstride_b),
+                                             (lds_ptr)(img + IMG + (4 * w + i) * 512), 16, 0, 0);
+    };
+    // fragment of k-step ks (elements k = 16ks + 8h .. +7) for image row R
+    auto frag_k = [&](const unsigned short* img, int R, int ks) {
+        const int c = (2 * ks + h) ^ ((R >> 1) & 7);
+        return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(img + R * BK + 8 * c));
+    };
+    auto frag_n = [&](const unsigned short* img, int col, int ks) {   // transposed read, n-contiguous
+        const int gi = lane & 15, q = gi >> 2, p = gi & 3;
+        const int cb = col - gi + 4 * p;                               // first of this lane's 4 columns
+        typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+        const int kr = 16 * ks + 8 * h + q;                            // kr & 3 = q for both reads
+        const int pos = ((cb >> 3) ^ (q << 2)) * 8 + (cb & 7);
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + kr * BN + pos));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + (kr + 4) * BN + pos));
+        typedef short s16x8 __attribute__((ext_vector_type(8)));
+        const s16x8 f = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        return __builtin_bit_cast(bf16x8, f);
+    };
+
+    f32x16 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+    struct Fr { bf16x8 a[TM], b[TN]; };
+    auto read = [&](const unsigned short* img, int ks, Fr& f) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) f.a[i] = frag_k(img, wm * WM + i * 32 + r, ks);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+            f.b[j] = B_MN ? frag_n(img + IMG, wn * WN + j * 32 + r, ks) : frag_k(img + IMG, wn * WN + j * 32 + r, ks);
+    };
+    auto mma = [&](const Fr& f) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                if constexpr (AB & 1) {
+                    acc[i][j][0] += __builtin_bit_cast(u32x4, f.a[i])[0] ^ __builtin_bit_cast(u32x4, f.b[j])[1];
+                } else {
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[i], f.b[j], acc[i][j], 0, 0, 0);
+                }
+            }
+    };
+
+    unsigned short* const buf0 = lds;
+    unsigned short* const buf1 = lds + BUF;
+    dma(0, buf0);
+    if (nk > 1) {
+        dma(1, buf1);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");     // tile 0's eight pieces (this wave's) landed
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    for (int j = 0; j < nk; ++j) {
+        unsigned short* cur = (j & 1) ? buf1 : buf0;
+        Fr f0, f1;
+        read(cur, 0, f0);
+        read(cur, 1, f1);
+        mma(f0);
+        read(cur, 2, f0);
+        mma(f1);
+        read(cur, 3, f1);
+        mma(f0);
+        mma(f1);
+        // every wave is done reading `cur`, and tile j+1 has landed: refill `cur` with tile j+2
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (j + 2 < nk && !(AB & 4)) dma(j + 2, cur);
+    }
+    stamp(1);
+    epilogue256<OP, BM, BN, TM, TN, NTH, TC>(a, acc, lds, m0, n0, wm, wn, tid, stamp);
+}
+
 using f32 = float;
 using b16 = unsigned short;
 
@@ -743,6 +915,37 @@ void launch_db(Args a) {
     PPO_LAUNCH_CHECK();
 }
 
+int g_dma16 = -1;           // LDS-DMA 256×256 kernel: -1 = read PPO_G16_DMA (default 1 = on), 0 off
+
+template <int OP, typename TC>
+bool launch_dma(Args a) {
+    if (g_dma16 < 0) {
+        const char* e = getenv("PPO_G16_DMA");
+        g_dma16 = e ? atoi(e) : 1;
+    }
+    const bool ok = g_dma16 >= 1 && a.vec && a.acopy == nullptr && a.K % 64 == 0 && a.lda % 8 == 0 &&
+                    a.ldb % 8 == 0 && (OP == OP_NT || a.N % 256 == 0) &&
+                    (long)a.M * a.lda < (1L << 31) && (long)(OP == OP_NT ? a.N : a.K) * a.ldb < (1L << 31) &&
+                    (((uintptr_t)a.A | (uintptr_t)a.B) & 15u) == 0;
+    if (!ok) return false;
+    a.tiles_m = ppo_divup(a.M, 256);
+    a.tiles_n = ppo_divup(a.N, 256);
+    a.splits = 1;
+    a.cvec = a.N % 8 == 0 && a.ldc % 8 == 0 && ((uintptr_t)a.C & 15u) == 0;
+    constexpr size_t lds = std::max<size_t>(2 * 2 * 2 * 256 * 64, 2 * 256 * (256 + 32));
+    static_assert(lds <= 160 * 1024, "gemm16 (dma): LDS");
+    auto kern = gemm_bf16_dma_kernel<OP, TC>;
+    static bool attr = false;                          // once per instantiation
+    if (!attr) {
+        PPO_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        attr = true;
+    }
+    const long grid = (long)a.tiles_m * a.tiles_n;
+    PPO_TIMED_LAUNCH(kern, dim3((unsigned)grid), dim3(512), lds, ppo::stream(), a);
+    PPO_LAUNCH_CHECK();
+    return true;
+}
+
 // tile configurations {BM, BN, BK}: 0 = 128x128 (4 waves of 64x64), 1 = 128x32 (skinny N),
 // 2 = 32x128 (skinny M), 3 = 64x64, 4 = 128x128 with BK = 64, 5 = 256x128/64, 6 = 128x256/64,
 // 7 = 256x128/32, 8 = 128x32 with BK = 64 (output-layer forward), 9 = 256x256/64 double-buffered
@@ -768,6 +971,9 @@ void launch_cfg(int c, const Args& a) {
         case 7: launch<OP, 256, 128, 2, 32, TA, TB, TC>(a); break;
         case 9:
             if constexpr (OP != OP_TN) {
+                if constexpr (sizeof(TA) == 2 && sizeof(TB) == 2) {
+                    if (launch_dma<OP, TC>(a)) break;
+                }
                 if (a.vec && a.acopy == nullptr) { launch_db<OP, TA, TB, TC>(a); break; }
             }
             launch<OP, 128, 256, 2, 64, TA, TB, TC>(a);
