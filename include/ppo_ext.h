@@ -128,6 +128,9 @@ double ppo_bench_gemm16(int op, int m, int n, int l, int iters, int cfg, int spl
  * bf16 MFMA, fp32 accumulation (fp32-accurate, 6/16 of the fp32 MFMA cycles).  engine < 0 only
  * queries; returns the previous engine.  Env PPO_F32_GEMM=exact|x3 sets the initial value. */
 int    ppo_gemm_f32_engine(int engine);
+/* bf16 mode's LDS-DMA GEMM kernel (forward / grad_x with bf16 operands, gemm16.hip): on = 1 / 0
+ * sets, −1 queries; returns the previous setting (initially PPO_G16_DMA, else on) */
+int    ppo_gemm16_dma(int on);
 /* x3 engine tuning: force a tile configuration (−1 = automatic) and the grad_W split-K workgroup
  * target (0 = automatic, < 0 keeps); returns the number of configurations */
 int    ppo_gemm_x3_tune(int force_cfg, int splitk_target);

@@ -40,7 +40,7 @@ constexpr int NT_ = 256;
 #ifndef PPO_G16_ABLATE
 #define PPO_G16_ABLATE 0          // diagnostic builds only (tools/build_variant.sh): 1 no MFMA, 2 no epilogue
 #endif                            // stores, 4 no steady-state global loads, 8 no steady-state LDS stores,
-                                  // 16 no fragment reads, 32 stamps, 64 no bias / mask loads
+                                  // 16 no fragment reads, 32 stamps, 64 no bias / mask loads, 128 grad_W plain stores
 #if PPO_G16_ABLATE & 32
 // s_memtime of wave 0 of each workgroup: start, after the mainloop, epilogue issued, stores drained;
 // s_memrealtime (100 MHz) at start and drained
@@ -383,8 +383,13 @@ __global__ __launch_bounds__(NT_, 2) void gemm_bf16_kernel(Args a) {
                     }
                 } else if (ok) {
                     float* dst = static_cast<float*>(a.C) + off;
-                    if (a.splits > 1) atomicAdd(dst, v);
-                    else *dst = v;
+                    if (PPO_G16_ABLATE & 128) {                 // diagnostic: plain stores
+                        *dst = v;
+                    } else if (a.splits > 1) {
+                        atomicAdd(dst, v);
+                    } else {
+                        *dst = v;
+                    }
                 }
             }
             if (OP == OP_NT && a.bits_out && r < 16) {
@@ -917,12 +922,17 @@ void launch_db(Args a) {
 
 int g_dma16 = -1;           // LDS-DMA 256×256 kernel: -1 = read PPO_G16_DMA (default 1 = on), 0 off
 
-template <int OP, typename TC>
-bool launch_dma(Args a) {
+int dma16_setting() {
     if (g_dma16 < 0) {
         const char* e = getenv("PPO_G16_DMA");
         g_dma16 = e ? atoi(e) : 1;
     }
+    return g_dma16;
+}
+
+template <int OP, typename TC>
+bool launch_dma(Args a) {
+    dma16_setting();
     const bool ok = g_dma16 >= 1 && a.vec && a.acopy == nullptr && a.K % 64 == 0 && a.lda % 8 == 0 &&
                     a.ldb % 8 == 0 && (OP == OP_NT || a.N % 256 == 0) &&
                     (long)a.M * a.lda < (1L << 31) && (long)(OP == OP_NT ? a.N : a.K) * a.ldb < (1L << 31) &&
@@ -1138,6 +1148,12 @@ int ppo_g16_stamps(unsigned long long* out, int n) {
     (void)out; (void)n;
     return 0;
 #endif
+}
+
+int ppo_gemm16_dma(int on) {
+    const int old = dma16_setting();
+    if (on == 0 || on == 1) g_dma16 = on;
+    return old;
 }
 
 }  // extern "C"

@@ -224,6 +224,76 @@ struct StageX3 {
 // ABL (timing ablations, results wrong; PPO_X3_ABLATE, -DPPO_X3_DIAG builds, cfgs 0 and 3): 1 = no
 // MFMAs, 2 = no split / LDS stores, 4 = no epilogue stores, 8 = no global loads after the prologue,
 // 32 = stamps, 64 = no split (raw bits stored to the planes)
+// forward / grad_x epilogue: 32×32 accumulator block (i, j): lane (r, h) holds column r, rows
+// 4h + (e&3) + 8(e>>2).  Branch-free per element: the bias loads hoisted, the ReLU′-bit ballots in a
+// loop version of their own, grad_x's mask words brought into LDS (BM·BN/32 words, free on entry) by
+// one coalesced pass (they were 16 dependent loads per block).  Element stores in the accumulator
+// layout (each wave store: two 128-B row segments).
+template <int OP, int BM, int BN, int TM, int TN, int NTH>
+__device__ __forceinline__ void x3_epilogue_out(const X3Args& a, f32x16 (&acc)[TM][TN], unsigned short* lds, int m0,
+                                                int n0, int wm, int wn, int tid) {
+    constexpr int WM = TM * 32, WN = TN * 32;
+    const int lane = tid & 63, r = lane & 31, h = lane >> 5;
+    float bcol[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int col = n0 + wn * WN + j * 32 + r;
+        bcol[j] = (OP == OP_NT && a.bias) ? a.bias[col < a.N ? col : a.N - 1] : 0.f;
+    }
+    constexpr int WPT = BN / 32;                            // mask words per tile row
+    unsigned* const mk = reinterpret_cast<unsigned*>(lds);  // images no longer read (last barrier)
+    const bool masked = OP == OP_NN && a.bits_in != nullptr;
+    if (masked) {
+        for (int idx = tid; idx < BM * WPT; idx += NTH) {
+            const int grow = min(m0 + idx / WPT, a.M - 1);
+            const int gw = min((n0 >> 5) + idx % WPT, a.wpr - 1);
+            mk[idx] = a.bits_in[(long)grow * a.wpr + gw];
+        }
+        __syncthreads();
+    }
+    auto body = [&](auto BITSc) {
+        constexpr bool BITS = decltype(BITSc)::value;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                const int c0 = n0 + wn * WN + j * 32;
+                const int col = c0 + r;
+                const int lr0 = wm * WM + i * 32 + 4 * h;      // tile row of element 0
+                const int r0 = m0 + lr0;
+                const bool col_ok = col < a.N;
+                unsigned word = 0;
+#pragma unroll
+                for (int e = 0; e < 16; ++e) {
+                    const int dr = (e & 3) + 8 * (e >> 2);
+                    const int row = r0 + dr;
+                    const bool ok = col_ok && row < a.M;
+                    float v = acc[i][j][e];
+                    float* dst = a.C + (long)row * a.ldc + col;
+                    if (OP == OP_NT) {
+                        v += bcol[j];
+                        if (a.relu) v = v > 0.f ? v : 0.f;
+                        if (ok) *dst = v;
+                        if constexpr (BITS) {
+                            const unsigned long long bb = __ballot(ok && v > 0.f);
+                            const unsigned half = h ? (unsigned)(bb >> 32) : (unsigned)bb;
+                            word = r == e ? half : word;
+                        }
+                    } else {
+                        if (masked && !((mk[(lr0 + dr) * WPT + ((c0 - n0) >> 5)] >> r) & 1u)) v = 0.f;
+                        if (ok) *dst = v;
+                    }
+                }
+                if (BITS && r < 16) {
+                    const int row = r0 + (r & 3) + 8 * (r >> 2);
+                    if (row < a.M && c0 < a.N) a.bits_out[(long)row * a.wpr + (c0 >> 5)] = word;
+                }
+            }
+    };
+    if (OP == OP_NT && a.bits_out) body(std::true_type{});
+    else body(std::false_type{});
+}
+
 template <int OP, int BM, int BN, int WARPS_M, int NTH, int OCC, int KG, int ABL = 0>
 __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     constexpr int NTG = NTH / KG;                                  // threads per k-group
@@ -486,71 +556,9 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
         if (t == 12345.678f) a.C[tid] = 1.f;
         return;
     }
-    // forward / grad_x epilogue: 32×32 accumulator block (i, j): lane (r, h) holds column r, rows
-    // 4h + (e&3) + 8(e>>2).  Branch-free per element: the bias loads hoisted, the ReLU′-bit ballots
-    // in a loop version of their own, grad_x's mask words brought into LDS by one coalesced pass
-    // (they were 16 dependent loads per block).  Element stores in the accumulator layout (each wave
-    // store: two 128-B row segments).
     if constexpr (OP != OP_TN) {
-        float bcol[TN];
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            const int col = n0 + wn * WN + j * 32 + r;
-            bcol[j] = (OP == OP_NT && a.bias) ? a.bias[col < a.N ? col : a.N - 1] : 0.f;
-        }
-        constexpr int WPT = BN / 32;                            // mask words per tile row
-        static_assert(BM * WPT * 4 <= KG * 2 * BUF * 2, "x3 epilogue: mask words exceed LDS");
-        unsigned* const mk = reinterpret_cast<unsigned*>(lds);  // images no longer read (last barrier)
-        const bool masked = OP == OP_NN && a.bits_in != nullptr;
-        if (masked) {
-            for (int idx = tid; idx < BM * WPT; idx += NTH) {
-                const int grow = min(m0 + idx / WPT, a.M - 1);
-                const int gw = min((n0 >> 5) + idx % WPT, a.wpr - 1);
-                mk[idx] = a.bits_in[(long)grow * a.wpr + gw];
-            }
-            __syncthreads();
-        }
-        auto body = [&](auto BITSc) {
-            constexpr bool BITS = decltype(BITSc)::value;
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j) {
-                    const int c0 = n0 + wn * WN + j * 32;
-                    const int col = c0 + r;
-                    const int lr0 = wm * WM + i * 32 + 4 * h;      // tile row of element 0
-                    const int r0 = m0 + lr0;
-                    const bool col_ok = col < a.N;
-                    unsigned word = 0;
-#pragma unroll
-                    for (int e = 0; e < 16; ++e) {
-                        const int dr = (e & 3) + 8 * (e >> 2);
-                        const int row = r0 + dr;
-                        const bool ok = col_ok && row < a.M;
-                        float v = acc[i][j][e];
-                        float* dst = a.C + (long)row * a.ldc + col;
-                        if (OP == OP_NT) {
-                            v += bcol[j];
-                            if (a.relu) v = v > 0.f ? v : 0.f;
-                            if (ok) *dst = v;
-                            if constexpr (BITS) {
-                                const unsigned long long bb = __ballot(ok && v > 0.f);
-                                const unsigned half = h ? (unsigned)(bb >> 32) : (unsigned)bb;
-                                word = r == e ? half : word;
-                            }
-                        } else {
-                            if (masked && !((mk[(lr0 + dr) * WPT + ((c0 - n0) >> 5)] >> r) & 1u)) v = 0.f;
-                            if (ok) *dst = v;
-                        }
-                    }
-                    if (BITS && r < 16) {
-                        const int row = r0 + (r & 3) + 8 * (r >> 2);
-                        if (row < a.M && c0 < a.N) a.bits_out[(long)row * a.wpr + (c0 >> 5)] = word;
-                    }
-                }
-        };
-        if (OP == OP_NT && a.bits_out) body(T{});
-        else body(F{});
+        static_assert(BM * (BN / 32) * 4 <= KG * 2 * BUF * 2, "x3 epilogue: mask words exceed LDS");
+        x3_epilogue_out<OP, BM, BN, TM, TN, NTH>(a, acc, lds, m0, n0, wm, wn, tid);
         if (ABL & 32) stamp(3);
         return;
     }

@@ -166,3 +166,37 @@ def test_bf16_out_head_matches_separate(lib, monkeypatch):
     close(y1, y0, 1e-4, "value output (fused vs separate)")
     close(g1, g0, 2e-3, "value grads (fused vs separate)")
     np.testing.assert_allclose(s1, s0, rtol=1e-3, atol=1e-6)
+
+
+@pytest.mark.parametrize("sizes,m", [([1024, 1024, 1024, 17], 2000), ([512, 512, 256, 1], 1100)])
+def test_bf16_dma_matches_register_staged(lib, sizes, m):
+    """The LDS-DMA kernel (gemm_bf16_dma_kernel: source-swizzled unpadded images) runs each
+    output's MFMAs in the register-staged 256×256 kernel's order: forward outputs bitwise equal with
+    it on and off, gradients equal up to grad_W's atomic arrival order (cfg 9 forced; M tails; bf16
+    hidden layers)."""
+    rng = np.random.default_rng(sum(sizes) + m)
+    names = ["relu"] * (len(sizes) - 2) + ["none"]
+    nn = lib.create_neural_network(ppo_ffi.c_ints(sizes), ppo_ffi.c_strings(names), len(sizes))
+    params = (rng.uniform(-1, 1, sum(a * b + b for a, b in zip(sizes[:-1], sizes[1:]))) /
+              np.sqrt(max(sizes))).astype(F32)
+    nn_set_params_packed(lib, nn, params)
+    assert lib.nn_set_compute_dtype(nn, 1) == 0
+    dx = dev(lib, rng.uniform(-1, 1, (m, sizes[0])).astype(F32))
+    dgo = dev(lib, rng.uniform(-1, 1, (m, sizes[-1])).astype(F32))
+    out = {}
+    old = lib.ppo_gemm16_dma(-1)
+    try:
+        lib.ppo_gemm16_tune(9)
+        for on in (0, 1):
+            lib.ppo_gemm16_dma(on)
+            lib.forward_propagation_cuda(nn, dx.ptr, m)
+            y = ppo_ffi.d2h(lib, nn.contents.d_output, F32, m * sizes[-1])
+            lib.backward_propagation_cuda(nn, dgo.ptr, m)
+            out[on] = (y, nn_grads_packed(lib, nn))
+    finally:
+        lib.ppo_gemm16_dma(old)
+        lib.ppo_gemm16_tune(-1)
+        lib.free_neural_network(nn)
+    np.testing.assert_array_equal(out[1][0], out[0][0])
+    # grad_W accumulates split-K partials with f32 atomics (arrival order varies run to run)
+    close(out[1][1], out[0][1], 1e-5, "grads, DMA vs register-staged")

@@ -125,3 +125,4 @@ def test_x3_mlp_matches_exact(lib, x3):
     err = np.abs(out[1][1] - out[0][1])
     tol = 1e-4 * np.abs(out[0][1]).max() * 2
     assert (err > tol).mean() < 1e-3, f"{(err > tol).sum()} gradient entries beyond {tol:.3g}"
+
