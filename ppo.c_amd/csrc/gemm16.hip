@@ -232,11 +232,8 @@ template <typename T> struct Bits;
 template <> struct Bits<float> { static constexpr int code = 0; };
 template <> struct Bits<unsigned short> { static constexpr int code = 1; };
 
-// KG k-groups (grad_W): the workgroup is KG groups of NT_ threads, each running the pipeline below
-// over every KG-th k-tile of the split with its own LDS image; the groups' accumulators (and bias
-// sums) meet in LDS before group 0's epilogue — KG× the waves per CU at the same split-K atomics
-template <int OP, int BM, int BN, int WARPS_M, int BK, typename TA, typename TB, typename TC, int KG = 1>
-__global__ __launch_bounds__(NT_ * KG, KG == 1 ? 2 : 1) void gemm_bf16_kernel(Args a) {
+template <int OP, int BM, int BN, int WARPS_M, int BK, typename TA, typename TB, typename TC>
+__global__ __launch_bounds__(NT_, 2) void gemm_bf16_kernel(Args a) {
     constexpr int WARPS_N = NT_ / 64 / WARPS_M;
     constexpr int WM = BM / WARPS_M, WN = BN / WARPS_N;
     constexpr int TM = WM / 32, TN = WN / 32;
@@ -245,9 +242,8 @@ __global__ __launch_bounds__(NT_ * KG, KG == 1 ? 2 : 1) void gemm_bf16_kernel(Ar
     using SB = Stage16<BN, BK, B_MN, TB>;
     static_assert(TM >= 1 && TN >= 1, "wave tile must be a multiple of 32x32");
     static_assert(!(OP == OP_TN) || sizeof(TC) == 4, "grad_W accumulates in fp32");
-    static_assert(KG == 1 || (KG == 2 && OP == OP_TN), "k-groups: grad_W, two");
 
-    extern __shared__ __attribute__((aligned(16))) unsigned short lds[];     // KG × (SA::IMG + SB::IMG)
+    extern __shared__ __attribute__((aligned(16))) unsigned short lds[];     // SA::IMG + SB::IMG
 
     // XCD-aware remap: each XCD gets a contiguous range of linear tiles (n fastest)
     const int nwg = gridDim.x, b = blockIdx.x;
@@ -260,12 +256,9 @@ __global__ __launch_bounds__(NT_ * KG, KG == 1 ? 2 : 1) void gemm_bf16_kernel(Ar
     const int kbeg = (rest / a.tiles_m) * a.kchunk;
     const int kend = min(a.K, kbeg + a.kchunk);
 
-    const int grp = KG > 1 ? (int)threadIdx.x / NT_ : 0;      // wave-uniform
-    const int tid = KG > 1 ? (int)threadIdx.x % NT_ : (int)threadIdx.x;
-    const int lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int wm = w / WARPS_N, wn = w % WARPS_N;
     const int r = lane & 31, h = lane >> 5;
-    unsigned short* const img = lds + grp * (SA::IMG + SB::IMG);
 
     f32x16 acc[TM][TN];
 #pragma unroll
@@ -290,8 +283,8 @@ __global__ __launch_bounds__(NT_ * KG, KG == 1 ? 2 : 1) void gemm_bf16_kernel(Ar
     const TB* __restrict__ PB = static_cast<const TB*>(a.B);
 
     auto compute = [&]() {
-        const unsigned short* As = img;
-        const unsigned short* Bs = img + SA::IMG;
+        const unsigned short* As = lds;
+        const unsigned short* Bs = lds + SA::IMG;
 #pragma unroll
         for (int ks = 0; ks < BK / 16; ++ks) {
             bf16x8 fa[TM], fb[TN];
@@ -307,51 +300,22 @@ __global__ __launch_bounds__(NT_ * KG, KG == 1 ? 2 : 1) void gemm_bf16_kernel(Ar
         }
     };
 
-    // this group's k-tiles: it = 0 … nit−1 at k0 = kbeg + (KG·it + grp)·BK; every group runs nit
-    // iterations (one barrier each) — a k-tile past the end loads as zeros
-    const int nkt = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
-    const int nit = (nkt + KG - 1) / KG;
-    auto k0_of = [&](int it) { return kbeg + (KG * it + grp) * BK; };
-    if (nit > 0) {
-        sa.load(PA, a.lda, m0, a.M, k0_of(0), kend, vec, tid);
-        sb.load(PB, a.ldb, n0, a.N, k0_of(0), kend, vec, tid);
+    if (kbeg < kend) {
+        sa.load(PA, a.lda, m0, a.M, kbeg, kend, vec, tid);
+        sb.load(PB, a.ldb, n0, a.N, kbeg, kend, vec, tid);
     }
-    for (int it = 0; it < nit; ++it) {
-        const int k0 = k0_of(it);
+    for (int k0 = kbeg; k0 < kend; k0 += BK) {
         if (do_copy) sa.copy_out(a.acopy, a.K, m0, a.M, k0, kend, tid);
-        sa.store(img, tid);
-        sb.store(img + SA::IMG, tid);
+        sa.store(lds, tid);
+        sb.store(lds + SA::IMG, tid);
         __syncthreads();
-        if (it + 1 < nit) {                                 // in flight during this tile's MFMAs
-            sa.load(PA, a.lda, m0, a.M, k0_of(it + 1), kend, vec, tid);
-            sb.load(PB, a.ldb, n0, a.N, k0_of(it + 1), kend, vec, tid);
+        if (k0 + BK < kend) {                               // in flight during this tile's MFMAs
+            sa.load(PA, a.lda, m0, a.M, k0 + BK, kend, vec, tid);
+            sb.load(PB, a.ldb, n0, a.N, k0 + BK, kend, vec, tid);
         }
-        if (do_bsum) bsum += SA::rowsum(img, tid / TPR, (tid % TPR) * KPT, KPT);
+        if (do_bsum) bsum += SA::rowsum(lds, tid / TPR, (tid % TPR) * KPT, KPT);
         compute();
         __syncthreads();
-    }
-
-    if constexpr (KG > 1) {                                 // group 1 hands its partials to group 0
-        float* xch = reinterpret_cast<float*>(lds);         // images no longer read (last barrier)
-        float* xb = xch + NT_ / 64 * TM * TN * 1024;
-        if (grp == 1) {
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j)
-#pragma unroll
-                    for (int e = 0; e < 16; ++e) xch[((w * TM * TN + i * TN + j) * 16 + e) * 64 + lane] = acc[i][j][e];
-            xb[tid] = bsum;
-        }
-        __syncthreads();
-        if (grp == 1) return;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-#pragma unroll
-                for (int e = 0; e < 16; ++e) acc[i][j][e] += xch[((w * TM * TN + i * TN + j) * 16 + e) * 64 + lane];
-        bsum += xb[tid];
     }
 
     if (do_bsum) {
@@ -911,7 +875,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_dma_kernel(Args a) {
 using f32 = float;
 using b16 = unsigned short;
 
-template <int OP, int BM, int BN, int WM_, int BK, typename TA, typename TB, typename TC, int KG = 1>
+template <int OP, int BM, int BN, int WM_, int BK, typename TA, typename TB, typename TC>
 void launch(Args a) {
     a.tiles_m = ppo_divup(a.M, BM);
     a.tiles_n = ppo_divup(a.N, BN);
@@ -919,12 +883,9 @@ void launch(Args a) {
     const long grid = (long)a.tiles_m * a.tiles_n * a.splits;
     PPO_REQUIRE(grid > 0 && grid < (1L << 31), "gemm16: grid out of range");
     constexpr bool A_MN = OP == OP_TN, B_MN = OP != OP_NT;
-    constexpr size_t img = sizeof(unsigned short) * (Stage16<BM, BK, A_MN, TA>::IMG + Stage16<BN, BK, B_MN, TB>::IMG);
-    // k-groups: the accumulator hand-over (4 waves × BM·BN/4 floats) and the bias partials reuse the images
-    constexpr size_t xch = KG > 1 ? sizeof(float) * ((size_t)BM * BN + NT_) : 0;
-    constexpr size_t lds = std::max(KG * img, xch);
+    constexpr size_t lds = sizeof(unsigned short) * (Stage16<BM, BK, A_MN, TA>::IMG + Stage16<BN, BK, B_MN, TB>::IMG);
     static_assert(lds <= 160 * 1024, "gemm16: LDS image exceeds 160 KiB");
-    auto kern = gemm_bf16_kernel<OP, BM, BN, WM_, BK, TA, TB, TC, KG>;
+    auto kern = gemm_bf16_kernel<OP, BM, BN, WM_, BK, TA, TB, TC>;
     if (lds > 64 * 1024) {
         static bool attr = false;                      // once per instantiation
         if (!attr) {
@@ -932,7 +893,7 @@ void launch(Args a) {
             attr = true;
         }
     }
-    PPO_TIMED_LAUNCH(kern, dim3((unsigned)grid), dim3(NT_ * KG), lds, ppo::stream(), a);
+    PPO_TIMED_LAUNCH(kern, dim3((unsigned)grid), dim3(NT_), lds, ppo::stream(), a);
     PPO_LAUNCH_CHECK();
 }
 
@@ -957,15 +918,6 @@ void launch_db(Args a) {
     }
     PPO_TIMED_LAUNCH(kern, dim3((unsigned)grid), dim3(NTH), lds, ppo::stream(), a);
     PPO_LAUNCH_CHECK();
-}
-
-int g_kg16 = -1;            // grad_W (cfg 6) k-groups: -1 = read PPO_G16_KG (default 2), 1 or 2
-int kg16_setting() {
-    if (g_kg16 < 0) {
-        const char* e = getenv("PPO_G16_KG");
-        g_kg16 = (e && atoi(e) == 1) ? 1 : 2;
-    }
-    return g_kg16;
 }
 
 int g_dma16 = -1;           // LDS-DMA 256×256 kernel: -1 = read PPO_G16_DMA (default 1 = on), 0 off
@@ -1025,12 +977,7 @@ void launch_cfg(int c, const Args& a) {
         case 3: launch<OP, 64, 64, 2, 32, TA, TB, TC>(a); break;
         case 4: launch<OP, 128, 128, 2, 64, TA, TB, TC>(a); break;
         case 5: launch<OP, 256, 128, 2, 64, TA, TB, TC>(a); break;       // waves of 128x64
-        case 6:                                                          // waves of 64x128
-            if constexpr (OP == OP_TN) {
-                if (kg16_setting() == 2) { launch<OP, 128, 256, 2, 64, TA, TB, TC, 2>(a); break; }
-            }
-            launch<OP, 128, 256, 2, 64, TA, TB, TC>(a);
-            break;
+        case 6: launch<OP, 128, 256, 2, 64, TA, TB, TC>(a); break;       // waves of 64x128
         case 7: launch<OP, 256, 128, 2, 32, TA, TB, TC>(a); break;
         case 9:
             if constexpr (OP != OP_TN) {
