@@ -399,6 +399,62 @@ __global__ __launch_bounds__(NT_, 2) void gemm_bf16_kernel(Args a) {
         }
 }
 
+// second half of the LDS-staged bf16 epilogue: the BM×BN tile image (pitch BN + 32 bf16, written by
+// every wave before this call's barrier) leaves as 16-B row stores; grad_x's incoming mask and the
+// forward's ReLU′ bits are applied on this row-major read-back, 8 columns per lane
+template <int OP, int BM, int BN, int NTH>
+__device__ __forceinline__ void c_image_out(const Args& a, const unsigned short* cimg, int m0, int n0, int tid) {
+    constexpr int AB = PPO_G16_ABLATE;
+    constexpr int CP = BN + 32;
+    __syncthreads();
+    constexpr int CH = BN / 8;                        // 16-B chunks per tile row (4 per 32-bit word)
+    constexpr int IT = BM * CH / NTH;
+    unsigned short* __restrict__ C = static_cast<unsigned short*>(a.C);
+    unsigned mword[IT];
+    if (OP == OP_NN) {                                // grad_x: the mask words, all loads first
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const int idx = tid + it * NTH;
+            const int grow = min(m0 + idx / CH, a.M - 1), gcol = n0 + (idx % CH) * 8;
+            mword[it] = (a.bits_in && !(AB & 64)) ? a.bits_in[(long)grow * a.wpr + (min(gcol, a.N - 1) >> 5)]
+                                                   : ~0u;
+        }
+    }
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+        const int idx = tid + it * NTH;
+        const int row = idx / CH, ch = idx % CH;
+        const int grow = m0 + row, gcol = n0 + ch * 8;
+        u32x4 v = *reinterpret_cast<const u32x4*>(cimg + row * CP + ch * 8);
+        if (OP == OP_NN) {
+            const unsigned byte = mword[it] >> (8 * (ch & 3));
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const unsigned keep = (0xffffu * ((byte >> (2 * q)) & 1u)) | (0xffff0000u * ((byte >> (2 * q + 1)) & 1u));
+                v[q] &= keep;
+            }
+        }
+        const bool ok = grow < a.M && gcol < a.N;
+        if (ok) *reinterpret_cast<u32x4*>(C + (long)grow * a.ldc + gcol) = v;
+        if (OP == OP_NT && a.bits_out) {
+            // bit c of the byte: column gcol + c stored > 0 (post-ReLU values are ≥ +0)
+            unsigned byte = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                byte |= (unsigned)((short)(v[q] & 0xffffu) > 0) << (2 * q);
+                byte |= (unsigned)((short)(v[q] >> 16) > 0) << (2 * q + 1);
+            }
+            if (!ok) byte = 0;                      // columns past N carry no bits
+            // the 4 lanes of a quad hold the 4 bytes of one 32-column word (ch & 3 = lane & 3)
+            const int b1 = __builtin_amdgcn_mov_dpp((int)byte, 0x55, 0xF, 0xF, true);   // quad lane 1
+            const int b2 = __builtin_amdgcn_mov_dpp((int)byte, 0xAA, 0xF, 0xF, true);   // quad lane 2
+            const int b3 = __builtin_amdgcn_mov_dpp((int)byte, 0xFF, 0xF, 0xF, true);   // quad lane 3
+            const unsigned word = byte | ((unsigned)b1 << 8) | ((unsigned)b2 << 16) | ((unsigned)b3 << 24);
+            if ((ch & 3) == 0 && ok) a.bits_out[(long)grow * a.wpr + (gcol >> 5)] = word;
+        }
+    }
+}
+
 // Epilogue of the 256×256 kernels (8 waves of (TM·32)×(TN·32), 32×32 accumulator blocks: lane (r, h)
 // holds column r, rows 4h + (e&3) + 8(e>>2)).  LDS (BM × (BN + 32) bf16) must be free on entry.
 template <int OP, int BM, int BN, int TM, int TN, int NTH, typename TC, typename S>
@@ -450,53 +506,7 @@ __device__ __forceinline__ void epilogue256(const Args& a, f32x16 (&acc)[TM][TN]
                         *reinterpret_cast<unsigned*>(cimg + lrow * CP + wn * WN + jj * 32 + (r & ~1)) = pack2(lo, hi);
                     }
                 }
-            __syncthreads();
-            constexpr int CH = BN / 8;                        // 16-B chunks per tile row (4 per 32-bit word)
-            constexpr int IT = BM * CH / NTH;
-            unsigned short* __restrict__ C = static_cast<unsigned short*>(a.C);
-            unsigned mword[IT];
-            if (OP == OP_NN) {                                // grad_x: the mask words, all loads first
-#pragma unroll
-                for (int it = 0; it < IT; ++it) {
-                    const int idx = tid + it * NTH;
-                    const int grow = min(m0 + idx / CH, a.M - 1), gcol = n0 + (idx % CH) * 8;
-                    mword[it] = (a.bits_in && !(AB & 64)) ? a.bits_in[(long)grow * a.wpr + (min(gcol, a.N - 1) >> 5)]
-                                                           : ~0u;
-                }
-            }
-#pragma unroll
-            for (int it = 0; it < IT; ++it) {
-                const int idx = tid + it * NTH;
-                const int row = idx / CH, ch = idx % CH;
-                const int grow = m0 + row, gcol = n0 + ch * 8;
-                u32x4 v = *reinterpret_cast<const u32x4*>(cimg + row * CP + ch * 8);
-                if (OP == OP_NN) {
-                    const unsigned byte = mword[it] >> (8 * (ch & 3));
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const unsigned keep = (0xffffu * ((byte >> (2 * q)) & 1u)) | (0xffff0000u * ((byte >> (2 * q + 1)) & 1u));
-                        v[q] &= keep;
-                    }
-                }
-                const bool ok = grow < a.M && gcol < a.N;
-                if (ok) *reinterpret_cast<u32x4*>(C + (long)grow * a.ldc + gcol) = v;
-                if (OP == OP_NT && a.bits_out) {
-                    // bit c of the byte: column gcol + c stored > 0 (post-ReLU values are ≥ +0)
-                    unsigned byte = 0;
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        byte |= (unsigned)((short)(v[q] & 0xffffu) > 0) << (2 * q);
-                        byte |= (unsigned)((short)(v[q] >> 16) > 0) << (2 * q + 1);
-                    }
-                    if (!ok) byte = 0;                      // columns past N carry no bits
-                    // the 4 lanes of a quad hold the 4 bytes of one 32-column word (ch & 3 = lane & 3)
-                    const int b1 = __builtin_amdgcn_mov_dpp((int)byte, 0x55, 0xF, 0xF, true);   // quad lane 1
-                    const int b2 = __builtin_amdgcn_mov_dpp((int)byte, 0xAA, 0xF, 0xF, true);   // quad lane 2
-                    const int b3 = __builtin_amdgcn_mov_dpp((int)byte, 0xFF, 0xF, 0xF, true);   // quad lane 3
-                    const unsigned word = byte | ((unsigned)b1 << 8) | ((unsigned)b2 << 16) | ((unsigned)b3 << 24);
-                    if ((ch & 3) == 0 && ok) a.bits_out[(long)grow * a.wpr + (gcol >> 5)] = word;
-                }
-            }
+            c_image_out<OP, BM, BN, NTH>(a, cimg, m0, n0, tid);
             if constexpr ((AB & 32) != 0) {
                 stamp(2);
                 __builtin_amdgcn_s_waitcnt(0);
@@ -872,6 +882,165 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_dma_kernel(Args a) {
     epilogue256<OP, BM, BN, TM, TN, NTH, TC>(a, acc, lds, m0, n0, wm, wn, tid, stamp);
 }
 
+// ---------------------------------------------------------------------------
+// The same LDS-DMA tile on v_mfma_f32_16x16x32_bf16 (bf16 output with the LDS-staged epilogue): per
+// 32-k step a wave's 64×128 tile is 4×8 blocks of 16×16, read as 4 A + 8 B fragments — the LDS
+// traffic of the 32×32×16 form — while the MFMA measured ≈ 1.12–1.14× the 32×32×16 FLOP rate with
+// operands re-read from LDS (MI355X_MICROARCH.md).  The k-contiguous swizzle is unchanged (its 16
+// rows per lane group stay on distinct bank slots); grad_x's transposed W reads take chunk
+// c ^ (((q & 3) << 2) | (((q >> 3) & 1) << 1)) for k-row q (the 16×16×32 B operand puts k-rows q
+// and q + 8 in one 32-lane group).
+// ---------------------------------------------------------------------------
+template <int OP>
+__global__ __launch_bounds__(512, 1) void gemm_bf16_dma16_kernel(Args a) {
+    static_assert(OP != OP_TN, "forward / grad_x only");
+    typedef float f32x4v __attribute__((ext_vector_type(4)));
+    constexpr int BM = 256, BN = 256, BK = 64, NTH = 512, WARPS_N = 2;
+    constexpr int WM = 64, WN = 128, TM = 4, TN = 8;           // 16×16 blocks per wave
+    constexpr bool B_MN = OP == OP_NN;
+    constexpr int IMG = BM * BK;
+    constexpr int BUF = 2 * IMG;
+    extern __shared__ __attribute__((aligned(16))) unsigned short lds[];     // max(2·BUF, C image)
+    typedef __attribute__((address_space(3))) void* lds_ptr;
+    typedef __attribute__((address_space(1))) void* g_ptr;
+
+    const int nwg = gridDim.x, b = blockIdx.x;
+    const int xcd = b & 7, qq = nwg >> 3, rr = nwg & 7;
+    const int t = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (b >> 3);
+    const int tn = t % a.tiles_n;
+    const int tm = (t / a.tiles_n) % a.tiles_m;
+    const int m0 = tm * BM, n0 = tn * BN;
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = w / WARPS_N, wn = w % WARPS_N;
+    const int l15 = lane & 15, g4 = lane >> 4;
+    auto swz_n = [](int kr) { return ((kr & 3) << 2) | (((kr >> 3) & 1) << 1); };
+
+    const unsigned short* __restrict__ PA = static_cast<const unsigned short*>(a.A);
+    const unsigned short* __restrict__ PB = static_cast<const unsigned short*>(a.B);
+    int offa[4], offb[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int q = 4 * w + i;
+        {
+            const int row = 8 * q + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7);
+            const int gr = min(m0 + row, a.M - 1);
+            offa[i] = (a.ridx ? a.ridx[gr] : gr) * a.lda + 8 * c;
+        }
+        if (!B_MN) {
+            const int row = 8 * q + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7);
+            offb[i] = min(n0 + row, a.N - 1) * a.ldb + 8 * c;
+        } else {
+            const int kr = 2 * q + (lane >> 5), c = (lane & 31) ^ swz_n(kr);
+            offb[i] = kr * a.ldb + n0 + 8 * c;
+        }
+    }
+    const int kstride_b = B_MN ? BK * a.ldb : BK;
+    auto dma = [&](int j, unsigned short* img) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            __builtin_amdgcn_global_load_lds((g_ptr)(PA + offa[i] + j * BK), (lds_ptr)(img + (4 * w + i) * 512), 16, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            __builtin_amdgcn_global_load_lds((g_ptr)(PB + offb[i] + (long)j * kstride_b),
+                                             (lds_ptr)(img + IMG + (4 * w + i) * 512), 16, 0, 0);
+    };
+    // 16×32 fragment of 32-k step s: row R = block base + (lane & 15), k = 32s + 8(lane >> 4) .. +7
+    auto frag_k = [&](const unsigned short* img, int R, int s) {
+        const int c = (4 * s + g4) ^ ((R >> 1) & 7);
+        return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(img + R * BK + 8 * c));
+    };
+    auto frag_n = [&](const unsigned short* img, int cbase, int s) {   // transposed read, n-contiguous
+        const int q = l15 >> 2, p = l15 & 3;
+        const int cb = cbase + 4 * p;
+        typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+        const int kr = 32 * s + 8 * g4 + q;                            // kr + 4: same swizzle
+        const int pos = ((cb >> 3) ^ swz_n(kr)) * 8 + (cb & 7);
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + kr * BN + pos));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + (kr + 4) * BN + pos));
+        typedef short s16x8 __attribute__((ext_vector_type(8)));
+        const s16x8 f = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        return __builtin_bit_cast(bf16x8, f);
+    };
+
+    f32x4v acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+
+    auto step = [&](const unsigned short* img, int s) {
+        bf16x8 fa[TM], fb[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) fa[i] = frag_k(img, wm * WM + i * 16 + l15, s);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+            fb[j] = B_MN ? frag_n(img + IMG, wn * WN + j * 16, s) : frag_k(img + IMG, wn * WN + j * 16 + l15, s);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    };
+
+    const int nk = a.K / BK;
+    unsigned short* const buf0 = lds;
+    unsigned short* const buf1 = lds + BUF;
+    dma(0, buf0);
+    if (nk > 1) {
+        dma(1, buf1);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    for (int j = 0; j < nk; ++j) {
+        unsigned short* cur = (j & 1) ? buf1 : buf0;
+        step(cur, 0);
+        step(cur, 1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (j + 2 < nk) dma(j + 2, cur);
+    }
+
+    // epilogue: 16×16 block (i, j): lane holds column (lane & 15), rows 4(lane >> 4) + e; bias /
+    // ReLU, then DPP-paired columns into the LDS C image (images free after the last barrier)
+    constexpr int CP = BN + 32;
+    unsigned short* const cimg = lds;
+    const bool odd = lane & 1;
+    float bcol[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+        const int col = n0 + wn * WN + j * 16 + l15;
+        bcol[j] = (OP == OP_NT && a.bias) ? a.bias[col < a.N ? col : a.N - 1] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            float vv[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                float v = acc[i][j][e];
+                if (OP == OP_NT) {
+                    v += bcol[j];
+                    if (a.relu) v = v > 0.f ? v : 0.f;
+                }
+                vv[e] = v;
+            }
+#pragma unroll
+            for (int e = 0; e < 4; e += 2) {
+                const float send = odd ? vv[e] : vv[e + 1];
+                const float recv = __builtin_bit_cast(
+                    float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, send), 0xB1, 0xF, 0xF, true));
+                const float lo = odd ? recv : vv[e], hi = odd ? vv[e + 1] : recv;
+                const int lrow = wm * WM + i * 16 + 4 * g4 + e + (odd ? 1 : 0);
+                *reinterpret_cast<unsigned*>(cimg + lrow * CP + wn * WN + j * 16 + (l15 & ~1)) = pack2(lo, hi);
+            }
+        }
+    c_image_out<OP, BM, BN, NTH>(a, cimg, m0, n0, tid);
+}
+
 using f32 = float;
 using b16 = unsigned short;
 
@@ -929,6 +1098,9 @@ int dma16_setting() {
     }
     return g_dma16;
 }
+// bf16-output DMA products on the 16×16×32 form (PPO_G16_MF16=0: the 32×32×16 form).  Measured at C5
+// 16384×1024×1024: forward 41.5 -> 37.3 µs, grad_x 42.1 -> 40.7 µs; C5 update 276.4 -> 271.9 ms
+int g_mf16 = [] { const char* e = getenv("PPO_G16_MF16"); return e ? atoi(e) : 1; }();
 
 template <int OP, typename TC>
 bool launch_dma(Args a) {
@@ -944,13 +1116,26 @@ bool launch_dma(Args a) {
     a.cvec = a.N % 8 == 0 && a.ldc % 8 == 0 && ((uintptr_t)a.C & 15u) == 0;
     constexpr size_t lds = std::max<size_t>(2 * 2 * 2 * 256 * 64, 2 * 256 * (256 + 32));
     static_assert(lds <= 160 * 1024, "gemm16 (dma): LDS");
+    const long grid = (long)a.tiles_m * a.tiles_n;
+    if constexpr (sizeof(TC) == 2) {
+        if (a.cvec && g_mf16 != 0) {                   // 16×16×32 MFMA form (bf16 output)
+            auto kern = gemm_bf16_dma16_kernel<OP>;
+            static bool attr = false;
+            if (!attr) {
+                PPO_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+                attr = true;
+            }
+            PPO_TIMED_LAUNCH(kern, dim3((unsigned)grid), dim3(512), lds, ppo::stream(), a);
+            PPO_LAUNCH_CHECK();
+            return true;
+        }
+    }
     auto kern = gemm_bf16_dma_kernel<OP, TC>;
     static bool attr = false;                          // once per instantiation
     if (!attr) {
         PPO_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         attr = true;
     }
-    const long grid = (long)a.tiles_m * a.tiles_n;
     PPO_TIMED_LAUNCH(kern, dim3((unsigned)grid), dim3(512), lds, ppo::stream(), a);
     PPO_LAUNCH_CHECK();
     return true;
