@@ -232,8 +232,9 @@ template <typename T> struct Bits;
 template <> struct Bits<float> { static constexpr int code = 0; };
 template <> struct Bits<unsigned short> { static constexpr int code = 1; };
 
-template <int OP, int BM, int BN, int WARPS_M, int BK, typename TA, typename TB, typename TC>
+template <int OP, int BM, int BN, int WARPS_M, int BK, typename TA, typename TB, typename TC, int MF = 32>
 __global__ __launch_bounds__(NT_, 2) void gemm_bf16_kernel(Args a) {
+    static_assert(MF == 32 || (MF == 16 && OP == OP_TN && BK % 32 == 0), "16×16×32 form: grad_W");
     constexpr int WARPS_N = NT_ / 64 / WARPS_M;
     constexpr int WM = BM / WARPS_M, WN = BN / WARPS_N;
     constexpr int TM = WM / 32, TN = WN / 32;
@@ -282,9 +283,45 @@ __global__ __launch_bounds__(NT_, 2) void gemm_bf16_kernel(Args a) {
     const TA* __restrict__ PA = static_cast<const TA*>(a.A);
     const TB* __restrict__ PB = static_cast<const TB*>(a.B);
 
+    // 16×16×32 form (grad_W): both operands row-contiguous; transposed reads of 16 columns × 8 k
+    typedef float f32x4v __attribute__((ext_vector_type(4)));
+    constexpr int TM16 = MF == 16 ? WM / 16 : 1, TN16 = MF == 16 ? WN / 16 : 1;
+    f32x4v acc16[TM16][TN16];
+    if constexpr (MF == 16) {
+#pragma unroll
+        for (int i = 0; i < TM16; ++i)
+#pragma unroll
+            for (int j = 0; j < TN16; ++j) acc16[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+    }
+    auto frag16 = [&](const unsigned short* im, int pitch, int cbase, int s) {
+        const int l15 = lane & 15, g4 = lane >> 4, q = l15 >> 2, p = l15 & 3;
+        typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+        const unsigned short* a0 = im + (32 * s + 8 * g4 + q) * pitch + cbase + 4 * p;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 4 * pitch));
+        typedef short s16x8 __attribute__((ext_vector_type(8)));
+        const s16x8 f = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        return __builtin_bit_cast(bf16x8, f);
+    };
     auto compute = [&]() {
         const unsigned short* As = lds;
         const unsigned short* Bs = lds + SA::IMG;
+        if constexpr (MF == 16) {
+#pragma unroll
+            for (int s = 0; s < BK / 32; ++s) {
+                bf16x8 fa[TM16], fb[TN16];
+#pragma unroll
+                for (int i = 0; i < TM16; ++i) fa[i] = frag16(As, SA::PR, wm * WM + i * 16, s);
+#pragma unroll
+                for (int j = 0; j < TN16; ++j) fb[j] = frag16(Bs, SB::PR, wn * WN + j * 16, s);
+#pragma unroll
+                for (int i = 0; i < TM16; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN16; ++j)
+                        acc16[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc16[i][j], 0, 0, 0);
+            }
+            return;
+        }
 #pragma unroll
         for (int ks = 0; ks < BK / 16; ++ks) {
             bf16x8 fa[TM], fb[TN];
@@ -328,6 +365,24 @@ __global__ __launch_bounds__(NT_, 2) void gemm_bf16_kernel(Args a) {
         }
     }
 
+    if constexpr (MF == 16) {                          // 16×16 block: column lane & 15, rows 4(lane >> 4) + e
+#pragma unroll
+        for (int i = 0; i < TM16; ++i)
+#pragma unroll
+            for (int j = 0; j < TN16; ++j) {
+                const int col = n0 + wn * WN + j * 16 + (lane & 15);
+                const int r0 = m0 + wm * WM + i * 16 + 4 * (lane >> 4);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    if (col < a.N && r0 + e < a.M) {
+                        float* dst = static_cast<float*>(a.C) + (long)(r0 + e) * a.ldc + col;
+                        if (a.splits > 1) atomicAdd(dst, acc16[i][j][e]);
+                        else *dst = acc16[i][j][e];
+                    }
+                }
+            }
+        return;
+    }
     // epilogue (C/D map as gemm.hip); every load a block needs is issued before its stores
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -1044,7 +1099,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_dma16_kernel(Args a) {
 using f32 = float;
 using b16 = unsigned short;
 
-template <int OP, int BM, int BN, int WM_, int BK, typename TA, typename TB, typename TC>
+template <int OP, int BM, int BN, int WM_, int BK, typename TA, typename TB, typename TC, int MF = 32>
 void launch(Args a) {
     a.tiles_m = ppo_divup(a.M, BM);
     a.tiles_n = ppo_divup(a.N, BN);
@@ -1054,7 +1109,7 @@ void launch(Args a) {
     constexpr bool A_MN = OP == OP_TN, B_MN = OP != OP_NT;
     constexpr size_t lds = sizeof(unsigned short) * (Stage16<BM, BK, A_MN, TA>::IMG + Stage16<BN, BK, B_MN, TB>::IMG);
     static_assert(lds <= 160 * 1024, "gemm16: LDS image exceeds 160 KiB");
-    auto kern = gemm_bf16_kernel<OP, BM, BN, WM_, BK, TA, TB, TC>;
+    auto kern = gemm_bf16_kernel<OP, BM, BN, WM_, BK, TA, TB, TC, MF>;
     if (lds > 64 * 1024) {
         static bool attr = false;                      // once per instantiation
         if (!attr) {
@@ -1098,8 +1153,9 @@ int dma16_setting() {
     }
     return g_dma16;
 }
-// bf16-output DMA products on the 16×16×32 form (PPO_G16_MF16=0: the 32×32×16 form).  Measured at C5
-// 16384×1024×1024: forward 41.5 -> 37.3 µs, grad_x 42.1 -> 40.7 µs; C5 update 276.4 -> 271.9 ms
+// the 16×16×32 MFMA form for bf16-output DMA products and for grad_W (PPO_G16_MF16=0: the 32×32×16 form
+// everywhere; 2: only the DMA products).  Measured at C5 16384×1024×1024: forward 41.5 -> 37.3 µs,
+// grad_x 42.1 -> 40.7 µs (C5 update 276.4 -> 271.9 ms); grad_W 82.6 -> 80.3 µs (273.7 -> 271.8 ms)
 int g_mf16 = [] { const char* e = getenv("PPO_G16_MF16"); return e ? atoi(e) : 1; }();
 
 template <int OP, typename TC>
@@ -1162,7 +1218,12 @@ void launch_cfg(int c, const Args& a) {
         case 3: launch<OP, 64, 64, 2, 32, TA, TB, TC>(a); break;
         case 4: launch<OP, 128, 128, 2, 64, TA, TB, TC>(a); break;
         case 5: launch<OP, 256, 128, 2, 64, TA, TB, TC>(a); break;       // waves of 128x64
-        case 6: launch<OP, 128, 256, 2, 64, TA, TB, TC>(a); break;       // waves of 64x128
+        case 6:                                                          // waves of 64x128
+            if constexpr (OP == OP_TN) {
+                if (g_mf16 != 0 && g_mf16 != 2) { launch<OP, 128, 256, 2, 64, TA, TB, TC, 16>(a); break; }
+            }
+            launch<OP, 128, 256, 2, 64, TA, TB, TC>(a);
+            break;
         case 7: launch<OP, 256, 128, 2, 32, TA, TB, TC>(a); break;
         case 9:
             if constexpr (OP != OP_TN) {
