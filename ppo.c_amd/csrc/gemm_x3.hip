@@ -212,22 +212,6 @@ struct StageX3 {
         const s16x8 f = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         return __builtin_bit_cast(bf16x8, f);
     }
-    // 16×16×32 form, planes paired along K: 16 rows from `rb` × 32 k' where lanes 0–31 (k' 0–15)
-    // carry plane PLO's k 0..15 and lanes 32–63 (k' 16–31) plane PHI's — one MFMA then sums two
-    // plane products.  Lane (g = lane >> 4, row rb + (lane & 15)) reads k 8(g & 1) .. +7.
-    template <int PLO, int PHI>
-    __device__ __forceinline__ static bf16x8 frag16(const unsigned short* img, int rb, int lane) {
-        const int g = lane >> 4, kh = g & 1;
-        const unsigned short* plane = img + (g < 2 ? PLO : PHI) * PLANE;
-        if (!MN) return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(plane + (rb + (lane & 15)) * PK + 8 * kh));
-        const int gi = lane & 15, q = gi >> 2, p = gi & 3;
-        typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-        const unsigned short* a0 = plane + (8 * kh + q) * PR + rb + 4 * p;
-        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
-        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 4 * PR));
-        const s16x8 f = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        return __builtin_bit_cast(bf16x8, f);
-    }
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -267,7 +251,7 @@ __device__ __forceinline__ void x3_epilogue_out(const X3Args& a, f32x16 (&acc)[T
         }
         __syncthreads();
     }
-    auto body = [&](auto BITSc) __attribute__((always_inline)) {
+    auto body = [&](auto BITSc) {
         constexpr bool BITS = decltype(BITSc)::value;
 #pragma unroll
         for (int i = 0; i < TM; ++i)
@@ -310,85 +294,8 @@ __device__ __forceinline__ void x3_epilogue_out(const X3Args& a, f32x16 (&acc)[T
     else body(std::false_type{});
 }
 
-// the same epilogue for the 16×16×32 form: 32×32 block (i, j) is four 16×16 sub-blocks
-// q = 2·si + sj; lane (g = lane >> 4, c = lane & 15) holds column 16·sj + c, rows 16·si + 4g + e4.
-// A row's 32-column ReLU′ word joins two ballots (sj = 0, 1): bits 16g.. of each are row 4g + e4.
-template <int OP, int BM, int BN, int TM, int TN, int NTH>
-__device__ __forceinline__ void x3_epilogue_out16(const X3Args& a, f32x4 (&acc)[TM][TN][4], unsigned short* lds, int m0,
-                                                  int n0, int wm, int wn, int tid) {
-    constexpr int WM = TM * 32, WN = TN * 32;
-    const int lane = tid & 63, c = lane & 15, g = lane >> 4;
-    float bcol[TN][2];
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int sj = 0; sj < 2; ++sj) {
-            const int col = n0 + wn * WN + j * 32 + 16 * sj + c;
-            bcol[j][sj] = (OP == OP_NT && a.bias) ? a.bias[col < a.N ? col : a.N - 1] : 0.f;
-        }
-    constexpr int WPT = BN / 32;
-    unsigned* const mk = reinterpret_cast<unsigned*>(lds);
-    const bool masked = OP == OP_NN && a.bits_in != nullptr;
-    if (masked) {
-        for (int idx = tid; idx < BM * WPT; idx += NTH) {
-            const int grow = min(m0 + idx / WPT, a.M - 1);
-            const int gw = min((n0 >> 5) + idx % WPT, a.wpr - 1);
-            mk[idx] = a.bits_in[(long)grow * a.wpr + gw];
-        }
-        __syncthreads();
-    }
-    auto body = [&](auto BITSc) __attribute__((always_inline)) {
-        constexpr bool BITS = decltype(BITSc)::value;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                const int c0 = n0 + wn * WN + j * 32;
-                const int lb = wm * WM + i * 32;
-                unsigned word = 0;
-#pragma unroll
-                for (int si = 0; si < 2; ++si)
-#pragma unroll
-                    for (int e4 = 0; e4 < 4; ++e4) {
-                        const int lr = lb + 16 * si + 4 * g + e4;
-                        const int row = m0 + lr;
-                        unsigned long long bb[2] = {0ull, 0ull};
-#pragma unroll
-                        for (int sj = 0; sj < 2; ++sj) {
-                            const int col = c0 + 16 * sj + c;
-                            const bool ok = col < a.N && row < a.M;
-                            float v = acc[i][j][2 * si + sj][e4];
-                            float* dst = a.C + (long)row * a.ldc + col;
-                            if (OP == OP_NT) {
-                                v += bcol[j][sj];
-                                if (a.relu) v = v > 0.f ? v : 0.f;
-                                if (ok) *dst = v;
-                                if constexpr (BITS) bb[sj] = __ballot(ok && v > 0.f);
-                            } else {
-                                if (masked && !((mk[lr * WPT + ((c0 - n0) >> 5)] >> (16 * sj + c)) & 1u)) v = 0.f;
-                                if (ok) *dst = v;
-                            }
-                        }
-                        if constexpr (BITS) {
-                            const int gg = lane & 3;
-                            const unsigned w32 = (unsigned)((bb[0] >> (16 * gg)) & 0xffffu) |
-                                                 ((unsigned)((bb[1] >> (16 * gg)) & 0xffffu) << 16);
-                            if ((lane >> 4) == si && ((lane >> 2) & 3) == e4) word = w32;
-                        }
-                    }
-                if (BITS && lane < 32) {
-                    const int row = m0 + lb + 16 * (lane >> 4) + 4 * (lane & 3) + ((lane >> 2) & 3);
-                    if (row < a.M && c0 < a.N) a.bits_out[(long)row * a.wpr + (c0 >> 5)] = word;
-                }
-            }
-    };
-    if (OP == OP_NT && a.bits_out) body(std::true_type{});
-    else body(std::false_type{});
-}
-
-template <int OP, int BM, int BN, int WARPS_M, int NTH, int OCC, int KG, int ABL = 0, int MF = 0>
+template <int OP, int BM, int BN, int WARPS_M, int NTH, int OCC, int KG, int ABL = 0>
 __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
-    static_assert(MF == 0 || ABL == 0, "ablations: 32×32×16 form only");
     constexpr int NTG = NTH / KG;                                  // threads per k-group
     constexpr int NW = NTG / 64, WARPS_N = NW / WARPS_M;
     constexpr int WM = BM / WARPS_M, WN = BN / WARPS_N;
@@ -419,7 +326,7 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     const int lt = KG > 1 ? tid % NTG : tid;
     const int w = lt >> 6;
     const int wm = w / WARPS_N, wn = w % WARPS_N;
-    auto stamp = [&](int slot) __attribute__((always_inline)) {
+    auto stamp = [&](int slot) {
         if (tid == 0 && b < 8192) {
             g_x3_stamps[b * 8 + slot] = __builtin_amdgcn_s_memtime();
             if (slot == 0 || slot == 3) g_x3_stamps[b * 8 + 4 + slot / 3] = __builtin_amdgcn_s_memrealtime();
@@ -428,20 +335,13 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     if (ABL & 32) stamp(0);
     const int r = lane & 31, h = lane >> 5;
 
-    f32x16 acc[TM][TN];                  // MF = 0: 32×32 blocks
-    f32x4 acc4[TM][TN][4];               // MF = 1: the 32×32 block's four 16×16 sub-blocks
+    f32x16 acc[TM][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            if constexpr (MF) {
+        for (int j = 0; j < TN; ++j)
 #pragma unroll
-                for (int q = 0; q < 4; ++q) acc4[i][j][q] = f32x4{0.f, 0.f, 0.f, 0.f};
-            } else {
-#pragma unroll
-                for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-            }
-        }
+            for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
     SA sa;
     SB sb;
@@ -456,38 +356,9 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
 
     // fragments of one k-tile, read in the order the plane products use them
     bf16x8 fa[3][TM], fb[3][TN];
-    // MF = 1: the six plane products as three paired MFMAs per 16×16 sub-block, smallest first:
-    // [A2|A0]·[B0|B2], [A1|A1]·[B1|B0], [A0|A0]·[B1|B0] (fragment types ta 0..2, tb 0, 1, 1)
-    // Each pair's fragments are read one MFMA group ahead of their use (pair 0 at the tile start,
-    // pair t + 1 inside pair t's second group): 28 fragments never live at once.
-    bf16x8 ga[3][2 * TM], gb[2][2 * TN];
-    const unsigned short* mf_img = nullptr;
-    auto read_pair = [&](int t) __attribute__((always_inline)) {
-        const unsigned short* As = mf_img;
-        const unsigned short* Bs = mf_img + SA::SIZE;
-#pragma unroll
-        for (int i = 0; i < 2 * TM; ++i) {
-            const int rb = wm * WM + i * 16;
-            if (t == 0) ga[0][i] = SA::template frag16<2, 0>(As, rb, lane);
-            else if (t == 1) ga[1][i] = SA::template frag16<1, 1>(As, rb, lane);
-            else ga[2][i] = SA::template frag16<0, 0>(As, rb, lane);
-        }
-        if (t == 2) return;                                       // pair 2 reuses gb[1]
-#pragma unroll
-        for (int j = 0; j < 2 * TN; ++j) {
-            const int cb = wn * WN + j * 16;
-            if (t == 0) gb[0][j] = SB::template frag16<0, 2>(Bs, cb, lane);
-            else gb[1][j] = SB::template frag16<1, 0>(Bs, cb, lane);
-        }
-    };
-    auto read_frags = [&](const unsigned short* img) __attribute__((always_inline)) {
+    auto read_frags = [&](const unsigned short* img) {
         const unsigned short* As = img;
         const unsigned short* Bs = img + SA::SIZE;
-        if constexpr (MF) {
-            mf_img = img;
-            read_pair(0);
-            return;
-        }
         constexpr int order[6][2] = {{0, 2}, {1, 0}, {0, 0}, {1, 2}, {0, 1}, {1, 1}};   // (operand, plane)
 #pragma unroll
         for (int o = 0; o < 6; ++o) {
@@ -502,20 +373,7 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
         }
     };
     // plane product q of the six with pa + pb ≤ 2 (smallest first)
-    auto mfma_group = [&](int q) __attribute__((always_inline)) {
-        if constexpr (MF) {               // group q: pair q >> 1 over the wave's row half q & 1
-            const int t = q >> 1, tb = t == 0 ? 0 : 1;
-            if ((q & 1) && t < 2) read_pair(t + 1);
-#pragma unroll
-            for (int i = 0; i < TM; ++i) {
-                const int ii = (q & 1) * TM + i;                 // 16-row block
-#pragma unroll
-                for (int j = 0; j < 2 * TN; ++j)
-                    acc4[ii >> 1][j >> 1][2 * (ii & 1) + (j & 1)] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                        ga[t][ii], gb[tb][j], acc4[ii >> 1][j >> 1][2 * (ii & 1) + (j & 1)], 0, 0, 0);
-            }
-            return;
-        }
+    auto mfma_group = [&](int q) {
         constexpr int pa_[6] = {2, 0, 1, 1, 0, 0}, pb_[6] = {0, 2, 1, 0, 1, 0};
         if (ABL & 1) {               // keep the fragment reads live
 #pragma unroll
@@ -530,7 +388,7 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
             for (int j = 0; j < TN; ++j)
                 acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[pa_[q]][i], fb[pb_[q]][j], acc[i][j], 0, 0, 0);
     };
-    auto compute = [&](const unsigned short* img) __attribute__((always_inline)) {
+    auto compute = [&](const unsigned short* img) {
         read_frags(img);
 #pragma unroll
         for (int q = 0; q < 6; ++q) mfma_group(q);
@@ -540,14 +398,14 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     // partial (or, for a k-group past the end, empty: every element masked to zero)
     const int nkt = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
     const int NK = (nkt + KG - 1) / KG;
-    auto k0_of = [&](int j) __attribute__((always_inline)) { return kbeg + (KG * j + grp) * BK; };
-    auto is_full = [&](int j) __attribute__((always_inline)) { return k0_of(j) + BK <= kend; };
+    auto k0_of = [&](int j) { return kbeg + (KG * j + grp) * BK; };
+    auto is_full = [&](int j) { return k0_of(j) + BK <= kend; };
     const bool tail = NK > 0 && !is_full(NK - 1);
     unsigned short* const buf0 = lds + (KG > 1 ? grp * 2 * BUF : 0);
     unsigned short* const buf1 = buf0 + BUF;
 
     // split + LDS store of the staged tile at k0 (FULL: no k tail); COPY: also the gathered rows
-    auto stage_a = [&](auto FULLc, auto COPYc, unsigned short* img, int k0) __attribute__((always_inline)) {
+    auto stage_a = [&](auto FULLc, auto COPYc, unsigned short* img, int k0) {
         constexpr bool FULL = decltype(FULLc)::value, COPY = decltype(COPYc)::value;
         if ((ABL & 2) && k0 != kbeg) return;
         if (COPY) sa.copy_out(a.acopy, a.K, m0, a.M, k0, kend);
@@ -557,12 +415,12 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
             for (int q = 0; q < SA::NV; ++q) bs[q] += sa.v[q];
         }
     };
-    auto stage_b = [&](auto FULLc, unsigned short* img, int k0) __attribute__((always_inline)) {
+    auto stage_b = [&](auto FULLc, unsigned short* img, int k0) {
         constexpr bool FULL = decltype(FULLc)::value;
         if ((ABL & 2) && k0 != kbeg) return;
         sb.template store<FULL, (ABL & 64) != 0>(img + SA::SIZE, k0, kend);
     };
-    auto load = [&](auto FULLc, int k0) __attribute__((always_inline)) {
+    auto load = [&](auto FULLc, int k0) {
         constexpr bool FULL = decltype(FULLc)::value;
         if ((ABL & 8) && k0 != kbeg) return;
         sa.template load<FULL>(k0, kend);
@@ -571,10 +429,10 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     using T = std::true_type;
     using F = std::false_type;
     // tile j through the full or the clamped path
-    auto load_t = [&](int j) __attribute__((always_inline)) {
+    auto load_t = [&](int j) {
         if (is_full(j)) load(T{}, k0_of(j)); else load(F{}, k0_of(j));
     };
-    auto stage_t = [&](auto COPYc, unsigned short* img, int j) __attribute__((always_inline)) {
+    auto stage_t = [&](auto COPYc, unsigned short* img, int j) {
         if (is_full(j)) { stage_a(T{}, COPYc, img, k0_of(j)); stage_b(T{}, img, k0_of(j)); }
         else { stage_a(F{}, COPYc, img, k0_of(j)); stage_b(F{}, img, k0_of(j)); }
     };
@@ -582,7 +440,7 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     // Pipeline, iteration j: MFMAs of tile j from one image; the split + LDS stores of tile j+1
     // (loaded one iteration ago) into the other; the loads of tile j+2; one barrier.  (Two register
     // sets — loads two tiles ahead — measured no faster and spill the 256×256 tile.)
-    auto mainloop = [&](auto COPYc) __attribute__((always_inline)) {
+    auto mainloop = [&](auto COPYc) {
         if (NK > 0) { load_t(0); stage_t(COPYc, buf0, 0); }
         if (NK > 1) load_t(1);
         __syncthreads();
@@ -655,7 +513,7 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     }
     // k-groups: block (i, j) of a wave's tile is finished by the group (i·TN + j) mod KG; every
     // other group's wave at the same position hands its partial block over through LDS
-    auto mine = [&](int i, int j) __attribute__((always_inline)) { return KG == 1 || ((i * TN + j) % KG) == grp; };
+    auto mine = [&](int i, int j) { return KG == 1 || ((i * TN + j) % KG) == grp; };
     if constexpr (KG > 1) {
         static_assert(KG == 2, "k-group exchange: two groups");
         static_assert((RED_FLOATS * 4 + NW * TM * TN * 4096) <= KG * 2 * BUF * 2, "k-group exchange: LDS");
@@ -669,8 +527,7 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q)
                     xch[((w * TM * TN + i * TN + j) * 4 + q) * 64 + lane] =
-                        MF ? acc4[i][j][q]
-                           : f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+                        f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
             }
         __syncthreads();
 #pragma unroll
@@ -681,11 +538,8 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const f32x4 o = xch[((w * TM * TN + i * TN + j) * 4 + q) * 64 + lane];
-                    if constexpr (MF) acc4[i][j][q] += o;
-                    else {
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) acc[i][j][4 * q + e] += o[e];
-                    }
+                    for (int e = 0; e < 4; ++e) acc[i][j][4 * q + e] += o[e];
                 }
             }
     }
@@ -704,32 +558,8 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     }
     if constexpr (OP != OP_TN) {
         static_assert(BM * (BN / 32) * 4 <= KG * 2 * BUF * 2, "x3 epilogue: mask words exceed LDS");
-        if constexpr (MF) x3_epilogue_out16<OP, BM, BN, TM, TN, NTH>(a, acc4, lds, m0, n0, wm, wn, tid);
-        else x3_epilogue_out<OP, BM, BN, TM, TN, NTH>(a, acc, lds, m0, n0, wm, wn, tid);
+        x3_epilogue_out<OP, BM, BN, TM, TN, NTH>(a, acc, lds, m0, n0, wm, wn, tid);
         if (ABL & 32) stamp(3);
-        return;
-    }
-    if constexpr (MF) {                   // grad_W, 16×16 sub-block layout
-        const int c = lane & 15, g = lane >> 4;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                if (!mine(i, j)) continue;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int col = n0 + wn * WN + j * 32 + 16 * (q & 1) + c;
-#pragma unroll
-                    for (int e4 = 0; e4 < 4; ++e4) {
-                        const int row = m0 + wm * WM + i * 32 + 16 * (q >> 1) + 4 * g + e4;
-                        if (col < a.N && row < a.M) {
-                            float* dst = a.C + (long)row * a.ldc + col;
-                            if (a.splits > 1) atomicAdd(dst, acc4[i][j][q][e4]);
-                            else *dst = acc4[i][j][q][e4];
-                        }
-                    }
-                }
-            }
         return;
     }
     // grad_W epilogue: every load a block needs is issued before its stores
@@ -803,7 +633,7 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
 int g_x3_ablate = -1;
 #endif
 
-template <int OP, int BM, int BN, int WARPS_M, int NTH, int OCC, int KG, int ABL = 0, int MF = 0>
+template <int OP, int BM, int BN, int WARPS_M, int NTH, int OCC, int KG, int ABL = 0>
 void launch_x3(X3Args a) {
     a.tiles_m = ppo_divup(a.M, BM);
     a.tiles_n = ppo_divup(a.N, BN);
@@ -815,7 +645,7 @@ void launch_x3(X3Args a) {
     using SB = StageX3<BN, OP != OP_NT, NTH / KG>;
     constexpr size_t lds = (size_t)KG * 2 * sizeof(unsigned short) * (SA::SIZE + SB::SIZE);
     static_assert(lds <= 160 * 1024, "gemm_x3: LDS images exceed 160 KiB");
-    auto kern = gemm_x3_kernel<OP, BM, BN, WARPS_M, NTH, OCC, KG, ABL, MF>;
+    auto kern = gemm_x3_kernel<OP, BM, BN, WARPS_M, NTH, OCC, KG, ABL>;
     if (lds > 64 * 1024) {
         static bool attr = false;                      // once per instantiation
         if (!attr) {
@@ -836,7 +666,6 @@ struct CfgX3 { int bm, bn, kg, slots_per_cu; };
 constexpr CfgX3 kCfgX3[] = {{256, 256, 1, 1}, {128, 128, 1, 2}, {128, 128, 1, 1}, {128, 128, 2, 1}, {64, 64, 1, 4}};
 int g_force_x3 = -1;
 int g_split_x3 = 0;
-int g_x3_mf = -1;                        // 1: the 16×16×32 paired form (PPO_X3_MF16)
 
 template <int OP>
 void launch_cfg_x3(int c, const X3Args& a) {
@@ -846,7 +675,7 @@ void launch_cfg_x3(int c, const X3Args& a) {
         g_x3_ablate = e ? atoi(e) : 0;
     }
     if (g_x3_ablate && (c == 0 || (c == 3 && OP == OP_TN))) {
-        auto run = [&](auto ABLc) __attribute__((always_inline)) {
+        auto run = [&](auto ABLc) {
             constexpr int A = decltype(ABLc)::value;
             if constexpr (OP == OP_TN) launch_x3<OP, 128, 128, 2, 512, 2, 2, A>(a);
             else launch_x3<OP, 256, 256, 4, 512, 2, 1, A>(a);
@@ -862,24 +691,15 @@ void launch_cfg_x3(int c, const X3Args& a) {
         }
     }
 #endif
-    if (g_x3_mf < 0) {
-        const char* e = getenv("PPO_X3_MF16");
-        g_x3_mf = e ? atoi(e) : 0;
+    switch (c) {
+        case 0: launch_x3<OP, 256, 256, 4, 512, 2, 1>(a); break;
+        case 2: launch_x3<OP, 128, 128, 4, 512, 2, 1>(a); break;
+        case 4: launch_x3<OP, 64, 64, 2, 256, 4, 1>(a); break;
+        case 3:
+            if constexpr (OP == OP_TN) { launch_x3<OP, 128, 128, 2, 512, 2, 2>(a); break; }
+            [[fallthrough]];
+        default: launch_x3<OP, 128, 128, 2, 256, 2, 1>(a); break;
     }
-    auto run = [&](auto MFc) __attribute__((always_inline)) {
-        constexpr int MF = decltype(MFc)::value;
-        switch (c) {
-            case 0: launch_x3<OP, 256, 256, 4, 512, 2, 1, 0, MF>(a); break;
-            case 2: launch_x3<OP, 128, 128, 4, 512, 2, 1, 0, MF>(a); break;
-            case 4: launch_x3<OP, 64, 64, 2, 256, 4, 1, 0, MF>(a); break;
-            case 3:
-                if constexpr (OP == OP_TN) { launch_x3<OP, 128, 128, 2, 512, 2, 2, 0, MF>(a); break; }
-                [[fallthrough]];
-            default: launch_x3<OP, 128, 128, 2, 256, 2, 1, 0, MF>(a); break;
-        }
-    };
-    if (g_x3_mf > 0) run(std::integral_constant<int, 1>{});
-    else run(std::integral_constant<int, 0>{});
 }
 
 // forward / grad_x: the largest tile whose grid still gives every CU a workgroup (one round of
@@ -887,7 +707,7 @@ void launch_cfg_x3(int c, const X3Args& a) {
 int pick_x3(int M, int N, int op) {
     if (g_force_x3 >= 0) return g_force_x3;
     if (op == OP_TN) return 3;
-    auto tiles = [&](int c) __attribute__((always_inline)) { return (long)ppo_divup(M, kCfgX3[c].bm) * ppo_divup(N, kCfgX3[c].bn); };
+    auto tiles = [&](int c) { return (long)ppo_divup(M, kCfgX3[c].bm) * ppo_divup(N, kCfgX3[c].bn); };
     if (tiles(0) >= 256) return 0;
     if (tiles(1) >= 256) return 1;
     return 4;
@@ -995,7 +815,7 @@ double ppo_bench_gemm_x3(int op, int m, int n, int l, int iters, int cfg, int sp
     const int saved = g_force_x3, saved_split = g_split_x3;
     g_force_x3 = cfg;
     g_split_x3 = splitk_target;
-    auto run = [&]() __attribute__((always_inline)) {
+    auto run = [&]() {
         if (op == 0) phip_x3_fwd(y, x, nullptr, nullptr, W, b, m, n, l, 1, bits);
         else if (op == 3) phip_x3_fwd(y, x, nullptr, nullptr, W, b, m, n, l, 0, nullptr);
         else if (op == 1) phip_x3_bwd_x(x, y, W, bits, m, n, l);
