@@ -120,11 +120,20 @@ __device__ __forceinline__ void tile_gemm(int M, int N, int K, const float* __re
             float av[8], bv[8];
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
+                const int kc = min(k0 + 4 * u + q, K - 1);
+                av[u] = Ar[(long)kc * a_sk];
+                bv[u] = Bc[(long)kc * b_sk];
+            }
+            // opaque, after all 16 loads are issued: otherwise the compiler sinks each load under
+            // its lane condition (an exec-mask branch and a wait per load)
+            asm("" : "+v"(av[0]), "+v"(av[1]), "+v"(av[2]), "+v"(av[3]), "+v"(av[4]), "+v"(av[5]), "+v"(av[6]),
+                     "+v"(av[7]), "+v"(bv[0]), "+v"(bv[1]), "+v"(bv[2]), "+v"(bv[3]), "+v"(bv[4]), "+v"(bv[5]),
+                     "+v"(bv[6]), "+v"(bv[7]));
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
                 const int k = k0 + 4 * u + q;
-                const int kc = min(k, K - 1);
-                const float x = Ar[(long)kc * a_sk], y = Bc[(long)kc * b_sk];
-                av[u] = (iok && k < K) ? x : 0.f;
-                bv[u] = (jok && k < K) ? y : 0.f;
+                av[u] = (iok && k < K) ? av[u] : 0.f;
+                bv[u] = (jok && k < K) ? bv[u] : 0.f;
             }
 #pragma unroll
             for (int u = 0; u < 8; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], acc, 0, 0, 0);
