@@ -392,9 +392,20 @@ __global__ __launch_bounds__(TPB) void tiny_update_kernel(TinyArgs a) {
                 const int n = a.sizes[l], o = a.sizes[l + 1];
                 const float* Wl = P + a.woff[l];
                 float* Tl = WT + a.wtoff[l];
-                for (int e = tid; e < n * o; e += TPB) {
-                    const int j = e / n, k = e - j * n;
-                    Tl[k * o + j] = Wl[e];
+                if (n == o) {
+                    // square: diagonal r, lane l takes (k = l, j = l + r mod n) — reads and writes on
+                    // distinct LDS banks (row-major order writes at stride o: a 64-way conflict)
+                    for (int e = tid; e < n * n; e += TPB) {
+                        const int r = e / n, k = e - r * n;
+                        int j = k + r;
+                        j = j >= n ? j - n : j;
+                        Tl[k * n + j] = Wl[j * n + k];
+                    }
+                } else {
+                    for (int e = tid; e < n * o; e += TPB) {
+                        const int j = e / n, k = e - j * n;
+                        Tl[k * o + j] = Wl[e];
+                    }
                 }
             }
             __threadfence_block();
