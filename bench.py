@@ -4,12 +4,15 @@
 A "step" is ONE PPO update over a device-resident synthetic rollout: GAE (two value
 forwards over the whole buffer + exact scan + global normalisation), then 10 value
 epochs and 4 policy epochs of ⌊N/B⌋ minibatches each (reference defaults, main.c:39-40).
-Workload (config C4 of BASELINE.json): Humanoid-shaped 376 → 3×512 → 17 MLPs, 4096 steps ×
-256 envs per GPU, B = N/32 = 32768, fp32.  Data-parallel runs shard by whole environments:
-every rank owns its own 4096×256 rollout (weak scaling), gradients are all-reduced with RCCL
-inside libppo each minibatch, advantage statistics are global.
+Workload (config C4 of BASELINE.json): Humanoid-shaped 376 → 3×512 → 17 MLPs, ONE 4096-step ×
+256-env rollout, B = N/32 = 32768, fp32.  Data-parallel runs split that rollout by whole
+environments (SURVEY §8(e), strong scaling — the default): rank r owns envs [r·E/G, (r+1)·E/G)
+and draws B/G rows per minibatch step, gradients are all-reduced with RCCL inside libppo each
+step (÷G: the gradient of the global B-row minibatch), advantage statistics are global.  `--weak`
+(opt-in, labelled "weak") gives every rank a whole 4096×256 rollout instead.  `--emulate-world G`
+runs rank 0's shard of a G-way split on one GPU (E/G envs, B/G rows), for tuning the shard shapes.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c3|c2|c5|c5f32] [--batch B]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c4|c3|c2|c5|c5f32] [--batch B] [--weak]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
     (torch.distributed.run is only the launcher: this process never imports torch)
 
@@ -179,7 +182,12 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c4", choices=sorted(CONFIGS))
     ap.add_argument("--batch", type=int, default=0)
-    ap.add_argument("--strong", action="store_true", help="split one 4096×256 rollout over the ranks")
+    ap.add_argument("--weak", action="store_true",
+                    help="weak scaling (opt-in): every rank owns a whole rollout of the config; default splits ONE "
+                         "rollout over the ranks (SURVEY §8(e))")
+    ap.add_argument("--emulate-world", type=int, default=0,
+                    help="one GPU runs rank 0's shard of a G-way split (E/G envs, B/G rows per step); the line is "
+                         "then a per-rank shard measurement, not the metric")
     ap.add_argument("--shuffle", type=int, default=1, help="1 = device Feistel shuffle, 0 = reference host rand()")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-events", action="store_true")
@@ -224,9 +232,14 @@ def main():
             raise SystemExit(f"ppo_comm_init (self) failed: {LIB.ppo_last_error().decode()}")
 
     S, H, A, T, E, B = CONFIGS[args.config]
-    if args.strong and world > 1:
-        E = E // world
-        B = max(1, B // world)
+    split = world if world > 1 else max(1, args.emulate_world)
+    if args.weak:
+        split = 1
+    if split > 1:
+        if E % split or B % split:
+            raise SystemExit(f"config {args.config}: E={E}, B={B} do not split over {split} ranks")
+        E = E // split
+        B = B // split
     if args.batch:
         B = args.batch
     N = T * E
@@ -354,14 +367,19 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": 1000.0 * t_update,
         "higher_is_better": True,
-        "scaling": "strong" if args.strong else "weak",
+        "scaling": "weak" if args.weak else "strong",
         "vs_baseline": None,
         "dtype": dtype,
         "data": "synthetic (seeded device generator: obs U(-1,1), actions from the policy, rewards 0.1·N(0,1), "
                 "terminated Bernoulli(1/500), truncated at env-segment ends); random-init weights",
         "config": {"workload": f"{args.config}: {S}->{'x'.join(map(str, H))}->{A} MLP (policy + value), "
-                               f"{T} steps x {E} envs per GPU, B={B}, 10 value + 4 policy epochs",
-                   "global_batch": B * world, "rollout_per_gpu": N, "parallelism": f"dp{world}",
+                               f"{T} steps x {E * split} envs" + (f" split over {split} ranks ({E} envs, B/{split}="
+                               f"{B} rows per rank per step)" if split > 1 else "") +
+                               (" per GPU (weak scaling)" if args.weak else "") +
+                               f", global B={B * (world if args.weak else split)}, 10 value + 4 policy epochs",
+                   "global_batch": B * (world if args.weak else split), "rollout_per_gpu": N,
+                   "parallelism": f"dp{world}",
+                   "emulated_world": args.emulate_world if (world == 1 and args.emulate_world > 1) else None,
                    "comm": "rccl-self (1-rank rehearsal)" if comm_self else ("rccl" if world > 1 else "none"),
                    "shuffle": "device-feistel" if args.shuffle else "host-rand"},
         "updates_per_sec": 1.0 / t_update,

@@ -107,6 +107,7 @@ typedef struct {
     int policy;                     /* 0 = value epochs (MSE), 1 = policy epochs (clipped surrogate) */
     const float *state, *action, *logprob, *adv, *adv_target;   /* device buffer arrays */
     int limit, B, num_batches, n_epochs;        /* n_epochs ≤ 16 */
+    long max_steps;                 /* ≤ 0: every step of the n_epochs; else the first max_steps */
     const int* perms;               /* [n_epochs][limit] permutations, or NULL: device Feistel */
     uint32_t feistel_k[64];         /* per epoch, 4 round keys (when perms == NULL) */
     const float *steps, *steps_ls;  /* device [n_steps][2] = {lr/bc1, bc2} per Adam step */

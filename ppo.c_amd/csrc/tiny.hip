@@ -73,6 +73,7 @@ struct TinyArgs {
     // buffer
     const float* state; const float* action; const float* logprob; const float* adv; const float* adv_target;
     int limit, B, num_batches, n_epochs;
+    int total_steps;                // n_epochs·num_batches, or the step cap (ppo_set_step_limit)
     const int* perms;               // [n_epochs][limit] host rand() permutations, or nullptr → Feistel
     Feistel fk[16];                 // per-epoch Feistel keys (device shuffle)
     const float* steps;             // per step: {lr/bc1, bc2} of the network's Adam (value / policy)
@@ -235,7 +236,7 @@ __global__ __launch_bounds__(TPB) void tiny_update_kernel(TinyArgs a) {
     __threadfence_block();
     __syncthreads();
     for (int ep = 0; ep < a.n_epochs; ++ep) {
-        for (int kb = 0; kb < a.num_batches; ++kb, ++step) {
+        for (int kb = 0; kb < a.num_batches && step < a.total_steps; ++kb, ++step) {
             TINY_STAMP(0);
             // ---- gather (trajectory_buffer.cu:168-200) ----
             for (int i = tid; i < B; i += TPB) {
@@ -462,6 +463,8 @@ int phip_tiny_update(const PhipTinyNet* net, const PhipTinyPhase* ph) {
     a.state = ph->state; a.action = ph->action; a.logprob = ph->logprob; a.adv = ph->adv;
     a.adv_target = ph->adv_target;
     a.limit = ph->limit; a.B = ph->B; a.num_batches = ph->num_batches; a.n_epochs = ph->n_epochs;
+    a.total_steps = ph->n_epochs * ph->num_batches;
+    if (ph->max_steps > 0 && ph->max_steps < a.total_steps) a.total_steps = (int)ph->max_steps;
     a.perms = ph->perms;
     for (int e = 0; e < ph->n_epochs && !ph->perms; ++e) {
         Feistel& f = a.fk[e];
@@ -518,12 +521,12 @@ int phip_tiny_update(const PhipTinyNet* net, const PhipTinyPhase* ph) {
         fprintf(stderr, "tiny: wall clock %.1f MHz\n", mhz);
         double acc[5] = {0, 0, 0, 0, 0};
         int n = 0;
-        for (int st = 1; st < 64 && st < ph->n_epochs * ph->num_batches; ++st, ++n)
+        for (int st = 1; st < 64 && st < a.total_steps; ++st, ++n)
             for (int k = 0; k < 5; ++k) acc[k] += (double)(h[st * 8 + k + 1] - h[st * 8 + k]) / mhz;
         const double clk = (double)(h[63 * 8 + 6] - h[1 * 8 + 6]) / ((double)(h[63 * 8] - h[1 * 8]) / mhz);
         if (n) fprintf(stderr, "tiny: shader clock %.0f MHz\n", clk);
         double fl[3] = {0, 0, 0};
-        for (int st = 1; st < 64 && st < ph->n_epochs * ph->num_batches; ++st) {
+        for (int st = 1; st < 64 && st < a.total_steps; ++st) {
             fl[0] += (double)(h[512 + st * 4 + 0] - h[st * 8 + 1]) / mhz;
             fl[1] += (double)(h[512 + st * 4 + 1] - h[512 + st * 4 + 0]) / mhz;
             fl[2] += (double)(h[512 + st * 4 + 2] - h[512 + st * 4 + 1]) / mhz;

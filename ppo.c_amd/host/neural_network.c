@@ -13,6 +13,7 @@
 #include "internal.h"
 
 #include <math.h>
+#include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -247,17 +248,24 @@ static int use_x3(int m) { return m > 1024 && ppo_gemm_f32_engine(-1) == 1; }
 /* per layer: the 1- and A-wide output layers are latency-bound skinny products where the exact
  * kernels (and their paired backward launch) measure faster (profiles/r01_x3_sweep.txt) */
 static int use_x3_layer(int m, int n, int l) { return use_x3(m) && n > 32 && l > 32; }
-/* the reference-API products (mat_mul*_cuda, layers.c) through the same engine choice (fp32 storage) */
+/* the reference-API products (mat_mul*_cuda, layers.c) through the same engine choice (fp32 storage).
+ * Callers may pass any valid device pointer (a row or element offset into a buffer); the x3 kernels
+ * need 16-B aligned operands, so an unaligned operand routes to the exact family, which has a scalar
+ * path for it. */
+static int al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 void lin_fwd(float* y, const float* x, const float* W, const float* b, int m, int n, int l) {
-    if (use_x3(m) && phip_x3_supported(0, m, n, l)) phip_x3_fwd(y, x, NULL, NULL, W, b, m, n, l, 0, NULL);
+    if (use_x3(m) && phip_x3_supported(0, m, n, l) && al16(y) && al16(x) && al16(W) && al16(b))
+        phip_x3_fwd(y, x, NULL, NULL, W, b, m, n, l, 0, NULL);
     else phip_linear_fwd(y, x, W, b, m, n, l, 0);
 }
 void lin_bwd_x(float* gx, const float* g, const float* W, int m, int n, int l) {
-    if (use_x3(m) && phip_x3_supported(1, m, n, l)) phip_x3_bwd_x(gx, g, W, NULL, m, n, l);
+    if (use_x3(m) && phip_x3_supported(1, m, n, l) && al16(gx) && al16(g) && al16(W))
+        phip_x3_bwd_x(gx, g, W, NULL, m, n, l);
     else phip_linear_bwd_x(gx, g, W, NULL, m, n, l);
 }
 void lin_bwd_w(float* gW, const float* g, const float* x, int m, int n, int l) {
-    if (use_x3(m) && phip_x3_supported(2, m, n, l)) phip_x3_bwd_w(gW, NULL, g, x, m, n, l, 0);
+    if (use_x3(m) && phip_x3_supported(2, m, n, l) && al16(gW) && al16(g) && al16(x))
+        phip_x3_bwd_w(gW, NULL, g, x, m, n, l, 0);
     else phip_linear_bwd_w(gW, NULL, g, x, m, n, l);
 }
 

@@ -375,7 +375,6 @@ static int ppo_update_tiny(PPO* ppo, PPODev* d, int B, int n_epochs_policy, int 
     const int limit = buf->full ? buf->capacity : buf->idx;
     const int num_batches = buf->capacity / B;
     if (getenv("PPO_NO_TINY") || phip_comm_world() > 1 || n_epochs_value > 16 || n_epochs_policy > 16) return -1;
-    if (d->max_v >= 0 || d->max_p >= 0) return -1;          /* step caps: the multi-launch path */
     PhipTinyNet nv, np;
     if (tiny_net(ppo->V, ppo->adam_V, &nv) || tiny_net(ppo->policy->mu, ppo->adam_policy, &np)) return -1;
     if (!ppo->adam_entropy->flat) return -1;
@@ -406,23 +405,29 @@ static int ppo_update_tiny(PPO* ppo, PPODev* d, int B, int n_epochs_policy, int 
      * (value on libppo's stream, policy on the side stream: they share only read-only buffer
      * arrays), each on its own CU.  PPO_SERIAL=1 runs them one after the other. */
     PhipTinyPhase pv = ph, pp = ph;
-    const int run_v = n_epochs_value > 0 && num_batches > 0, run_p = n_epochs_policy > 0 && num_batches > 0;
+    /* step caps (ppo_set_step_limit): the first max steps of each phase, as in the multi-launch loop */
+    long cap_v = (long)n_epochs_value * num_batches, cap_p = (long)n_epochs_policy * num_batches;
+    if (d->max_v >= 0 && cap_v > d->max_v) cap_v = d->max_v;
+    if (d->max_p >= 0 && cap_p > d->max_p) cap_p = d->max_p;
+    const int run_v = cap_v > 0, run_p = cap_p > 0;
     if (run_v) {
         pv.policy = 0;
         pv.n_epochs = n_epochs_value;
+        pv.max_steps = cap_v;
         pv.perms = tiny_perms(ppo, d, shuffle_mode, n_epochs_value, limit, &pv);
-        pv.steps = tiny_steps(d, 0, ppo->adam_V, ppo->lr_V, n_epochs_value * num_batches);
+        pv.steps = tiny_steps(d, 0, ppo->adam_V, ppo->lr_V, (int)cap_v);
     } else if (n_epochs_value > 0) {
         for (int j = 0; j < n_epochs_value; j++) { uint64_t key; next_perm(ppo, d, shuffle_mode, &key); }
     }
     if (run_p) {
         pp.policy = 1;
         pp.n_epochs = n_epochs_policy;
+        pp.max_steps = cap_p;
         pp.perms = tiny_perms(ppo, d, shuffle_mode, n_epochs_policy, limit, &pp);
         /* per step the entropy Adam steps before the policy Adam (ppo.cu:440-442); their step
          * counters are independent, so the two sequences can be generated one after the other */
-        pp.steps_ls = tiny_steps(d, 1, ppo->adam_entropy, ppo->lr_policy, n_epochs_policy * num_batches);
-        pp.steps = tiny_steps(d, 2, ppo->adam_policy, ppo->lr_policy, n_epochs_policy * num_batches);
+        pp.steps_ls = tiny_steps(d, 1, ppo->adam_entropy, ppo->lr_policy, (int)cap_p);
+        pp.steps = tiny_steps(d, 2, ppo->adam_policy, ppo->lr_policy, (int)cap_p);
     } else if (n_epochs_policy > 0) {
         for (int j = 0; j < n_epochs_policy; j++) { uint64_t key; next_perm(ppo, d, shuffle_mode, &key); }
     }
@@ -431,13 +436,13 @@ static int ppo_update_tiny(PPO* ppo, PPODev* d, int B, int n_epochs_policy, int 
     if (concurrent) phip_side_fork();
     if (run_v) {
         if (phip_tiny_update(&nv, &pv) != 0) die("ppo_update: tiny value phase failed to launch");
-        d->n_v += (long)n_epochs_value * num_batches;
+        d->n_v += cap_v;
     }
     if (run_p) {
         if (concurrent) phip_side_use(1);
         if (phip_tiny_update(&np, &pp) != 0) die("ppo_update: tiny policy phase failed to launch");
         if (concurrent) phip_side_use(0);
-        d->n_p += (long)n_epochs_policy * num_batches;
+        d->n_p += cap_p;
     }
     if (concurrent) phip_side_join();
     return 0;

@@ -1,0 +1,344 @@
+"""Production-size parity for the bench configurations C2, C3 and C5 (C4's is in test_gpu_index.py).
+
+Each config runs at the exact shape bench.py times, on the kernels the bench runs, against the
+oracle (reference ppo.cu:391-447 per minibatch; mat_mul.cu:132-217 for every product):
+
+* C2 (Pendulum 3 → 2×64 → 1, N = 4096, B = 64): the single-workgroup path (csrc/tiny.hip) that the
+  C2 bench line runs — one value and one policy minibatch (gradients and Adam deltas vs the oracle),
+  then the first 16 value and 16 policy steps element by element against the oracle's update;
+* C3 (17 → 2×256 → 6, N = 4096×64 = 262,144, B = 8192): one value and one policy minibatch on the x3
+  engine's production 64×64 / split-K grids and the fused output heads;
+* C5 (1024 → 4×1024 → 17, bf16, N = 8192×64 = 524,288, B = 16384: the bench's per-GPU shard): one
+  value and one policy minibatch against a bf16 emulation that rounds what the kernels round
+  (2e-3·max|ref|) and against the fp32 oracle (3e-2·max|ref|, SURVEY §8c's bf16 bound); the bf16
+  gathered layer-0 copy equals bf16(state[rows]) bit for bit.
+
+Inputs are bench.py's own: ppo_fill_synthetic (seeded device generator) after create_ppo from srand.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import ppo_ffi
+from helpers import (F32, assert_gemm_close, assert_rel_close, gpu_relu_masks, nn_grads_packed, nn_params_packed,
+                     oracle_grads_with_masks)
+from test_gpu_bf16 import bf16, unpack
+from test_gpu_update import adam_first_step, assert_adam_delta, make_ppo, policy_state
+
+pytestmark = pytest.mark.gpu
+
+RELU = lambda sizes: [1] * (len(sizes) - 2) + [0]  # noqa: E731
+LR = 3e-4
+
+
+def device_buffer(lib, ppo, N, S, A):
+    """The device rollout as the oracle's buffer dict (whole arrays)."""
+    b = ppo.contents.buffer.contents
+    return dict(state=ppo_ffi.d2h(lib, b.d_state_p, F32, N * S).reshape(N, S),
+                next_state=ppo_ffi.d2h(lib, b.d_next_state_p, F32, N * S).reshape(N, S),
+                action=ppo_ffi.d2h(lib, b.d_action_p, F32, N * A).reshape(N, A),
+                reward=ppo_ffi.d2h(lib, b.d_reward_p, F32, N),
+                logprob=ppo_ffi.d2h(lib, b.d_logprob_p, F32, N),
+                terminated=ppo_ffi.d2h(lib, b.d_terminated_p, np.uint8, N),
+                truncated=ppo_ffi.d2h(lib, b.d_truncated_p, np.uint8, N))
+
+
+def bench_ppo(lib, oracle, sizes, E, T, seed, dtype=0):
+    ppo = make_ppo(lib, oracle, sizes, E * T, seed=seed)
+    assert lib.ppo_set_compute_dtype(ppo, dtype) == 0
+    lib.ppo_fill_synthetic(ppo, E, T, seed, 1.0 / 500)
+    lib.ppo_synchronize()
+    return ppo
+
+
+def ref_value_grads(oracle, sv, v0, x, tgt, masks, what):
+    acts = oracle.mlp_forward(sv, RELU(sv), v0, x)
+    y = oracle.mlp_layer_outputs(sv, acts, x.shape[0])[-1].ravel()
+    _, g = oracle.mse(y, tgt)
+    return oracle_grads_with_masks(oracle, sv, RELU(sv), v0, x, g.reshape(-1, 1), masks, what, max_flips=256)
+
+
+def ref_policy_grads(oracle, sizes, mu0, ls0, x, a, adv, old, masks, what, ent_coeff=0.0):
+    acts = oracle.mlp_forward(sizes, RELU(sizes), mu0, x)
+    mu = oracle.mlp_layer_outputs(sizes, acts, x.shape[0])[-1]
+    lp = oracle.log_prob(mu, ls0, a)
+    _, glp, gent = oracle.policy_loss_and_grad(adv, lp, old, oracle.entropy(ls0), ent_coeff, 0.2)
+    gmu_out, gls = oracle.log_prob_backwards(mu, ls0, a, glp)
+    g, _ = oracle_grads_with_masks(oracle, sizes, RELU(sizes), mu0, x, gmu_out, masks, what, max_flips=256)
+    return g, gls + gent
+
+
+# ----------------------------------------------------------------------------- C2: the tiny path
+C2 = [3, 64, 64, 1]
+
+
+@pytest.fixture(scope="module")
+def c2_state(lib, oracle):
+    oracle.load(use_openblas=True)
+    ppo = bench_ppo(lib, oracle, C2, 1, 4096, seed=2024)
+    mu0, ls0 = policy_state(lib, ppo)
+    v0 = nn_params_packed(lib, ppo.contents.V)
+    buf = device_buffer(lib, ppo, 4096, 3, 1)
+    lib.free_ppo(ppo)
+    return mu0, ls0, v0, buf
+
+
+def _c2_run(lib, oracle, n_val_steps, n_pol_steps, seed):
+    """A fresh C2 PPO from the fixture's seed: GAE + the first n value / policy steps on the tiny path."""
+    ppo = bench_ppo(lib, oracle, C2, 1, 4096, seed=2024)
+    lib.ppo_set_step_limit(ppo, n_val_steps, n_pol_steps)
+    lib.ppo_reset_stats(ppo)
+    lib.ppo_update(ppo, 0.99, 64, 1, 1, 1, seed)
+    lib.ppo_synchronize()
+    # the tiny path leaves no multi-launch forward behind (the last bits / d_x0 are GAE's, m = N)
+    assert ppo.contents.V.contents.bits_m != 64, "C2 did not take the single-workgroup path"
+    return ppo
+
+
+def test_c2_tiny_single_steps_vs_oracle(lib, oracle, c2_state):
+    """One value and one policy minibatch (B = 64) of the C2 bench update on the tiny path vs the oracle."""
+    mu0, ls0, v0, buf = c2_state
+    N, B, seed = 4096, 64, 515
+    ppo = _c2_run(lib, oracle, 1, 1, seed)
+    pol = ppo.contents.policy.contents
+    gV, v1 = nn_grads_packed(lib, ppo.contents.V), nn_params_packed(lib, ppo.contents.V)
+    gmu, mu1 = nn_grads_packed(lib, pol.mu), nn_params_packed(lib, pol.mu)
+    gls = ppo_ffi.d2h(lib, pol.d_log_std_grad, F32, 1)
+    b = ppo.contents.buffer.contents
+    tgt_all = ppo_ffi.d2h(lib, b.d_adv_target_p, F32, N)
+    adv_all = ppo_ffi.d2h(lib, b.d_advantage_p, F32, N)
+    st = (C.c_double * 7)()
+    lib.ppo_read_stats(ppo, st, 7)
+    lib.free_ppo(ppo)
+    ref = oracle.ppo_update(C2, RELU(C2), mu0, ls0, v0, buf, batch_size=B, n_epochs_policy=1, n_epochs_value=1,
+                            shuffle_mode=1, seed=seed, max_value_steps=1, max_policy_steps=1)
+    assert st[1] == ref["n_v"] == 1 and st[3] == ref["n_p"] == 1
+    assert_rel_close(tgt_all, ref["adv_target"], 2e-4, 2e-4 * np.abs(ref["adv_target"]).max(), "C2 adv_target")
+    assert_rel_close(adv_all, ref["advantage"], 2e-3, 2e-3, "C2 advantage")
+    key = oracle.splitmix64(seed)
+    rows_v = oracle.feistel_perm(N, key)[:B]
+    rows_p = oracle.feistel_perm(N, (key + 1) & (2**64 - 1))[:B]
+    sv = C2[:-1] + [1]
+    g_ref, _ = ref_value_grads(oracle, sv, v0, buf["state"][rows_v], ref["adv_target"][rows_v], None, "C2 value")
+    assert_gemm_close(gV, g_ref, B, "C2 value grads (tiny)")
+    flips = assert_adam_delta(v1, ref["v"], g_ref, LR, "C2 value params")
+    assert flips <= 2
+    g_ref, gls_ref = ref_policy_grads(oracle, C2, mu0, ls0, buf["state"][rows_p], buf["action"][rows_p],
+                                      ref["advantage"][rows_p], buf["logprob"][rows_p], None, "C2 policy")
+    assert_gemm_close(gmu, g_ref, B, "C2 policy grads (tiny)")
+    assert_rel_close(gls, gls_ref, 1e-3, 1e-5 * max(1.0, float(np.abs(gls_ref).max())), "C2 log_std grad")
+    flips = assert_adam_delta(mu1, ref["mu"], g_ref, LR, "C2 policy params")
+    assert flips <= 2
+
+
+def test_c2_tiny_first_steps_elementwise(lib, oracle, c2_state):
+    """The first 16 value and 16 policy steps of the C2 bench update (tiny path) against the oracle's
+    update of the same buffer, element by element (bounds of test_short_update_elementwise)."""
+    mu0, ls0, v0, buf = c2_state
+    B, seed, n = 64, 616, 16
+    ppo = _c2_run(lib, oracle, n, n, seed)
+    mu1, ls1 = policy_state(lib, ppo)
+    v1 = nn_params_packed(lib, ppo.contents.V)
+    st = (C.c_double * 7)()
+    lib.ppo_read_stats(ppo, st, 7)
+    t = (ppo.contents.adam_V.contents.time_step, ppo.contents.adam_policy.contents.time_step,
+         ppo.contents.adam_entropy.contents.time_step)
+    lib.free_ppo(ppo)
+    ref = oracle.ppo_update(C2, RELU(C2), mu0, ls0, v0, buf, batch_size=B, n_epochs_policy=1, n_epochs_value=1,
+                            shuffle_mode=1, seed=seed, max_value_steps=n, max_policy_steps=n)
+    assert t == (ref["t_v"], ref["t_mu"], ref["t_ent"]) == (n, n, n)
+    assert st[1] == ref["n_v"] == n and st[3] == ref["n_p"] == n
+    for got, want, what in ((v1, ref["v"], "V"), (mu1, ref["mu"], "mu"), (ls1, ref["log_std"], "log_std")):
+        err = np.abs(got.astype(np.float64) - want)
+        q = float((err <= 0.1 * LR).mean())
+        print(f"C2 {what}: max err {err.max() / LR:.4f} lr, {100 * q:.3f} % within 0.1 lr")
+        assert err.max() <= 2 * LR * n, f"{what}: max err {err.max()}"
+        assert q >= 0.99, f"{what}: only {q * 100:.2f} % within 0.1·lr"
+    np.testing.assert_allclose(st[0], ref["sum_v_loss"], rtol=1e-3)
+    np.testing.assert_allclose(st[2], ref["sum_policy_loss"], rtol=1e-3, atol=1e-5)
+
+
+# ----------------------------------------------------------------------------- C3: x3 production grids
+C3 = [17, 256, 256, 6]
+
+
+@pytest.fixture(scope="module")
+def c3(lib, oracle):
+    oracle.load(use_openblas=True)
+    oracle.load().ref_blas_threads(16)
+    ppo = bench_ppo(lib, oracle, C3, 64, 4096, seed=3131)
+    yield ppo, 64 * 4096
+    lib.ppo_set_step_limit(ppo, -1, -1)
+    lib.free_ppo(ppo)
+
+
+def _gathered(lib, nn_ptr, B, S):
+    nn = nn_ptr.contents
+    assert nn.bits_m == B and nn.x0_dtype == 0
+    return ppo_ffi.d2h(lib, nn.d_x0, F32, B * S).reshape(B, S)
+
+
+def test_c3_timed_value_step(lib, oracle, c3):
+    """One value minibatch of the C3 bench update (N = 262,144, B = 8192, x3 grids, fused head) vs the oracle."""
+    ppo, N = c3
+    B, seed = 8192, 71
+    assert lib.ppo_gemm_f32_engine(-1) == 1
+    v0 = nn_params_packed(lib, ppo.contents.V)
+    lib.ppo_set_step_limit(ppo, 1, 0)
+    lib.ppo_update(ppo, 0.99, B, 0, 1, 1, seed)
+    lib.ppo_synchronize()
+    gV, v1 = nn_grads_packed(lib, ppo.contents.V), nn_params_packed(lib, ppo.contents.V)
+    b = ppo.contents.buffer.contents
+    rows = oracle.feistel_perm(N, oracle.splitmix64(seed))[:B]
+    x = ppo_ffi.d2h(lib, b.d_state_p, F32, N * 17).reshape(N, 17)[rows]
+    np.testing.assert_array_equal(_gathered(lib, ppo.contents.V, B, 17), x)
+    tgt = ppo_ffi.d2h(lib, b.d_adv_target_p, F32, N)[rows]
+    sv = C3[:-1] + [1]
+    g_ref, _ = ref_value_grads(oracle, sv, v0, x, tgt, gpu_relu_masks(lib, ppo.contents.V, x), "C3 value")
+    assert_gemm_close(gV, g_ref, B, "C3 value grads")
+    flips = assert_adam_delta(v1, adam_first_step(v0, g_ref, LR), g_ref, LR, "C3 value params")
+    assert flips <= v1.size // 1000
+
+
+def test_c3_timed_policy_step(lib, oracle, c3):
+    """One policy minibatch of the C3 bench update (A = 6 fused clipped-surrogate head) vs the oracle."""
+    ppo, N = c3
+    B, seed, A = 8192, 93, 6
+    pol = ppo.contents.policy.contents
+    mu0 = nn_params_packed(lib, pol.mu)
+    ls0 = ppo_ffi.d2h(lib, pol.d_log_std, F32, A)
+    lib.ppo_set_step_limit(ppo, 0, 1)
+    lib.ppo_update(ppo, 0.99, B, 1, 0, 1, seed)
+    lib.ppo_synchronize()
+    gmu, mu1 = nn_grads_packed(lib, pol.mu), nn_params_packed(lib, pol.mu)
+    gls = ppo_ffi.d2h(lib, pol.d_log_std_grad, F32, A)
+    b = ppo.contents.buffer.contents
+    rows = oracle.feistel_perm(N, oracle.splitmix64(seed))[:B]
+    x = ppo_ffi.d2h(lib, b.d_state_p, F32, N * 17).reshape(N, 17)[rows]
+    np.testing.assert_array_equal(_gathered(lib, pol.mu, B, 17), x)
+    a = ppo_ffi.d2h(lib, b.d_action_p, F32, N * A).reshape(N, A)[rows]
+    adv = ppo_ffi.d2h(lib, b.d_advantage_p, F32, N)[rows]
+    old = ppo_ffi.d2h(lib, b.d_logprob_p, F32, N)[rows]
+    g_ref, gls_ref = ref_policy_grads(oracle, C3, mu0, ls0, x, a, adv, old, gpu_relu_masks(lib, pol.mu, x),
+                                      "C3 policy")
+    assert_gemm_close(gmu, g_ref, B, "C3 policy grads")
+    assert_rel_close(gls, gls_ref, 1e-3, 1e-4 * max(1.0, float(np.abs(gls_ref).max())), "C3 log_std grad")
+    flips = assert_adam_delta(mu1, adam_first_step(mu0, g_ref, LR), g_ref, LR, "C3 policy params")
+    assert flips <= mu1.size // 1000
+
+
+# ----------------------------------------------------------------------------- C5: bf16 at the bench shard
+C5 = [1024, 1024, 1024, 1024, 1024, 17]
+
+
+def emu_forward(sizes, params, x):
+    """bf16-mode forward as the kernels compute it (float64 accumulation; test_gpu_bf16.emulate)."""
+    layers = unpack(sizes, params)
+    hs = [bf16(x)]
+    for i, (W, b) in enumerate(layers):
+        z = hs[-1].astype(np.float64) @ bf16(W).astype(np.float64).T + b
+        if i < len(layers) - 1:
+            hs.append(bf16(np.maximum(z, 0.0).astype(F32)))
+        else:
+            y = z.astype(F32)
+    return hs, y
+
+
+def emu_backward(sizes, params, hs, gout):
+    layers = unpack(sizes, params)
+    grads = [None] * len(layers)
+    g = gout.astype(F32)
+    for i in range(len(layers) - 1, -1, -1):
+        W, _ = layers[i]
+        gb16 = bf16(g).astype(np.float64)
+        grads[i] = ((gb16.T @ hs[i].astype(np.float64)).astype(F32).ravel(), gb16.sum(axis=0).astype(F32))
+        if i > 0:
+            gx = np.where(hs[i] > 0, gb16 @ bf16(W).astype(np.float64), 0.0)
+            g = bf16(gx.astype(F32))
+    return np.concatenate([np.concatenate([gw, gb]) for gw, gb in grads])
+
+
+def close(got, ref, rel, what):
+    err = float(np.abs(got - ref).max())
+    tol = rel * float(np.abs(ref).max()) + 1e-6
+    assert err <= tol, f"{what}: max |err| {err:.3g} > {tol:.3g}"
+
+
+@pytest.fixture(scope="module")
+def c5(lib, oracle):
+    oracle.load(use_openblas=True)
+    oracle.load().ref_blas_threads(16)
+    ppo = bench_ppo(lib, oracle, C5, 64, 8192, seed=5151, dtype=1)
+    N = 64 * 8192
+    b = ppo.contents.buffer.contents
+    state = ppo_ffi.d2h(lib, b.d_state_p, F32, N * 1024).reshape(N, 1024)
+    yield ppo, N, state
+    lib.ppo_set_step_limit(ppo, -1, -1)
+    lib.free_ppo(ppo)
+
+
+def _gathered_bf16(lib, nn_ptr, B, S):
+    nn = nn_ptr.contents
+    assert nn.x0_dtype == 1
+    u = ppo_ffi.d2h(lib, nn.d_x0, np.uint16, B * S).reshape(B, S)
+    return (u.astype(np.uint32) << 16).view(F32)
+
+
+def test_c5_bf16_timed_value_step(lib, oracle, c5):
+    """One bf16 value minibatch at the bench's C5 shard (N = 524,288, B = 16384, fused bf16 value head)."""
+    ppo, N, state = c5
+    B, seed = 16384, 57
+    V = ppo.contents.V
+    v0 = nn_params_packed(lib, V)
+    lib.ppo_set_step_limit(ppo, 1, 0)
+    lib.ppo_update(ppo, 0.99, B, 0, 1, 1, seed)
+    lib.ppo_synchronize()
+    gV, v1 = nn_grads_packed(lib, V), nn_params_packed(lib, V)
+    b = ppo.contents.buffer.contents
+    rows = oracle.feistel_perm(N, oracle.splitmix64(seed))[:B]
+    x = state[rows]
+    np.testing.assert_array_equal(_gathered_bf16(lib, V, B, 1024), bf16(x))      # the gather, bit for bit
+    tgt = ppo_ffi.d2h(lib, b.d_adv_target_p, F32, N)[rows]
+    sv = C5[:-1] + [1]
+    hs, y = emu_forward(sv, v0, x)
+    g_emu = emu_backward(sv, v0, hs, (2 * (y.ravel() - tgt) / B).reshape(-1, 1))
+    close(gV, g_emu, 2e-3, "C5 value grads vs bf16 emulation")
+    g_ref, _ = ref_value_grads(oracle, sv, v0, x, tgt, None, "C5 value")
+    close(gV, g_ref, 3e-2, "C5 value grads vs fp32 oracle")
+    # Adam's first step is lr·sign(g) wherever |g| ≫ ε: exact against the emulated gradient's step
+    flips = assert_adam_delta(v1, adam_first_step(v0, g_emu, LR), g_emu, LR, "C5 value params")
+    assert flips <= v1.size // 1000
+
+
+def test_c5_bf16_timed_policy_step(lib, oracle, c5):
+    """One bf16 policy minibatch at the bench's C5 shard (A = 17 clipped surrogate)."""
+    ppo, N, state = c5
+    B, seed, A = 16384, 59, 17
+    pol = ppo.contents.policy.contents
+    mu0 = nn_params_packed(lib, pol.mu)
+    ls0 = ppo_ffi.d2h(lib, pol.d_log_std, F32, A)
+    lib.ppo_set_step_limit(ppo, 0, 1)
+    lib.ppo_update(ppo, 0.99, B, 1, 0, 1, seed)
+    lib.ppo_synchronize()
+    gmu, mu1 = nn_grads_packed(lib, pol.mu), nn_params_packed(lib, pol.mu)
+    gls = ppo_ffi.d2h(lib, pol.d_log_std_grad, F32, A)
+    b = ppo.contents.buffer.contents
+    rows = oracle.feistel_perm(N, oracle.splitmix64(seed))[:B]
+    x = state[rows]
+    np.testing.assert_array_equal(_gathered_bf16(lib, pol.mu, B, 1024), bf16(x))
+    a = ppo_ffi.d2h(lib, b.d_action_p, F32, N * A).reshape(N, A)[rows]
+    adv = ppo_ffi.d2h(lib, b.d_advantage_p, F32, N)[rows]
+    old = ppo_ffi.d2h(lib, b.d_logprob_p, F32, N)[rows]
+    hs, mu = emu_forward(C5, mu0, x)
+    lp = oracle.log_prob(mu, ls0, a)
+    _, glp, gent = oracle.policy_loss_and_grad(adv, lp, old, oracle.entropy(ls0), 0.0, 0.2)
+    gmu_out, gls_emu = oracle.log_prob_backwards(mu, ls0, a, glp)
+    g_emu = emu_backward(C5, mu0, hs, gmu_out)
+    close(gmu, g_emu, 2e-3, "C5 policy grads vs bf16 emulation")
+    close(gls, gls_emu + gent, 2e-3, "C5 log_std grad vs bf16 emulation")
+    g_ref, gls_ref = ref_policy_grads(oracle, C5, mu0, ls0, x, a, adv, old, None, "C5 policy")
+    close(gmu, g_ref, 3e-2, "C5 policy grads vs fp32 oracle")
+    close(gls, gls_ref, 3e-2, "C5 log_std grad vs fp32 oracle")
+    flips = assert_adam_delta(mu1, adam_first_step(mu0, g_emu, LR), g_emu, LR, "C5 policy params")
+    assert flips <= mu1.size // 1000
