@@ -335,8 +335,8 @@ def main():
         engines = ["exact-fp32", "x3", "bf16"]
         for i in range(n_sh):
             k = keys[i]
-            shapes.append({"op": ops[(k >> 58) & 0xF], "engine": engines[(k >> 54) & 0xF], "m": (k >> 24) & 0x3FFFFFFF,
-                           "n": (k >> 12) & 0xFFF, "l": k & 0xFFF, "launches": kl[i], "ms": kms[i],
+            shapes.append({"op": ops[(k >> 60) & 0xF], "engine": engines[(k >> 56) & 0xF], "m": (k >> 32) & 0xFFFFFF,
+                           "n": (k >> 16) & 0xFFFF, "l": k & 0xFFFF, "launches": kl[i], "ms": kms[i],
                            "avg_us": 1000.0 * kms[i] / kl[i], "tflops": kw[i] / (kms[i] * 1e-3) / 1e12})
         shapes.sort(key=lambda d: -d["ms"])
 

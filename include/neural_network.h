@@ -92,7 +92,8 @@ typedef struct {
      * mirrors, host mirrors edited by the caller are pushed to HBM — never blindly overwritten */
     float* h_sync;          /* host-mirror snapshot at the last sync: packed [W0,b0,...] then extra_floats */
     long   dev_version;     /* bumped by every HBM parameter update */
-    long   host_version;    /* dev_version the host mirrors last matched */
+    long   host_version;    /* dev_version the host mirrors (weights and extra floats) last matched */
+    long   host_version_w;  /* dev_version the host weight mirrors last matched (a weights-only sync) */
 } NeuralNetwork;
 
 typedef struct {

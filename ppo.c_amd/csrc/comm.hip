@@ -39,6 +39,19 @@ __global__ void replicate_kernel(const double* __restrict__ src, double* __restr
     for (long i = blockIdx.x * 256L + threadIdx.x; i < n * k; i += (long)gridDim.x * 256)
         dst[i] = src[i % n];
 }
+// loopback stand-in of an integer min all-reduce: lane r < k holds rank r's (identical) value
+__global__ void min_i32_loopback_kernel(int* __restrict__ x, int k) {
+    const int r = threadIdx.x;
+    int v = x[0];
+    __syncthreads();
+    if (r < k && r < 64) x[r] = v;
+    __syncthreads();
+    if (r == 0) {
+        int m = x[0];
+        for (int i = 1; i < k && i < 64; ++i) m = min(m, x[i]);
+        x[0] = m;
+    }
+}
 hipStream_t g_comm_stream = nullptr;
 constexpr int kEvents = 16;                  // ring: a wait captures the record at enqueue time
 hipEvent_t g_ready[kEvents], g_done[kEvents];
@@ -238,12 +251,17 @@ void ppo_comm_barrier(void) {
 // min over ranks of a host integer (synchronous; a few µs per call).  The update uses it to agree
 // on whether any rank has an empty shard, so either every rank trains or none does.
 int phip_comm_min_i32(int v) {
-    if (!g_comm) return v;                     // world 1 or loopback (identical ranks)
-    if (!g_i32) g_i32 = (int*)phip_malloc(sizeof(int));
+    if (!g_comm && !g_loopback) return v;      // world 1
+    if (!g_i32) g_i32 = (int*)phip_malloc(sizeof(int) * 64);
     phip_h2d(g_i32, &v, sizeof(int));
     int slot;
     hipStream_t cs = comm_enter(&slot);
-    nccl_check(ncclAllReduce(g_i32, g_i32, 1, ncclInt32, ncclMin, g_comm, cs), "ncclAllReduce(min)", __LINE__);
+    if (g_loopback) {                          // k identical ranks: replicate, then the min over the k copies
+        hipLaunchKernelGGL(min_i32_loopback_kernel, dim3(1), dim3(64), 0, cs, g_i32, g_loopback);
+        PPO_LAUNCH_CHECK();
+    } else {
+        nccl_check(ncclAllReduce(g_i32, g_i32, 1, ncclInt32, ncclMin, g_comm, cs), "ncclAllReduce(min)", __LINE__);
+    }
     comm_leave(slot);
     int out = v;
     phip_d2h(&out, g_i32, sizeof(int));

@@ -32,9 +32,11 @@ struct ProfScope {
 // dispatch itself (hipExtLaunchKernel) — the kernel's own duration, as rocprofv3 reports it.
 bool take_kernel_events(hipEvent_t* start, hipEvent_t* stop);
 
-// shape tag of a GEMM launch: op (0 fwd, 1 grad_x, 2 grad_W, 3 paired bwd) | engine | m | n | l
+// shape tag of a GEMM launch: op (0 fwd, 1 grad_x, 2 grad_W, 3 paired bwd) [60..63] | engine [56..59] |
+// m [32..55] | n [16..31] | l [0..15]; fields masked so an out-of-range width cannot alias another shape
 inline long long gemm_key(int op, int engine, long m, long n, long l) {
-    return ((long long)op << 58) | ((long long)engine << 54) | ((long long)m << 24) | ((long long)n << 12) | l;
+    return ((long long)(op & 0xF) << 60) | ((long long)(engine & 0xF) << 56) | ((long long)(m & 0xFFFFFF) << 32) |
+           ((long long)(n & 0xFFFF) << 16) | (long long)(l & 0xFFFF);
 }
 
 }  // namespace ppo

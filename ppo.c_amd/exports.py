@@ -10,7 +10,7 @@ import re
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-INCLUDE = os.path.join(HERE, "..", "..", "include")
+INCLUDE = os.path.join(HERE, "..", "include")
 
 _DECL = re.compile(r"^\s*(?:[A-Za-z_][\w\s\*]*?[\s\*])([A-Za-z_]\w*)\s*\([^;{]*\)\s*;", re.M)
 _SKIP = {"if", "while", "for", "switch", "return", "sizeof"}

@@ -60,37 +60,62 @@ static long packed_offset(const NeuralNetwork* nn, int layer) {
     return off;
 }
 
+/* the caller edited a weight mirror since the last sync (it differs from the h_sync snapshot) */
+static int nn_mirrors_edited(const NeuralNetwork* nn) {
+    for (int i = 0; i < nn->num_layers - 1; i++) {
+        const Layer* ly = &nn->layers[i];
+        const size_t nw = (size_t)ly->input_size * ly->output_size, nb = (size_t)ly->output_size;
+        const float* sw = nn->h_sync + packed_offset(nn, i);
+        if (memcmp(sw, ly->weights, sizeof(float) * nw) || memcmp(sw + nw, ly->biases, sizeof(float) * nb)) return 1;
+    }
+    return 0;
+}
+
+/* Weights and the caller-owned extra floats (policy log σ behind μ) are reconciled separately:
+ * host_version_w records the HBM version the weight mirrors were last pulled at, so a weights-only
+ * sync (extra == NULL: forward_propagation / save_neural_network on μ itself) pulls once per HBM
+ * update and afterwards pushes the caller's mirror edits, instead of pulling again on every call.
+ * When HBM moved AND the caller edited a mirror since the last sync, HBM wins (it holds the
+ * update's result) and the lost edit is reported on stderr. */
 void nn_host_sync(NeuralNetwork* nn, float* extra) {
     const int L = nn->num_layers - 1;
     const long ne = extra ? nn->extra_floats : 0;
-    if (nn->dev_version != nn->host_version) {            /* HBM is newer: pull */
+    int pushed = 0;
+    if (nn->dev_version != nn->host_version_w) {          /* HBM weights are newer: pull */
+        if (nn_mirrors_edited(nn))
+            fprintf(stderr, "libppo: warning: host weight edits dropped: the device parameters were updated "
+                            "since the last sync (ppo_update / Adam)\n");
         nn_write_weights_to_host(nn);
-        if (ne) {
+        nn->host_version_w = nn->dev_version;
+    } else {                                              /* push the tensors the caller edited */
+        for (int i = 0; i < L; i++) {
+            Layer* ly = &nn->layers[i];
+            const size_t nw = (size_t)ly->input_size * ly->output_size, nb = (size_t)ly->output_size;
+            float* sw = nn->h_sync + packed_offset(nn, i);
+            if (memcmp(sw, ly->weights, sizeof(float) * nw)) {
+                phip_h2d(ly->d_weights, ly->weights, sizeof(float) * nw);
+                memcpy(sw, ly->weights, sizeof(float) * nw);
+                pushed = 1;
+            }
+            if (memcmp(sw + nw, ly->biases, sizeof(float) * nb)) {
+                phip_h2d(ly->d_biases, ly->biases, sizeof(float) * nb);
+                memcpy(sw + nw, ly->biases, sizeof(float) * nb);
+                pushed = 1;
+            }
+        }
+    }
+    if (ne) {
+        float* snap = nn->h_sync + nn->num_params_packed;
+        if (nn->dev_version != nn->host_version) {        /* HBM extras newer: pull */
             phip_d2h(extra, nn->d_params + nn->num_params, sizeof(float) * (size_t)ne);
-            memcpy(nn->h_sync + nn->num_params_packed, extra, sizeof(float) * (size_t)ne);
+            memcpy(snap, extra, sizeof(float) * (size_t)ne);
+        } else if (memcmp(snap, extra, sizeof(float) * (size_t)ne)) {
+            phip_h2d(nn->d_params + nn->num_params, extra, sizeof(float) * (size_t)ne);
+            memcpy(snap, extra, sizeof(float) * (size_t)ne);
         }
-        if (ne || !nn->extra_floats) nn->host_version = nn->dev_version;
-        return;
-    }
-    int pushed = 0;                                       /* push the tensors the caller edited */
-    for (int i = 0; i < L; i++) {
-        Layer* ly = &nn->layers[i];
-        const size_t nw = (size_t)ly->input_size * ly->output_size, nb = (size_t)ly->output_size;
-        float* sw = nn->h_sync + packed_offset(nn, i);
-        if (memcmp(sw, ly->weights, sizeof(float) * nw)) {
-            phip_h2d(ly->d_weights, ly->weights, sizeof(float) * nw);
-            memcpy(sw, ly->weights, sizeof(float) * nw);
-            pushed = 1;
-        }
-        if (memcmp(sw + nw, ly->biases, sizeof(float) * nb)) {
-            phip_h2d(ly->d_biases, ly->biases, sizeof(float) * nb);
-            memcpy(sw + nw, ly->biases, sizeof(float) * nb);
-            pushed = 1;
-        }
-    }
-    if (ne && memcmp(nn->h_sync + nn->num_params_packed, extra, sizeof(float) * (size_t)ne)) {
-        phip_h2d(nn->d_params + nn->num_params, extra, sizeof(float) * (size_t)ne);
-        memcpy(nn->h_sync + nn->num_params_packed, extra, sizeof(float) * (size_t)ne);
+        nn->host_version = nn->dev_version;
+    } else if (!nn->extra_floats) {
+        nn->host_version = nn->dev_version;
     }
     if (pushed) nn_sync_w16(nn);
 }
@@ -524,6 +549,7 @@ void nn_write_weights_to_host(NeuralNetwork* nn) {
         memcpy(nn->h_sync + off + nw, ly->biases, sizeof(float) * nb);
         off += (long)(nw + nb);
     }
+    nn->host_version_w = nn->dev_version;
     if (!nn->extra_floats) nn->host_version = nn->dev_version;   /* with extras: the owner syncs them too */
 }
 

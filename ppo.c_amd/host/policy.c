@@ -143,7 +143,7 @@ void policy_to_host(GaussianPolicy* policy) {
     nn_write_weights_to_host(policy->mu);
     phip_d2h(policy->log_std, policy->d_log_std, sizeof(float) * (size_t)policy->action_size);
     nn_sync_extra_snapshot(policy->mu, policy->log_std);
-    policy->mu->host_version = policy->mu->dev_version;
+    policy->mu->host_version = policy->mu->host_version_w = policy->mu->dev_version;
 }
 
 /* before a host-pointer entry point: μ's mirrors and log_std reconciled with HBM (nn_host_sync) */
@@ -168,6 +168,6 @@ GaussianPolicy* load_policy(FILE* file, int state_size, int action_size) {
     attach_log_std(p);
     phip_h2d(p->d_log_std, p->log_std, sizeof(float) * (size_t)action_size);
     nn_sync_extra_snapshot(p->mu, p->log_std);
-    p->mu->host_version = p->mu->dev_version;
+    p->mu->host_version = p->mu->host_version_w = p->mu->dev_version;
     return p;
 }

@@ -199,6 +199,7 @@ static int gae_full_forwards(void) {
 
 void ppo_gae_device(NeuralNetwork* V, TrajectoryBuffer* b, float gamma, float lambda) {
     const int n = b->full ? b->capacity : b->idx;
+    g_gae_own_rows = 0;                     /* an empty buffer reports no own-row forward */
     ensure_gae_ws(n);
     if (n > 0 && gae_full_forwards()) {     /* the reference's two full forwards (ppo.cu:333-336) */
         nn_forward_dev(V, b->next_state_p, n);

@@ -7,7 +7,7 @@ mkdir -p $O
 for rep in 1 2; do
   for v in "$@"; do
     if [ "$v" = base ]; then L=$R/ppo.c_amd/lib/libppo.so; else L=$R/ppo.c_amd/lib/variants/libppo_$v.so; fi
-    PPO_LIB=$L timeout -k 10 120 python3 $R/ppo.c_amd/tools/x3_bench.py --shapes "0,32768,512,512;1,32768,512,512;2,32768,512,512" --iters 50 | sed "s/^/$v /" >> $O/x3.txt || exit 1
+    PPO_LIB=$L timeout -k 10 120 python3 $R/tools/x3_bench.py --shapes "0,32768,512,512;1,32768,512,512;2,32768,512,512" --iters 50 | sed "s/^/$v /" >> $O/x3.txt || exit 1
     PPO_LIB=$L timeout -k 10 120 python3 $R/bench.py --no-cpu-baseline --no-rollout --no-kernel-events | grep '^{' | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$v', round(d['ms_per_step'],2))" >> $O/bench.txt || exit 1
   done
 done

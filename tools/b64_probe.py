@@ -2,7 +2,7 @@
 """Small-minibatch probe (the reference's own B = 64): wall µs per minibatch step of a
 step-limited update at CONFIG's network, host-issue vs GPU time.
 
-    python ppo.c_amd/tools/b64_probe.py [c4|c3] [B] [value_steps] [policy_steps]
+    python tools/b64_probe.py [c4|c3] [B] [value_steps] [policy_steps]
 Prints µs per step with both loops concurrent and with PPO_SERIAL=1 semantics (serial run last).
 """
 import ctypes as C
@@ -10,7 +10,7 @@ import os
 import sys
 import time
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "ppo.c_amd"))
 import ppo_ffi  # noqa: E402
 
 NETS = {"c4": (376, [512, 512, 512], 17, 4096, 256), "c3": (17, [256, 256], 6, 4096, 64)}

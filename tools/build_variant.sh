@@ -3,7 +3,7 @@
 # under extra defines in place of csrc/REPLACES.hip (default SRC), for A/B sweeps and diagnostics on the GPU box (tools/*.py --lib
 # ppo.c_amd/lib/variants/libppo_NAME.so); e.g. `build_variant.sh diag -DPPO_X3_DIAG gemm_x3`
 set -e
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../ppo.c_amd"
 SRC=${3:-gemm}
 REP=${4:-$SRC}
 mkdir -p build/variants lib/variants

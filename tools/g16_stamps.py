@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-phase cycles of the double-buffered bf16 GEMM (cfg 9, C5 16384x1024x1024) from in-kernel
-stamps (diagnostic build: `sh ppo.c_amd/tools/build_variant.sh g16ab32 -DPPO_G16_ABLATE=32 gemm16`):
+stamps (diagnostic build: `sh tools/build_variant.sh g16ab32 -DPPO_G16_ABLATE=32 gemm16`):
 mainloop, epilogue issue, store drain per workgroup (s_memtime), and from s_memrealtime the span of
 the workgroups against the launch's event time."""
 import ctypes as C
@@ -9,10 +9,10 @@ import sys
 
 import numpy as np
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "ppo.c_amd"))
 import ppo_ffi  # noqa: E402
 
-lib = ppo_ffi.load(os.environ.get("PPO_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "lib",
+lib = ppo_ffi.load(os.environ.get("PPO_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "ppo.c_amd", "lib",
                                                              "variants", "libppo_g16ab32.so"))
 lib.ppo_set_device(0)
 m, n, l = 16384, 1024, 1024

@@ -1,14 +1,14 @@
 #!/usr/bin/env python3
 """bf16 GEMM (gemm16.hip) sweep on the MI355X: device µs and TFLOP/s per (op, shape, config, split-K).
 
-    python ppo.c_amd/tools/gemm16_sweep.py [--cfgs 0,4] [--shape M,N,L]
+    python tools/gemm16_sweep.py [--cfgs 0,4] [--shape M,N,L]
 op 0 = forward (bias+ReLU+bits), 1 = grad_x (bit mask), 2 = grad_W (split-K, fp32 atomics).
 """
 import argparse
 import os
 import sys
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "ppo.c_amd"))
 import ppo_ffi  # noqa: E402
 
 NAMES = {0: "128x128/bk32", 1: "128x32/bk32", 2: "32x128/bk32", 3: "64x64/bk32", 4: "128x128/bk64",

@@ -1,13 +1,13 @@
 #!/usr/bin/env python3
 """Run one GEMM shape/op/config repeatedly (a target for rocprofv3 --pmc passes).
 
-    python ppo.c_amd/tools/gemm_one.py OP M N L [CFG] [ITERS] [SPLITK_TARGET]
+    python tools/gemm_one.py OP M N L [CFG] [ITERS] [SPLITK_TARGET]
 env GEMM_ENGINE=x3 runs the x3 engine (fp32 operands on the bf16 MFMA) instead of the exact fp32 one.
 """
 import os
 import sys
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "ppo.c_amd"))
 import ppo_ffi  # noqa: E402
 
 op, m, n, l = (int(v) for v in sys.argv[1:5])

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """GEMM tile/split sweep on the MI355X: device µs and TFLOP/s per (op, shape, tile config).
 
-    python ppo.c_amd/tools/gemm_sweep.py [--quick]
+    python tools/gemm_sweep.py [--quick]
 op 0 = forward (bias+ReLU), 1 = grad_x, 2 = grad_W (+bias grad, split-K).
 """
 import argparse
@@ -10,7 +10,7 @@ import json
 import os
 import sys
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "ppo.c_amd"))
 import ppo_ffi  # noqa: E402
 
 CFG_NAMES = {0: "128x128/bk16", 1: "128x128/bk32", 2: "128x32/bk16", 3: "32x128/bk16", 4: "64x64/bk16",

@@ -3,13 +3,13 @@
 → buffer_to_device, pageable malloc'd arrays), so one update costs the H2D copy of the buffer plus
 the update itself.  Reported in DESIGN §5 beside bench.py's HBM-resident `value` (never as it).
 
-    python ppo.c_amd/tools/pcie_rate.py
+    python tools/pcie_rate.py
 """
 import os
 import sys
 import time
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "ppo.c_amd"))
 import ppo_ffi  # noqa: E402
 
 S, H, A, T, E, B = 376, [512, 512, 512], 17, 4096, 256, 32768

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-launch averages of rocprofv3 --pmc counters for the GEMM kernel of pmc_gemm.sh passes.
 
-    python ppo.c_amd/tools/pmc_summary.py gpurun_out/pmc [OPS]
+    python tools/pmc_summary.py gpurun_out/pmc [OPS]
 SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_* count quad-cycles (MI355X_MICROARCH.md); the shares below
 are of SQ_WAVE_CYCLES.  MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE/8 · 256 CUs · 4 SIMDs).
 """

@@ -2,12 +2,12 @@
 """Small-M exact-fp32 products (B = 64 minibatches, rollout steps): the automatic choice (small-M
 kernel where it applies) against forced tiled configurations, µs per launch (ppo_bench_gemm).
 
-    python ppo.c_amd/tools/smallm_sweep.py
+    python tools/smallm_sweep.py
 """
 import os
 import sys
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "ppo.c_amd"))
 import ppo_ffi  # noqa: E402
 
 SHAPES = [(64, 376, 512), (64, 512, 512), (64, 512, 17), (64, 17, 256), (64, 256, 256), (64, 256, 6),

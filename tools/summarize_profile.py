@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 CSV output into the files committed under profiles/.
 
-    python ppo.c_amd/tools/summarize_profile.py --trace DIR/r1_kernel_trace.csv --stats DIR/r1_kernel_stats.csv \
+    python tools/summarize_profile.py --trace DIR/r1_kernel_trace.csv --stats DIR/r1_kernel_stats.csv \
         [--fetch pmc/fetch_counter_collection.csv --write pmc/write_counter_collection.csv] --tag r01
 
 Writes profiles/<tag>_kernel_stats.csv (copy), profiles/<tag>_gemm_by_shape.txt (per tile/grid:
@@ -16,7 +16,7 @@ import json
 import os
 import shutil
 
-ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..")
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
 
 
 def gemm_key(name, grid_threads):

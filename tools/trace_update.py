@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-kernel breakdown of the LAST PPO update in a rocprofv3 --kernel-trace CSV.
 
-    python ppo.c_amd/tools/trace_update.py gpurun_out/prof/run_kernel_trace.csv [--top 30]
+    python tools/trace_update.py gpurun_out/prof/run_kernel_trace.csv [--top 30]
 """
 import argparse
 import collections

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """libppo's GEMM kernels beside the vendor library at the PPO layer shapes (context for the roofline).
 
-    python ppo.c_amd/tools/vendor_gemm_ref.py > profiles/r01_vendor_gemm_ref.txt
+    python tools/vendor_gemm_ref.py > profiles/r01_vendor_gemm_ref.txt
 
 Per shape and op (0 forward y = x·Wᵀ, 1 grad_x = g·W, 2 grad_W = gᵀ·x): torch.matmul (hipBLASLt /
 rocBLAS) in bf16 and fp32, libppo's bf16 kernel (C5 mode) and its x3 engine (fp32 on the bf16 MFMA).
@@ -13,7 +13,7 @@ import sys
 
 import torch  # first: libppo binds to the HIP runtime torch already loaded
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "ppo.c_amd"))
 import ppo_ffi  # noqa: E402
 
 SHAPES = [("c4 512->512", 32768, 512, 512), ("c4 376->512", 32768, 376, 512), ("c5 1024->1024", 16384, 1024, 1024)]

@@ -7,6 +7,6 @@ R=$GRAFT_REPO_ROOT
 export PPO_LIB=${PPO_LIB:-$R/ppo.c_amd/lib/variants/libppo_diag.so}
 for op in 0 1 2; do
   for ab in 0 1 2 4 8 64; do
-    PPO_X3_ABLATE=$ab GEMM_ENGINE=x3 timeout -k 10 60 python3 $R/ppo.c_amd/tools/gemm_one.py $op 32768 512 512 -1 50 | sed "s/^/ablate=$ab /" || exit 1
+    PPO_X3_ABLATE=$ab GEMM_ENGINE=x3 timeout -k 10 60 python3 $R/tools/gemm_one.py $op 32768 512 512 -1 50 | sed "s/^/ablate=$ab /" || exit 1
   done
 done

@@ -2,13 +2,13 @@
 """Time the x3 engine's launches at the C4 (and C3/C5-fp32) layer shapes: µs per launch and TF/s
 (fp32-equivalent 2·m·n·l) per tile configuration and split-K target.
 
-    python ppo.c_amd/tools/x3_bench.py [--cfgs 0,1,2] [--splits 0,256,512] [--iters 50]
+    python tools/x3_bench.py [--cfgs 0,1,2] [--splits 0,256,512] [--iters 50]
 """
 import argparse
 import os
 import sys
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "ppo.c_amd"))
 import ppo_ffi  # noqa: E402
 
 SHAPES = [(0, 32768, 512, 512), (0, 32768, 376, 512), (1, 32768, 512, 512), (2, 32768, 512, 512),

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-phase cycles of the x3 forward (C4 512x512, cfg 0) from in-kernel stamps (diagnostic build:
-`sh ppo.c_amd/tools/build_variant.sh diag -DPPO_X3_DIAG gemm_x3`, run with --lib): prologue, mainloop,
+`sh tools/build_variant.sh diag -DPPO_X3_DIAG gemm_x3`, run with --lib): prologue, mainloop,
 epilogue per workgroup (s_memtime, shader cycles), and from s_memrealtime (100 MHz, common to all
 XCDs) the span of the workgroups against the launch's event time and the shader clock."""
 import argparse
@@ -11,7 +11,7 @@ import sys
 import numpy as np
 
 os.environ["PPO_X3_ABLATE"] = "32"
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "ppo.c_amd"))
 import ppo_ffi  # noqa: E402
 
 ap = argparse.ArgumentParser()
@@ -19,7 +19,7 @@ ap.add_argument("--lib", default=None)
 ap.add_argument("--op", type=int, default=0, help="0 forward, 1 grad_x")
 ap.add_argument("shape", nargs="*", type=int, default=[32768, 512, 512])
 args = ap.parse_args()
-lib = ppo_ffi.load(args.lib or os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "lib", "variants", "libppo_diag.so"))
+lib = ppo_ffi.load(args.lib or os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "ppo.c_amd", "lib", "variants", "libppo_diag.so"))
 lib.ppo_set_device(0)
 m, n, l = args.shape
 lib.ppo_bench_gemm_x3(args.op, m, n, l, 400, 0, 0)          # ≥ 2 s of back-to-back launches: settled clock
