@@ -272,10 +272,10 @@ def _bf16_dev(lib, ptr, rows, width):
     return (u.astype(np.uint32) << 16).view(F32)
 
 
-def assert_bf16_rounding(got, want, what, max_frac=None):
+def assert_bf16_rounding(got, want, sum_abs, what):
     """got (bf16 storage) is the bf16 rounding of an fp32 accumulation of want (float64): within half
-    a bf16 ulp of want, plus the fp32 accumulation bound (1e-5 of the tensor's max)."""
-    tol = ULP * np.abs(want) + 1e-5 * float(np.abs(want).max())
+    a bf16 ulp of want, plus the fp32 accumulation bound 2^-15·Σ|terms| (sum_abs)."""
+    tol = ULP * np.abs(want) + 2.0 ** -15 * sum_abs + 1e-12
     bad = np.abs(got - want) > tol
     assert not bad.any(), f"{what}: {int(bad.sum())} elements off by more than a bf16 rounding, worst " \
                           f"{float(np.abs(got - want)[bad].max()):.3g}"
@@ -296,7 +296,8 @@ def check_bf16_layers(lib, nn_ptr, sizes, params, x, gtop, top_rounded, what):
     for i in range(L - 1):                                  # hidden layers: bf16(relu(x·Wᵀ + b))
         W, b = layers[i]
         z = hs[i].astype(np.float64) @ bf16(W).astype(np.float64).T + b
-        assert_bf16_rounding(hs[i + 1], np.maximum(z, 0.0), f"{what} forward layer {i}")
+        sa = np.abs(hs[i]).astype(np.float64) @ np.abs(bf16(W)).astype(np.float64).T + np.abs(b)
+        assert_bf16_rounding(hs[i + 1], np.maximum(z, 0.0), sa, f"{what} forward layer {i}")
     W, b = layers[L - 1]
     y = ppo_ffi.d2h(lib, nn.d_output, F32, B * sizes[L]).reshape(B, sizes[L])
     z = hs[L - 1].astype(np.float64) @ bf16(W).astype(np.float64).T + b
@@ -311,12 +312,23 @@ def check_bf16_layers(lib, nn_ptr, sizes, params, x, gtop, top_rounded, what):
         else:
             g = _bf16_dev(lib, nn.layers[i + 1].d_grad_x, B, sizes[i + 1]).astype(np.float64)
         gW = g.T @ hs[i].astype(np.float64)
-        close(grads[off:off + nw].reshape(W.shape), gW, 1e-4, f"{what} grad_W layer {i}")
-        close(grads[off + nw:off + nw + b.size], g.sum(axis=0), 1e-4, f"{what} bias grad layer {i}")
+        # fp32 sums over B = 16384 rows (split-K partials, wave-level chains, f32 atomics): bounded by
+        # the fp32 summation error of those terms, c·Σ|g·h| with c = 2^-15 (≈ 256 chained additions
+        # of unit roundoff 2^-24 — the chains the kernels use are shorter), not by max|gW|: the
+        # MSE / surrogate gradients change sign row to row, so |Σ g·h| ≪ Σ|g·h|
+        c = 2.0 ** -15
+        sum_abs = np.abs(g).T @ np.abs(hs[i]).astype(np.float64)
+        err = np.abs(grads[off:off + nw].reshape(W.shape) - gW)
+        assert (err <= c * sum_abs + 1e-9).all(), f"{what} grad_W layer {i}: worst err / Σ|g·h| " \
+            f"{float((err / np.maximum(sum_abs, 1e-30)).max()):.3g}"
+        errb = np.abs(grads[off + nw:off + nw + b.size] - g.sum(axis=0))
+        assert (errb <= c * np.abs(g).sum(axis=0) + 1e-9).all(), f"{what} bias grad layer {i}"
         off += nw + b.size
         if i > 0:
             gx = np.where(hs[i] > 0, g @ bf16(W).astype(np.float64), 0.0)
-            assert_bf16_rounding(_bf16_dev(lib, nn.layers[i].d_grad_x, B, sizes[i]), gx, f"{what} grad_x layer {i}")
+            sa = np.abs(g) @ np.abs(bf16(W)).astype(np.float64)
+            assert_bf16_rounding(_bf16_dev(lib, nn.layers[i].d_grad_x, B, sizes[i]), gx, sa,
+                                 f"{what} grad_x layer {i}")
     return grads
 
 
