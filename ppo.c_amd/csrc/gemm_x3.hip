@@ -14,15 +14,18 @@
 // the exact fp32 MFMA (tests/test_gpu_x3.py).  Ceiling: 2.5 PF/s ÷ 6 = 417 TF/s fp32-equivalent.
 //
 // Pipeline (one workgroup per CU):
-//   * BK = 16 k-tiles; the three planes of both operand tiles live in an LDS image that is DOUBLE
-//     buffered, so each k-tile costs ONE barrier and the split + LDS stores of tile t+1 and the
-//     global loads of tile t+2 are issued in the same basic block as tile t's MFMAs (the
-//     scheduler interleaves them; nothing waits for a whole staging phase);
+//   * BK = 16 k-tiles; the three planes of both operand tiles live in a TRIPLE-buffered LDS ring,
+//     one barrier per k-tile: while tile t's MFMAs run, the split + LDS stores of tile t+2 and the
+//     global loads of tile t+3 are issued, and tile t+1's fragments (complete since the previous
+//     barrier) are read into the fragment registers as tile t's plane products retire them — so
+//     the MFMAs after a barrier start on fragments already in registers (no LDS-latency bubble per
+//     k-tile, no extra registers: the plane-product order frees each fragment plane early);
 //   * the split happens once per staged element (at LDS-store time), not once per wave reading it;
-//   * k-contiguous operands (x and W of the forward) are staged [row][24] bf16 per plane — a
-//     fragment is one conflict-free ds_read_b128 (48-B pitch: every 16-lane group of the read hits
-//     each of the 64 banks once); row-contiguous operands (W in grad_x, g and x in grad_W) are staged
-//     [k][R+pad] as loaded and read with two ds_read_b64_tr_b16 hardware transposes per fragment;
+//   * images are unpadded and XOR-swizzled (the ring fits in 144 KiB): k-contiguous operands (x and
+//     W of the forward) are staged [row][16] bf16 per plane with the two 16-B k-chunks of a row
+//     swapped on odd 8-row groups — a fragment is one conflict-free ds_read_b128; row-contiguous
+//     operands (W in grad_x, g and x in grad_W) are staged [k][R] with 32-B row segments XOR-permuted
+//     per k-row and read with two ds_read_b64_tr_b16 hardware transposes per fragment, conflict-free;
 //   * grad_W (split-K, f32 atomics) runs two k-groups per workgroup that sum through LDS, halving
 //     the atomics per output element;
 //   * XCD-aware block remap: tiles that share an operand panel run on one XCD's L2.
@@ -95,13 +98,22 @@ template <int R, bool MN, int NTH>
 struct StageX3 {
     static constexpr int NV = R * BK / (4 * NTH);            // float4 loads per thread
     static_assert(NV >= 1 && R * BK == 4 * NTH * NV, "tile / thread count");
-    static constexpr int PK = BK + 8;                        // k-contiguous pitch (bf16) = 48 B
-    static constexpr int PR = ((R / 2) % 64 == 16 || (R / 2) % 64 == 48) ? R : R + 32;   // row-contiguous pitch
-    static constexpr int PLANE = MN ? BK * PR : R * PK;      // bf16 elements per plane
+    static_assert(R == 64 || R == 128 || R == 256, "x3 operand tile rows");
+    static constexpr int PLANE = R * BK;                     // bf16 elements per plane (unpadded)
     static constexpr int SIZE = 3 * PLANE;
+    // k-contiguous [row][16]: element (row, k) — the 16-B chunks of rows with bit 3 set are swapped
+    __device__ __forceinline__ static int kc_off(int row, int k) {
+        return row * BK + 8 * ((k >> 3) ^ ((row >> 3) & 1)) + (k & 7);
+    }
+    // row-contiguous [k][R]: element (k, row) — 32-B segment s of k-row k sits at s ^ sw(k), so the
+    // 4 k-rows × 2 segments a 32-lane group of ds_read_b64_tr_b16 touches cover the 8 bank groups
+    __device__ __forceinline__ static int sw(int k) { return R >= 128 ? 2 * (k & 3) : 2 * ((k >> 1) & 1); }
+    __device__ __forceinline__ static int mn_off(int k, int row) {
+        return k * R + 16 * ((row >> 4) ^ sw(k)) + (row & 15);
+    }
     static constexpr int TPR = BK / (4 * NV);                // k-contiguous: threads per row
     static constexpr int KSTEP = 4 * NTH / R;                // row-contiguous: k distance of the q-th load
-    static_assert(MN || (TPR >= 1 && NTH % (8 * TPR) == 0), "k-contiguous mapping");
+    static_assert(MN || (TPR >= 1 && NTH * 4 * NV == R * BK), "k-contiguous mapping");
 
     f32x4 v[NV];
     const float* base;                                       // this thread's element (row, k) at k0 = 0
@@ -118,10 +130,11 @@ struct StageX3 {
             k = tid / (R / 4);
             base = p + (long)k * ld + min(r0 + row, Rmax - 4);
         } else {
-            // 8 consecutive lanes take 8 rows at one k offset: with the 48-B pitch their
-            // ds_write_b128s cover the 32 write banks once (row-major lane order: 2-way conflicts)
-            row = (tid % 8) + 8 * (tid / (8 * TPR));
-            k = ((tid / 8) % TPR) * 4 * NV;
+            // TPR consecutive lanes take one row's 16 k, the next TPR the next row: 8 lanes (a
+            // ds_write_b128 lane group; 16 for ds_write_b64) then cover 4 rows × 32 B = 128 B, every
+            // write bank ((a/4) mod 32) once; the global loads stay whole 64-B row segments
+            row = tid / TPR;
+            k = (tid % TPR) * 4 * NV;
             const int gr = min(r0 + row, Rmax - 1);
             base = p + (long)(ridx ? ridx[gr] : gr) * ld + k;
         }
@@ -164,7 +177,7 @@ struct StageX3 {
             for (int q = 0; q < NV; ++q) {
                 u32x2 p0, p1, p2;
                 split(vv[q], p0, p1, p2);
-                unsigned short* d = img + (k + q * KSTEP) * PR + row;
+                unsigned short* d = img + mn_off(k + q * KSTEP, row);
                 *reinterpret_cast<u32x2*>(d) = p0;
                 *reinterpret_cast<u32x2*>(d + PLANE) = p1;
                 *reinterpret_cast<u32x2*>(d + 2 * PLANE) = p2;
@@ -173,7 +186,7 @@ struct StageX3 {
             u32x2 a0, a1, a2, b0, b1, b2;
             split(vv[0], a0, a1, a2);
             split(vv[NV - 1], b0, b1, b2);
-            unsigned short* d = img + row * PK + k;
+            unsigned short* d = img + kc_off(row, k);
             *reinterpret_cast<u32x4*>(d) = u32x4{a0[0], a0[1], b0[0], b0[1]};
             *reinterpret_cast<u32x4*>(d + PLANE) = u32x4{a1[0], a1[1], b1[0], b1[1]};
             *reinterpret_cast<u32x4*>(d + 2 * PLANE) = u32x4{a2[0], a2[1], b2[0], b2[1]};
@@ -182,7 +195,7 @@ struct StageX3 {
             for (int q = 0; q < NV; ++q) {
                 u32x2 p0, p1, p2;
                 split(vv[q], p0, p1, p2);
-                unsigned short* d = img + row * PK + k + 4 * q;
+                unsigned short* d = img + kc_off(row, k + 4 * q);
                 *reinterpret_cast<u32x2*>(d) = p0;
                 *reinterpret_cast<u32x2*>(d + PLANE) = p1;
                 *reinterpret_cast<u32x2*>(d + 2 * PLANE) = p2;
@@ -201,14 +214,15 @@ struct StageX3 {
     // MFMA fragment (32 rows × 16 k, bf16x8 per lane: row `rr`, k = 8h..8h+7) of one plane
     __device__ __forceinline__ static bf16x8 frag(const unsigned short* plane, int rr, int lane) {
         const int h = lane >> 5;
-        if (!MN) return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(plane + rr * PK + 8 * h));
+        if (!MN) return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(plane + kc_off(rr, 8 * h)));
         // hardware transpose: in each 16-lane group lane 4q+p addresses k-row q, rows 4p..4p+3 of
-        // the group's 16; lane i receives row i of the 4 k-rows (two reads: k 8h+0..3, 8h+4..7)
+        // the group's 16; lane i receives row i of the 4 k-rows (two reads: k 8h+0..3, 8h+4..7;
+        // sw(k + 4) = sw(k), so the second read is 4 k-rows further)
         const int gi = lane & 15, q = gi >> 2, p = gi & 3;
         typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-        const unsigned short* a0 = plane + (8 * h + q) * PR + (rr - gi) + 4 * p;
+        const unsigned short* a0 = plane + mn_off(8 * h + q, rr - gi) + 4 * p;
         const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
-        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 4 * PR));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 4 * R));
         const s16x8 f = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
         return __builtin_bit_cast(bf16x8, f);
     }
@@ -307,7 +321,8 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     using SB = StageX3<BN, B_MN, NTG>;
     constexpr int BUF = SA::SIZE + SB::SIZE;
 
-    extern __shared__ __attribute__((aligned(16))) unsigned short lds[];     // KG × 2 × BUF
+    constexpr int NS = 3;                                          // LDS ring stages
+    extern __shared__ __attribute__((aligned(16))) unsigned short lds[];     // KG × NS × BUF
 
     // XCD-aware remap: hardware deals blocks round-robin over the 8 XCDs; give each XCD a
     // contiguous range of linear tiles (n fastest), so tiles sharing an A panel share an L2
@@ -354,44 +369,30 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
 #pragma unroll
     for (int q = 0; q < SA::NV; ++q) bs[q] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    // fragments of one k-tile, read in the order the plane products use them
+    // fragment registers: plane p of the A (fa) and B (fb) operand tiles of the current k-tile
     bf16x8 fa[3][TM], fb[3][TN];
-    auto read_frags = [&](const unsigned short* img) {
-        const unsigned short* As = img;
-        const unsigned short* Bs = img + SA::SIZE;
-        constexpr int order[6][2] = {{0, 2}, {1, 0}, {0, 0}, {1, 2}, {0, 1}, {1, 1}};   // (operand, plane)
+    auto rd_a = [&](const unsigned short* img, int p) {
 #pragma unroll
-        for (int o = 0; o < 6; ++o) {
-            const int p = order[o][1];
-            if (order[o][0] == 0) {
-#pragma unroll
-                for (int i = 0; i < TM; ++i) fa[p][i] = SA::frag(As + p * SA::PLANE, wm * WM + i * 32 + r, lane);
-            } else {
-#pragma unroll
-                for (int j = 0; j < TN; ++j) fb[p][j] = SB::frag(Bs + p * SB::PLANE, wn * WN + j * 32 + r, lane);
-            }
-        }
+        for (int i = 0; i < TM; ++i) fa[p][i] = SA::frag(img + p * SA::PLANE, wm * WM + i * 32 + r, lane);
     };
-    // plane product q of the six with pa + pb ≤ 2 (smallest first)
-    auto mfma_group = [&](int q) {
-        constexpr int pa_[6] = {2, 0, 1, 1, 0, 0}, pb_[6] = {0, 2, 1, 0, 1, 0};
+    auto rd_b = [&](const unsigned short* img, int p) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) fb[p][j] = SB::frag(img + SA::SIZE + p * SB::PLANE, wn * WN + j * 32 + r, lane);
+    };
+    // plane product A_pa·B_pb of the current k-tile (the six with pa + pb ≤ 2)
+    auto mm = [&](int pa, int pb) {
         if (ABL & 1) {               // keep the fragment reads live
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
-                for (int j = 0; j < TN; ++j) acc[i][j][0] += (float)fa[pa_[q]][i][0] + (float)fb[pb_[q]][j][1];
+                for (int j = 0; j < TN; ++j) acc[i][j][0] += (float)fa[pa][i][0] + (float)fb[pb][j][1];
             return;
         }
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[pa_[q]][i], fb[pb_[q]][j], acc[i][j], 0, 0, 0);
-    };
-    auto compute = [&](const unsigned short* img) {
-        read_frags(img);
-#pragma unroll
-        for (int q = 0; q < 6; ++q) mfma_group(q);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[pa][i], fb[pb][j], acc[i][j], 0, 0, 0);
     };
 
     // this group's k-tiles: j = 0 … NK−1 at k0 = kbeg + (KG·j + grp)·BK; only the last one can be
@@ -400,9 +401,8 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     const int NK = (nkt + KG - 1) / KG;
     auto k0_of = [&](int j) { return kbeg + (KG * j + grp) * BK; };
     auto is_full = [&](int j) { return k0_of(j) + BK <= kend; };
-    const bool tail = NK > 0 && !is_full(NK - 1);
-    unsigned short* const buf0 = lds + (KG > 1 ? grp * 2 * BUF : 0);
-    unsigned short* const buf1 = buf0 + BUF;
+    const int tail = NK > 0 && !is_full(NK - 1) ? 1 : 0;
+    unsigned short* const ring = lds + (KG > 1 ? grp * NS * BUF : 0);
 
     // split + LDS store of the staged tile at k0 (FULL: no k tail); COPY: also the gathered rows
     auto stage_a = [&](auto FULLc, auto COPYc, unsigned short* img, int k0) {
@@ -428,64 +428,118 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     };
     using T = std::true_type;
     using F = std::false_type;
-    // tile j through the full or the clamped path
     auto load_t = [&](int j) {
         if (is_full(j)) load(T{}, k0_of(j)); else load(F{}, k0_of(j));
     };
-    auto stage_t = [&](auto COPYc, unsigned short* img, int j) {
-        if (is_full(j)) { stage_a(T{}, COPYc, img, k0_of(j)); stage_b(T{}, img, k0_of(j)); }
-        else { stage_a(F{}, COPYc, img, k0_of(j)); stage_b(F{}, img, k0_of(j)); }
+    auto stage_a_t = [&](auto COPYc, unsigned short* img, int j) {
+        if (is_full(j)) stage_a(T{}, COPYc, img, k0_of(j)); else stage_a(F{}, COPYc, img, k0_of(j));
+    };
+    auto stage_b_t = [&](unsigned short* img, int j) {
+        if (is_full(j)) stage_b(T{}, img, k0_of(j)); else stage_b(F{}, img, k0_of(j));
     };
 
-    // Pipeline, iteration j: MFMAs of tile j from one image; the split + LDS stores of tile j+1
-    // (loaded one iteration ago) into the other; the loads of tile j+2; one barrier.  (Two register
-    // sets — loads two tiles ahead — measured no faster and spill the 256×256 tile.)
-    auto mainloop = [&](auto COPYc) {
-        if (NK > 0) { load_t(0); stage_t(COPYc, buf0, 0); }
-        if (NK > 1) load_t(1);
+    // Pipeline, iteration j over the ring (cur = tile j, n1 = tile j+1, n2 ← tile j+2):
+    //   a1, b1 of tile j (needed from the third product on) ← cur
+    //   A2·B0 | fa2 ← n1      A0·B0 | split + store A of tile j+2 → n2
+    //   A1·B0 | fb0 ← n1, split + store B of tile j+2     A0·B2 | fb2 ← n1, loads of tile j+3
+    //   A0·B1 | fa0 ← n1      A1·B1
+    //   barrier
+    // Each fragment plane of tile j+1 is read right after tile j's last product that uses it (into
+    // the same registers), at least one product group ahead of its first use; tile j+1's image was
+    // completed by the previous iteration's barrier, tile j+2's by this one.  WAR: the ring slot
+    // restaged in iteration j+1 (tile j+3 → cur) was last read in iteration j's first block.
+    // region boundary: a full scheduling barrier, preceded (forward / grad_x) by an interleave request
+    // — each of the region's MFMAs followed by NV VALU, one DS and one VMEM instruction.  Without it
+    // the compiler front-loads a region's split VALU (≈30 in a row) ahead of its MFMAs, and the two
+    // lock-stepped waves of a SIMD leave the matrix pipe idle together: 3761 → 3400 cycles per k-tile
+    // at C4 (profiles/r03_x3_stamps.txt).  grad_W measured no gain (PPO_X3_SGB=0/1 builds).
+    auto region_end = [&](auto NVc) {
+#if defined(PPO_X3_SGB) || !defined(PPO_X3_NO_SGB)
+        constexpr int NVV = decltype(NVc)::value;
+#ifdef PPO_X3_SGB
+        constexpr bool SGB = true;
+#else
+        constexpr bool SGB = OP != OP_TN;
+#endif
+        if constexpr (SGB) {
+#pragma unroll
+            for (int q = 0; q < TM * TN; ++q) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                if (NVV) __builtin_amdgcn_sched_group_barrier(0x002, NVV, 0);
+                __builtin_amdgcn_sched_group_barrier(0x080, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
+            }
+        }
+#endif
+        __builtin_amdgcn_sched_barrier(0);
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I2 = std::integral_constant<int, 2>;
+    using I6 = std::integral_constant<int, 6>;
+    auto iter = [&](auto STEADYc, auto COPYc, int j, unsigned short* cur, unsigned short* n1, unsigned short* n2) {
+        constexpr bool STEADY = decltype(STEADYc)::value;
+        const bool has1 = STEADY || j + 1 < NK, has2 = STEADY || j + 2 < NK, has3 = STEADY || j + 3 < NK;
+        rd_a(cur, 1);
+        rd_b(cur, 1);
+#ifdef PPO_X3_PRIO
+        __builtin_amdgcn_s_setprio(1);
+#endif
+        mm(2, 0);
+        if (has1) rd_a(n1, 2);
+        region_end(I0{});
+        mm(0, 0);
+        if (STEADY) stage_a(T{}, COPYc, n2, k0_of(j + 2));
+        else if (has2) stage_a_t(COPYc, n2, j + 2);
+        region_end(I6{});
+        mm(1, 0);
+        if (has1) rd_b(n1, 0);
+        if (STEADY) stage_b(T{}, n2, k0_of(j + 2));
+        else if (has2) stage_b_t(n2, j + 2);
+        region_end(I6{});
+        mm(0, 2);
+        if (has1) rd_b(n1, 2);
+        if (STEADY) load(T{}, k0_of(j + 3));
+        else if (has3) load_t(j + 3);
+        region_end(I2{});
+        mm(0, 1);
+        if (has1) rd_a(n1, 0);
+        region_end(I0{});
+        mm(1, 1);
+#ifdef PPO_X3_PRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
         __syncthreads();
+    };
+    auto mainloop = [&](auto COPYc) {
+        unsigned short* cur = ring;
+        unsigned short* n1 = ring + BUF;
+        unsigned short* n2 = ring + 2 * BUF;
+        if (NK > 0) { load_t(0); stage_a_t(COPYc, cur, 0); stage_b_t(cur, 0); }
+        if (NK > 1) { load_t(1); stage_a_t(COPYc, n1, 1); stage_b_t(n1, 1); }
+        if (NK > 2) load_t(2);
+        __syncthreads();
+        if (NK > 0) { rd_a(cur, 2); rd_b(cur, 0); rd_b(cur, 2); rd_a(cur, 0); }
         if (ABL & 32) stamp(1);
-        // steady state (tiles j+1, j+2 full): one basic block per k-tile, each plane-product group
-        // of MFMAs sharing its scheduling region with one slice of the staging work
-        const int steady = NK - 2 - (tail ? 1 : 0);
+        // steady state: tiles j+2 and j+3 exist and are full
+        const int steady = NK - 3 - tail;
         int j = 0;
         for (; j < steady; ++j) {
-            const unsigned short* cur = (j & 1) ? buf1 : buf0;
-            unsigned short* nxt = (j & 1) ? buf0 : buf1;
-            const int k1 = k0_of(j + 1);
-            read_frags(cur);
-#ifdef PPO_X3_PRIO
-            __builtin_amdgcn_s_setprio(1);
-#endif
-            mfma_group(0);
-            __builtin_amdgcn_sched_barrier(0);
-            mfma_group(1);
-            stage_a(T{}, COPYc, nxt, k1);
-            __builtin_amdgcn_sched_barrier(0);
-            mfma_group(2);
-            stage_b(T{}, nxt, k1);
-            __builtin_amdgcn_sched_barrier(0);
-            mfma_group(3);
-            load(T{}, k0_of(j + 2));
-            __builtin_amdgcn_sched_barrier(0);
-            mfma_group(4);
-            mfma_group(5);
-#ifdef PPO_X3_PRIO
-            __builtin_amdgcn_s_setprio(0);
-#endif
-            __syncthreads();
+            iter(T{}, COPYc, j, cur, n1, n2);
+            unsigned short* t = cur; cur = n1; n1 = n2; n2 = t;
         }
-        for (; j < NK; ++j) {                                 // the last one or two tiles
-            const unsigned short* cur = (j & 1) ? buf1 : buf0;
-            unsigned short* nxt = (j & 1) ? buf0 : buf1;
-            compute(cur);
-            if (j + 1 < NK) stage_t(COPYc, nxt, j + 1);
-            if (j + 2 < NK) load_t(j + 2);
-            __syncthreads();
+        for (; j < NK; ++j) {                                  // the last two or three tiles
+            iter(F{}, COPYc, j, cur, n1, n2);
+            unsigned short* t = cur; cur = n1; n1 = n2; n2 = t;
         }
     };
+#ifdef PPO_X3_PRIO2
+    if ((tid >> 6) >= NTH / 128) __builtin_amdgcn_s_setprio(1);   // the second-dispatched half wins VALU arbitration
+#endif
     if (do_copy) mainloop(T{});
     else mainloop(F{});
+#ifdef PPO_X3_PRIO2
+    __builtin_amdgcn_s_setprio(0);
+#endif
 
     // LDS scratch after the mainloop (the images are no longer read): bias-gradient partial sums,
     // then the k-groups' accumulator exchange
@@ -516,7 +570,7 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     auto mine = [&](int i, int j) { return KG == 1 || ((i * TN + j) % KG) == grp; };
     if constexpr (KG > 1) {
         static_assert(KG == 2, "k-group exchange: two groups");
-        static_assert((RED_FLOATS * 4 + NW * TM * TN * 4096) <= KG * 2 * BUF * 2, "k-group exchange: LDS");
+        static_assert((RED_FLOATS * 4 + NW * TM * TN * 4096) <= KG * NS * BUF * 2, "k-group exchange: LDS");
         f32x4* xch = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(lds) + RED_FLOATS);
         __syncthreads();
 #pragma unroll
@@ -557,7 +611,7 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
         return;
     }
     if constexpr (OP != OP_TN) {
-        static_assert(BM * (BN / 32) * 4 <= KG * 2 * BUF * 2, "x3 epilogue: mask words exceed LDS");
+        static_assert(BM * (BN / 32) * 4 <= KG * NS * BUF * 2, "x3 epilogue: mask words exceed LDS");
         x3_epilogue_out<OP, BM, BN, TM, TN, NTH>(a, acc, lds, m0, n0, wm, wn, tid);
         if (ABL & 32) stamp(3);
         return;
@@ -643,7 +697,7 @@ void launch_x3(X3Args a) {
     PPO_REQUIRE(a.kchunk % (KG * BK) == 0 || a.splits == 1, "gemm_x3: split-K chunk vs k-groups");
     using SA = StageX3<BM, OP == OP_TN, NTH / KG>;
     using SB = StageX3<BN, OP != OP_NT, NTH / KG>;
-    constexpr size_t lds = (size_t)KG * 2 * sizeof(unsigned short) * (SA::SIZE + SB::SIZE);
+    constexpr size_t lds = (size_t)KG * 3 * sizeof(unsigned short) * (SA::SIZE + SB::SIZE);   // 3-stage ring
     static_assert(lds <= 160 * 1024, "gemm_x3: LDS images exceed 160 KiB");
     auto kern = gemm_x3_kernel<OP, BM, BN, WARPS_M, NTH, OCC, KG, ABL>;
     if (lds > 64 * 1024) {
@@ -674,10 +728,11 @@ void launch_cfg_x3(int c, const X3Args& a) {
         const char* e = getenv("PPO_X3_ABLATE");
         g_x3_ablate = e ? atoi(e) : 0;
     }
-    if (g_x3_ablate && (c == 0 || (c == 3 && OP == OP_TN))) {
+    if (g_x3_ablate && (c == 0 || c == 4 || (c == 3 && OP == OP_TN))) {
         auto run = [&](auto ABLc) {
             constexpr int A = decltype(ABLc)::value;
-            if constexpr (OP == OP_TN) launch_x3<OP, 128, 128, 2, 512, 2, 2, A>(a);
+            if (c == 4) launch_x3<OP, 64, 64, 2, 256, 4, 1, A>(a);
+            else if constexpr (OP == OP_TN) launch_x3<OP, 128, 128, 2, 512, 2, 2, A>(a);
             else launch_x3<OP, 256, 256, 4, 512, 2, 1, A>(a);
         };
         switch (g_x3_ablate) {
@@ -703,13 +758,15 @@ void launch_cfg_x3(int c, const X3Args& a) {
 }
 
 // forward / grad_x: the largest tile whose grid still gives every CU a workgroup (one round of
-// 256×256 tiles, else 128×128 at two per CU, else 64×64)
+// 256×256 tiles, else 128×128 over 8 waves, one per CU, else 64×64 at up to four per CU).  At the
+// data-parallel shard shapes (profiles/r03_x3_small_shapes.txt): 8192×512×512 forward 32.1 µs on
+// 128×128 at two per CU (4 waves of 64×64) vs 28.0 µs on 8 waves of 32×64; 16384 rows 50.4 vs 47.9
 int pick_x3(int M, int N, int op) {
     if (g_force_x3 >= 0) return g_force_x3;
     if (op == OP_TN) return 3;
     auto tiles = [&](int c) { return (long)ppo_divup(M, kCfgX3[c].bm) * ppo_divup(N, kCfgX3[c].bn); };
     if (tiles(0) >= 256) return 0;
-    if (tiles(1) >= 256) return 1;
+    if (tiles(2) >= 256) return 2;
     return 4;
 }
 

@@ -229,6 +229,77 @@ __global__ void policy_head_kernel(const float* __restrict__ mu, const float* __
     }
 }
 
+// The same head for A ≤ 32 over ROWS-row tiles: μ and action rows staged through LDS by coalesced
+// loads (the one-thread-per-row form reads them at a 4·A-byte lane stride), the per-row log-prob /
+// surrogate chain unchanged (log_prob_row, surrogate: identical values), grad_μ stored coalesced,
+// the log σ column sums from the staged tile (8 partial sums per column, then one f32 atomic per
+// column per workgroup).  Grid: ⌈m / ROWS⌉ (512 workgroups at C4's B = 32768, every CU busy).
+template <int ROWS>
+__global__ __launch_bounds__(TPB) void policy_head_tiled_kernel(
+    const float* __restrict__ mu, const float* __restrict__ log_std, const float* __restrict__ action,
+    const float* __restrict__ adv, const float* __restrict__ old_lp, int m, int A, float eps, float ent_coeff,
+    float* __restrict__ grad_mu, float* grad_log_std, float* d_loss_accum) {
+    extern __shared__ float smem[];
+    float* e2 = smem;                    // [32] exp(−2 log σ)
+    float* lsd = smem + 32;              // [32] log σ
+    float* mt = smem + 64;               // [ROWS][A] μ
+    float* at = mt + ROWS * A;           // [ROWS][A] actions
+    float* gr = at + ROWS * A;           // [ROWS] ∂L/∂lp
+    float* cp = gr + ROWS;               // [8][32] column partial sums
+    float* red = cp + 8 * 32;            // [TPB/64]
+    const int tid = threadIdx.x;
+    const int r0 = blockIdx.x * ROWS;
+    const int nr = min(ROWS, m - r0);
+    if (tid < A) {
+        e2[tid] = expf(-2 * log_std[tid]);
+        lsd[tid] = log_std[tid];
+    }
+    const long base = (long)r0 * A;
+    for (int e = tid; e < nr * A; e += TPB) {
+        mt[e] = mu[base + e];
+        at[e] = action[base + e];
+    }
+    __syncthreads();
+    float s = 0.f;
+    if (tid < nr) {
+        float g;
+        const float lp = log_prob_row(mt + tid * A, lsd, at + tid * A, A);
+        s = surrogate(adv[r0 + tid], lp, old_lp[r0 + tid], eps, m, &g);
+        gr[tid] = g;
+    }
+    __syncthreads();
+    for (int e = tid; e < nr * A; e += TPB) {
+        const int row = e / A, j = e - row * A;
+        const float d = at[e] - mt[e];
+        grad_mu[base + e] = d * e2[j] * gr[row];
+    }
+    if (tid < 8 * A) {
+        const int j = tid % A, q = tid / A;
+        float c = 0.f;
+        for (int row = q; row < nr; row += 8) {
+            const float d = at[row * A + j] - mt[row * A + j];
+            c += (-1 + d * d * e2[j]) * gr[row];
+        }
+        cp[q * 32 + j] = c;
+    }
+    s = block_sum(s, red);
+    if (tid < A) {
+        float v = 0.f;
+        for (int q = 0; q < 8; ++q) v += cp[q * 32 + tid];
+        if (blockIdx.x == 0) v += -ent_coeff;                     // ppo.cu:436-438 (D4)
+        atomicAdd(grad_log_std + tid, v);
+    }
+    if (tid == 0 && d_loss_accum) {
+        float contrib = -s / m;
+        if (blockIdx.x == 0) {
+            float ent = (float)(A * 0.5 * (1 + log(2 * M_PI)));
+            for (int j = 0; j < A; ++j) ent += log_std[j];
+            contrib -= ent_coeff * ent;
+        }
+        atomicAdd(d_loss_accum, contrib);
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -319,9 +390,17 @@ void phip_policy_head(const float* mu, const float* log_std, const float* action
     if (m <= 0) return;
     PPO_REQUIRE(A > 0 && A <= 4096, "phip_policy_head: action size out of range");
     ppo::ProfScope ps(PPO_K_HEAD, 4.0 * m * (3 * A + 2));
-    hipLaunchKernelGGL(policy_head_kernel, dim3(ppo_divup(m, TPB)), dim3(TPB), sizeof(float) * (2 * A + 4),
-                       ppo::stream(), mu, log_std, action, adv, old_lp, m, A, epsilon, ent_coeff, grad_mu,
-                       grad_log_std, d_loss_accum);
+    if (A <= 32) {
+        constexpr int ROWS = 64;
+        const size_t lds = sizeof(float) * (64 + 2 * ROWS * A + ROWS + 8 * 32 + TPB / 64);
+        hipLaunchKernelGGL(policy_head_tiled_kernel<ROWS>, dim3(ppo_divup(m, ROWS)), dim3(TPB), lds, ppo::stream(),
+                           mu, log_std, action, adv, old_lp, m, A, epsilon, ent_coeff, grad_mu, grad_log_std,
+                           d_loss_accum);
+    } else {
+        hipLaunchKernelGGL(policy_head_kernel, dim3(ppo_divup(m, TPB)), dim3(TPB), sizeof(float) * (2 * A + 4),
+                           ppo::stream(), mu, log_std, action, adv, old_lp, m, A, epsilon, ent_coeff, grad_mu,
+                           grad_log_std, d_loss_accum);
+    }
     PPO_LAUNCH_CHECK();
 }
 
