@@ -399,14 +399,30 @@ def main():
         achieved = s_work / (s_ms * 1e-3) / 1e12
         pmc, traffic_src = pmc_traffic() if args.config == "c4" else ({}, None)   # PMC passes are of c4
         traffic = pmc.get("hbm_bytes_per_launch")
-        dom = dict(shapes[0]) if shapes else None
-        if dom:
-            dom["frac"] = dom["tflops"] / peak
-            m_, n_, l_ = dom["m"], dom["n"], dom["l"]
+        # dominant kernel = the kernel TEMPLATE (op × engine: one compiled kernel family, e.g. the x3
+        # forward NT) with the most time in the serialised update, over all its shapes: Σ 2mnl ÷ Σ time
+        groups = {}
+        for sh in shapes:
+            g = groups.setdefault((sh["op"], sh["engine"]), {"op": sh["op"], "engine": sh["engine"], "launches": 0,
+                                                           "ms": 0.0, "work": 0.0, "bytes": 0.0, "shapes": []})
+            g["launches"] += sh["launches"]
+            g["ms"] += sh["ms"]
+            g["work"] += sh["tflops"] * 1e12 * sh["ms"] * 1e-3
+            m_, n_, l_ = sh["m"], sh["n"], sh["l"]
             # operands read once, output written once (fp32; grad_W: + its bias-gradient vector)
-            dom["algorithmic_bytes"] = 4 * (m_ * n_ + n_ * l_ + m_ * l_ + (l_ if dom["op"] == "grad_W" else 0))
+            g["bytes"] += sh["launches"] * 4 * (m_ * n_ + n_ * l_ + m_ * l_ + (l_ if sh["op"] == "grad_W" else 0))
+            g["shapes"].append([m_, n_, l_, round(sh["avg_us"], 2)])
+        dom = None
+        if groups:
+            g = max(groups.values(), key=lambda v: v["ms"])
+            dom = {"op": g["op"], "engine": g["engine"], "template": {"forward": "NT", "grad_x": "NN", "grad_W": "TN",
+                                                                      "grad_W+grad_x": "pair"}.get(g["op"]),
+                   "launches": g["launches"], "ms": g["ms"], "avg_us": 1000.0 * g["ms"] / g["launches"],
+                   "tflops": g["work"] / (g["ms"] * 1e-3) / 1e12,
+                   "algorithmic_bytes": g["bytes"] / g["launches"], "shapes": g["shapes"]}
+            dom["frac"] = dom["tflops"] / peak
             # the PMC pass's kernel of this op (template's first parameter) with the most launches
-            # in the traced update: for C4 the 512-wide hidden-layer instance of the dominant shape
+            # in the traced update: for C4 the 512-wide hidden-layer instance of the dominant op
             code = {"forward": "0", "grad_x": "1", "grad_W": "2"}.get(dom["op"])
             cand = [(v.get("launches_in_update", 0), k, v) for k, v in (pmc.get("by_kernel") or {}).items()
                     if k.startswith(f"gemm<{code}, ") and "true" not in k and "false" not in k   # x3 template

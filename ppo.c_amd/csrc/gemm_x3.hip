@@ -59,6 +59,9 @@ struct X3Args {
     unsigned* bits_out; const unsigned* bits_in; int wpr;
     float* gbias;                         // grad_W: bias gradient (Σ over the batch of g)
     int kchunk, splits, tiles_m, tiles_n;
+    float* slab;                          // grad_W split-K: per-split partial tiles [splits][M][N] (plain
+                                          // stores, summed by slab_reduce_kernel) instead of f32 atomics
+    hipEvent_t ev_start, ev_stop;         // explicit dispatch-stamped events (ppo_prof kernel timing)
 };
 
 // fp32 → bf16 round to nearest even (NaN stays NaN): v_cvt_pk_bf16_f32
@@ -671,7 +674,8 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
                     if (ok) *dst = keep[e] ? v : 0.f;
 #endif
                 } else if (ok) {
-                    if (a.splits > 1) atomicAdd(dst, v);
+                    if (a.slab) a.slab[(long)(kbeg / a.kchunk) * a.M * a.N + (long)row * a.N + col] = v;
+                    else if (a.splits > 1) atomicAdd(dst, v);
                     else *dst = v;
                 }
             }
@@ -707,9 +711,36 @@ void launch_x3(X3Args a) {
             attr = true;
         }
     }
-    PPO_TIMED_LAUNCH(kern, dim3((unsigned)grid), dim3(NTH), lds, ppo::stream(), a);
+    if (a.ev_start || a.ev_stop)
+        hipExtLaunchKernelGGL(kern, dim3((unsigned)grid), dim3(NTH), lds, ppo::stream(), a.ev_start, a.ev_stop, 0, a);
+    else
+        PPO_TIMED_LAUNCH(kern, dim3((unsigned)grid), dim3(NTH), lds, ppo::stream(), a);
     PPO_LAUNCH_CHECK();
 }
+
+// grad_W split-K partials: out[i] = Σ_s slab[s][i] in split order (deterministic), float4 lanes
+__global__ __launch_bounds__(256) void slab_reduce_kernel(const f32x4* __restrict__ slab, f32x4* __restrict__ out,
+                                                          long n4, int splits) {
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
+        f32x4 acc = slab[i];
+        for (int s = 1; s < splits; ++s) acc += slab[(long)s * n4 + i];
+        out[i] = acc;
+    }
+}
+
+// per-stream slab buffers (the value and policy loops run their grad_W launches on two streams)
+float* g_slab[2] = {nullptr, nullptr};
+size_t g_slab_cap[2] = {0, 0};
+float* slab_for(size_t floats) {
+    const int s = phip_side_active() ? 1 : 0;
+    if (floats > g_slab_cap[s]) {
+        phip_free(g_slab[s]);
+        g_slab[s] = (float*)phip_malloc(sizeof(float) * floats);
+        g_slab_cap[s] = floats;
+    }
+    return g_slab[s];
+}
+int g_x3_atomics = -1;                   // PPO_X3_ATOMICS=1: split-K partials by f32 atomics (A/B)
 
 // tile configurations: 0 = 256×256 over 8 waves of 64×128 (forward, grad_x; one workgroup per CU),
 // 1 = 128×128 over 4 waves of 64×64, two workgroups per CU (narrow products), 2 = 128×128 over 8
@@ -840,11 +871,39 @@ void phip_x3_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, 
     a.A = g; a.lda = l; a.B = x; a.ldb = n; a.C = gW; a.ldc = n;
     a.M = l; a.N = n; a.K = m; a.kchunk = kchunk; a.splits = splits;
     a.gbias = gb;
+    if (g_x3_atomics < 0) {
+        const char* e = getenv("PPO_X3_ATOMICS");
+        g_x3_atomics = e && *e && *e != '0';
+    }
+    // split-K partials: per-split slabs written with plain stores and summed by one reduce launch
+    // (16 MB of f32 atomics at ≈1.3 TB/s set the grad_W time of small batches; the slab path moves
+    // the same bytes at store / load rate, and its sum is deterministic); the bias gradient keeps
+    // its per-workgroup atomics (l floats per split)
+    const bool use_slab = splits > 1 && !g_x3_atomics && al16(gW);
     if (splits > 1 && !zeroed) {
-        phip_memset(gW, 0, sizeof(float) * (size_t)l * n);
+        if (!use_slab) phip_memset(gW, 0, sizeof(float) * (size_t)l * n);
         if (gb) phip_memset(gb, 0, sizeof(float) * (size_t)l);
     }
+    if (!use_slab) {
+        launch_cfg_x3<OP_TN>(c, a);
+        return;
+    }
+    a.slab = slab_for((size_t)splits * l * n);
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    const bool timed = ppo::take_kernel_events(&e0, &e1);     // one duration: GEMM start → reduce end
+    a.ev_start = timed ? e0 : nullptr;
+    a.ev_stop = nullptr;
     launch_cfg_x3<OP_TN>(c, a);
+    if (timed) a.ev_start = nullptr;
+    const long n4 = (long)l * n / 4;
+    const int grid = (int)std::min<long>(2048, (n4 + 255) / 256);
+    if (timed)
+        hipExtLaunchKernelGGL(slab_reduce_kernel, dim3(grid), dim3(256), 0, ppo::stream(), nullptr, e1, 0,
+                              (const f32x4*)a.slab, (f32x4*)gW, n4, splits);
+    else
+        hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid), dim3(256), 0, ppo::stream(), (const f32x4*)a.slab,
+                           (f32x4*)gW, n4, splits);
+    PPO_LAUNCH_CHECK();
 }
 
 int ppo_gemm_x3_tune(int force_cfg, int splitk_target) {
