@@ -28,19 +28,9 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
 // w16 (bf16 mode): the parameters' bf16 shadow for the first n16 elements, written in the same pass.
 // zero_g: the gradient is cleared once read (ppo_update: the next backward's split-K atomics then
 // accumulate into zeros without a memset launch per minibatch step).
-// the x3 engine's exact three-plane split of one fp32 value (gemm_x3.hip split4, element-wise):
-// v0 = bf16(x), v1 = bf16(x − v0), v2 = bf16(x − v0 − v1), round to nearest even
-__device__ __forceinline__ void split3(float x, __bf16& v0, __bf16& v1, __bf16& v2) {
-    v0 = (__bf16)x;
-    const float r = x - (float)v0;
-    v1 = (__bf16)r;
-    v2 = (__bf16)(r - (float)v1);
-}
-
 __global__ void adam_flat_vec_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
                                      float* __restrict__ v, long n, float step, float b1, float b2, float bc2,
-                                     float scale, __bf16* __restrict__ w16, long n16, __bf16* __restrict__ wp,
-                                     long n_wp, long wps, int zero_g) {
+                                     float scale, __bf16* __restrict__ w16, long n16, int zero_g) {
     typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
     const long n4 = n >> 2;
     for (long i = blockIdx.x * (long)TPB + threadIdx.x; i < n4; i += (long)gridDim.x * TPB) {
@@ -63,25 +53,6 @@ __global__ void adam_flat_vec_kernel(float* __restrict__ p, float* __restrict__ 
                 for (long j = 4 * i; j < n16; ++j) w16[j] = (__bf16)e[j - 4 * i];
             }
         }
-        if (wp && 4 * i < n_wp) {                  // x3 weight planes (fp32 mode, inside ppo_update)
-            const float e[4] = {pp.x, pp.y, pp.z, pp.w};
-            bf16x4 q0, q1, q2;
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                __bf16 a0, a1, a2;
-                split3(e[u], a0, a1, a2);
-                q0[u] = a0; q1[u] = a1; q2[u] = a2;
-            }
-            if (4 * i + 4 <= n_wp) {
-                reinterpret_cast<bf16x4*>(wp)[i] = q0;
-                reinterpret_cast<bf16x4*>(wp + wps)[i] = q1;
-                reinterpret_cast<bf16x4*>(wp + 2 * wps)[i] = q2;
-            } else {
-                for (long j = 4 * i; j < n_wp; ++j) {
-                    wp[j] = q0[j - 4 * i]; wp[wps + j] = q1[j - 4 * i]; wp[2 * wps + j] = q2[j - 4 * i];
-                }
-            }
-        }
     }
     if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
         const long j = 4 * n4 + threadIdx.x;
@@ -90,11 +61,6 @@ __global__ void adam_flat_vec_kernel(float* __restrict__ p, float* __restrict__ 
         p[j] = pp; m[j] = mm; v[j] = vv;
         if (zero_g) g[j] = 0.f;
         if (w16 && j < n16) w16[j] = (__bf16)pp;
-        if (wp && j < n_wp) {
-            __bf16 a0, a1, a2;
-            split3(pp, a0, a1, a2);
-            wp[j] = a0; wp[wps + j] = a1; wp[2 * wps + j] = a2;
-        }
     }
 }
 
@@ -140,34 +106,24 @@ int grid_for(long n) {
 
 extern "C" {
 
-void phip_adam_flat_ex(float* p, float* g, float* m, float* v, long n, float lr, float beta1, float beta2,
-                       float bias_correction1, float bias_correction2, float grad_scale, unsigned short* w16,
-                       long n16, unsigned short* wp, long n_wp, long wp_stride, int zero_g) {
+void phip_adam_flat_w16(float* p, float* g, float* m, float* v, long n, float lr, float beta1, float beta2,
+                        float bias_correction1, float bias_correction2, float grad_scale, unsigned short* w16,
+                        long n16, int zero_g) {
     if (n <= 0) return;
     const float step = lr / bias_correction1;
-    ppo::ProfScope ps(PPO_K_ADAM, 28.0 * n + (w16 ? 2.0 * n16 : 0.0) + (wp ? 6.0 * n_wp : 0.0) +
-                                      (zero_g ? 4.0 * n : 0.0));
+    ppo::ProfScope ps(PPO_K_ADAM, 28.0 * n + (w16 ? 2.0 * n16 : 0.0) + (zero_g ? 4.0 * n : 0.0));
     const bool vec = (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15u) == 0 &&
-                     ((uintptr_t)w16 & 7u) == 0 && ((uintptr_t)wp & 7u) == 0 && wp_stride % 4 == 0;
+                     ((uintptr_t)w16 & 7u) == 0;
     if (vec) {
         hipLaunchKernelGGL(adam_flat_vec_kernel, dim3(grid_for((n + 3) / 4)), dim3(TPB), 0, ppo::stream(), p, g, m,
                            v, n, step, beta1, beta2, bias_correction2, grad_scale,
-                           reinterpret_cast<__bf16*>(w16), n16, reinterpret_cast<__bf16*>(wp), n_wp, wp_stride,
-                           zero_g);
+                           reinterpret_cast<__bf16*>(w16), n16, zero_g);
     } else {
-        PPO_REQUIRE(!w16 && !wp && !zero_g,
-                    "phip_adam_flat: unaligned span with a bf16 shadow, weight planes or gradient clear");
+        PPO_REQUIRE(!w16 && !zero_g, "phip_adam_flat_w16: unaligned span with a bf16 shadow or gradient clear");
         hipLaunchKernelGGL(adam_flat_kernel, dim3(grid_for(n)), dim3(TPB), 0, ppo::stream(), p, g, m, v, n, step,
                            beta1, beta2, bias_correction2, grad_scale);
     }
     PPO_LAUNCH_CHECK();
-}
-
-void phip_adam_flat_w16(float* p, float* g, float* m, float* v, long n, float lr, float beta1, float beta2,
-                        float bias_correction1, float bias_correction2, float grad_scale, unsigned short* w16,
-                        long n16, int zero_g) {
-    phip_adam_flat_ex(p, g, m, v, n, lr, beta1, beta2, bias_correction1, bias_correction2, grad_scale, w16, n16,
-                      nullptr, 0, 0, zero_g);
 }
 
 void phip_adam_flat(float* p, const float* g, float* m, float* v, long n, float lr, float beta1, float beta2,

@@ -62,7 +62,6 @@ struct X3Args {
     float* slab;                          // grad_W split-K: per-split partial tiles [splits][M][N] (plain
                                           // stores, summed by slab_reduce_kernel) instead of f32 atomics
     hipEvent_t ev_start, ev_stop;         // explicit dispatch-stamped events (ppo_prof kernel timing)
-    const unsigned short* Bp; long bp_stride;   // B pre-split into three bf16 planes (BPRE kernels)
 };
 
 // fp32 → bf16 round to nearest even (NaN stays NaN): v_cvt_pk_bf16_f32
@@ -98,7 +97,7 @@ __device__ __forceinline__ void split4(f32x4 f, u32x2& p0, u32x2& p1, u32x2& p2)
 // k-group), each owning NV float4 loads per k-tile.
 // MN = the operand is contiguous along its rows (its k is the HBM row).
 // ---------------------------------------------------------------------------------------------
-template <int R, bool MN, int NTH, bool PRE = false>
+template <int R, bool MN, int NTH>
 struct StageX3 {
     static constexpr int NV = R * BK / (4 * NTH);            // float4 loads per thread
     static_assert(NV >= 1 && R * BK == 4 * NTH * NV, "tile / thread count");
@@ -123,25 +122,6 @@ struct StageX3 {
     const float* base;                                       // this thread's element (row, k) at k0 = 0
     int row, k;                                              // this thread's first element in the tile
     int ld;
-    // PRE: the operand is already split — three bf16 planes in HBM (plane stride pst elements, the
-    // fp32 operand's layout), loaded and stored as they are (no split VALU)
-    u32x2 pv[NV][3];
-    const unsigned short* pbase;
-    long pst;
-    __device__ __forceinline__ void init_pre(const unsigned short* __restrict__ p, int ld_, long pst_, int r0,
-                                             int Rmax, int tid) {
-        ld = ld_;
-        pst = pst_;
-        if (MN) {
-            row = (tid % (R / 4)) * 4;
-            k = tid / (R / 4);
-            pbase = p + (long)k * ld + min(r0 + row, Rmax - 4);
-        } else {
-            row = tid / TPR;
-            k = (tid % TPR) * 4 * NV;
-            pbase = p + (long)min(r0 + row, Rmax - 1) * ld + k;
-        }
-    }
 
     // src row (k-contiguous: after the gather, clamped into the operand); rows past the end read row
     // Rmax − 1 (their products land in output rows that are never stored)
@@ -165,17 +145,6 @@ struct StageX3 {
     // FULL: the whole k-tile lies inside [kbeg, kend) — no clamping
     template <bool FULL>
     __device__ __forceinline__ void load(int k0, int kend) {
-        if constexpr (PRE) {
-#pragma unroll
-            for (int q = 0; q < NV; ++q) {
-                const int dk = MN ? (FULL ? k0 + q * KSTEP : min(k0 + k + q * KSTEP, kend - 1) - k)
-                                  : (FULL ? k0 + 4 * q : min(k0 + k + 4 * q, kend - 4) - k);
-                const unsigned short* src = pbase + (MN ? (long)dk * ld : (long)dk);
-#pragma unroll
-                for (int p = 0; p < 3; ++p) pv[q][p] = *reinterpret_cast<const u32x2*>(src + p * pst);
-            }
-            return;
-        }
         if (MN) {
 #pragma unroll
             for (int q = 0; q < NV; ++q) {
@@ -195,34 +164,6 @@ struct StageX3 {
     }
     template <bool FULL, bool NOSPLIT = false>
     __device__ __forceinline__ void store(unsigned short* img, int k0, int kend) {
-        if constexpr (PRE) {
-#pragma unroll
-            for (int q = 0; q < NV; ++q) {
-                if (!FULL && !kvalid(q, k0, kend)) pv[q][0] = pv[q][1] = pv[q][2] = u32x2{0u, 0u};
-            }
-            if (MN) {
-#pragma unroll
-                for (int q = 0; q < NV; ++q) {
-                    unsigned short* d = img + mn_off(k + q * KSTEP, row);
-#pragma unroll
-                    for (int p = 0; p < 3; ++p) *reinterpret_cast<u32x2*>(d + p * PLANE) = pv[q][p];
-                }
-            } else if (NV == 2) {
-                unsigned short* d = img + kc_off(row, k);
-#pragma unroll
-                for (int p = 0; p < 3; ++p)
-                    *reinterpret_cast<u32x4*>(d + p * PLANE) = u32x4{pv[0][p][0], pv[0][p][1], pv[NV - 1][p][0],
-                                                                      pv[NV - 1][p][1]};
-            } else {
-#pragma unroll
-                for (int q = 0; q < NV; ++q) {
-                    unsigned short* d = img + kc_off(row, k + 4 * q);
-#pragma unroll
-                    for (int p = 0; p < 3; ++p) *reinterpret_cast<u32x2*>(d + p * PLANE) = pv[q][p];
-                }
-            }
-            return;
-        }
         f32x4* vv = v;
         if (!FULL) {
 #pragma unroll
@@ -370,7 +311,7 @@ __device__ __forceinline__ void x3_epilogue_out(const X3Args& a, f32x16 (&acc)[T
     else body(std::false_type{});
 }
 
-template <int OP, int BM, int BN, int WARPS_M, int NTH, int OCC, int KG, int ABL = 0, bool BPRE = false>
+template <int OP, int BM, int BN, int WARPS_M, int NTH, int OCC, int KG, int ABL = 0>
 __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     constexpr int NTG = NTH / KG;                                  // threads per k-group
     constexpr int NW = NTG / 64, WARPS_N = NW / WARPS_M;
@@ -380,7 +321,7 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     static_assert(KG == 1 || OP == OP_TN, "k-groups: grad_W only");
     constexpr bool A_MN = OP == OP_TN, B_MN = OP != OP_NT;
     using SA = StageX3<BM, A_MN, NTG>;
-    using SB = StageX3<BN, B_MN, NTG, BPRE>;
+    using SB = StageX3<BN, B_MN, NTG>;
     constexpr int BUF = SA::SIZE + SB::SIZE;
 
     constexpr int NS = 3;                                          // LDS ring stages
@@ -423,8 +364,7 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     SA sa;
     SB sb;
     sa.init(a.A, a.lda, OP == OP_NT ? a.ridx : nullptr, m0, a.M, lt);
-    if constexpr (BPRE) sb.init_pre(a.Bp, a.ldb, a.bp_stride, n0, a.N, lt);
-    else sb.init(a.B, a.ldb, nullptr, n0, a.N, lt);
+    sb.init(a.B, a.ldb, nullptr, n0, a.N, lt);
     const bool do_copy = OP == OP_NT && a.acopy != nullptr && tn == 0;
     // grad_W bias: Σ over this split's k of the A (= g) tile, from the staging registers
     const bool do_bsum = OP == OP_TN && a.gbias != nullptr && tn == 0;
@@ -751,7 +691,7 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
 int g_x3_ablate = -1;
 #endif
 
-template <int OP, int BM, int BN, int WARPS_M, int NTH, int OCC, int KG, int ABL = 0, bool BPRE = false>
+template <int OP, int BM, int BN, int WARPS_M, int NTH, int OCC, int KG, int ABL = 0>
 void launch_x3(X3Args a) {
     a.tiles_m = ppo_divup(a.M, BM);
     a.tiles_n = ppo_divup(a.N, BN);
@@ -763,7 +703,7 @@ void launch_x3(X3Args a) {
     using SB = StageX3<BN, OP != OP_NT, NTH / KG>;
     constexpr size_t lds = (size_t)KG * 3 * sizeof(unsigned short) * (SA::SIZE + SB::SIZE);   // 3-stage ring
     static_assert(lds <= 160 * 1024, "gemm_x3: LDS images exceed 160 KiB");
-    auto kern = gemm_x3_kernel<OP, BM, BN, WARPS_M, NTH, OCC, KG, ABL, BPRE>;
+    auto kern = gemm_x3_kernel<OP, BM, BN, WARPS_M, NTH, OCC, KG, ABL>;
     if (lds > 64 * 1024) {
         static bool attr = false;                      // once per instantiation
         if (!attr) {
@@ -785,35 +725,6 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const f32x4* __restric
         f32x4 acc = slab[i];
         for (int s = 1; s < splits; ++s) acc += slab[(long)s * n4 + i];
         out[i] = acc;
-    }
-}
-
-__global__ __launch_bounds__(256) void split_planes_kernel(unsigned short* __restrict__ dst, long pst,
-                                                           const float* __restrict__ src, long n) {
-    const long n4 = (n + 3) / 4;
-    for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
-        f32x4 f;
-        if (4 * i + 4 <= n) f = reinterpret_cast<const f32x4*>(src)[i];
-        else {
-            f = f32x4{0.f, 0.f, 0.f, 0.f};
-            for (long j = 4 * i; j < n; ++j) f[j - 4 * i] = src[j];
-        }
-        u32x2 p0, p1, p2;
-        split4(f, p0, p1, p2);
-        if (4 * i + 4 <= n) {
-            reinterpret_cast<u32x2*>(dst)[i] = p0;
-            reinterpret_cast<u32x2*>(dst + pst)[i] = p1;
-            reinterpret_cast<u32x2*>(dst + 2 * pst)[i] = p2;
-        } else {
-            const unsigned short* q0 = reinterpret_cast<const unsigned short*>(&p0);
-            const unsigned short* q1 = reinterpret_cast<const unsigned short*>(&p1);
-            const unsigned short* q2 = reinterpret_cast<const unsigned short*>(&p2);
-            for (long j = 4 * i; j < n; ++j) {
-                dst[j] = q0[j - 4 * i];
-                dst[pst + j] = q1[j - 4 * i];
-                dst[2 * pst + j] = q2[j - 4 * i];
-            }
-        }
     }
 }
 
@@ -841,7 +752,7 @@ constexpr CfgX3 kCfgX3[] = {{256, 256, 1, 1}, {128, 128, 1, 2}, {128, 128, 1, 1}
 int g_force_x3 = -1;
 int g_split_x3 = 0;
 
-template <int OP, bool BPRE = false>
+template <int OP>
 void launch_cfg_x3(int c, const X3Args& a) {
 #ifdef PPO_X3_DIAG
     if (g_x3_ablate < 0) {
@@ -866,16 +777,6 @@ void launch_cfg_x3(int c, const X3Args& a) {
         }
     }
 #endif
-    if constexpr (BPRE) {
-        static_assert(OP != OP_TN, "pre-split B: forward / grad_x (B = W)");
-        switch (c) {
-            case 0: launch_x3<OP, 256, 256, 4, 512, 2, 1, 0, true>(a); break;
-            case 2: launch_x3<OP, 128, 128, 4, 512, 2, 1, 0, true>(a); break;
-            case 4: launch_x3<OP, 64, 64, 2, 256, 4, 1, 0, true>(a); break;
-            default: launch_x3<OP, 128, 128, 2, 256, 2, 1, 0, true>(a); break;
-        }
-        return;
-    }
     switch (c) {
         case 0: launch_x3<OP, 256, 256, 4, 512, 2, 1>(a); break;
         case 2: launch_x3<OP, 128, 128, 4, 512, 2, 1>(a); break;
@@ -916,61 +817,29 @@ int phip_x3_supported(int op, int m, int n, int l) {
     return n % 4 == 0 && l % 4 == 0;                           // K = m; g rows l, x rows n
 }
 
-// Wp (optional): W already split into three bf16 planes (phip_x3_split_planes / the Adam pass),
-// plane p of element e at Wp[p·wp_stride + e] — the kernel then stages W without splitting it (every
-// row tile of the product re-split the same W: 128 times per C4 launch)
-void phip_x3_fwd_p(float* y, const float* x, const int* ridx, float* xcopy, const float* W,
-                   const unsigned short* Wp, long wp_stride, const float* b, int m, int n, int l, int relu,
-                   unsigned* bits) {
+void phip_x3_fwd(float* y, const float* x, const int* ridx, float* xcopy, const float* W, const float* b, int m,
+                 int n, int l, int relu, unsigned* bits) {
     if (m <= 0 || l <= 0) return;
     PPO_REQUIRE(y && x && W && n > 0 && n % 4 == 0 && al16(x) && al16(W), "phip_x3_fwd: unsupported operands");
-    PPO_REQUIRE(!Wp || ((uintptr_t)Wp & 7u) == 0, "phip_x3_fwd: unaligned weight planes");
     ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l, ppo::gemm_key(0, 1, m, n, l));
     X3Args a{};
     a.A = x; a.lda = n; a.B = W; a.ldb = n; a.C = y; a.ldc = l;
     a.M = m; a.N = l; a.K = n; a.kchunk = n; a.splits = 1;
     a.bias = b; a.relu = relu; a.ridx = ridx; a.acopy = ridx ? xcopy : nullptr;
     a.bits_out = relu ? bits : nullptr; a.wpr = ppo_divup(l, 32);
-    a.Bp = Wp; a.bp_stride = wp_stride;
-    if (Wp) launch_cfg_x3<OP_NT, true>(pick_x3(m, l, OP_NT), a);
-    else launch_cfg_x3<OP_NT>(pick_x3(m, l, OP_NT), a);
+    launch_cfg_x3<OP_NT>(pick_x3(m, l, OP_NT), a);
 }
 
-void phip_x3_fwd(float* y, const float* x, const int* ridx, float* xcopy, const float* W, const float* b, int m,
-                 int n, int l, int relu, unsigned* bits) {
-    phip_x3_fwd_p(y, x, ridx, xcopy, W, nullptr, 0, b, m, n, l, relu, bits);
-}
-
-void phip_x3_bwd_x_p(float* gx, const float* g, const float* W, const unsigned short* Wp, long wp_stride,
-                     const unsigned* bits, int m, int n, int l) {
+void phip_x3_bwd_x(float* gx, const float* g, const float* W, const unsigned* bits, int m, int n, int l) {
     if (m <= 0 || n <= 0) return;
     PPO_REQUIRE(gx && g && W && l > 0 && l % 4 == 0 && n % 4 == 0 && al16(g) && al16(W),
                 "phip_x3_bwd_x: unsupported operands");
-    PPO_REQUIRE(!Wp || ((uintptr_t)Wp & 7u) == 0, "phip_x3_bwd_x: unaligned weight planes");
     ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l, ppo::gemm_key(1, 1, m, n, l));
     X3Args a{};
     a.A = g; a.lda = l; a.B = W; a.ldb = n; a.C = gx; a.ldc = n;
     a.M = m; a.N = n; a.K = l; a.kchunk = l; a.splits = 1;
     a.bits_in = bits; a.wpr = ppo_divup(n, 32);
-    a.Bp = Wp; a.bp_stride = wp_stride;
-    if (Wp) launch_cfg_x3<OP_NN, true>(pick_x3(m, n, OP_NN), a);
-    else launch_cfg_x3<OP_NN>(pick_x3(m, n, OP_NN), a);
-}
-
-void phip_x3_bwd_x(float* gx, const float* g, const float* W, const unsigned* bits, int m, int n, int l) {
-    phip_x3_bwd_x_p(gx, g, W, nullptr, 0, bits, m, n, l);
-}
-
-// three bf16 planes of n fp32 values (the x3 split, bit for bit as the kernels' staging computes it)
-void phip_x3_split_planes(unsigned short* dst, long plane_stride, const float* src, long n) {
-    if (n <= 0) return;
-    PPO_REQUIRE(((uintptr_t)src & 15u) == 0 && ((uintptr_t)dst & 7u) == 0 && plane_stride % 4 == 0,
-                "phip_x3_split_planes: alignment");
-    ppo::ProfScope ps(PPO_K_OTHER, 10.0 * n);
-    const long n4 = (n + 3) / 4;
-    const int grid = (int)std::min<long>(2048, (n4 + 255) / 256);
-    hipLaunchKernelGGL(split_planes_kernel, dim3(grid), dim3(256), 0, ppo::stream(), dst, plane_stride, src, n);
-    PPO_LAUNCH_CHECK();
+    launch_cfg_x3<OP_NN>(pick_x3(m, n, OP_NN), a);
 }
 
 // zeroed: gW / gb already hold zeros (one memset per backward); otherwise they are cleared here

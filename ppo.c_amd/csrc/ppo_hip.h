@@ -77,13 +77,6 @@ int  phip_x3_supported(int op, int m, int n, int l);
 void phip_x3_fwd(float* y, const float* x, const int* ridx, float* xcopy, const float* W, const float* b, int m,
                  int n, int l, int relu, unsigned* bits);
 void phip_x3_bwd_x(float* gx, const float* g, const float* W, const unsigned* bits, int m, int n, int l);
-/* the same with W pre-split into three bf16 planes (Wp + p·wp_stride), NULL Wp = split in the kernel */
-void phip_x3_fwd_p(float* y, const float* x, const int* ridx, float* xcopy, const float* W,
-                   const unsigned short* Wp, long wp_stride, const float* b, int m, int n, int l, int relu,
-                   unsigned* bits);
-void phip_x3_bwd_x_p(float* gx, const float* g, const float* W, const unsigned short* Wp, long wp_stride,
-                     const unsigned* bits, int m, int n, int l);
-void phip_x3_split_planes(unsigned short* dst, long plane_stride, const float* src, long n);
 void phip_x3_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, int n, int l, int zeroed);
 /* dst[i, :] = bf16(src[rows[i], :]) for i < m (S % 4 == 0): layer 0's gather in bf16 mode */
 void phip_gather_rows_bf16(unsigned short* dst, const float* src, const int* rows, int m, int S);
@@ -200,10 +193,6 @@ void phip_adam_flat(float* p, const float* g, float* m, float* v, long n, float 
 void phip_adam_flat_w16(float* p, float* g, float* m, float* v, long n, float lr, float beta1, float beta2,
                         float bias_correction1, float bias_correction2, float grad_scale, unsigned short* w16,
                         long n16, int zero_g);
-/* the same, also writing the x3 planes of the first n_wp updated parameters (wp, plane stride wp_stride) */
-void phip_adam_flat_ex(float* p, float* g, float* m, float* v, long n, float lr, float beta1, float beta2,
-                       float bias_correction1, float bias_correction2, float grad_scale, unsigned short* w16,
-                       long n16, unsigned short* wp, long n_wp, long wp_stride, int zero_g);
 /* multi-tensor: ptrs/lengths are HOST arrays describing device tensors; m/v are flat */
 void phip_adam_multi(float* const* params, float* const* grads, const int* lengths, int num_tensors,
                      float* m, float* v, float lr, float beta1, float beta2,

@@ -169,12 +169,6 @@ void adam_update_cuda(Adam* adam, float lr) { adam_update_cuda_w16(adam, lr, NUL
  * zero_g: clear the gradient span once read (flat spans only).  Returns bit 0: shadow refreshed,
  * bit 1: gradients cleared. */
 int adam_update_cuda_w16(Adam* adam, float lr, unsigned short* w16, long n16, int zero_g) {
-    return adam_update_cuda_ex(adam, lr, w16, n16, NULL, 0, zero_g);
-}
-
-/* wp != NULL: also write the x3 weight planes of the first n_wp parameters (flat spans only) */
-int adam_update_cuda_ex(Adam* adam, float lr, unsigned short* w16, long n16, unsigned short* wp, long n_wp,
-                        int zero_g) {
     float bc1, bc2;
     bias_corrections(adam, &bc1, &bc2);
     nn_note_device_update(adam->weights[0]);          /* the network's host mirrors are now stale */
@@ -183,11 +177,9 @@ int adam_update_cuda_ex(Adam* adam, float lr, unsigned short* w16, long n16, uns
         const uintptr_t al = (uintptr_t)adam->weights[0] | (uintptr_t)adam->grad_weights[0] | (uintptr_t)adam->m |
                              (uintptr_t)adam->v;
         if (al & 15u) zero_g = 0;
-        if (al & 15u) wp = NULL;
-        phip_adam_flat_ex(adam->weights[0], adam->grad_weights[0], adam->m, adam->v, adam->span, lr, adam->beta1,
-                          adam->beta2, bc1, bc2, adam->grad_scale, w16, w16 ? n16 : 0, wp,
-                          wp ? (n_wp < adam->span ? n_wp : adam->span) : 0, n_wp, zero_g);
-        return (w16 != NULL) | (zero_g ? 2 : 0) | (wp ? 4 : 0);
+        phip_adam_flat_w16(adam->weights[0], adam->grad_weights[0], adam->m, adam->v, adam->span, lr, adam->beta1,
+                           adam->beta2, bc1, bc2, adam->grad_scale, w16, w16 ? n16 : 0, zero_g);
+        return (w16 != NULL) | (zero_g ? 2 : 0);
     } else {
         phip_adam_multi(adam->weights, adam->grad_weights, adam->lengths, adam->num_layers, adam->m, adam->v, lr,
                         adam->beta1, adam->beta2, bc1, bc2, adam->grad_scale);

@@ -321,10 +321,7 @@ static int tiny_net(NeuralNetwork* nn, Adam* adam, PhipTinyNet* t) {
 static int adam_update_net(Adam* adam, float lr, NeuralNetwork* nn, int zero_grads) {
     const int own = adam->flat && adam->weights[0] == nn->d_params && adam->grad_weights[0] == nn->d_grads;
     const int fused = nn->dtype == 1 && own;
-    unsigned short* wp = own && nn->wp_valid ? nn->d_wp : NULL;           /* x3 weight planes kept current */
-    const int r = adam_update_cuda_ex(adam, lr, fused ? nn->d_w16 : NULL, nn->num_params, wp, nn->num_params,
-                                      zero_grads && own);
-    if (nn->wp_valid && !(r & 4)) nn->wp_valid = 0;                       /* not refreshed: stop using them */
+    const int r = adam_update_cuda_w16(adam, lr, fused ? nn->d_w16 : NULL, nn->num_params, zero_grads && own);
     if (!(r & 1) && nn->dtype == 1) nn_sync_w16(nn);
     return (r & 2) != 0;                 /* the network's gradients are zero again */
 }
@@ -458,12 +455,7 @@ static void ppo_update_body(PPO* ppo, float gamma, int batch_size, int n_epochs_
 void ppo_update(void* vppo, float gamma, int batch_size, int n_epochs_policy, int n_epochs_value, int shuffle_mode,
                 unsigned long long seed) {
     PPO* ppo = (PPO*)vppo;
-    /* inside the update libppo owns every parameter write (Adam), so the x3 weight planes stay current */
-    nn_planes_begin(ppo->V);
-    nn_planes_begin(ppo->policy->mu);
     ppo_update_body(ppo, gamma, batch_size, n_epochs_policy, n_epochs_value, shuffle_mode, seed);
-    nn_planes_end(ppo->V);
-    nn_planes_end(ppo->policy->mu);
     ppo->V->dev_version++;               /* HBM parameters moved (also by the single-workgroup path) */
     ppo->policy->mu->dev_version++;
 }
