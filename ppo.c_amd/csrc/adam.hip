@@ -64,6 +64,56 @@ __global__ void adam_flat_vec_kernel(float* __restrict__ p, float* __restrict__ 
     }
 }
 
+// the flat Adam with its step size / bias correction from the step table (graph replay); which = 0
+// (the network's Adam) also advances the step counter: its last workgroup to finish, after every
+// workgroup has read the entry (a workgroup takes its ticket only at its end)
+__global__ void adam_flat_tab_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
+                                     float* __restrict__ v, long n, const PhipStepArgs* __restrict__ tab, int* ctr,
+                                     unsigned* ticket, int which, float b1, float b2, float scale,
+                                     __bf16* __restrict__ w16, long n16, int zero_g) {
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    const PhipStepArgs& s = tab[*ctr];
+    const float step = which ? s.step_ls : s.step, bc2 = which ? s.bc2_ls : s.bc2;
+    const long n4 = n >> 2;
+    for (long i = blockIdx.x * (long)TPB + threadIdx.x; i < n4; i += (long)gridDim.x * TPB) {
+        float4 pp = reinterpret_cast<float4*>(p)[i], gg = reinterpret_cast<const float4*>(g)[i];
+        float4 mm = reinterpret_cast<float4*>(m)[i], vv = reinterpret_cast<float4*>(v)[i];
+        adam_elem(pp.x, gg.x, mm.x, vv.x, step, b1, b2, bc2, scale);
+        adam_elem(pp.y, gg.y, mm.y, vv.y, step, b1, b2, bc2, scale);
+        adam_elem(pp.z, gg.z, mm.z, vv.z, step, b1, b2, bc2, scale);
+        adam_elem(pp.w, gg.w, mm.w, vv.w, step, b1, b2, bc2, scale);
+        reinterpret_cast<float4*>(p)[i] = pp;
+        reinterpret_cast<float4*>(m)[i] = mm;
+        reinterpret_cast<float4*>(v)[i] = vv;
+        if (zero_g) reinterpret_cast<float4*>(g)[i] = float4{0.f, 0.f, 0.f, 0.f};
+        if (w16 && 4 * i + 4 <= n16) {
+            bf16x4 o = {(__bf16)pp.x, (__bf16)pp.y, (__bf16)pp.z, (__bf16)pp.w};
+            reinterpret_cast<bf16x4*>(w16)[i] = o;
+        } else if (w16 && 4 * i < n16) {
+            const float e[4] = {pp.x, pp.y, pp.z, pp.w};
+            for (long j = 4 * i; j < n16; ++j) w16[j] = (__bf16)e[j - 4 * i];
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+        const long j = 4 * n4 + threadIdx.x;
+        float pp = p[j], mm = m[j], vv = v[j];
+        adam_elem(pp, g[j], mm, vv, step, b1, b2, bc2, scale);
+        p[j] = pp; m[j] = mm; v[j] = vv;
+        if (zero_g) g[j] = 0.f;
+        if (w16 && j < n16) w16[j] = (__bf16)pp;
+    }
+    if (which == 0) {
+        __syncthreads();                                   // every wave of this workgroup read the entry
+        if (threadIdx.x == 0) {
+            const unsigned t = atomicAdd(ticket, 1u);
+            if (t == gridDim.x - 1) {                      // the last workgroup: all have read it
+                *ticket = 0u;
+                *ctr += 1;
+            }
+        }
+    }
+}
+
 __global__ void adam_flat_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                                  float* __restrict__ v, long n, float step, float b1, float b2, float bc2,
                                  float scale) {
@@ -123,6 +173,17 @@ void phip_adam_flat_w16(float* p, float* g, float* m, float* v, long n, float lr
         hipLaunchKernelGGL(adam_flat_kernel, dim3(grid_for(n)), dim3(TPB), 0, ppo::stream(), p, g, m, v, n, step,
                            beta1, beta2, bias_correction2, grad_scale);
     }
+    PPO_LAUNCH_CHECK();
+}
+
+void phip_adam_flat_tab(float* p, float* g, float* m, float* v, long n, const PhipStepArgs* tab, int* ctr,
+                        unsigned* ticket, int which, float beta1, float beta2, float grad_scale, unsigned short* w16,
+                        long n16, int zero_g) {
+    if (n <= 0) return;
+    PPO_REQUIRE((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15u) == 0 && ((uintptr_t)w16 & 7u) == 0,
+                "phip_adam_flat_tab: unaligned span");
+    hipLaunchKernelGGL(adam_flat_tab_kernel, dim3(grid_for((n + 3) / 4)), dim3(TPB), 0, ppo::stream(), p, g, m, v, n,
+                       tab, ctr, ticket, which, beta1, beta2, grad_scale, reinterpret_cast<__bf16*>(w16), n16, zero_g);
     PPO_LAUNCH_CHECK();
 }
 

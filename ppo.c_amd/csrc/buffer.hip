@@ -92,6 +92,34 @@ __global__ void gather_small_kernel(const int* __restrict__ perm, Feistel f, int
     }
 }
 
+// the same gather with its per-step arguments from the step table (graph replay)
+__global__ void gather_small_tab_kernel(const PhipStepArgs* __restrict__ tab, const int* __restrict__ ctr,
+                                        const int* __restrict__ perm_base, int limit, int batch, int A,
+                                        const float* __restrict__ action, const float* __restrict__ logprob,
+                                        const float* __restrict__ advantage, const float* __restrict__ adv_target,
+                                        float* __restrict__ actions, float* __restrict__ logprobs,
+                                        float* __restrict__ advs, float* __restrict__ adv_targets,
+                                        int* __restrict__ rows) {
+    const int i = blockIdx.x * TPB + threadIdx.x;
+    if (i >= batch) return;
+    const PhipStepArgs& s = tab[*ctr];
+    Feistel f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) f.k[r] = s.fk[r];
+    f.half = s.fhalf; f.mask = s.fmask; f.n = s.fn;
+    const int list = (int)(((long)s.offset + i) % limit);
+    const int src = s.perm_off >= 0 ? perm_base[s.perm_off + list] : (int)feistel_index((uint32_t)list, f);
+    if (rows) rows[i] = src;
+    if (logprobs) logprobs[i] = logprob[src];
+    if (advs) advs[i] = advantage[src];
+    if (adv_targets) adv_targets[i] = adv_target[src];
+    if (actions) {
+        const float* sp = action + (long)src * A;
+        float* dp = actions + (long)i * A;
+        for (int c = 0; c < A; ++c) dp[c] = sp[c];
+    }
+}
+
 uint64_t splitmix64(uint64_t z) {
     z += 0x9E3779B97F4A7C15ULL;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
@@ -129,6 +157,27 @@ void phip_gather_rows(const int* perm, uint64_t key, int offset, int limit, int 
     hipLaunchKernelGGL(gather_kernel, dim3(grid), dim3(TPB), 0, ppo::stream(), perm, f, offset, limit, batch, S, A,
                        state, action, logprob, advantage, adv_target, states, actions, logprobs, advs, adv_targets,
                        rows);
+    PPO_LAUNCH_CHECK();
+}
+
+void phip_step_feistel(PhipStepArgs* s, unsigned long long key, int limit) {
+    int bits = 2;
+    while ((1ULL << bits) < (unsigned long long)limit) bits++;
+    s->fhalf = (unsigned)((bits + 1) / 2);
+    s->fmask = (1u << s->fhalf) - 1u;
+    s->fn = (unsigned)limit;
+    for (int r = 0; r < 4; ++r) s->fk[r] = (unsigned)splitmix64(key + (uint64_t)r);
+}
+
+void phip_gather_rows_tab(const PhipStepArgs* tab, const int* ctr, const int* perm_base, int limit, int batch, int A,
+                          const float* action, const float* logprob, const float* advantage,
+                          const float* adv_target, float* actions, float* logprobs, float* advs, float* adv_targets,
+                          int* rows) {
+    if (batch <= 0) return;
+    PPO_REQUIRE(limit > 0 && (!actions || A <= 32), "phip_gather_rows_tab: unsupported shape");
+    hipLaunchKernelGGL(gather_small_tab_kernel, dim3(ppo_divup(batch, TPB)), dim3(TPB), 0, ppo::stream(), tab, ctr,
+                       perm_base, limit, batch, A, action, logprob, advantage, adv_target, actions, logprobs, advs,
+                       adv_targets, rows);
     PPO_LAUNCH_CHECK();
 }
 

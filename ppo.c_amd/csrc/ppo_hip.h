@@ -190,6 +190,34 @@ void phip_adam_flat(float* p, const float* g, float* m, float* v, long n, float 
                     float beta2, float bias_correction1, float bias_correction2, float grad_scale);
 /* the same, also writing bf16(p) into w16[0, n16) (bf16 mode's parameter shadow); zero_g: g is
  * cleared once read (the next backward accumulates into it without a memset) */
+/* ---- launch-free minibatch steps (hipGraph replay with a device step table) ----
+ * One minibatch step is captured once as a graph whose per-step arguments — the gather's
+ * permutation offset / Feistel round keys and row offset, the Adam step sizes — live in a device
+ * table indexed by a device step counter; the network's Adam kernel advances the counter (its last
+ * workgroup to finish), so every replay of the same graph performs the next step. */
+typedef struct {
+    long perm_off;                  /* ≥ 0: host-rand permutation at perm_base + perm_off; −1: Feistel */
+    unsigned fk[4];                 /* Feistel round keys of the epoch */
+    unsigned fhalf, fmask, fn;      /* Feistel domain (the buffer's limit) */
+    int offset;                     /* k·B: the minibatch's first position in the epoch order */
+    float step, bc2;                /* the network Adam's lr / (1 − β1^t) and 1 − β2^t */
+    float step_ls, bc2_ls;          /* the entropy Adam's (policy log σ) */
+} PhipStepArgs;
+void phip_step_feistel(PhipStepArgs* s, unsigned long long key, int limit);   /* fills fk / fhalf / fmask / fn */
+void phip_gather_rows_tab(const PhipStepArgs* tab, const int* ctr, const int* perm_base, int limit, int batch, int A,
+                          const float* action, const float* logprob, const float* advantage,
+                          const float* adv_target, float* actions, float* logprobs, float* advs, float* adv_targets,
+                          int* rows);
+/* which = 0: the network's Adam (step / bc2; advances *ctr); 1: the entropy Adam (step_ls / bc2_ls) */
+void phip_adam_flat_tab(float* p, float* g, float* m, float* v, long n, const PhipStepArgs* tab, int* ctr,
+                        unsigned* ticket, int which, float beta1, float beta2, float grad_scale, unsigned short* w16,
+                        long n16, int zero_g);
+int  phip_graph_begin(void);                 /* capture the current stream's launches (returns 0 on success) */
+void* phip_graph_end(void);                  /* → instantiated executable graph (NULL on failure) */
+void phip_graph_launch(void* exec);          /* replay on the current stream */
+void phip_graph_destroy(void* exec);
+int  phip_capturing(void);                   /* 1 while a capture is open (profiling scopes stay out) */
+
 void phip_adam_flat_w16(float* p, float* g, float* m, float* v, long n, float lr, float beta1, float beta2,
                         float bias_correction1, float bias_correction2, float grad_scale, unsigned short* w16,
                         long n16, int zero_g);

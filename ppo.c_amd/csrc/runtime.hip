@@ -139,8 +139,10 @@ using namespace ppo;
 
 extern "C" {
 
+static int g_capturing = 0;                  // a hipGraph capture is open on libppo's stream
+
 int phip_prof_begin_key(int cls, double work, long long key) {
-    if (!g_prof_on) return -1;
+    if (!g_prof_on || g_capturing) return -1;
     g_issued_work[cls] += work;
     if (g_issued[cls]++ % g_prof_stride != 0) return -1;
     if (g_slots.size() >= (1u << 16)) harvest();
@@ -163,6 +165,32 @@ void phip_prof_end(int slot) {
 }
 
 void phip_init(void) { ensure_device(); }
+
+int phip_graph_begin(void) {
+    if (g_capturing) return -1;
+    if (hipStreamBeginCapture(stream(), hipStreamCaptureModeRelaxed) != hipSuccess) return -1;
+    g_capturing = 1;
+    return 0;
+}
+
+void* phip_graph_end(void) {
+    if (!g_capturing) return nullptr;
+    hipGraph_t graph = nullptr;
+    g_capturing = 0;
+    if (hipStreamEndCapture(stream(), &graph) != hipSuccess || !graph) return nullptr;
+    hipGraphExec_t exec = nullptr;
+    const hipError_t e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(graph);
+    return e == hipSuccess ? (void*)exec : nullptr;
+}
+
+void phip_graph_launch(void* exec) { PPO_CHECK(hipGraphLaunch((hipGraphExec_t)exec, stream())); }
+
+void phip_graph_destroy(void* exec) {
+    if (exec) PPO_CHECK(hipGraphExecDestroy((hipGraphExec_t)exec));
+}
+
+int phip_capturing(void) { return g_capturing; }
 
 void* phip_malloc(size_t bytes) {
     ensure_device();

@@ -32,7 +32,10 @@ namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int TPB = 1024;
+#ifndef PPO_TINY_TPB
+#define PPO_TINY_TPB 1024
+#endif
+constexpr int TPB = PPO_TINY_TPB;
 constexpr int NWAVES = TPB / 64;
 constexpr int MAXL = 8;            // linear layers
 
@@ -136,8 +139,12 @@ __device__ __forceinline__ void tile_gemm(int M, int N, int K, const float* __re
                 av[u] = (iok && k < K) ? av[u] : 0.f;
                 bv[u] = (jok && k < K) ? bv[u] : 0.f;
             }
+            // a short K tail (layer 0's K = S, the A-wide output layer's grad_x K = A): only the
+            // MFMAs whose 4-k slice holds real k (wave-uniform count) — the rest would add zeros
+            const int nu = K - k0 >= 32 ? 8 : (K - k0 + 3) >> 2;
 #pragma unroll
-            for (int u = 0; u < 8; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], acc, 0, 0, 0);
+            for (int u = 0; u < 8; ++u)
+                if (u < nu) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], acc, 0, 0, 0);
         }
         const int j = j0 + c;
         if (j < N) {

@@ -39,6 +39,13 @@ typedef struct {
     unsigned long long seed;
     int seeded;
     long max_v, max_p;            /* ppo_set_step_limit: cap on value / policy minibatch steps (−1: none) */
+    /* launch-free minibatch steps (graph replay): per phase (0 value, 1 policy) a device step table,
+     * its step counter and the Adam kernel's ticket */
+    PhipStepArgs* tab[2];
+    long tab_cap[2];
+    int* ctr;                     /* [2] step counters, [2] tickets (as unsigned) */
+    PhipStepArgs* h_tab;
+    long h_tab_cap;
 } PPODev;
 
 static float* g_v = NULL;         /* V(state), V(next_state) for compute_gae_cuda */
@@ -118,6 +125,8 @@ static void free_dev_ws(PPO* ppo) {
     phip_free(d->ro_rows); phip_free(d->env_state); phip_free(d->perm[0]); phip_free(d->perm[1]);
     phip_free(d->rows_p); phip_free(d->states_p);
     for (int i = 0; i < 3; i++) phip_free(d->tiny_steps[i]);
+    phip_free(d->tab[0]); phip_free(d->tab[1]); phip_free(d->ctr);
+    free(d->h_tab);
     free(d);
     ppo->dev = NULL;
 }
@@ -326,6 +335,17 @@ static int adam_update_net(Adam* adam, float lr, NeuralNetwork* nn, int zero_gra
     return (r & 2) != 0;                 /* the network's gradients are zero again */
 }
 
+/* the step-table form of adam_update_net / the entropy Adam (graph replay): flat span, gradients
+ * cleared, step sizes from the table; which = 0 advances the step counter (the network's Adam,
+ * the step's last kernel), 1 reads the entropy entry */
+static void adam_net_tab(Adam* adam, NeuralNetwork* nn, PPODev* d, int ph, int which) {
+    const int fused = nn && nn->dtype == 1;
+    phip_adam_flat_tab(adam->weights[0], adam->grad_weights[0], adam->m, adam->v, adam->span, d->tab[ph], d->ctr + ph,
+                       (unsigned*)(d->ctr + 2 + ph), which, adam->beta1, adam->beta2,
+                       adam->grad_scale, fused ? nn->d_w16 : NULL, fused ? nn->num_params : 0, 1);
+    nn_note_device_update(adam->weights[0]);
+}
+
 static float* tiny_steps(PPODev* d, int slot, Adam* adam, float lr, int n) {
     float* h = (float*)xmalloc(sizeof(float) * 2 * (size_t)n);
     for (int i = 0; i < n; i++) adam_next_step(adam, lr, &h[2 * i], &h[2 * i + 1]);
@@ -449,6 +469,189 @@ static int ppo_update_tiny(PPO* ppo, PPODev* d, int B, int n_epochs_policy, int 
     return 0;
 }
 
+/* ------------------------------------------------------------------ */
+/* one value / policy minibatch step (ppo.cu:395-443 bodies)           */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    PPO* ppo;
+    PPODev* d;
+    int B, S, A, limit, num_batches, comm, fuse_v, fuse_p;
+    const int *perms_v, *perms_p;
+    const uint64_t *keys_v, *keys_p;
+    long nv, np;
+    void *gv, *gp;                /* captured graphs of K steps each (value, policy) */
+    void *gv1, *gp1;              /* … and of one step (the remainder) */
+    int K;                        /* requested steps per graph (PPO_GRAPH_STEPS, default 16) */
+    long Kv, Kp;                  /* steps per graph as captured */
+} StepCtx;
+
+/* value step iv (tab: the step-table form captured into a graph: gather and Adam read their
+ * per-step arguments from d->tab[0] at the device step counter); returns whether its Adam cleared
+ * the gradients */
+static int value_step(StepCtx* c, long iv, int v_zero, int tab) {
+    PPO* ppo = c->ppo;
+    PPODev* d = c->d;
+    TrajectoryBuffer* buf = ppo->buffer;
+    NeuralNetwork* V = ppo->V;
+    const int B = c->B;
+    if (tab) {
+        phip_gather_rows_tab(d->tab[0], d->ctr + 0, c->perms_v, c->limit, B, c->A, buf->action_p, buf->logprob_p,
+                             buf->advantage_p, buf->adv_target_p, NULL, NULL, NULL, d->tgt, d->rows);
+    } else {
+        const int j = (int)(iv / c->num_batches), k = (int)(iv % c->num_batches);
+        const int* perm = c->perms_v ? c->perms_v + (long)j * c->limit : NULL;
+        /* gather fused into layer 0: the kernel emits row indices (+ targets); the layer-0 GEMM
+         * reads the buffer rows through them and leaves the gathered copy for its grad_W */
+        phip_gather_rows(perm, c->keys_v[j], k * B, c->limit, B, c->S, c->A, buf->state_p, buf->action_p,
+                         buf->logprob_p, buf->advantage_p, buf->adv_target_p, NULL, NULL, NULL, NULL, d->tgt, d->rows);
+    }
+    /* with a communicator: gradients all-reduced in per-layer buckets as the backward produces them
+     * (comm.hip's comm stream), joined before Adam */
+    if (c->fuse_v) {       /* output layer + MSE + output-layer backward in one pass (out_head.hip) */
+        nn_out_head_step(V, 0, buf->state_p, d->rows, d->states, B, v_zero, c->comm ? 0 : -1, d->tgt, NULL, NULL,
+                         NULL, NULL, 0.f, 0.f, NULL, d->stats + 0);
+    } else {
+        nn_forward_dev_rows(V, buf->state_p, d->rows, d->states, B);
+        phip_mse(V->d_output, d->tgt, B, d->gv, NULL, d->stats + 0);
+        nn_backward_dev_z(V, d->gv, B, 0, v_zero, c->comm ? 0 : -1);
+    }
+    phip_allreduce_join();
+    if (tab) {
+        adam_net_tab(ppo->adam_V, V, d, 0, 0);
+        return 1;
+    }
+    return adam_update_net(ppo->adam_V, ppo->lr_V, V, iv + 1 < c->nv);
+}
+
+static void policy_step(StepCtx* c, long ip, int* p_zero, int* ls_zero, int tab) {
+    PPO* ppo = c->ppo;
+    PPODev* d = c->d;
+    TrajectoryBuffer* buf = ppo->buffer;
+    GaussianPolicy* pol = ppo->policy;
+    NeuralNetwork* mu = pol->mu;
+    const int B = c->B, A = c->A;
+    if (tab) {
+        phip_gather_rows_tab(d->tab[1], d->ctr + 1, c->perms_p, c->limit, B, A, buf->action_p, buf->logprob_p,
+                             buf->advantage_p, buf->adv_target_p, d->actions, d->old_lp, d->adv, NULL, d->rows_p);
+    } else {
+        const int j = (int)(ip / c->num_batches), k = (int)(ip % c->num_batches);
+        const int* perm = c->perms_p ? c->perms_p + (long)j * c->limit : NULL;
+        phip_gather_rows(perm, c->keys_p[j], k * B, c->limit, B, c->S, A, buf->state_p, buf->action_p,
+                         buf->logprob_p, buf->advantage_p, buf->adv_target_p, NULL, d->actions, d->old_lp, d->adv,
+                         NULL, d->rows_p);
+    }
+    /* μ grads + (top bucket) the log σ gradient behind them */
+    if (c->fuse_p) {       /* output layer + clipped surrogate + output-layer backward (out_head.hip) */
+        if (!*ls_zero) phip_memset(pol->d_log_std_grad, 0, sizeof(float) * (size_t)A);
+        nn_out_head_step(mu, 1, buf->state_p, d->rows_p, d->states_p, B, *p_zero, c->comm ? align4(A) : -1, NULL,
+                         pol->d_log_std, d->actions, d->adv, d->old_lp, ppo->epsilon, ppo->ent_coeff,
+                         pol->d_log_std_grad, d->stats + 1);
+    } else {
+        nn_forward_dev_rows(mu, buf->state_p, d->rows_p, d->states_p, B);
+        phip_policy_head(mu->d_output, pol->d_log_std, d->actions, d->adv, d->old_lp, B, A, ppo->epsilon,
+                         ppo->ent_coeff, d->gmu, pol->d_log_std_grad, d->stats + 1, *ls_zero);
+        nn_backward_dev_z(mu, d->gmu, B, 0, *p_zero, c->comm ? align4(A) : -1);
+    }
+    phip_allreduce_join();
+    /* ppo.cu:440-442 order; the entropy Adam clears the log σ gradient it read (the next policy head
+     * accumulates into zeros) */
+    if (tab) {
+        adam_net_tab(ppo->adam_entropy, NULL, d, 1, 1);
+        adam_net_tab(ppo->adam_policy, mu, d, 1, 0);
+        *ls_zero = *p_zero = 1;
+        return;
+    }
+    *ls_zero = ppo->adam_entropy->flat && ppo->adam_entropy->grad_weights[0] == pol->d_log_std_grad &&
+               (adam_update_cuda_w16(ppo->adam_entropy, ppo->lr_policy, NULL, 0, ip + 1 < c->np) & 2);
+    *p_zero = adam_update_net(ppo->adam_policy, ppo->lr_policy, mu, ip + 1 < c->np);
+}
+
+/* graph replay (opt-in, PPO_GRAPH=1; PPO_GRAPH_STEPS = steps per captured graph, default 16) for
+ * small minibatches on one GPU when every Adam of the step is a flat, 16-B aligned span that owns its
+ * network (the table kernels' form).  Measured at C3, B = 64 (profiles/r03_graph_replay.txt): eager
+ * 2062 ms per update, graphs of 1 / 4 / 16 / 64 steps 2375 / 2156 / 2104 / 2091 ms — on this ROCm a
+ * graph replays its kernel nodes at the eager launch cost, and the step is GPU-bound (≈ 36 µs for 8–9
+ * dependent small kernels), so it stays off by default. */
+static int step_graphs_ok(const StepCtx* c) {
+    const char* e = getenv("PPO_GRAPH");
+    if (!(e && *e && *e != '0') || c->comm || phip_comm_world() > 1 || c->B > 2048 || c->A > 32) return 0;
+    PPO* ppo = c->ppo;
+    Adam* ads[3] = {ppo->adam_V, ppo->adam_policy, ppo->adam_entropy};
+    for (int i = 0; i < 3; i++) {
+        Adam* a = ads[i];
+        const uintptr_t al = (uintptr_t)a->weights[0] | (uintptr_t)a->grad_weights[0] | (uintptr_t)a->m |
+                             (uintptr_t)a->v;
+        if (!a->flat || (al & 15u)) return 0;
+    }
+    if (ppo->adam_V->weights[0] != ppo->V->d_params || ppo->adam_policy->weights[0] != ppo->policy->mu->d_params ||
+        ppo->adam_entropy->grad_weights[0] != ppo->policy->d_log_std_grad)
+        return 0;
+    if ((ppo->V->dtype == 1 && ppo->V->num_params > ppo->adam_V->span) ||
+        (ppo->policy->mu->dtype == 1 && ppo->policy->mu->num_params > ppo->adam_policy->span))
+        return 0;
+    return 1;
+}
+
+/* the step table of phase ph (0 value, 1 policy) for steps 1 … n−2 — epoch order, minibatch offset
+ * and the Adam step sizes in the reference's step order (advancing the host Adam step counters as
+ * the eager path does) — uploaded, the counter reset, and one step captured as a graph */
+static void* capture_graph(StepCtx* c, int ph, int steps) {
+    if (phip_graph_begin() != 0) die("ppo_update: graph capture could not start");
+    for (int s = 0; s < steps; s++) {
+        if (ph) {
+            int pz = 1, lz = 1;
+            policy_step(c, 1, &pz, &lz, 1);
+        } else {
+            (void)value_step(c, 1, 1, 1);
+        }
+    }
+    void* exec = phip_graph_end();
+    if (!exec) die("ppo_update: graph capture failed");
+    return exec;
+}
+
+static void capture_steps(StepCtx* c, int ph) {
+    PPO* ppo = c->ppo;
+    PPODev* d = c->d;
+    const long n = (ph ? c->np : c->nv) - 2;
+    if (n <= 0) return;
+    if (n > d->h_tab_cap) {
+        free(d->h_tab);
+        d->h_tab = (PhipStepArgs*)xmalloc(sizeof(PhipStepArgs) * (size_t)n);
+        d->h_tab_cap = n;
+    }
+    if (n > d->tab_cap[ph]) {
+        phip_free(d->tab[ph]);
+        d->tab[ph] = (PhipStepArgs*)phip_malloc(sizeof(PhipStepArgs) * (size_t)n);
+        d->tab_cap[ph] = n;
+    }
+    if (!d->ctr) d->ctr = (int*)phip_malloc(sizeof(int) * 4);
+    const int* perms = ph ? c->perms_p : c->perms_v;
+    const uint64_t* keys = ph ? c->keys_p : c->keys_v;
+    for (long t = 0; t < n; t++) {
+        const long i = t + 1;
+        const int j = (int)(i / c->num_batches), k = (int)(i % c->num_batches);
+        PhipStepArgs* e = &d->h_tab[t];
+        memset(e, 0, sizeof(*e));
+        e->perm_off = perms ? (long)j * c->limit : -1;
+        if (!perms) phip_step_feistel(e, keys[j], c->limit);
+        e->offset = k * c->B;
+        if (ph) {
+            adam_next_step(ppo->adam_entropy, ppo->lr_policy, &e->step_ls, &e->bc2_ls);   /* ppo.cu:440-442 */
+            adam_next_step(ppo->adam_policy, ppo->lr_policy, &e->step, &e->bc2);
+        } else {
+            adam_next_step(ppo->adam_V, ppo->lr_V, &e->step, &e->bc2);
+        }
+    }
+    phip_h2d(d->tab[ph], d->h_tab, sizeof(PhipStepArgs) * (size_t)n);
+    phip_memset(d->ctr + ph, 0, sizeof(int));
+    phip_memset(d->ctr + 2 + ph, 0, sizeof(int));
+    const int K = (int)(n < c->K ? n : c->K);
+    void* gk = capture_graph(c, ph, K);
+    void* g1 = K > 1 ? capture_graph(c, ph, 1) : NULL;
+    if (ph) { c->gp = gk; c->gp1 = g1; c->Kp = K; } else { c->gv = gk; c->gv1 = g1; c->Kv = K; }
+}
+
 static void ppo_update_body(PPO* ppo, float gamma, int batch_size, int n_epochs_policy, int n_epochs_value,
                             int shuffle_mode, unsigned long long seed);
 
@@ -512,65 +715,53 @@ static void ppo_update_body(PPO* ppo, float gamma, int batch_size, int n_epochs_
     const char* serial_env = getenv("PPO_SERIAL");
     const int concurrent = nv > 0 && np > 0 && !(serial_env && *serial_env && *serial_env != '0');
     if (concurrent) phip_side_fork();
+    StepCtx c = {ppo, d, B, S, A, limit, num_batches, comm, nn_out_head_ok(V, 0), nn_out_head_ok(mu, 1),
+                 perms_v, perms_p, keys_v, keys_p, nv, np, NULL, NULL, NULL, NULL, 16, 1, 1};
+    {
+        const char* ge = getenv("PPO_GRAPH_STEPS");
+        if (ge && atoi(ge) > 0) c.K = atoi(ge);
+    }
+    /* graph replay (opt-in): steps 1 … n−2 of a phase replay captured graphs of K steps (the first
+     * step runs eagerly — workspaces allocated, gradients cleared — and the last one too, so the
+     * caller can read its gradients) */
+    const int graphs = step_graphs_ok(&c);
     long iv = 0, ip = 0;
     /* gradients cleared by the previous Adam step (not after a loop's last step: a caller may read
      * the last minibatch's gradients after the update) */
     int v_zero = 0, p_zero = 0, ls_zero = 0;
-    const int fuse_v = nn_out_head_ok(V, 0), fuse_p = nn_out_head_ok(mu, 1);
     while (iv < nv || ip < np) {
         /* serial: every value step first (the reference's order); concurrent: issue in proportion */
         const int take_v = iv < nv && (ip >= np || !concurrent || iv * np <= ip * nv);
         if (take_v) {
-            const int j = (int)(iv / num_batches), k = (int)(iv % num_batches);
-            const int* perm = perms_v ? perms_v + (long)j * limit : NULL;
-            /* gather fused into layer 0: the kernel emits row indices (+ targets); the layer-0 GEMM
-             * reads the buffer rows through them and leaves the gathered copy for its grad_W */
-            phip_gather_rows(perm, keys_v[j], k * B, limit, B, S, A, buf->state_p, buf->action_p, buf->logprob_p,
-                             buf->advantage_p, buf->adv_target_p, NULL, NULL, NULL, NULL, d->tgt, d->rows);
-            /* with a communicator: gradients all-reduced in per-layer buckets as the backward
-             * produces them (comm.hip's comm stream), joined before Adam */
-            if (fuse_v) {       /* output layer + MSE + output-layer backward in one pass (out_head.hip) */
-                nn_out_head_step(V, 0, buf->state_p, d->rows, d->states, B, v_zero, comm ? 0 : -1, d->tgt, NULL,
-                                 NULL, NULL, NULL, 0.f, 0.f, NULL, d->stats + 0);
+            long done = 1;
+            if (c.gv && iv >= 1 && iv + 1 < nv) {
+                if (nv - 1 - iv >= c.Kv) { phip_graph_launch(c.gv); done = c.Kv; }
+                else phip_graph_launch(c.gv1 ? c.gv1 : c.gv);
             } else {
-                nn_forward_dev_rows(V, buf->state_p, d->rows, d->states, B);
-                phip_mse(V->d_output, d->tgt, B, d->gv, NULL, d->stats + 0);
-                nn_backward_dev_z(V, d->gv, B, 0, v_zero, comm ? 0 : -1);
+                v_zero = value_step(&c, iv, v_zero, 0);
+                if (iv == 0 && graphs && nv >= 3) capture_steps(&c, 0);
             }
-            phip_allreduce_join();
-            v_zero = adam_update_net(ppo->adam_V, ppo->lr_V, V, iv + 1 < nv);
-            d->n_v++;
-            iv++;
+            d->n_v += done;
+            iv += done;
         } else {
-            const int j = (int)(ip / num_batches), k = (int)(ip % num_batches);
-            const int* perm = perms_p ? perms_p + (long)j * limit : NULL;
+            long done = 1;
             if (concurrent) phip_side_use(1);
-            phip_gather_rows(perm, keys_p[j], k * B, limit, B, S, A, buf->state_p, buf->action_p, buf->logprob_p,
-                             buf->advantage_p, buf->adv_target_p, NULL, d->actions, d->old_lp, d->adv, NULL,
-                             d->rows_p);
-            /* μ grads + (top bucket) the log σ gradient behind them */
-            if (fuse_p) {       /* output layer + clipped surrogate + output-layer backward (out_head.hip) */
-                if (!ls_zero) phip_memset(pol->d_log_std_grad, 0, sizeof(float) * (size_t)A);
-                nn_out_head_step(mu, 1, buf->state_p, d->rows_p, d->states_p, B, p_zero, comm ? align4(A) : -1, NULL,
-                                 pol->d_log_std, d->actions, d->adv, d->old_lp, ppo->epsilon, ppo->ent_coeff,
-                                 pol->d_log_std_grad, d->stats + 1);
+            if (c.gp && ip >= 1 && ip + 1 < np) {
+                if (np - 1 - ip >= c.Kp) { phip_graph_launch(c.gp); done = c.Kp; }
+                else phip_graph_launch(c.gp1 ? c.gp1 : c.gp);
             } else {
-                nn_forward_dev_rows(mu, buf->state_p, d->rows_p, d->states_p, B);
-                phip_policy_head(mu->d_output, pol->d_log_std, d->actions, d->adv, d->old_lp, B, A, ppo->epsilon,
-                                 ppo->ent_coeff, d->gmu, pol->d_log_std_grad, d->stats + 1, ls_zero);
-                nn_backward_dev_z(mu, d->gmu, B, 0, p_zero, comm ? align4(A) : -1);
+                policy_step(&c, ip, &p_zero, &ls_zero, 0);
+                if (ip == 0 && graphs && np >= 3) capture_steps(&c, 1);
             }
-            phip_allreduce_join();
-            /* ppo.cu:440-442 order; the entropy Adam clears the log σ gradient it read (the next
-             * policy head accumulates into zeros) */
-            ls_zero = ppo->adam_entropy->flat && ppo->adam_entropy->grad_weights[0] == pol->d_log_std_grad &&
-                      (adam_update_cuda_w16(ppo->adam_entropy, ppo->lr_policy, NULL, 0, ip + 1 < np) & 2);
-            p_zero = adam_update_net(ppo->adam_policy, ppo->lr_policy, mu, ip + 1 < np);
             if (concurrent) phip_side_use(0);
-            d->n_p++;
-            ip++;
+            d->n_p += done;
+            ip += done;
         }
     }
+    phip_graph_destroy(c.gv);
+    phip_graph_destroy(c.gp);
+    phip_graph_destroy(c.gv1);
+    phip_graph_destroy(c.gp1);
     if (concurrent) phip_side_join();
     free(keys);
 }

@@ -506,3 +506,48 @@ def test_out_head_matches_separate(lib, oracle, cfg, monkeypatch):
     assert_gemm_close(b["yV"], a["yV"], sizes[-2], f"{cfg} value output (fused vs separate)")
     assert_rel_close(b["gls"], a["gls"], 1e-3, 1e-4 * max(1.0, np.abs(a["gls"]).max()), "log_std grad")
     np.testing.assert_allclose(b["stats"], a["stats"], rtol=1e-3, atol=1e-6)
+
+
+@pytest.mark.parametrize("shuffle_mode", [0, 1])
+def test_graph_replay_matches_eager(lib, oracle, shuffle_mode, monkeypatch):
+    """Graph replay of minibatch steps (PPO_GRAPH=1, B = 64: steps 1 … n−2 of each phase replay captured
+    16-step graphs whose gather / Adam arguments come from the device step table) against the eager
+    launches from identical state: the same minibatch order (host rand() permutations and the
+    device Feistel order), the same Adam step counts and sizes, so parameters and loss sums agree to
+    the rounding of the fused heads' per-workgroup f32 atomics."""
+    sizes, N, B = [17, 256, 256, 6], 4096, 64
+    out = {}
+    for mode in ("eager", "graph"):
+        if mode == "eager":
+            monkeypatch.delenv("PPO_GRAPH", raising=False)
+        else:
+            monkeypatch.setenv("PPO_GRAPH", "1")
+            monkeypatch.setenv("PPO_GRAPH_STEPS", "16")
+        ppo = make_ppo(lib, oracle, sizes, N, init_std=0.7, ent_coeff=0.01)
+        mu0, ls0 = policy_state(lib, ppo)
+        buf = synthetic_buffer(oracle, sizes, mu0, ls0, N, seed=44, n_envs=8)
+        load_buffer(lib, ppo, buf)
+        lib.ppo_reset_stats(ppo)
+        oracle.srand(321)
+        lib.ppo_update(ppo, 0.99, B, 1, 2, shuffle_mode, 77)
+        lib.ppo_synchronize()
+        st = (C.c_double * 7)()
+        lib.ppo_read_stats(ppo, st, 7)
+        mu, ls = policy_state(lib, ppo)
+        out[mode] = dict(stats=np.array(st[:4]), v=nn_params_packed(lib, ppo.contents.V), mu=mu, ls=ls,
+                         gv=nn_grads_packed(lib, ppo.contents.V), next_rand=oracle.libc().rand(),
+                         t=(ppo.contents.adam_V.contents.time_step, ppo.contents.adam_policy.contents.time_step,
+                            ppo.contents.adam_entropy.contents.time_step))
+        lib.free_ppo(ppo)
+    a, b = out["eager"], out["graph"]
+    assert a["t"] == b["t"] == (2 * N // B, N // B, N // B)
+    assert a["next_rand"] == b["next_rand"]
+    assert a["stats"][1] == b["stats"][1] and a["stats"][3] == b["stats"][3]
+    np.testing.assert_allclose(b["stats"], a["stats"], rtol=1e-4, atol=1e-6)
+    lr, n_steps = 3e-4, 2 * N // B
+    for key in ("v", "mu", "ls"):
+        err = np.abs(a[key].astype(np.float64) - b[key])
+        assert err.max() <= 2 * lr * n_steps, (key, err.max())
+        assert (err <= 0.1 * lr).mean() >= 0.99, (key, (err <= 0.1 * lr).mean())
+    # the last value minibatch ran eagerly in both: its gradients are there to read
+    assert np.abs(b["gv"]).max() > 0
