@@ -879,7 +879,10 @@ void phip_x3_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, 
     // (16 MB of f32 atomics at ≈1.3 TB/s set the grad_W time of small batches; the slab path moves
     // the same bytes at store / load rate, and its sum is deterministic); the bias gradient keeps
     // its per-workgroup atomics (l floats per split)
-    const bool use_slab = splits > 1 && !g_x3_atomics && al16(gW);
+    // (when each split is short: at C4's 32768 rows, 2048 per split, the atomics hide behind the
+    // mainloop and the extra launch costs more — 326.1 vs 323.3 ms per update; at the G = 8 shard's
+    // 4096 rows, 256 per split, the slabs win — 89.4 vs 93.4 ms, profiles/r03i_*)
+    const bool use_slab = splits > 1 && kchunk <= 1024 && !g_x3_atomics && al16(gW);
     if (splits > 1 && !zeroed) {
         if (!use_slab) phip_memset(gW, 0, sizeof(float) * (size_t)l * n);
         if (gb) phip_memset(gb, 0, sizeof(float) * (size_t)l);
