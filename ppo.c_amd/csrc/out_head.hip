@@ -199,19 +199,27 @@ __global__ __launch_bounds__(NTH) void out_head_kernel(OutArgs p) {
 
     int it = 0;
     const int stride = gridDim.x * SLOTS;
-    // the next row's slice is loaded while this row is processed (one row of latency hidden)
-    float xn[NPL];
-    {
-        const int r0 = blockIdx.x * SLOTS + slot;
-        if (r0 < m) load_cols<NPL>(X + (long)r0 * N + c0, xn);
+    // rows in flight per wave: PF rows' slices are loaded ahead (a ring of registers, statically
+    // indexed by unrolling PF rows per iteration); one wave per row keeps up to PF·NPL loads in
+    // flight instead of one row's (3.5 -> ≈5 TB/s of x read + gx written at C4's value head)
+    constexpr int PF = WPR == 1 ? 4 : 1;
+    float xr[PF][NPL];
+    const int first = blockIdx.x * SLOTS + slot;
+#pragma unroll
+    for (int f = 0; f < PF; ++f) {
+        const int r0 = first + f * stride;
+        if (r0 < m) load_cols<NPL>(X + (long)r0 * N + c0, xr[f]);
     }
-    for (int base = blockIdx.x * SLOTS; base < m; base += stride, ++it) {
-        const int row = base + slot;
+    for (int base = blockIdx.x * SLOTS; base < m; base += PF * stride) {
+#pragma unroll
+    for (int f = 0; f < PF; ++f, ++it) {
+        const int row = base + f * stride + slot;
+        if (WPR == 1 && base + f * stride >= m) break;  // (WPR > 1: PF = 1, the loop condition)
         const bool valid = row < m;                    // every wave reaches the barrier
         float xv[NPL];
 #pragma unroll
-        for (int q = 0; q < NPL; ++q) xv[q] = valid ? xn[q] : 0.f;
-        if (row + stride < m) load_cols<NPL>(X + (long)(row + stride) * N + c0, xn);
+        for (int q = 0; q < NPL; ++q) xv[q] = valid ? xr[f][q] : 0.f;
+        if (row + PF * stride < m) load_cols<NPL>(X + (long)(row + PF * stride) * N + c0, xr[f]);
         float yv[A];
 #pragma unroll
         for (int a = 0; a < A; ++a) {
@@ -282,6 +290,7 @@ __global__ __launch_bounds__(NTH) void out_head_kernel(OutArgs p) {
 #pragma unroll
             for (int q = 0; q < NPL; ++q) gWacc[a][q] += g[a] * xv[q];
         }
+    }
     }
 
     // workgroup sums (row slots in order), then one atomic per element
