@@ -32,6 +32,12 @@ struct ProfScope {
 // dispatch itself (hipExtLaunchKernel) — the kernel's own duration, as rocprofv3 reports it.
 bool take_kernel_events(hipEvent_t* start, hipEvent_t* stop);
 
+// split-K grad_W partials (gemm_x3.hip): a per-stream scratch of `floats` floats, and
+// out[i] = Σ_s slab[s·n + i] in a fixed order (n % 4 == 0, 16-B aligned); `stop`: an event recorded
+// by the reduce's dispatch (or null)
+float* slab_scratch(size_t floats);
+void slab_reduce(const float* slab, float* out, long n, int splits, hipEvent_t stop);
+
 // shape tag of a GEMM launch: op (0 fwd, 1 grad_x, 2 grad_W, 3 paired bwd) [60..63] | engine [56..59] |
 // m [32..55] | n [16..31] | l [0..15]; fields masked so an out-of-range width cannot alias another shape
 inline long long gemm_key(int op, int engine, long m, long n, long l) {

@@ -1096,6 +1096,194 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_dma16_kernel(Args a) {
     c_image_out<OP, BM, BN, NTH>(a, cimg, m0, n0, tid);
 }
 
+// ---------------------------------------------------------------------------
+// grad_W on the LDS-DMA tile (bf16 g and x, fp32 partials): gW[l, n] = gᵀ·x over one split of the
+// batch.  Both operands are row-contiguous along the output's dimensions, so both images are
+// [64 k][R] n-contiguous ones (the swizzle of gemm_bf16_dma16_kernel's grad_x W), every fragment a
+// pair of hardware transposes; 256×BN tiles over 8 waves of 64×(BN/2) as 16×16×32 blocks, two
+// images, one barrier per k-tile.  A split's partial tile leaves with plain stores into its slab
+// (ppo::slab_reduce sums the slabs in a fixed order; 16 MB of f32 atomics per launch had set the
+// register-staged kernel's time) or straight into gW for one split.  The bias gradient (Σ_k g) of
+// the tiles in column 0 is summed from the g image: thread t adds 8 columns of 4 k-rows per k-tile
+// (one ds_read_b128 each), the 16 k-row groups meet in LDS after the mainloop.
+// ---------------------------------------------------------------------------
+template <int BN>
+__global__ __launch_bounds__(512, 1) void gemm_bf16_dma_tn_kernel(Args a, float* __restrict__ slab) {
+    typedef float f32x4v __attribute__((ext_vector_type(4)));
+    constexpr int BM = 256, BK = 64, WARPS_N = 2;
+    constexpr int WM = 64, WN = BN / 2, TM = WM / 16, TN = WN / 16;
+    constexpr int IMGA = BK * BM, IMGB = BK * BN, BUF = IMGA + IMGB;
+    constexpr int PA_ = IMGA / 512 / 8, PB_ = IMGB / 512 / 8;      // 1-KiB pieces per wave
+    static_assert(BN == 256 || BN == 128, "tile width");
+    extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
+    typedef __attribute__((address_space(3))) void* lds_ptr;
+    typedef __attribute__((address_space(1))) void* g_ptr;
+
+    // XCD-aware remap (n fastest, then m, then split: one split's tiles share an XCD's L2)
+    const int nwg = gridDim.x, b = blockIdx.x;
+    const int xcd = b & 7, qq = nwg >> 3, rr = nwg & 7;
+    const int t = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (b >> 3);
+    const int tn = t % a.tiles_n;
+    const int rest = t / a.tiles_n;
+    const int tm = rest % a.tiles_m;
+    const int split = rest / a.tiles_m;
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int kbeg = split * a.kchunk;
+    const int nk = (min(a.K, kbeg + a.kchunk) - kbeg) / BK;
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wm = w / WARPS_N, wn = w % WARPS_N;
+    const int l15 = lane & 15, g4 = lane >> 4;
+    auto swz = [](int kr) { return ((kr & 3) << 2) | (((kr >> 3) & 1) << 1); };
+
+    const unsigned short* __restrict__ PA = static_cast<const unsigned short*>(a.A);
+    const unsigned short* __restrict__ PB = static_cast<const unsigned short*>(a.B);
+    int offa[PA_], offb[PB_];
+#pragma unroll
+    for (int i = 0; i < PA_; ++i) {                  // piece q: k-rows 2q, 2q+1 of the [64][256] image
+        const int q = PA_ * w + i, kr = 2 * q + (lane >> 5), c = (lane & 31) ^ swz(kr);
+        offa[i] = (kbeg + kr) * a.lda + m0 + 8 * c;
+    }
+#pragma unroll
+    for (int i = 0; i < PB_; ++i) {
+        const int q = PB_ * w + i;
+        if constexpr (BN == 256) {
+            const int kr = 2 * q + (lane >> 5), c = (lane & 31) ^ swz(kr);
+            offb[i] = (kbeg + kr) * a.ldb + n0 + 8 * c;
+        } else {                                     // [64][128]: k-rows 4q .. 4q+3 per piece
+            const int kr = 4 * q + (lane >> 4), c = (lane & 15) ^ swz(kr);
+            offb[i] = (kbeg + kr) * a.ldb + n0 + 8 * c;
+        }
+    }
+    const long sa = (long)BK * a.lda, sb = (long)BK * a.ldb;
+    auto dma = [&](int j, unsigned short* img) {
+#pragma unroll
+        for (int i = 0; i < PA_; ++i)
+            __builtin_amdgcn_global_load_lds((g_ptr)(PA + offa[i] + j * sa), (lds_ptr)(img + (PA_ * w + i) * 512), 16, 0, 0);
+#pragma unroll
+        for (int i = 0; i < PB_; ++i)
+            __builtin_amdgcn_global_load_lds((g_ptr)(PB + offb[i] + j * sb),
+                                             (lds_ptr)(img + IMGA + (PB_ * w + i) * 512), 16, 0, 0);
+    };
+    // transposed read of an n-contiguous image of pitch P: lane gets column cbase + (lane & 15),
+    // k = 32s + 8(lane >> 4) .. +7
+    auto frag = [&](const unsigned short* img, int P, int cbase, int s) {
+        const int q = l15 >> 2, p = l15 & 3;
+        const int cb = cbase + 4 * p;
+        typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+        const int kr = 32 * s + 8 * g4 + q;                            // kr + 4: same swizzle
+        const int pos = ((cb >> 3) ^ swz(kr)) * 8 + (cb & 7);
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + kr * P + pos));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + (kr + 4) * P + pos));
+        typedef short s16x8 __attribute__((ext_vector_type(8)));
+        const s16x8 f = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        return __builtin_bit_cast(bf16x8, f);
+    };
+
+    f32x4v acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+
+    auto step = [&](const unsigned short* img, int s) {
+        bf16x8 fa[TM], fb[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) fa[i] = frag(img, BM, wm * WM + i * 16, s);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) fb[j] = frag(img + IMGA, BN, wn * WN + j * 16, s);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                if constexpr (PPO_G16_ABLATE & 1)
+                    acc[i][j][0] += __builtin_bit_cast(u32x4, fa[i])[0] ^ __builtin_bit_cast(u32x4, fb[j])[1];
+                else
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+            }
+    };
+
+    const bool do_bias = a.gbias != nullptr && tn == 0;
+    const int bcg = tid & 31, bkq = tid >> 5;           // bias: columns 8·bcg .. +7, k-rows 4·bkq .. +3
+    float bs[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bs[e] = 0.f;
+    auto bias_tile = [&](const unsigned short* img) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int kr = 4 * bkq + r;
+            const u32x4 v = *reinterpret_cast<const u32x4*>(img + kr * BM + 8 * (bcg ^ swz(kr)));
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                bs[2 * e] += bf_lo(v[e]);
+                bs[2 * e + 1] += __builtin_bit_cast(float, v[e] & 0xffff0000u);
+            }
+        }
+    };
+
+    unsigned short* const buf0 = lds;
+    unsigned short* const buf1 = lds + BUF;
+    dma(0, buf0);
+    if (nk > 1) {
+        dma(1, buf1);
+        if constexpr (BN == 256) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // tile 0's pieces landed
+        else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    for (int j = 0; j < nk; ++j) {
+        unsigned short* cur = (j & 1) ? buf1 : buf0;
+        step(cur, 0);
+        if (do_bias) bias_tile(cur);
+        step(cur, 1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (j + 2 < nk && !(PPO_G16_ABLATE & 4)) dma(j + 2, cur);
+    }
+    if constexpr (PPO_G16_ABLATE & 2) {                       // keep the accumulators live
+        float t = 0.f;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int jj = 0; jj < TN; ++jj)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) t += acc[i][jj][e];
+        if (t == 1234.5f) static_cast<float*>(a.C)[tid] = t;
+        return;
+    }
+
+    // a.cvec (split-K with gb = gW + l·n, the flat gradient layout): each split's bias partial goes
+    // to its slab behind the gW partial and the slab reduce sums both — no atomics, no memset
+    const long sstride = (long)a.M * a.N + (a.cvec ? a.M : 0);
+    float* const out = a.splits > 1 ? slab + (long)split * sstride : static_cast<float*>(a.C);
+    if (do_bias) {                                       // images free after the last barrier
+        float* red = reinterpret_cast<float*>(lds);      // [16][256]
+#pragma unroll
+        for (int e = 0; e < 8; ++e) red[bkq * 256 + 8 * bcg + e] = bs[e];
+        __syncthreads();
+        if (tid < 256) {
+            float s = 0.f;
+#pragma unroll
+            for (int q = 0; q < 16; ++q) s += red[q * 256 + tid];
+            if (a.splits == 1) a.gbias[m0 + tid] = s;
+            else if (a.cvec) out[(long)a.M * a.N + m0 + tid] = s;
+            else atomicAdd(a.gbias + m0 + tid, s);
+        }
+    }
+    // partial tile stores straight from the accumulators (16 lanes = 64 contiguous bytes per row;
+    // staging through LDS for whole-row float4 stores measured 1.3 µs slower at C5)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int col = n0 + wn * WN + j * 16 + l15;
+            const int r0 = m0 + wm * WM + i * 16 + 4 * g4;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) out[(long)(r0 + e) * a.N + col] = acc[i][j][e];
+        }
+}
+
 using f32 = float;
 using b16 = unsigned short;
 
@@ -1255,6 +1443,62 @@ int pick16(int M, int N, int op = OP_NT) {
 inline bool al16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 inline int epl(int t) { return t ? 8 : 4; }
 
+// grad_W on the LDS-DMA TN tile (bf16 g and x): l a multiple of 256, n of 128, the batch of 64;
+// PPO_G16_TN=0 keeps the register-staged kernel, PPO_G16_TN_BN=128|256 forces the tile width
+int g_tn_dma = [] { const char* e = getenv("PPO_G16_TN"); return e ? atoi(e) : 1; }();
+int g_tn_bn = [] { const char* e = getenv("PPO_G16_TN_BN"); return e ? atoi(e) : 0; }();
+
+bool launch_dma_tn(float* gW, float* gb, const void* g, const void* x, int m, int n, int l, int zeroed) {
+    if (g_tn_dma == 0 || dma16_setting() == 0 || g_force16 >= 0) return false;
+    if (l % 256 != 0 || n % 128 != 0 || m % 64 != 0 || !al16(g) || !al16(x) || !al16(gW)) return false;
+    if ((long)m * l >= (1L << 31) || (long)m * n >= (1L << 31)) return false;
+    const int BN = g_tn_bn == 128 || g_tn_bn == 256 ? g_tn_bn : (n % 256 == 0 ? 256 : 128);
+    if (n % BN != 0) return false;
+    Args a{};
+    a.A = g; a.lda = l; a.B = x; a.ldb = n; a.C = gW; a.ldc = n;
+    a.M = l; a.N = n; a.K = m; a.gbias = gb;
+    a.tiles_m = l / 256;
+    a.tiles_n = n / BN;
+    const long tiles = (long)a.tiles_m * a.tiles_n;
+    const int target = g_split16 > 0 ? g_split16 : 256;              // one workgroup per CU
+    int splits = (int)std::max<long>(1, target / tiles);
+    splits = std::min(splits, std::max(1, m / (4 * 64)));              // ≥ 4 k-tiles per split
+    a.kchunk = ppo_divup(ppo_divup(m, splits), 64) * 64;
+    a.splits = splits = ppo_divup(m, a.kchunk);
+    PPO_REQUIRE(tiles * splits < (1L << 31), "gemm16 (dma tn): grid out of range");
+    a.cvec = gb && splits > 1 && gb == gW + (long)l * n;            // bias partials through the slabs
+    if (gb && splits > 1 && !a.cvec && !zeroed) phip_memset(gb, 0, sizeof(float) * (size_t)l);
+    const long sstride = (long)l * n + (a.cvec ? l : 0);
+    float* slab = splits > 1 ? ppo::slab_scratch((size_t)splits * sstride) : nullptr;
+    constexpr size_t lds256 = 2 * 2 * (64 * 256 + 64 * 256), lds128 = 2 * 2 * (64 * 256 + 64 * 128);
+    static_assert(lds256 <= 160 * 1024 && lds128 <= 160 * 1024, "gemm16 (dma tn): LDS");
+    static bool attr[2] = {false, false};
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    const bool timed = ppo::take_kernel_events(&e0, &e1);      // one duration: GEMM start → reduce end
+    hipEvent_t stop_k = timed && splits == 1 ? e1 : nullptr;
+    const dim3 grid((unsigned)(tiles * splits));
+    if (BN == 256) {
+        auto kern = gemm_bf16_dma_tn_kernel<256>;
+        if (!attr[0]) {
+            PPO_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds256));
+            attr[0] = true;
+        }
+        if (timed) hipExtLaunchKernelGGL(kern, grid, dim3(512), lds256, ppo::stream(), e0, stop_k, 0, a, slab);
+        else hipLaunchKernelGGL(kern, grid, dim3(512), lds256, ppo::stream(), a, slab);
+    } else {
+        auto kern = gemm_bf16_dma_tn_kernel<128>;
+        if (!attr[1]) {
+            PPO_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds128));
+            attr[1] = true;
+        }
+        if (timed) hipExtLaunchKernelGGL(kern, grid, dim3(512), lds128, ppo::stream(), e0, stop_k, 0, a, slab);
+        else hipLaunchKernelGGL(kern, grid, dim3(512), lds128, ppo::stream(), a, slab);
+    }
+    PPO_LAUNCH_CHECK();
+    if (splits > 1) ppo::slab_reduce(slab, gW, sstride, splits, timed ? e1 : nullptr);
+    return true;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1307,6 +1551,7 @@ void phip_linear16_bwd_w(float* gW, float* gb, const void* g, int tg, const void
         }
         return;
     }
+    if (tg == 1 && tx == 1 && launch_dma_tn(gW, gb, g, x, m, n, l, zeroed)) return;
     const int c = pick16(l, n, OP_TN);
     const int BK = kCfgs[c].bk;
     const long tiles = (long)ppo_divup(l, kCfgs[c].bm) * ppo_divup(n, kCfgs[c].bn);

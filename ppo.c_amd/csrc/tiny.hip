@@ -431,6 +431,359 @@ __global__ __launch_bounds__(TPB) void tiny_update_kernel(TinyArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// The same phase for the Pendulum-shaped networks of C1/C2 (S → H → H → 1, ReLU, B = BB rows), with
+// every width, pitch and LDS offset a compile-time constant: all operand addresses fold into LDS
+// instruction offsets (the generic kernel spends most of its step on 64-bit address arithmetic and
+// clamps), the k-contiguous operands are read as float4 pairs, the 1-wide output layer and the
+// 3-wide input layer's gradient run on the VALU instead of 1/16-occupied MFMA tiles, and the weights
+// stay in their [out][in] layout (pitch H + 4), so no transposed copy is refreshed after each Adam
+// step.  GEMM k-slices: in a 32-k chunk, MFMA u takes k = k0 + 8q + u from lane group q (A and B
+// alike), so a k-contiguous lane reads 8 consecutive floats.
+// Parameters, gradients and Adam moments live in LDS in that padded layout (pads stay zero: a zero
+// gradient leaves a zero parameter unchanged under Adam) and are mapped from / to the flat buffers
+// at the phase's start / end.
+// ---------------------------------------------------------------------------
+template <int S, int H, int BB>
+struct C2Lay {
+    static constexpr int SP = 4, P = H + 4;
+    static_assert(S <= SP && H % 32 == 0 && BB % 32 == 0 && BB * SP <= TPB && H <= 64, "C2 shape");
+    // padded parameter image: W0 [H][SP], b0 [H], W1 [H][P], b1 [H], W2 [H], b2 [4]
+    static constexpr int oW0 = 0, ob0 = oW0 + H * SP, oW1 = ob0 + H, ob1 = oW1 + H * P, oW2 = ob1 + H,
+                         ob2 = oW2 + H, NPAR = ob2 + 4;
+    // flat (reference) layout: W0 [H][S], b0, W1 [H][H], b1, W2 [1][H], b2
+    static constexpr int fb0 = H * S, fW1 = fb0 + H, fb1 = fW1 + H * H, fW2 = fb1 + H, fb2 = fW2 + H,
+                         NFLAT = fb2 + 1;
+    // activations / gradients [BB][P] (X0 [BB][SP]), then rows, targets, old log-probs, actions
+    static constexpr int aX0 = 0, aY1 = aX0 + BB * SP, aY2 = aY1 + BB * P, aG2 = aY2 + BB * P, aG1 = aG2 + BB * P,
+                         aG3 = aG1 + BB * P, aT = aG3 + BB, aMisc = aT + 4 * H, aRes = (aMisc + 4 * BB + 3) & ~3,
+                         TOTAL = aRes + 4 * NPAR;
+    __device__ static int pad_index(int f) {
+        if (f < fb0) return oW0 + (f / S) * SP + f % S;
+        if (f < fW1) return ob0 + (f - fb0);
+        if (f < fb1) return oW1 + ((f - fW1) / H) * P + (f - fW1) % H;
+        if (f < fW2) return ob1 + (f - fb1);
+        if (f < fb2) return oW2 + (f - fW2);
+        return ob2;
+    }
+};
+
+// 16×16 output tile over K (a multiple of 32): A(i, k), B(k, j) — KC: element (r, k) at base[r·PITCH + k]
+// (k-contiguous), else at base[k·PITCH + r]
+template <bool KC, int PITCH>
+__device__ __forceinline__ void c2_fetch(const float* __restrict__ base, int r, int k0, int q, float (&v)[8]) {
+    if constexpr (KC) {
+        const f32x4 x = *reinterpret_cast<const f32x4*>(base + r * PITCH + k0 + 8 * q);
+        const f32x4 y = *reinterpret_cast<const f32x4*>(base + r * PITCH + k0 + 8 * q + 4);
+        v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3]; v[4] = y[0]; v[5] = y[1]; v[6] = y[2]; v[7] = y[3];
+    } else {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = base[(k0 + 8 * q + u) * PITCH + r];
+    }
+}
+template <int K, bool AKC, int PA, bool BKC, int PB>
+__device__ __forceinline__ f32x4 c2_tile(const float* __restrict__ A, int i0, const float* __restrict__ B, int j0,
+                                         int lane) {
+    const int c = lane & 15, q = lane >> 4;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k0 = 0; k0 < K; k0 += 32) {
+        float av[8], bv[8];
+        c2_fetch<AKC, PA>(A, i0 + c, k0, q, av);
+        c2_fetch<BKC, PB>(B, j0 + c, k0, q, bv);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], acc, 0, 0, 0);
+    }
+    return acc;
+}
+
+template <int S, int H, int BB>
+__global__ __launch_bounds__(TPB) void tiny_c2_kernel(TinyArgs a) {
+    using Ly = C2Lay<S, H, BB>;
+    constexpr int P = Ly::P, SP = Ly::SP, NT = (BB / 16) * (H / 16);   // 16×16 tiles of a [BB][H] product
+    extern __shared__ float lds[];
+    float* const X0 = lds + Ly::aX0;
+    float* const Y1 = lds + Ly::aY1;
+    float* const Y2 = lds + Ly::aY2;
+    float* const G2 = lds + Ly::aG2;
+    float* const G1 = lds + Ly::aG1;
+    float* const G3 = lds + Ly::aG3;
+    float* const T = lds + Ly::aT;                        // [4][H] partial sums
+    int* const rows = reinterpret_cast<int*>(lds + Ly::aMisc);
+    float* const tgt = lds + Ly::aMisc + BB;              // value: target; policy: advantage
+    float* const olp = tgt + BB;
+    float* const act = olp + BB;                          // policy: actions (A = 1)
+    float* const Pp = lds + Ly::aRes;
+    float* const Gd = Pp + Ly::NPAR;
+    float* const Mv = Gd + Ly::NPAR;
+    float* const Vv = Mv + Ly::NPAR;
+    __shared__ float red[NWAVES];
+    __shared__ float gls_red[NWAVES];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int c = lane & 15, q = lane >> 4;
+
+    for (int e = tid; e < 4 * Ly::NPAR; e += TPB) Pp[e] = 0.f;     // pads stay zero
+    __syncthreads();
+    for (int f = tid; f < Ly::NFLAT; f += TPB) {
+        const int d = Ly::pad_index(f);
+        Pp[d] = a.params[f];
+        Mv[d] = a.m[f];
+        Vv[d] = a.v[f];
+    }
+    __syncthreads();
+
+    int step = 0;
+    for (int ep = 0; ep < a.n_epochs; ++ep) {
+        for (int kb = 0; kb < a.num_batches && step < a.total_steps; ++kb, ++step) {
+            TINY_STAMP(0);
+            // ---- gather (trajectory_buffer.cu:168-200): SP threads per row ----
+            if (tid < BB * SP) {
+                const int i = tid / SP, k = tid % SP;
+                const int list = (int)(((long)kb * BB + i) % a.limit);
+                const int src = a.perms ? a.perms[(long)ep * a.limit + list]
+                                        : (int)feistel_index((uint32_t)list, a.fk[ep & 15]);
+                X0[i * SP + k] = k < S ? a.state[(long)src * S + k] : 0.f;
+                if (k == 0) {
+                    rows[i] = src;
+                    if (a.policy) {
+                        tgt[i] = a.adv[src];
+                        olp[i] = a.logprob[src];
+                        act[i] = a.action[src];
+                    } else {
+                        tgt[i] = a.adv_target[src];
+                    }
+                }
+            }
+            __syncthreads();
+            TINY_STAMP(1);
+            // ---- forward (neural_network.cu:74-105) ----
+            for (int t = w; t < NT; t += NWAVES) {             // layer 0: K = S < 4, one MFMA
+                const int i0 = (t / (H / 16)) * 16, j0 = (t % (H / 16)) * 16;
+                const float av = q < S ? X0[(i0 + c) * SP + q] : 0.f;
+                const float bv = q < S ? Pp[Ly::oW0 + (j0 + c) * SP + q] : 0.f;
+                const f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+                const float bj = Pp[Ly::ob0 + j0 + c];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float v = acc[e] + bj;
+                    Y1[(i0 + 4 * q + e) * P + j0 + c] = v > 0.f ? v : 0.f;
+                }
+            }
+            __syncthreads();
+            if (a.stamps && tid == 0 && step < 64) a.stamps[64 * 8 + step * 4 + 0] = wall_clock64();
+            for (int t = w; t < NT; t += NWAVES) {             // layer 1: Y1 · W1ᵀ
+                const int i0 = (t / (H / 16)) * 16, j0 = (t % (H / 16)) * 16;
+                const f32x4 acc = c2_tile<H, true, P, true, P>(Y1, i0, Pp + Ly::oW1, j0, lane);
+                const float bj = Pp[Ly::ob1 + j0 + c];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float v = acc[e] + bj;
+                    Y2[(i0 + 4 * q + e) * P + j0 + c] = v > 0.f ? v : 0.f;
+                }
+            }
+            __syncthreads();
+            if (a.stamps && tid == 0 && step < 64) a.stamps[64 * 8 + step * 4 + 1] = wall_clock64();
+            TINY_STAMP(2);
+            // ---- output layer (1 wide, VALU: 16 lanes per row) + head ----
+            float part = 0.f, glsp = 0.f;
+            {
+                constexpr int LPR = TPB / BB;                  // lanes per row (16 at BB = 64)
+                constexpr int KPL = H / LPR;                   // k per lane
+                static_assert(KPL % 4 == 0 && LPR <= 64 && (LPR & (LPR - 1)) == 0, "output layer split");
+                const int i = tid / LPR, pk = tid % LPR;
+                float d = 0.f;
+#pragma unroll
+                for (int k = 0; k < KPL; k += 4) {
+                    const f32x4 x = *reinterpret_cast<const f32x4*>(Y2 + i * P + pk * KPL + k);
+                    const f32x4 wv = *reinterpret_cast<const f32x4*>(Pp + Ly::oW2 + pk * KPL + k);
+                    d += x[0] * wv[0] + x[1] * wv[1] + x[2] * wv[2] + x[3] * wv[3];
+                }
+#pragma unroll
+                for (int o = LPR / 2; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+                if (pk == 0) {
+                    const float y = d + Pp[Ly::ob2];
+                    if (!a.policy) {                           // loss.cu:5-23
+                        const float t = tgt[i], dd = t - y;
+                        part = dd * dd;
+                        G3[i] = 2 * (y - t) / (float)BB;
+                    } else {                                   // ppo.cu:82-107, policy.cu:67-111 (A = 1)
+                        float g;
+                        const float lp = log_prob_row(&y, a.log_std, act + i, 1);
+                        part = surrogate(tgt[i], lp, olp[i], a.eps, BB, &g);
+                        const float e2 = expf(-2 * a.log_std[0]);
+                        const float dd = act[i] - y;
+                        G3[i] = dd * e2 * g;
+                        glsp = (-1 + dd * dd * e2) * g;
+                    }
+                }
+            }
+            part = wave_sum(part);
+            if (a.policy) glsp = wave_sum(glsp);
+            if (lane == 0) {
+                red[w] = part;
+                gls_red[w] = glsp;
+            }
+            __syncthreads();
+            if (a.stamps && tid == 0 && step < 64) a.stamps[64 * 8 + step * 4 + 2] = wall_clock64();
+            if (tid == 0) {
+                float s = 0.f, gl = 0.f;
+                for (int v = 0; v < NWAVES; ++v) { s += red[v]; gl += gls_red[v]; }
+                if (!a.policy) {
+                    atomicAdd(a.stats + 0, s * (1.0f / (float)BB));
+                } else {
+                    const float ent = (float)(0.5 * (1 + log(2 * M_PI))) + a.log_std[0];
+                    atomicAdd(a.stats + 1, -s / BB - a.ent_coeff * ent);
+                    a.log_std_grad[0] = gl + -a.ent_coeff;          // ppo.cu:436-438
+                }
+            }
+            TINY_STAMP(3);
+            // ---- backward (neural_network.cu:121-161) ----
+            // output layer: gW2[k] = Σ_b g[b]·Y2[b][k] (4 row quarters, combined below), gb2 = Σ g,
+            // G2 = (g ⊗ W2) ⊙ 1[Y2 > 0]
+            if (tid < 4 * H) {
+                const int k = tid % H, qq = tid / H;
+                float sacc = 0.f;
+#pragma unroll 4
+                for (int b = qq * (BB / 4); b < (qq + 1) * (BB / 4); ++b) sacc += G3[b] * Y2[b * P + k];
+                T[qq * H + k] = sacc;
+            } else if (tid < 4 * H + 64) {
+                float g = 0.f;
+                for (int b = lane; b < BB; b += 64) g += G3[b];
+                g = wave_sum(g);
+                if (lane == 0) Gd[Ly::ob2] = g;
+            }
+            for (int e = tid; e < BB * H / 4; e += TPB) {
+                const int b = e / (H / 4), k = (e % (H / 4)) * 4;
+                const f32x4 y = *reinterpret_cast<const f32x4*>(Y2 + b * P + k);
+                const f32x4 wv = *reinterpret_cast<const f32x4*>(Pp + Ly::oW2 + k);
+                const float g = G3[b];
+                f32x4 o;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) o[u] = y[u] > 0.f ? g * wv[u] : 0.f;
+                *reinterpret_cast<f32x4*>(G2 + b * P + k) = o;
+            }
+            __syncthreads();
+            // hidden layer 1: gW1 = G2ᵀ·Y1, gx = (G2·W1) ⊙ 1[Y1 > 0], gb1 = Σ_b G2; gW2 combined
+            for (int t = w; t < 2 * NT; t += NWAVES) {
+                if (t < NT) {                                   // gW1[j][k]: A(j, b) = G2, B(b, k) = Y1
+                    const int i0 = (t / (H / 16)) * 16, j0 = (t % (H / 16)) * 16;
+                    const f32x4 acc = c2_tile<BB, false, P, false, P>(G2, i0, Y1, j0, lane);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) Gd[Ly::oW1 + (i0 + 4 * q + e) * P + j0 + c] = acc[e];
+                } else {                                        // G1[b][k]: A(b, j) = G2, B(j, k) = W1
+                    const int tt = t - NT;
+                    const int i0 = (tt / (H / 16)) * 16, j0 = (tt % (H / 16)) * 16;
+                    const f32x4 acc = c2_tile<H, true, P, false, P>(G2, i0, Pp + Ly::oW1, j0, lane);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int b = i0 + 4 * q + e, k = j0 + c;
+                        G1[b * P + k] = Y1[b * P + k] > 0.f ? acc[e] : 0.f;
+                    }
+                }
+            }
+            if (tid < H) {
+                float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll 4
+                for (int b = 0; b < BB; b += 4) {
+                    s0 += G2[b * P + tid];
+                    s1 += G2[(b + 1) * P + tid];
+                    s2 += G2[(b + 2) * P + tid];
+                    s3 += G2[(b + 3) * P + tid];
+                }
+                Gd[Ly::ob1 + tid] = (s0 + s1) + (s2 + s3);
+                Gd[Ly::oW2 + tid] = (T[tid] + T[H + tid]) + (T[2 * H + tid] + T[3 * H + tid]);
+            }
+            __syncthreads();
+            // layer 0: gW0[j][k] = Σ_b G1[b][j]·X0[b][k] (4 lanes per output), gb0 = Σ_b G1
+            if (tid < 4 * H * S) {
+                const int o = tid >> 2, pr = tid & 3;
+                const int j = o / S, k = o % S;
+                float sacc = 0.f;
+#pragma unroll 4
+                for (int b = pr * (BB / 4); b < (pr + 1) * (BB / 4); ++b) sacc += G1[b * P + j] * X0[b * SP + k];
+                sacc += __shfl_xor(sacc, 1, 64);
+                sacc += __shfl_xor(sacc, 2, 64);
+                if (pr == 0) Gd[Ly::oW0 + j * SP + k] = sacc;
+            } else if (tid >= 4 * H * S && tid < 4 * H * S + H) {
+                const int j = tid - 4 * H * S;
+                float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll 4
+                for (int b = 0; b < BB; b += 4) {
+                    s0 += G1[b * P + j];
+                    s1 += G1[(b + 1) * P + j];
+                    s2 += G1[(b + 2) * P + j];
+                    s3 += G1[(b + 3) * P + j];
+                }
+                Gd[Ly::ob0 + j] = (s0 + s1) + (s2 + s3);
+            }
+            __threadfence_block();
+            __syncthreads();
+            TINY_STAMP(4);
+            // ---- Adam: entropy (log σ) first, then the network (ppo.cu:440-442) ----
+            if (a.policy && tid == 0) {
+                float p = a.log_std[0], mm = a.m_ls[0], vv = a.v_ls[0];
+                adam_elem(p, a.log_std_grad[0], mm, vv, a.steps_ls[2 * step], a.b1, a.b2, a.steps_ls[2 * step + 1]);
+                a.log_std[0] = p; a.m_ls[0] = mm; a.v_ls[0] = vv;
+            }
+            const float st = a.steps[2 * step], bc2 = a.steps[2 * step + 1];
+            for (int e = 4 * tid; e < Ly::NPAR; e += 4 * TPB) {
+                f32x4 p = *reinterpret_cast<const f32x4*>(Pp + e);
+                const f32x4 g = *reinterpret_cast<const f32x4*>(Gd + e);
+                f32x4 mm = *reinterpret_cast<const f32x4*>(Mv + e);
+                f32x4 vv = *reinterpret_cast<const f32x4*>(Vv + e);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    float pu = p[u], mu = mm[u], vu = vv[u];
+                    adam_elem(pu, g[u], mu, vu, st, a.b1, a.b2, bc2);
+                    p[u] = pu; mm[u] = mu; vv[u] = vu;
+                }
+                *reinterpret_cast<f32x4*>(Pp + e) = p;
+                *reinterpret_cast<f32x4*>(Mv + e) = mm;
+                *reinterpret_cast<f32x4*>(Vv + e) = vv;
+            }
+            __threadfence_block();
+            __syncthreads();
+            TINY_STAMP(5);
+        }
+    }
+    for (int f = tid; f < Ly::NFLAT; f += TPB) {
+        const int d = Ly::pad_index(f);
+        a.params[f] = Pp[d];
+        a.grads[f] = Gd[d];
+        a.m[f] = Mv[d];
+        a.v[f] = Vv[d];
+    }
+}
+
+void print_stamps(const TinyArgs& a, const PhipTinyPhase* ph) {
+    if (!a.stamps) return;
+    {                      // diagnostics: mean µs per phase over steps 1..63
+        unsigned long long h[64 * 12];
+        phip_d2h(h, a.stamps, sizeof(h));
+        int dev = 0, khz = 0;
+        PPO_CHECK(hipGetDevice(&dev));
+        PPO_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+        const double mhz = khz > 0 ? khz / 1000.0 : 100.0;     // wall_clock64() ticks per µs
+        fprintf(stderr, "tiny: wall clock %.1f MHz\n", mhz);
+        double acc[5] = {0, 0, 0, 0, 0};
+        int n = 0;
+        for (int st = 1; st < 64 && st < a.total_steps; ++st, ++n)
+            for (int k = 0; k < 5; ++k) acc[k] += (double)(h[st * 8 + k + 1] - h[st * 8 + k]) / mhz;
+        const double clk = (double)(h[63 * 8 + 6] - h[1 * 8 + 6]) / ((double)(h[63 * 8] - h[1 * 8]) / mhz);
+        if (n) fprintf(stderr, "tiny: shader clock %.0f MHz\n", clk);
+        double fl[3] = {0, 0, 0};
+        for (int st = 1; st < 64 && st < a.total_steps; ++st) {
+            fl[0] += (double)(h[512 + st * 4 + 0] - h[st * 8 + 1]) / mhz;
+            fl[1] += (double)(h[512 + st * 4 + 1] - h[512 + st * 4 + 0]) / mhz;
+            fl[2] += (double)(h[512 + st * 4 + 2] - h[512 + st * 4 + 1]) / mhz;
+        }
+        if (n) fprintf(stderr, "tiny: forward layers (us): %.2f %.2f %.2f\n", fl[0] / n, fl[1] / n, fl[2] / n);
+        if (n)
+            fprintf(stderr, "tiny %s step phases (us): gather %.2f fwd %.2f head %.2f bwd %.2f adam %.2f\n",
+                    ph->policy ? "policy" : "value", acc[0] / n, acc[1] / n, acc[2] / n, acc[3] / n, acc[4] / n);
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -485,6 +838,36 @@ int phip_tiny_update(const PhipTinyNet* net, const PhipTinyPhase* ph) {
     a.steps = ph->steps; a.steps_ls = ph->steps_ls;
     a.b1 = ph->b1; a.b2 = ph->b2; a.eps = ph->eps; a.ent_coeff = ph->ent_coeff;
     a.stats = ph->stats;
+    static unsigned long long* stamps = nullptr;
+    if (getenv("PPO_TINY_STAMPS")) {
+        if (!stamps) stamps = (unsigned long long*)phip_malloc(sizeof(unsigned long long) * 64 * 12);
+        a.stamps = stamps;
+    }
+    // C1/C2 shape (3 → 64 → 64 → 1, ReLU, B = 64, the flat reference layout): the specialised kernel
+    {
+        using Ly = C2Lay<3, 64, 64>;
+        const bool shape = net->L == 3 && net->sizes[0] == 3 && net->sizes[1] == 64 && net->sizes[2] == 64 &&
+                           net->sizes[3] == 1 && net->relu[0] && net->relu[1] && !net->relu[2] && ph->B == 64;
+        const bool layout = net->woff[0] == 0 && net->boff[0] == Ly::fb0 && net->woff[1] == Ly::fW1 &&
+                            net->boff[1] == Ly::fb1 && net->woff[2] == Ly::fW2 && net->boff[2] == Ly::fb2 &&
+                            net->span == Ly::NFLAT;
+        if (shape && layout && !getenv("PPO_TINY_GENERIC")) {
+            const size_t bytes = sizeof(float) * (size_t)Ly::TOTAL;
+            static_assert(sizeof(float) * (size_t)Ly::TOTAL <= 160 * 1024 - 1024, "tiny C2: LDS");
+            if (ph->n_epochs <= 0 || ph->num_batches <= 0) return 0;     // fit check only
+            auto kfn = tiny_c2_kernel<3, 64, 64>;
+            static bool attr = false;
+            if (!attr) {
+                PPO_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+                attr = true;
+            }
+            ppo::ProfScope ps(PPO_K_OTHER, 0.0);
+            hipLaunchKernelGGL(kfn, dim3(1), dim3(TPB), bytes, ppo::stream(), a);
+            PPO_LAUNCH_CHECK();
+            print_stamps(a, ph);
+            return 0;
+        }
+    }
     // LDS: activations [B][w+1] (odd pitch: conflict-free column reads), two gradient buffers, misc
     int off = 0;
     for (int l = 0; l <= net->L; ++l) {
@@ -509,40 +892,11 @@ int phip_tiny_update(const PhipTinyNet* net, const PhipTinyPhase* ph) {
     if (ph->n_epochs <= 0 || ph->num_batches <= 0) return 0;     // fit check only
     const void* kfn = resident ? (const void*)tiny_update_kernel<true> : (const void*)tiny_update_kernel<false>;
     PPO_CHECK(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
-    static unsigned long long* stamps = nullptr;
-    if (getenv("PPO_TINY_STAMPS")) {
-        if (!stamps) stamps = (unsigned long long*)phip_malloc(sizeof(unsigned long long) * 64 * 12);
-        a.stamps = stamps;
-    }
     ppo::ProfScope ps(PPO_K_OTHER, 0.0);
     if (resident) hipLaunchKernelGGL(tiny_update_kernel<true>, dim3(1), dim3(TPB), bytes, ppo::stream(), a);
     else hipLaunchKernelGGL(tiny_update_kernel<false>, dim3(1), dim3(TPB), bytes, ppo::stream(), a);
     PPO_LAUNCH_CHECK();
-    if (a.stamps) {                      // diagnostics: mean µs per phase over steps 1..63
-        unsigned long long h[64 * 12];
-        phip_d2h(h, a.stamps, sizeof(h));
-        int dev = 0, khz = 0;
-        PPO_CHECK(hipGetDevice(&dev));
-        PPO_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
-        const double mhz = khz > 0 ? khz / 1000.0 : 100.0;     // wall_clock64() ticks per µs
-        fprintf(stderr, "tiny: wall clock %.1f MHz\n", mhz);
-        double acc[5] = {0, 0, 0, 0, 0};
-        int n = 0;
-        for (int st = 1; st < 64 && st < a.total_steps; ++st, ++n)
-            for (int k = 0; k < 5; ++k) acc[k] += (double)(h[st * 8 + k + 1] - h[st * 8 + k]) / mhz;
-        const double clk = (double)(h[63 * 8 + 6] - h[1 * 8 + 6]) / ((double)(h[63 * 8] - h[1 * 8]) / mhz);
-        if (n) fprintf(stderr, "tiny: shader clock %.0f MHz\n", clk);
-        double fl[3] = {0, 0, 0};
-        for (int st = 1; st < 64 && st < a.total_steps; ++st) {
-            fl[0] += (double)(h[512 + st * 4 + 0] - h[st * 8 + 1]) / mhz;
-            fl[1] += (double)(h[512 + st * 4 + 1] - h[512 + st * 4 + 0]) / mhz;
-            fl[2] += (double)(h[512 + st * 4 + 2] - h[512 + st * 4 + 1]) / mhz;
-        }
-        if (n) fprintf(stderr, "tiny: forward layers (us): %.2f %.2f %.2f\n", fl[0] / n, fl[1] / n, fl[2] / n);
-        if (n)
-            fprintf(stderr, "tiny %s step phases (us): gather %.2f fwd %.2f head %.2f bwd %.2f adam %.2f\n",
-                    ph->policy ? "policy" : "value", acc[0] / n, acc[1] / n, acc[2] / n, acc[3] / n, acc[4] / n);
-    }
+    print_stamps(a, ph);
     return 0;
 }
 

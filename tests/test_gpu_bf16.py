@@ -200,3 +200,38 @@ def test_bf16_dma_matches_register_staged(lib, sizes, m):
     np.testing.assert_array_equal(out[1][0], out[0][0])
     # grad_W accumulates split-K partials with f32 atomics (arrival order varies run to run)
     close(out[1][1], out[0][1], 1e-5, "grads, DMA vs register-staged")
+
+
+@pytest.mark.parametrize("sizes,m", [([1024, 1024, 1024, 1024, 17], 4096), ([1024, 1024, 1024, 17], 1024),
+                                     ([384, 384, 512, 256, 1], 2048), ([1024, 1024, 1024, 17], 16384)])
+def test_bf16_dma_tn_grad_w(lib, oracle, sizes, m):
+    """grad_W on the LDS-DMA TN tile (gemm_bf16_dma_tn_kernel: both operands by hardware-transposed
+    reads, split partials summed by the slab reduce, bias from the g image) — the automatic choice
+    for bf16 g and x with l % 256 = 0, n % 128 = 0 (256- and 128-wide tiles here) — against the bf16
+    emulation (2e-3·max|ref|, the file's bar, up to 2048 rows) and against the register-staged kernel (DMA off): the
+    same rounded products, summed in another order (1e-4·max|ref|)."""
+    rng = np.random.default_rng(sum(sizes) + m)
+    names = ["relu"] * (len(sizes) - 2) + ["none"]
+    nn = lib.create_neural_network(ppo_ffi.c_ints(sizes), ppo_ffi.c_strings(names), len(sizes))
+    params = (rng.uniform(-1, 1, oracle.mlp_num_params(sizes)) * (1.0 / np.sqrt(max(sizes)))).astype(F32)
+    nn_set_params_packed(lib, nn, params)
+    assert lib.nn_set_compute_dtype(nn, 1) == 0
+    x = rng.uniform(-1, 1, (m, sizes[0])).astype(F32)
+    gout = rng.uniform(-1, 1, (m, sizes[-1])).astype(F32)
+    _, g_emu = emulate(sizes, params, x, gout)
+    dx, dgo = dev(lib, x), dev(lib, gout)
+    out = {}
+    old = lib.ppo_gemm16_dma(-1)
+    try:
+        lib.ppo_gemm16_tune(-1)
+        for on in (1, 0):
+            lib.ppo_gemm16_dma(on)
+            lib.forward_propagation_cuda(nn, dx.ptr, m)
+            lib.backward_propagation_cuda(nn, dgo.ptr, m)
+            out[on] = nn_grads_packed(lib, nn)
+    finally:
+        lib.ppo_gemm16_dma(old)
+        lib.free_neural_network(nn)
+    if m <= 2048:      # deeper / longer: hidden bf16 rounding flips compound against the emulation
+        close(out[1], g_emu, 2e-3, "grads (DMA TN) vs bf16 emulation")
+    close(out[1], out[0], 1e-4, "grads, DMA TN vs register-staged")

@@ -90,3 +90,31 @@ def test_tiny_full_update_c2(lib, oracle, shuffle):
         cos = float(a[k] @ b[k] / (np.linalg.norm(a[k]) * np.linalg.norm(b[k])))
         assert cos > 0.95, (k, cos)
         assert abs(np.linalg.norm(a[k]) / np.linalg.norm(b[k]) - 1) < 0.1, k
+
+
+@pytest.mark.parametrize("shuffle", [0, 1])
+def test_tiny_c2_kernel_matches_generic(lib, oracle, shuffle, monkeypatch):
+    """The compile-time C2 kernel (tiny_c2_kernel: padded LDS weight image, VALU output layer) against the
+    generic single-workgroup kernel (PPO_TINY_GENERIC=1): one value and one policy step (the same
+    gradients within the fp32 GEMM tolerance, Adam deltas within two steps' worth), then 16 + 16 steps."""
+    sizes, N, B = [3, 64, 64, 1], 1024, 64
+    for n_pol, n_val in ((0, 1), (1, 0), (1, 4)):
+        monkeypatch.delenv("PPO_TINY_GENERIC", raising=False)
+        a = run(lib, oracle, sizes, N, B, n_pol, n_val, shuffle, tiny=True)
+        monkeypatch.setenv("PPO_TINY_GENERIC", "1")
+        b = run(lib, oracle, sizes, N, B, n_pol, n_val, shuffle, tiny=True)
+        monkeypatch.delenv("PPO_TINY_GENERIC", raising=False)
+        assert a["t"] == b["t"] and a["next_rand"] == b["next_rand"]
+        if n_val == 4:                                   # 64 + 16 steps: the trajectories stay together
+            np.testing.assert_allclose(a["stats"], b["stats"], rtol=2e-2, atol=1e-6)
+            for k in ("dv", "dmu"):
+                cos = float(a[k] @ b[k] / (np.linalg.norm(a[k]) * np.linalg.norm(b[k])))
+                assert cos > 0.99, (k, cos)
+            continue
+        np.testing.assert_allclose(a["stats"], b["stats"], rtol=2e-4, atol=1e-6)
+        assert_gemm_close(a["gv"], b["gv"], B, "value grads")
+        assert_gemm_close(a["gmu"], b["gmu"], B, "policy grads")
+        lr = 3e-4
+        for k in ("v", "mu", "ls"):
+            err = np.abs(a[k] - b[k])
+            assert err.max() <= 2 * lr * 1.0001 + 1e-7, (k, err.max())
