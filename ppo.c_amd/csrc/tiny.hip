@@ -435,18 +435,18 @@ __global__ __launch_bounds__(TPB) void tiny_update_kernel(TinyArgs a) {
 // The same phase for the Pendulum-shaped networks of C1/C2 (S → H → H → 1, ReLU, B = BB rows), with
 // every width, pitch and LDS offset a compile-time constant: all operand addresses fold into LDS
 // instruction offsets (the generic kernel spends most of its step on 64-bit address arithmetic and
-// clamps), the k-contiguous operands are read as float4 pairs, the 1-wide output layer and the
-// 3-wide input layer's gradient run on the VALU instead of 1/16-occupied MFMA tiles, and the weights
-// stay in their [out][in] layout (pitch H + 4), so no transposed copy is refreshed after each Adam
-// step.  GEMM k-slices: in a 32-k chunk, MFMA u takes k = k0 + 8q + u from lane group q (A and B
-// alike), so a k-contiguous lane reads 8 consecutive floats.
-// Parameters, gradients and Adam moments live in LDS in that padded layout (pads stay zero: a zero
-// gradient leaves a zero parameter unchanged under Adam) and are mapped from / to the flat buffers
-// at the phase's start / end.
-// ---------------------------------------------------------------------------
+// clamps), the 1-wide output layer and the 3-wide input layer's weight gradient run on the VALU
+// instead of 1/16-occupied MFMA tiles, and the weights stay in their [out][in] layout (pitch H + 2),
+// so no transposed copy is refreshed after each Adam step.  The hidden GEMMs keep the generic
+// kernel's k order (MFMA u of a 32-k chunk takes k = k0 + 4u + q from lane group q), so both kernels
+// round every hidden pre-activation alike (a different order can flip a ReLU mask at z ≈ 0).
+// Pitch H + 2 ≡ 2 (mod 32): a k-contiguous read (rows c, k = .. + q) is conflict-free, a k-strided
+// one 2-way.  Parameters, gradients and Adam moments live in LDS in that padded layout (pads stay
+// zero: a zero gradient leaves a zero parameter unchanged under Adam) and are mapped from / to the
+// flat buffers at the phase's start / end.
 template <int S, int H, int BB>
 struct C2Lay {
-    static constexpr int SP = 4, P = H + 4;
+    static constexpr int SP = 4, P = H + 2;
     static_assert(S <= SP && H % 32 == 0 && BB % 32 == 0 && BB * SP <= TPB && H <= 64, "C2 shape");
     // padded parameter image: W0 [H][SP], b0 [H], W1 [H][P], b1 [H], W2 [H], b2 [4]
     static constexpr int oW0 = 0, ob0 = oW0 + H * SP, oW1 = ob0 + H, ob1 = oW1 + H * P, oW2 = ob1 + H,
@@ -469,17 +469,11 @@ struct C2Lay {
 };
 
 // 16×16 output tile over K (a multiple of 32): A(i, k), B(k, j) — KC: element (r, k) at base[r·PITCH + k]
-// (k-contiguous), else at base[k·PITCH + r]
+// (k-contiguous), else at base[k·PITCH + r]; lane group q holds k = k0 + 4u + q for MFMA u
 template <bool KC, int PITCH>
 __device__ __forceinline__ void c2_fetch(const float* __restrict__ base, int r, int k0, int q, float (&v)[8]) {
-    if constexpr (KC) {
-        const f32x4 x = *reinterpret_cast<const f32x4*>(base + r * PITCH + k0 + 8 * q);
-        const f32x4 y = *reinterpret_cast<const f32x4*>(base + r * PITCH + k0 + 8 * q + 4);
-        v[0] = x[0]; v[1] = x[1]; v[2] = x[2]; v[3] = x[3]; v[4] = y[0]; v[5] = y[1]; v[6] = y[2]; v[7] = y[3];
-    } else {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = base[(k0 + 8 * q + u) * PITCH + r];
-    }
+    for (int u = 0; u < 8; ++u) v[u] = KC ? base[r * PITCH + k0 + 4 * u + q] : base[(k0 + 4 * u + q) * PITCH + r];
 }
 template <int K, bool AKC, int PA, bool BKC, int PB>
 __device__ __forceinline__ f32x4 c2_tile(const float* __restrict__ A, int i0, const float* __restrict__ B, int j0,
@@ -497,18 +491,31 @@ __device__ __forceinline__ f32x4 c2_tile(const float* __restrict__ A, int i0, co
     return acc;
 }
 
+// 16-lane group sum (lanes l, l^1, …, l^8: one row-slice group of a wave)
+__device__ __forceinline__ float sum16(float v) {
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Per step: forward layer 0 | layer 1 | output layer + head + the output layer's grad_x | hidden-layer
+// gW1 / grad_x tiles with the bias / output-layer column sums | layer-0 weight + bias gradients |
+// Adam with the next minibatch's gather in flight — six barriers.  Measured A/B of the alternatives
+// (profiles/r03_c2_kernel_ab.txt): the next gather inside the Adam phase −0.3 ms per C2 update, the
+// output layer's grad_x inside the head phase −1.2 ms; layer 0 recomputed per wave instead of a
+// barrier +0.5 ms; interleaving the two hidden-layer MFMA chains of a wave ±0.
 template <int S, int H, int BB>
 __global__ __launch_bounds__(TPB) void tiny_c2_kernel(TinyArgs a) {
     using Ly = C2Lay<S, H, BB>;
-    constexpr int P = Ly::P, SP = Ly::SP, NT = (BB / 16) * (H / 16);   // 16×16 tiles of a [BB][H] product
+    constexpr int P = Ly::P, SP = Ly::SP, HT = H / 16;
+    static_assert((BB / 16) * HT == NWAVES && BB == H && TPB / BB == 16 && S < SP, "C2 phase split");
     extern __shared__ float lds[];
-    float* const X0 = lds + Ly::aX0;
+    float* const X0 = lds + Ly::aX0;                      // [BB][SP]; column S holds 1 (bias gradient)
     float* const Y1 = lds + Ly::aY1;
     float* const Y2 = lds + Ly::aY2;
     float* const G2 = lds + Ly::aG2;
     float* const G1 = lds + Ly::aG1;
     float* const G3 = lds + Ly::aG3;
-    float* const T = lds + Ly::aT;                        // [4][H] partial sums
     int* const rows = reinterpret_cast<int*>(lds + Ly::aMisc);
     float* const tgt = lds + Ly::aMisc + BB;              // value: target; policy: advantage
     float* const olp = tgt + BB;
@@ -519,8 +526,11 @@ __global__ __launch_bounds__(TPB) void tiny_c2_kernel(TinyArgs a) {
     float* const Vv = Mv + Ly::NPAR;
     __shared__ float red[NWAVES];
     __shared__ float gls_red[NWAVES];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    __shared__ float s_ls, s_lsg, s_mls, s_vls;           // policy: log σ (A = 1), its gradient and moments
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform values in SGPRs
     const int c = lane & 15, q = lane >> 4;
+    const int ti0 = (w / HT) * 16, tj0 = (w % HT) * 16;  // this wave's 16×16 tile
 
     for (int e = tid; e < 4 * Ly::NPAR; e += TPB) Pp[e] = 0.f;     // pads stay zero
     __syncthreads();
@@ -530,92 +540,113 @@ __global__ __launch_bounds__(TPB) void tiny_c2_kernel(TinyArgs a) {
         Mv[d] = a.m[f];
         Vv[d] = a.v[f];
     }
+    if (tid == 0 && a.policy) s_ls = a.log_std[0];
+    if (tid == 0 && a.policy) { s_mls = a.m_ls[0]; s_vls = a.v_ls[0]; }
+
+    // gather of minibatch (ep, kb) (trajectory_buffer.cu:168-200): SP threads per row; the loads
+    // (fetch) are issued before the Adam pass, the LDS stores (put) after it
+    struct Row { float x, t, o, ac; int src; };
+    constexpr int G0 = TPB - BB * SP;                    // gather threads: the last BB·SP (one Adam
+    const int gt = tid - G0;                             // float4 each, the first ones take two)
+    auto fetch = [&](int ep, int kb) {
+        Row r{0.f, 0.f, 0.f, 0.f, 0};
+        const int i = gt / SP, k = gt % SP;
+        const int list = (int)(((long)kb * BB + i) % a.limit);
+        r.src = a.perms ? a.perms[(long)ep * a.limit + list] : (int)feistel_index((uint32_t)list, a.fk[ep & 15]);
+        r.x = k < S ? a.state[(long)r.src * S + k] : (k == S ? 1.f : 0.f);
+        if (k == 0) {
+            if (a.policy) {
+                r.t = a.adv[r.src];
+                r.o = a.logprob[r.src];
+                r.ac = a.action[r.src];
+            } else {
+                r.t = a.adv_target[r.src];
+            }
+        }
+        return r;
+    };
+    auto put = [&](const Row& r) {
+        const int i = gt / SP, k = gt % SP;
+        X0[i * SP + k] = r.x;
+        if (k == 0) {
+            rows[i] = r.src;
+            tgt[i] = r.t;
+            if (a.policy) { olp[i] = r.o; act[i] = r.ac; }
+        }
+    };
+    if (gt >= 0 && a.total_steps > 0) put(fetch(0, 0));
     __syncthreads();
 
     int step = 0;
     for (int ep = 0; ep < a.n_epochs; ++ep) {
         for (int kb = 0; kb < a.num_batches && step < a.total_steps; ++kb, ++step) {
             TINY_STAMP(0);
-            // ---- gather (trajectory_buffer.cu:168-200): SP threads per row ----
-            if (tid < BB * SP) {
-                const int i = tid / SP, k = tid % SP;
-                const int list = (int)(((long)kb * BB + i) % a.limit);
-                const int src = a.perms ? a.perms[(long)ep * a.limit + list]
-                                        : (int)feistel_index((uint32_t)list, a.fk[ep & 15]);
-                X0[i * SP + k] = k < S ? a.state[(long)src * S + k] : 0.f;
-                if (k == 0) {
-                    rows[i] = src;
-                    if (a.policy) {
-                        tgt[i] = a.adv[src];
-                        olp[i] = a.logprob[src];
-                        act[i] = a.action[src];
-                    } else {
-                        tgt[i] = a.adv_target[src];
-                    }
-                }
-            }
-            __syncthreads();
             TINY_STAMP(1);
             // ---- forward (neural_network.cu:74-105) ----
-            for (int t = w; t < NT; t += NWAVES) {             // layer 0: K = S < 4, one MFMA
-                const int i0 = (t / (H / 16)) * 16, j0 = (t % (H / 16)) * 16;
-                const float av = q < S ? X0[(i0 + c) * SP + q] : 0.f;
-                const float bv = q < S ? Pp[Ly::oW0 + (j0 + c) * SP + q] : 0.f;
+            {                                                  // layer 0: K = S < 4, one MFMA
+                const float av = q < S ? X0[(ti0 + c) * SP + q] : 0.f;
+                const float bv = q < S ? Pp[Ly::oW0 + (tj0 + c) * SP + q] : 0.f;
                 const f32x4 acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-                const float bj = Pp[Ly::ob0 + j0 + c];
+                const float bj = Pp[Ly::ob0 + tj0 + c];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const float v = acc[e] + bj;
-                    Y1[(i0 + 4 * q + e) * P + j0 + c] = v > 0.f ? v : 0.f;
+                    Y1[(ti0 + 4 * q + e) * P + tj0 + c] = v > 0.f ? v : 0.f;
                 }
             }
             __syncthreads();
             if (a.stamps && tid == 0 && step < 64) a.stamps[64 * 8 + step * 4 + 0] = wall_clock64();
-            for (int t = w; t < NT; t += NWAVES) {             // layer 1: Y1 · W1ᵀ
-                const int i0 = (t / (H / 16)) * 16, j0 = (t % (H / 16)) * 16;
-                const f32x4 acc = c2_tile<H, true, P, true, P>(Y1, i0, Pp + Ly::oW1, j0, lane);
-                const float bj = Pp[Ly::ob1 + j0 + c];
+            {                                                  // layer 1: Y1 · W1ᵀ
+                const f32x4 acc = c2_tile<H, true, P, true, P>(Y1, ti0, Pp + Ly::oW1, tj0, lane);
+                const float bj = Pp[Ly::ob1 + tj0 + c];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const float v = acc[e] + bj;
-                    Y2[(i0 + 4 * q + e) * P + j0 + c] = v > 0.f ? v : 0.f;
+                    Y2[(ti0 + 4 * q + e) * P + tj0 + c] = v > 0.f ? v : 0.f;
                 }
             }
             __syncthreads();
             if (a.stamps && tid == 0 && step < 64) a.stamps[64 * 8 + step * 4 + 1] = wall_clock64();
             TINY_STAMP(2);
-            // ---- output layer (1 wide, VALU: 16 lanes per row) + head ----
+            // ---- output layer (1 wide, VALU: 16 lanes per row), head, and the output layer's grad_x
+            // G2[i] = (g_i ⊗ W2) ⊙ 1[Y2 > 0] by the row's own lanes ----
             float part = 0.f, glsp = 0.f;
             {
-                constexpr int LPR = TPB / BB;                  // lanes per row (16 at BB = 64)
-                constexpr int KPL = H / LPR;                   // k per lane
-                static_assert(KPL % 4 == 0 && LPR <= 64 && (LPR & (LPR - 1)) == 0, "output layer split");
-                const int i = tid / LPR, pk = tid % LPR;
+                constexpr int KPL = H / 16;
+                const int i = tid >> 4, pk = tid & 15;
+                float2 yv[KPL / 2], wv[KPL / 2];
                 float d = 0.f;
 #pragma unroll
-                for (int k = 0; k < KPL; k += 4) {
-                    const f32x4 x = *reinterpret_cast<const f32x4*>(Y2 + i * P + pk * KPL + k);
-                    const f32x4 wv = *reinterpret_cast<const f32x4*>(Pp + Ly::oW2 + pk * KPL + k);
-                    d += x[0] * wv[0] + x[1] * wv[1] + x[2] * wv[2] + x[3] * wv[3];
+                for (int h = 0; h < KPL / 2; ++h) {
+                    yv[h] = *reinterpret_cast<const float2*>(Y2 + i * P + pk * KPL + 2 * h);
+                    wv[h] = *reinterpret_cast<const float2*>(Pp + Ly::oW2 + pk * KPL + 2 * h);
+                    d += yv[h].x * wv[h].x + yv[h].y * wv[h].y;
                 }
-#pragma unroll
-                for (int o = LPR / 2; o > 0; o >>= 1) d += __shfl_xor(d, o, 64);
+                d = sum16(d);
+                float g = 0.f;
                 if (pk == 0) {
                     const float y = d + Pp[Ly::ob2];
                     if (!a.policy) {                           // loss.cu:5-23
                         const float t = tgt[i], dd = t - y;
                         part = dd * dd;
-                        G3[i] = 2 * (y - t) / (float)BB;
+                        g = 2 * (y - t) / (float)BB;
                     } else {                                   // ppo.cu:82-107, policy.cu:67-111 (A = 1)
-                        float g;
-                        const float lp = log_prob_row(&y, a.log_std, act + i, 1);
-                        part = surrogate(tgt[i], lp, olp[i], a.eps, BB, &g);
-                        const float e2 = expf(-2 * a.log_std[0]);
+                        float gl;
+                        const float ls = s_ls;
+                        const float lp = log_prob_row(&y, &ls, act + i, 1);
+                        part = surrogate(tgt[i], lp, olp[i], a.eps, BB, &gl);
+                        const float e2 = expf(-2 * ls);
                         const float dd = act[i] - y;
-                        G3[i] = dd * e2 * g;
-                        glsp = (-1 + dd * dd * e2) * g;
+                        g = dd * e2 * gl;
+                        glsp = (-1 + dd * dd * e2) * gl;
                     }
+                    G3[i] = g;
                 }
+                g = __shfl(g, lane & ~15, 64);
+#pragma unroll
+                for (int h = 0; h < KPL / 2; ++h)
+                    *reinterpret_cast<float2*>(G2 + i * P + pk * KPL + 2 * h) =
+                        float2{yv[h].x > 0.f ? g * wv[h].x : 0.f, yv[h].y > 0.f ? g * wv[h].y : 0.f};
             }
             part = wave_sum(part);
             if (a.policy) glsp = wave_sum(glsp);
@@ -625,105 +656,93 @@ __global__ __launch_bounds__(TPB) void tiny_c2_kernel(TinyArgs a) {
             }
             __syncthreads();
             if (a.stamps && tid == 0 && step < 64) a.stamps[64 * 8 + step * 4 + 2] = wall_clock64();
-            if (tid == 0) {
-                float s = 0.f, gl = 0.f;
-                for (int v = 0; v < NWAVES; ++v) { s += red[v]; gl += gls_red[v]; }
-                if (!a.policy) {
-                    atomicAdd(a.stats + 0, s * (1.0f / (float)BB));
-                } else {
-                    const float ent = (float)(0.5 * (1 + log(2 * M_PI))) + a.log_std[0];
-                    atomicAdd(a.stats + 1, -s / BB - a.ent_coeff * ent);
-                    a.log_std_grad[0] = gl + -a.ent_coeff;          // ppo.cu:436-438
-                }
-            }
             TINY_STAMP(3);
-            // ---- backward (neural_network.cu:121-161) ----
-            // output layer: gW2[k] = Σ_b g[b]·Y2[b][k] (4 row quarters, combined below), gb2 = Σ g,
-            // G2 = (g ⊗ W2) ⊙ 1[Y2 > 0]
-            if (tid < 4 * H) {
-                const int k = tid % H, qq = tid / H;
-                float sacc = 0.f;
-#pragma unroll 4
-                for (int b = qq * (BB / 4); b < (qq + 1) * (BB / 4); ++b) sacc += G3[b] * Y2[b * P + k];
-                T[qq * H + k] = sacc;
-            } else if (tid < 4 * H + 64) {
-                float g = 0.f;
-                for (int b = lane; b < BB; b += 64) g += G3[b];
-                g = wave_sum(g);
-                if (lane == 0) Gd[Ly::ob2] = g;
-            }
-            for (int e = tid; e < BB * H / 4; e += TPB) {
-                const int b = e / (H / 4), k = (e % (H / 4)) * 4;
-                const f32x4 y = *reinterpret_cast<const f32x4*>(Y2 + b * P + k);
-                const f32x4 wv = *reinterpret_cast<const f32x4*>(Pp + Ly::oW2 + k);
-                const float g = G3[b];
-                f32x4 o;
+            // ---- backward (neural_network.cu:121-161), hidden layer 1: this wave's gW1 = G2ᵀ·Y1 and
+            // G1 = (G2·W1) ⊙ 1[Y1 > 0] tiles; columns 4w .. 4w+3 of gb1 = Σ_b G2 and gW2 = Σ_b g·Y2
+            // (16 row slices of 4 per column, lanes 16s + col); gb2 and the loss sums by wave 15 ----
+            {
+                const f32x4 aw = c2_tile<BB, false, P, false, P>(G2, ti0, Y1, tj0, lane);
+                const f32x4 ax = c2_tile<H, true, P, false, P>(G2, ti0, Pp + Ly::oW1, tj0, lane);
 #pragma unroll
-                for (int u = 0; u < 4; ++u) o[u] = y[u] > 0.f ? g * wv[u] : 0.f;
-                *reinterpret_cast<f32x4*>(G2 + b * P + k) = o;
-            }
-            __syncthreads();
-            // hidden layer 1: gW1 = G2ᵀ·Y1, gx = (G2·W1) ⊙ 1[Y1 > 0], gb1 = Σ_b G2; gW2 combined
-            for (int t = w; t < 2 * NT; t += NWAVES) {
-                if (t < NT) {                                   // gW1[j][k]: A(j, b) = G2, B(b, k) = Y1
-                    const int i0 = (t / (H / 16)) * 16, j0 = (t % (H / 16)) * 16;
-                    const f32x4 acc = c2_tile<BB, false, P, false, P>(G2, i0, Y1, j0, lane);
+                for (int e = 0; e < 4; ++e) {
+                    const int r = ti0 + 4 * q + e, k = tj0 + c;
+                    Gd[Ly::oW1 + r * P + k] = aw[e];
+                    G1[r * P + k] = Y1[r * P + k] > 0.f ? ax[e] : 0.f;
+                }
+                static_assert(H == 4 * NWAVES, "four columns per wave");
+                const int col = 4 * w + (lane & 3), rs = lane >> 2;     // 16 slices of BB / 16 rows
+                float sb = 0.f, sw = 0.f;
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) Gd[Ly::oW1 + (i0 + 4 * q + e) * P + j0 + c] = acc[e];
-                } else {                                        // G1[b][k]: A(b, j) = G2, B(j, k) = W1
-                    const int tt = t - NT;
-                    const int i0 = (tt / (H / 16)) * 16, j0 = (tt % (H / 16)) * 16;
-                    const f32x4 acc = c2_tile<H, true, P, false, P>(G2, i0, Pp + Ly::oW1, j0, lane);
+                for (int r = 0; r < BB / 16; ++r) {
+                    const int b = rs * (BB / 16) + r;
+                    sb += G2[b * P + col];
+                    sw += G3[b] * Y2[b * P + col];
+                }
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) {
-                        const int b = i0 + 4 * q + e, k = j0 + c;
-                        G1[b * P + k] = Y1[b * P + k] > 0.f ? acc[e] : 0.f;
+                for (int o = 4; o < 64; o <<= 1) {
+                    sb += __shfl_xor(sb, o, 64);
+                    sw += __shfl_xor(sw, o, 64);
+                }
+                if (lane < 4) {
+                    Gd[Ly::ob1 + col] = sb;
+                    Gd[Ly::oW2 + col] = sw;
+                }
+                if (w == NWAVES - 1) {
+                    float g = 0.f;
+                    for (int b = lane; b < BB; b += 64) g += G3[b];
+                    g = wave_sum(g);
+                    if (lane == 0) Gd[Ly::ob2] = g;
+                    if (lane == 1) {
+                        float sl = 0.f, gl = 0.f;
+                        for (int v = 0; v < NWAVES; ++v) { sl += red[v]; gl += gls_red[v]; }
+                        if (!a.policy) {
+                            atomicAdd(a.stats + 0, sl * (1.0f / (float)BB));
+                        } else {
+                            const float ent = (float)(0.5 * (1 + log(2 * M_PI))) + s_ls;
+                            atomicAdd(a.stats + 1, -sl / BB - a.ent_coeff * ent);
+                            s_lsg = gl + -a.ent_coeff;                      // ppo.cu:436-438
+                            a.log_std_grad[0] = s_lsg;
+                        }
                     }
                 }
             }
-            if (tid < H) {
-                float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-#pragma unroll 4
-                for (int b = 0; b < BB; b += 4) {
-                    s0 += G2[b * P + tid];
-                    s1 += G2[(b + 1) * P + tid];
-                    s2 += G2[(b + 2) * P + tid];
-                    s3 += G2[(b + 3) * P + tid];
-                }
-                Gd[Ly::ob1 + tid] = (s0 + s1) + (s2 + s3);
-                Gd[Ly::oW2 + tid] = (T[tid] + T[H + tid]) + (T[2 * H + tid] + T[3 * H + tid]);
-            }
             __syncthreads();
-            // layer 0: gW0[j][k] = Σ_b G1[b][j]·X0[b][k] (4 lanes per output), gb0 = Σ_b G1
-            if (tid < 4 * H * S) {
-                const int o = tid >> 2, pr = tid & 3;
-                const int j = o / S, k = o % S;
-                float sacc = 0.f;
-#pragma unroll 4
-                for (int b = pr * (BB / 4); b < (pr + 1) * (BB / 4); ++b) sacc += G1[b * P + j] * X0[b * SP + k];
-                sacc += __shfl_xor(sacc, 1, 64);
-                sacc += __shfl_xor(sacc, 2, 64);
-                if (pr == 0) Gd[Ly::oW0 + j * SP + k] = sacc;
-            } else if (tid >= 4 * H * S && tid < 4 * H * S + H) {
-                const int j = tid - 4 * H * S;
-                float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-#pragma unroll 4
-                for (int b = 0; b < BB; b += 4) {
-                    s0 += G1[b * P + j];
-                    s1 += G1[(b + 1) * P + j];
-                    s2 += G1[(b + 2) * P + j];
-                    s3 += G1[(b + 3) * P + j];
+            if (a.stamps && tid == 0 && step < 64) a.stamps[64 * 8 + step * 4 + 3] = wall_clock64();
+            // layer 0: gW0[j][k] = Σ_b G1[b][j]·X0[b][k], and gb0[j] from X0's ones column (k = S):
+            // 16 lanes per j, 4 rows each
+            {
+                const int j = tid >> 4, rs = tid & 15;
+                float s4[SP] = {};
+#pragma unroll
+                for (int r = 0; r < BB / 16; ++r) {
+                    const int b = rs * (BB / 16) + r;
+                    const float g = G1[b * P + j];
+                    const f32x4 x = *reinterpret_cast<const f32x4*>(X0 + b * SP);
+#pragma unroll
+                    for (int k = 0; k < SP; ++k) s4[k] += g * x[k];
                 }
-                Gd[Ly::ob0 + j] = (s0 + s1) + (s2 + s3);
+#pragma unroll
+                for (int k = 0; k < SP; ++k) s4[k] = sum16(s4[k]);
+                float v = s4[0];
+#pragma unroll
+                for (int k = 1; k < SP; ++k) v = rs == k ? s4[k] : v;
+                if (rs < S) Gd[Ly::oW0 + j * SP + rs] = v;
+                else if (rs == S) Gd[Ly::ob0 + j] = v;
             }
-            __threadfence_block();
-            __syncthreads();
+            __syncthreads();                                   // (LDS only: no global-memory fence)
             TINY_STAMP(4);
-            // ---- Adam: entropy (log σ) first, then the network (ppo.cu:440-442) ----
-            if (a.policy && tid == 0) {
-                float p = a.log_std[0], mm = a.m_ls[0], vv = a.v_ls[0];
-                adam_elem(p, a.log_std_grad[0], mm, vv, a.steps_ls[2 * step], a.b1, a.b2, a.steps_ls[2 * step + 1]);
-                a.log_std[0] = p; a.m_ls[0] = mm; a.v_ls[0] = vv;
+            // ---- Adam: entropy (log σ) first, then the network (ppo.cu:440-442); the next
+            // minibatch's gather loads are in flight meanwhile ----
+            int nep = ep, nkb = kb + 1;
+            if (nkb >= a.num_batches) { nep = ep + 1; nkb = 0; }
+            const bool next = step + 1 < a.total_steps && nep < a.n_epochs && gt >= 0;
+            Row nr{};
+            if (next) nr = fetch(nep, nkb);
+            if (a.policy && tid == TPB / 2) {
+                float p = s_ls, mls = s_mls, vls = s_vls;
+                adam_elem(p, s_lsg, mls, vls, a.steps_ls[2 * step], a.b1, a.b2, a.steps_ls[2 * step + 1]);
+                s_ls = p; s_mls = mls; s_vls = vls;
+                a.log_std[0] = p; a.m_ls[0] = mls; a.v_ls[0] = vls;
             }
             const float st = a.steps[2 * step], bc2 = a.steps[2 * step + 1];
             for (int e = 4 * tid; e < Ly::NPAR; e += 4 * TPB) {
@@ -741,8 +760,8 @@ __global__ __launch_bounds__(TPB) void tiny_c2_kernel(TinyArgs a) {
                 *reinterpret_cast<f32x4*>(Mv + e) = mm;
                 *reinterpret_cast<f32x4*>(Vv + e) = vv;
             }
-            __threadfence_block();
-            __syncthreads();
+            if (next) put(nr);
+            __syncthreads();                                   // (LDS only: no global-memory fence)
             TINY_STAMP(5);
         }
     }
@@ -771,13 +790,15 @@ void print_stamps(const TinyArgs& a, const PhipTinyPhase* ph) {
             for (int k = 0; k < 5; ++k) acc[k] += (double)(h[st * 8 + k + 1] - h[st * 8 + k]) / mhz;
         const double clk = (double)(h[63 * 8 + 6] - h[1 * 8 + 6]) / ((double)(h[63 * 8] - h[1 * 8]) / mhz);
         if (n) fprintf(stderr, "tiny: shader clock %.0f MHz\n", clk);
-        double fl[3] = {0, 0, 0};
+        double fl[4] = {0, 0, 0, 0};
         for (int st = 1; st < 64 && st < a.total_steps; ++st) {
             fl[0] += (double)(h[512 + st * 4 + 0] - h[st * 8 + 1]) / mhz;
             fl[1] += (double)(h[512 + st * 4 + 1] - h[512 + st * 4 + 0]) / mhz;
             fl[2] += (double)(h[512 + st * 4 + 2] - h[512 + st * 4 + 1]) / mhz;
+            fl[3] += (double)(h[512 + st * 4 + 3] - h[st * 8 + 3]) / mhz;
         }
-        if (n) fprintf(stderr, "tiny: forward layers (us): %.2f %.2f %.2f\n", fl[0] / n, fl[1] / n, fl[2] / n);
+        if (n) fprintf(stderr, "tiny: sub-phases (us): layer 0 %.2f, layer 1 %.2f, head %.2f, first backward %.2f\n",
+                       fl[0] / n, fl[1] / n, fl[2] / n, fl[3] / n);
         if (n)
             fprintf(stderr, "tiny %s step phases (us): gather %.2f fwd %.2f head %.2f bwd %.2f adam %.2f\n",
                     ph->policy ? "policy" : "value", acc[0] / n, acc[1] / n, acc[2] / n, acc[3] / n, acc[4] / n);
