@@ -454,8 +454,9 @@ struct C2Lay {
     // flat (reference) layout: W0 [H][S], b0, W1 [H][H], b1, W2 [1][H], b2
     static constexpr int fb0 = H * S, fW1 = fb0 + H, fb1 = fW1 + H * H, fW2 = fb1 + H, fb2 = fW2 + H,
                          NFLAT = fb2 + 1;
-    // activations / gradients [BB][P] (X0 [BB][SP]), then rows, targets, old log-probs, actions
-    static constexpr int aX0 = 0, aY1 = aX0 + BB * SP, aY2 = aY1 + BB * P, aG2 = aY2 + BB * P, aG1 = aG2 + BB * P,
+    // activations / gradients [BB][P] (X0: two [BB][SP] buffers, this step's and the next's), then
+    // rows, targets, old log-probs, actions
+    static constexpr int aX0 = 0, aY1 = aX0 + 2 * BB * SP, aY2 = aY1 + BB * P, aG2 = aY2 + BB * P, aG1 = aG2 + BB * P,
                          aG3 = aG1 + BB * P, aT = aG3 + BB, aMisc = aT + 4 * H, aRes = (aMisc + 4 * BB + 3) & ~3,
                          TOTAL = aRes + 4 * NPAR;
     __device__ static int pad_index(int f) {
@@ -491,11 +492,32 @@ __device__ __forceinline__ f32x4 c2_tile(const float* __restrict__ A, int i0, co
     return acc;
 }
 
-// 16-lane group sum (lanes l, l^1, …, l^8: one row-slice group of a wave)
+#ifndef PPO_C2_ADAM_U
+#define PPO_C2_ADAM_U 2   // Adam rounds interleaved per batch
+#endif
+#ifndef PPO_C2_AB
+#define PPO_C2_AB 0       // diagnostic builds only: 1 no Adam arithmetic, 2 no next-minibatch gather,
+#endif                    // 4 no layer-0 gradient phase work, 8 no hidden-layer MFMA tiles
+// sum over a 16-lane DPP row (the xor-1 / xor-2 / quad-swap / half-swap tree, the order of a
+// __shfl_xor tree) on DPP moves: no LDS round trips (ds_bpermute chains cost ≈1.4 µs per phase)
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
 __device__ __forceinline__ float sum16(float v) {
-#pragma unroll
-    for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    v += dpp_mov<0xB1>(v);            // quad_perm [1,0,3,2]
+    v += dpp_mov<0x4E>(v);            // quad_perm [2,3,0,1]
+    v += dpp_mov<0x141>(v);           // row_half_mirror
+    v += dpp_mov<0x140>(v);           // row_mirror
     return v;
+}
+// sum over the wave: row sums, then the four rows' lane-0 values through scalar reads (in row order)
+__device__ __forceinline__ float lane_value(float v, int l) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+__device__ __forceinline__ float sum64(float v) {
+    v = sum16(v);
+    return ((lane_value(v, 0) + lane_value(v, 16)) + lane_value(v, 32)) + lane_value(v, 48);
 }
 
 // Per step: forward layer 0 | layer 1 | output layer + head + the output layer's grad_x | hidden-layer
@@ -510,7 +532,7 @@ __global__ __launch_bounds__(TPB) void tiny_c2_kernel(TinyArgs a) {
     constexpr int P = Ly::P, SP = Ly::SP, HT = H / 16;
     static_assert((BB / 16) * HT == NWAVES && BB == H && TPB / BB == 16 && S < SP, "C2 phase split");
     extern __shared__ float lds[];
-    float* const X0 = lds + Ly::aX0;                      // [BB][SP]; column S holds 1 (bias gradient)
+    float* const X0b = lds + Ly::aX0;                     // 2 × [BB][SP]; column S holds 1 (bias gradient)
     float* const Y1 = lds + Ly::aY1;
     float* const Y2 = lds + Ly::aY2;
     float* const G2 = lds + Ly::aG2;
@@ -565,7 +587,7 @@ __global__ __launch_bounds__(TPB) void tiny_c2_kernel(TinyArgs a) {
         }
         return r;
     };
-    auto put = [&](const Row& r) {
+    auto put = [&](const Row& r, float* X0) {
         const int i = gt / SP, k = gt % SP;
         X0[i * SP + k] = r.x;
         if (k == 0) {
@@ -574,7 +596,7 @@ __global__ __launch_bounds__(TPB) void tiny_c2_kernel(TinyArgs a) {
             if (a.policy) { olp[i] = r.o; act[i] = r.ac; }
         }
     };
-    if (gt >= 0 && a.total_steps > 0) put(fetch(0, 0));
+    if (gt >= 0 && a.total_steps > 0) put(fetch(0, 0), X0b);
     __syncthreads();
 
     int step = 0;
@@ -582,6 +604,7 @@ __global__ __launch_bounds__(TPB) void tiny_c2_kernel(TinyArgs a) {
         for (int kb = 0; kb < a.num_batches && step < a.total_steps; ++kb, ++step) {
             TINY_STAMP(0);
             TINY_STAMP(1);
+            const float* const X0 = X0b + (step & 1) * (BB * SP);
             // ---- forward (neural_network.cu:74-105) ----
             {                                                  // layer 0: K = S < 4, one MFMA
                 const float av = q < S ? X0[(ti0 + c) * SP + q] : 0.f;
@@ -622,9 +645,9 @@ __global__ __launch_bounds__(TPB) void tiny_c2_kernel(TinyArgs a) {
                     wv[h] = *reinterpret_cast<const float2*>(Pp + Ly::oW2 + pk * KPL + 2 * h);
                     d += yv[h].x * wv[h].x + yv[h].y * wv[h].y;
                 }
-                d = sum16(d);
-                float g = 0.f;
-                if (pk == 0) {
+                d = sum16(d);                                  // every lane of the row: y, the head
+                float g;
+                {
                     const float y = d + Pp[Ly::ob2];
                     if (!a.policy) {                           // loss.cu:5-23
                         const float t = tgt[i], dd = t - y;
@@ -640,16 +663,16 @@ __global__ __launch_bounds__(TPB) void tiny_c2_kernel(TinyArgs a) {
                         g = dd * e2 * gl;
                         glsp = (-1 + dd * dd * e2) * gl;
                     }
-                    G3[i] = g;
+                    if (pk == 0) G3[i] = g;
+                    else part = glsp = 0.f;                    // row sums counted once
                 }
-                g = __shfl(g, lane & ~15, 64);
 #pragma unroll
                 for (int h = 0; h < KPL / 2; ++h)
                     *reinterpret_cast<float2*>(G2 + i * P + pk * KPL + 2 * h) =
                         float2{yv[h].x > 0.f ? g * wv[h].x : 0.f, yv[h].y > 0.f ? g * wv[h].y : 0.f};
             }
-            part = wave_sum(part);
-            if (a.policy) glsp = wave_sum(glsp);
+            part = sum64(part);
+            if (a.policy) glsp = sum64(glsp);
             if (lane == 0) {
                 red[w] = part;
                 gls_red[w] = glsp;
@@ -661,8 +684,11 @@ __global__ __launch_bounds__(TPB) void tiny_c2_kernel(TinyArgs a) {
             // G1 = (G2·W1) ⊙ 1[Y1 > 0] tiles; columns 4w .. 4w+3 of gb1 = Σ_b G2 and gW2 = Σ_b g·Y2
             // (16 row slices of 4 per column, lanes 16s + col); gb2 and the loss sums by wave 15 ----
             {
-                const f32x4 aw = c2_tile<BB, false, P, false, P>(G2, ti0, Y1, tj0, lane);
-                const f32x4 ax = c2_tile<H, true, P, false, P>(G2, ti0, Pp + Ly::oW1, tj0, lane);
+                f32x4 aw = {0.f, 0.f, 0.f, 0.f}, ax = aw;
+                if constexpr (!(PPO_C2_AB & 8)) {
+                    aw = c2_tile<BB, false, P, false, P>(G2, ti0, Y1, tj0, lane);
+                    ax = c2_tile<H, true, P, false, P>(G2, ti0, Pp + Ly::oW1, tj0, lane);
+                }
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
                     const int r = ti0 + 4 * q + e, k = tj0 + c;
@@ -670,7 +696,7 @@ __global__ __launch_bounds__(TPB) void tiny_c2_kernel(TinyArgs a) {
                     G1[r * P + k] = Y1[r * P + k] > 0.f ? ax[e] : 0.f;
                 }
                 static_assert(H == 4 * NWAVES, "four columns per wave");
-                const int col = 4 * w + (lane & 3), rs = lane >> 2;     // 16 slices of BB / 16 rows
+                const int col = 4 * w + (lane >> 4), rs = lane & 15;    // a DPP row per column, 16 slices
                 float sb = 0.f, sw = 0.f;
 #pragma unroll
                 for (int r = 0; r < BB / 16; ++r) {
@@ -678,19 +704,16 @@ __global__ __launch_bounds__(TPB) void tiny_c2_kernel(TinyArgs a) {
                     sb += G2[b * P + col];
                     sw += G3[b] * Y2[b * P + col];
                 }
-#pragma unroll
-                for (int o = 4; o < 64; o <<= 1) {
-                    sb += __shfl_xor(sb, o, 64);
-                    sw += __shfl_xor(sw, o, 64);
-                }
-                if (lane < 4) {
+                sb = sum16(sb);
+                sw = sum16(sw);
+                if (rs == 0) {
                     Gd[Ly::ob1 + col] = sb;
                     Gd[Ly::oW2 + col] = sw;
                 }
                 if (w == NWAVES - 1) {
                     float g = 0.f;
                     for (int b = lane; b < BB; b += 64) g += G3[b];
-                    g = wave_sum(g);
+                    g = sum64(g);
                     if (lane == 0) Gd[Ly::ob2] = g;
                     if (lane == 1) {
                         float sl = 0.f, gl = 0.f;
@@ -708,9 +731,18 @@ __global__ __launch_bounds__(TPB) void tiny_c2_kernel(TinyArgs a) {
             }
             __syncthreads();
             if (a.stamps && tid == 0 && step < 64) a.stamps[64 * 8 + step * 4 + 3] = wall_clock64();
-            // layer 0: gW0[j][k] = Σ_b G1[b][j]·X0[b][k], and gb0[j] from X0's ones column (k = S):
-            // 16 lanes per j, 4 rows each
-            {
+            TINY_STAMP(4);
+            // ---- layer 0 + Adam (ppo.cu:440-442: entropy first, then the network), one phase: the
+            // next minibatch's gather loads go out first; gW0[j][k] = Σ_b G1[b][j]·X0[b][k] and gb0[j]
+            // (X0's ones column, k = S) by 16 lanes per j, and the lane holding each of them applies
+            // its Adam step at once; every other parameter's gradient is complete since the barrier ----
+            int nep = ep, nkb = kb + 1;
+            if (nkb >= a.num_batches) { nep = ep + 1; nkb = 0; }
+            const bool next = !(PPO_C2_AB & 2) && step + 1 < a.total_steps && nep < a.n_epochs && gt >= 0;
+            Row nr{};
+            if (next) nr = fetch(nep, nkb);
+            const float st = a.steps[2 * step], bc2 = a.steps[2 * step + 1];
+            if (!(PPO_C2_AB & 4)) {
                 const int j = tid >> 4, rs = tid & 15;
                 float s4[SP] = {};
 #pragma unroll
@@ -726,41 +758,45 @@ __global__ __launch_bounds__(TPB) void tiny_c2_kernel(TinyArgs a) {
                 float v = s4[0];
 #pragma unroll
                 for (int k = 1; k < SP; ++k) v = rs == k ? s4[k] : v;
-                if (rs < S) Gd[Ly::oW0 + j * SP + rs] = v;
-                else if (rs == S) Gd[Ly::ob0 + j] = v;
+                if (rs <= S) {
+                    const int e = rs < S ? Ly::oW0 + j * SP + rs : Ly::ob0 + j;
+                    Gd[e] = v;
+                    float pu = Pp[e], mu = Mv[e], vu = Vv[e];
+                    adam_elem(pu, v, mu, vu, st, a.b1, a.b2, bc2);
+                    Pp[e] = pu; Mv[e] = mu; Vv[e] = vu;
+                }
             }
-            __syncthreads();                                   // (LDS only: no global-memory fence)
-            TINY_STAMP(4);
-            // ---- Adam: entropy (log σ) first, then the network (ppo.cu:440-442); the next
-            // minibatch's gather loads are in flight meanwhile ----
-            int nep = ep, nkb = kb + 1;
-            if (nkb >= a.num_batches) { nep = ep + 1; nkb = 0; }
-            const bool next = step + 1 < a.total_steps && nep < a.n_epochs && gt >= 0;
-            Row nr{};
-            if (next) nr = fetch(nep, nkb);
             if (a.policy && tid == TPB / 2) {
                 float p = s_ls, mls = s_mls, vls = s_vls;
                 adam_elem(p, s_lsg, mls, vls, a.steps_ls[2 * step], a.b1, a.b2, a.steps_ls[2 * step + 1]);
                 s_ls = p; s_mls = mls; s_vls = vls;
                 a.log_std[0] = p; a.m_ls[0] = mls; a.v_ls[0] = vls;
             }
-            const float st = a.steps[2 * step], bc2 = a.steps[2 * step + 1];
-            for (int e = 4 * tid; e < Ly::NPAR; e += 4 * TPB) {
-                f32x4 p = *reinterpret_cast<const f32x4*>(Pp + e);
-                const f32x4 g = *reinterpret_cast<const f32x4*>(Gd + e);
-                f32x4 mm = *reinterpret_cast<const f32x4*>(Mv + e);
-                f32x4 vv = *reinterpret_cast<const f32x4*>(Vv + e);
+            // the rest of the image (W1, b1, W2, b2 and their pads), one element per thread per round,
+            // the rounds unrolled so their dependent Adam chains interleave
+            {
+                constexpr int NR = (Ly::NPAR - Ly::oW1 + TPB - 1) / TPB, U = PPO_C2_ADAM_U;
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    float pu = p[u], mu = mm[u], vu = vv[u];
-                    adam_elem(pu, g[u], mu, vu, st, a.b1, a.b2, bc2);
-                    p[u] = pu; mm[u] = mu; vv[u] = vu;
+                for (int r0 = 0; r0 < NR; r0 += U) {
+                    float pu[U], gu[U], mu[U], vu[U];
+#pragma unroll
+                    for (int r = 0; r < U; ++r) {
+                        const int e = min(Ly::oW1 + tid + (r0 + r) * TPB, Ly::NPAR - 1);
+                        pu[r] = Pp[e]; gu[r] = Gd[e]; mu[r] = Mv[e]; vu[r] = Vv[e];
+                    }
+#pragma unroll
+                    for (int r = 0; r < U; ++r) {
+                        if constexpr (PPO_C2_AB & 1) pu[r] += gu[r] * st;
+                        else adam_elem(pu[r], gu[r], mu[r], vu[r], st, a.b1, a.b2, bc2);
+                    }
+#pragma unroll
+                    for (int r = 0; r < U; ++r) {
+                        const int e = Ly::oW1 + tid + (r0 + r) * TPB;
+                        if (r0 + r < NR && e < Ly::NPAR) { Pp[e] = pu[r]; Mv[e] = mu[r]; Vv[e] = vu[r]; }
+                    }
                 }
-                *reinterpret_cast<f32x4*>(Pp + e) = p;
-                *reinterpret_cast<f32x4*>(Mv + e) = mm;
-                *reinterpret_cast<f32x4*>(Vv + e) = vv;
             }
-            if (next) put(nr);
+            if (next) put(nr, X0b + ((step + 1) & 1) * (BB * SP));
             __syncthreads();                                   // (LDS only: no global-memory fence)
             TINY_STAMP(5);
         }
