@@ -45,6 +45,28 @@ inline long long gemm_key(int op, int engine, long m, long n, long l) {
            ((long long)(n & 0xFFFF) << 16) | (long long)(l & 0xFFFF);
 }
 
+// Cross-lane sums on DPP moves (no LDS round trips; a __shfl_xor tree compiles to ds_bpermute,
+// ≈ 100+ cycles of latency per step): sum over each 16-lane DPP row — the xor-1 / xor-2 / quad-swap /
+// half-swap tree — and over the wave (row sums in row order, read as scalars)
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float row_sum16(float v) {
+    v += dpp_mov<0xB1>(v);            // quad_perm [1,0,3,2]
+    v += dpp_mov<0x4E>(v);            // quad_perm [2,3,0,1]
+    v += dpp_mov<0x141>(v);           // row_half_mirror
+    v += dpp_mov<0x140>(v);           // row_mirror
+    return v;
+}
+__device__ __forceinline__ float lane_value(float v, int l) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+__device__ __forceinline__ float wave_sum64(float v) {
+    v = row_sum16(v);
+    return ((lane_value(v, 0) + lane_value(v, 16)) + lane_value(v, 32)) + lane_value(v, 48);
+}
+
 }  // namespace ppo
 
 #define PPO_TIMED_LAUNCH(kernel, grid, block, lds, strm, ...)                                         \

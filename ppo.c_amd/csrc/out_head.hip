@@ -33,11 +33,7 @@ namespace {
 constexpr int NTH = 256;                   // 4 waves
 constexpr int NW = NTH / 64;
 
-__device__ __forceinline__ float wsum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
+__device__ __forceinline__ float wsum(float v) { return ppo::wave_sum64(v); }   // DPP rows + scalar reads
 
 // policy.cu:67-74 with the reference's double temporaries (kernels.hip log_prob_row)
 template <int A>

@@ -498,27 +498,9 @@ __device__ __forceinline__ f32x4 c2_tile(const float* __restrict__ A, int i0, co
 #ifndef PPO_C2_AB
 #define PPO_C2_AB 0       // diagnostic builds only: 1 no Adam arithmetic, 2 no next-minibatch gather,
 #endif                    // 4 no layer-0 gradient phase work, 8 no hidden-layer MFMA tiles
-// sum over a 16-lane DPP row (the xor-1 / xor-2 / quad-swap / half-swap tree, the order of a
-// __shfl_xor tree) on DPP moves: no LDS round trips (ds_bpermute chains cost ≈1.4 µs per phase)
-template <int CTRL>
-__device__ __forceinline__ float dpp_mov(float v) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
-}
-__device__ __forceinline__ float sum16(float v) {
-    v += dpp_mov<0xB1>(v);            // quad_perm [1,0,3,2]
-    v += dpp_mov<0x4E>(v);            // quad_perm [2,3,0,1]
-    v += dpp_mov<0x141>(v);           // row_half_mirror
-    v += dpp_mov<0x140>(v);           // row_mirror
-    return v;
-}
-// sum over the wave: row sums, then the four rows' lane-0 values through scalar reads (in row order)
-__device__ __forceinline__ float lane_value(float v, int l) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
-}
-__device__ __forceinline__ float sum64(float v) {
-    v = sum16(v);
-    return ((lane_value(v, 0) + lane_value(v, 16)) + lane_value(v, 32)) + lane_value(v, 48);
-}
+using ppo::row_sum16;
+__device__ __forceinline__ float sum16(float v) { return ppo::row_sum16(v); }
+__device__ __forceinline__ float sum64(float v) { return ppo::wave_sum64(v); }
 
 // Per step: forward layer 0 | layer 1 | output layer + head + the output layer's grad_x | hidden-layer
 // gW1 / grad_x tiles with the bias / output-layer column sums | layer-0 weight + bias gradients |
