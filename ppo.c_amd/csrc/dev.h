@@ -33,10 +33,10 @@ struct ProfScope {
 bool take_kernel_events(hipEvent_t* start, hipEvent_t* stop);
 
 // split-K grad_W partials (gemm_x3.hip): a per-stream scratch of `floats` floats, and
-// out[i] = Σ_s slab[s·n + i] in a fixed order (n % 4 == 0, 16-B aligned); `stop`: an event recorded
-// by the reduce's dispatch (or null)
+// out[i] = Σ_s slab[s·stride + i] for i < n in a fixed order (stride % 4 == 0, 16-B aligned slab and
+// out); `stop`: an event recorded by the reduce's dispatch (or null)
 float* slab_scratch(size_t floats);
-void slab_reduce(const float* slab, float* out, long n, int splits, hipEvent_t stop);
+void slab_reduce(const float* slab, float* out, long n, long stride, int splits, hipEvent_t stop);
 
 // shape tag of a GEMM launch: op (0 fwd, 1 grad_x, 2 grad_W, 3 paired bwd) [60..63] | engine [56..59] |
 // m [32..55] | n [16..31] | l [0..15]; fields masked so an out-of-range width cannot alias another shape

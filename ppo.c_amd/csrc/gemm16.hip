@@ -1495,7 +1495,7 @@ bool launch_dma_tn(float* gW, float* gb, const void* g, const void* x, int m, in
         else hipLaunchKernelGGL(kern, grid, dim3(512), lds128, ppo::stream(), a, slab);
     }
     PPO_LAUNCH_CHECK();
-    if (splits > 1) ppo::slab_reduce(slab, gW, sstride, splits, timed ? e1 : nullptr);
+    if (splits > 1) ppo::slab_reduce(slab, gW, sstride, sstride, splits, timed ? e1 : nullptr);
     return true;
 }
 

@@ -719,24 +719,38 @@ void launch_x3(X3Args a) {
 }
 
 // grad_W split-K partials: out[i] = Σ_s slab[s][i] in a fixed order (run-to-run deterministic).
-// 64 float4 columns per workgroup × 4 split quarters: quarter q sums its splits in order, then the
-// quarter partials are added in order through LDS.  (One thread per column over all splits kept
-// 256 workgroups with a serial chain of loads: 25.6 µs for 32 × 1 MB slabs, ≈1.3 TB/s.)
-__global__ __launch_bounds__(256) void slab_reduce_kernel(const f32x4* __restrict__ slab, f32x4* __restrict__ out,
-                                                          long n4, int splits) {
-    __shared__ f32x4 part[3][64];
-    const int c = threadIdx.x & 63, q = threadIdx.x >> 6;
-    const long i = (long)blockIdx.x * 64 + c;
-    const int per = (splits + 3) >> 2;
+// 256/Q float4 columns per workgroup × Q split groups: group q sums its splits in order, then the
+// group partials are added in order through LDS (Q = 4; Q = 16 for many splits of few columns, the
+// per-workgroup partials of the wide output layer).  (One thread per column over all splits kept 256
+// workgroups with a serial chain of loads: 25.6 µs for 32 × 1 MB slabs, ≈1.3 TB/s.)
+template <int Q>
+__global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ slab, float* __restrict__ out,
+                                                          long n, long stride, int splits) {
+    constexpr int C = 256 / Q;
+    __shared__ f32x4 part[Q - 1][C];
+    const int c = threadIdx.x % C, q = threadIdx.x / C;
+    const long n4 = (n + 3) >> 2, s4 = stride >> 2;      // the last quad may be partial (stride pads it)
+    const long i = (long)blockIdx.x * C + c;
+    const int per = (splits + Q - 1) / Q;
     const int s0 = q * per, s1 = min(splits, s0 + per);
+    const f32x4* __restrict__ sv = reinterpret_cast<const f32x4*>(slab);
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     if (i < n4) {
 #pragma unroll 8
-        for (int s = s0; s < s1; ++s) acc += slab[(long)s * n4 + i];
+        for (int s = s0; s < s1; ++s) acc += sv[(long)s * s4 + i];
     }
     if (q) part[q - 1][c] = acc;
     __syncthreads();
-    if (q == 0 && i < n4) out[i] = ((acc + part[0][c]) + part[1][c]) + part[2][c];
+    if (q == 0 && i < n4) {
+#pragma unroll
+        for (int v = 0; v < Q - 1; ++v) acc += part[v][c];
+        if (4 * i + 4 <= n) {
+            reinterpret_cast<f32x4*>(out)[i] = acc;
+        } else {
+            for (int e = 0; e < 4; ++e)
+                if (4 * i + e < n) out[4 * i + e] = acc[e];
+        }
+    }
 }
 
 int g_x3_atomics = -1;                   // PPO_X3_ATOMICS=1: split-K partials by f32 atomics (A/B)
@@ -819,17 +833,18 @@ float* slab_scratch(size_t floats) {
     return g_slab[s];
 }
 
-void slab_reduce(const float* slab, float* out, long n, int splits, hipEvent_t stop) {
-    PPO_REQUIRE(n % 4 == 0 && al16(slab) && al16(out) && splits >= 1, "slab_reduce: operands");
-    const long n4 = n / 4;
-    PPO_REQUIRE((n4 + 63) / 64 < (1L << 31), "slab_reduce: grid");
-    const int grid = (int)((n4 + 63) / 64);
+void slab_reduce(const float* slab, float* out, long n, long stride, int splits, hipEvent_t stop) {
+    PPO_REQUIRE(stride % 4 == 0 && stride >= n && al16(slab) && al16(out) && splits >= 1, "slab_reduce: operands");
+    const long n4 = (n + 3) / 4;
+    const bool many = splits >= 64;
+    const int C = many ? 16 : 64;
+    PPO_REQUIRE(n4 / C + 1 < (1L << 31), "slab_reduce: grid");
+    const int grid = (int)std::max<long>(1, (n4 + C - 1) / C);
+    auto kern = many ? slab_reduce_kernel<16> : slab_reduce_kernel<4>;
     if (stop)
-        hipExtLaunchKernelGGL(slab_reduce_kernel, dim3(grid), dim3(256), 0, stream(), nullptr, stop, 0,
-                              (const f32x4*)slab, (f32x4*)out, n4, splits);
+        hipExtLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, stream(), nullptr, stop, 0, slab, out, n, stride, splits);
     else
-        hipLaunchKernelGGL(slab_reduce_kernel, dim3(grid), dim3(256), 0, stream(), (const f32x4*)slab,
-                           (f32x4*)out, n4, splits);
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, stream(), slab, out, n, stride, splits);
     PPO_LAUNCH_CHECK();
 }
 
@@ -927,7 +942,7 @@ void phip_x3_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, 
     a.ev_start = timed ? e0 : nullptr;
     a.ev_stop = nullptr;
     launch_cfg_x3<OP_TN>(c, a);
-    ppo::slab_reduce(a.slab, gW, (long)l * n, splits, timed ? e1 : nullptr);
+    ppo::slab_reduce(a.slab, gW, (long)l * n, (long)l * n, splits, timed ? e1 : nullptr);
 }
 
 int ppo_gemm_x3_tune(int force_cfg, int splitk_target) {

@@ -379,9 +379,102 @@ bool launch_n(const OutArgs& a) {
     }
 }
 
+// Backward of a wide output layer (policy A = 17 at C4) in one pass over the rows: a 256-thread
+// workgroup takes a chunk of rows; thread t owns columns NPT·t .. NPT·t+NPT-1 — their A weights and
+// A gW accumulators in registers — and per row reads x (NPT floats), the row's A head gradients as
+// wave-uniform scalar loads, and writes gx = (g·W) ⊙ 1[x > 0]; lanes a < A of wave 0 also sum gb.
+// Each workgroup's gW / gb partial goes to its slab and ppo::slab_reduce sums them in order.  Replaces
+// the paired grad_W + grad_x GEMM launch (x read once for both; HBM ≈ 8·n bytes per row).
+template <int A, int NPT, int U>
+__global__ __launch_bounds__(256) void out_bwd_wide_kernel(const float* __restrict__ g, const float* __restrict__ x,
+                                                           const float* __restrict__ W, float* __restrict__ gx,
+                                                           float* __restrict__ slab, long slab_stride, int m,
+                                                           int rows_per_wg, int relu_in) {
+    constexpr int N = 256 * NPT;
+    extern __shared__ float gs[];                        // this workgroup's rows of g [rows][A]
+    const int t = threadIdx.x, k0 = t * NPT;
+    const int r0 = blockIdx.x * rows_per_wg;
+    const int nr = min(m, r0 + rows_per_wg) - r0;
+    for (int e = t; e < nr * A; e += 256) gs[e] = g[(long)r0 * A + e];
+    float Wr[A][NPT], acc[A][NPT];
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+        load_cols<NPT>(W + (long)a * N + k0, Wr[a]);
+#pragma unroll
+        for (int q = 0; q < NPT; ++q) acc[a][q] = 0.f;
+    }
+    __syncthreads();
+    for (int rb = 0; rb < nr; rb += U) {
+        float xv[U][NPT];                                // U rows in flight
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (rb + u < nr) load_cols<NPT>(x + (long)(r0 + rb + u) * N + k0, xv[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int r = rb + u;
+            if (r >= nr) break;                          // workgroup-uniform
+            float gv[A];
+#pragma unroll
+            for (int a = 0; a < A; ++a) gv[a] = gs[r * A + a];   // uniform address: LDS broadcast
+            float o[NPT];
+#pragma unroll
+            for (int q = 0; q < NPT; ++q) {
+                float sacc = 0.f;
+#pragma unroll
+                for (int a = 0; a < A; ++a) sacc += gv[a] * Wr[a][q];
+                o[q] = (!relu_in || xv[u][q] > 0.f) ? sacc : 0.f;
+            }
+            store_cols<NPT>(gx + (long)(r0 + r) * N + k0, o);
+#pragma unroll
+            for (int a = 0; a < A; ++a)
+#pragma unroll
+                for (int q = 0; q < NPT; ++q) acc[a][q] += gv[a] * xv[u][q];
+        }
+    }
+    float* __restrict__ out = slab + (long)blockIdx.x * slab_stride;
+#pragma unroll
+    for (int a = 0; a < A; ++a) store_cols<NPT>(out + a * N + k0, acc[a]);
+    if (t < A) {                                         // gb partial: the rows in order
+        float sb = 0.f;
+        for (int r = 0; r < nr; ++r) sb += gs[r * A + t];
+        out[A * N + t] = sb;
+    }
+}
+
 }  // namespace
 
 extern "C" {
+
+int phip_out_bwd_wide(float* gW, float* gb, float* gx, const float* g, const float* x, const float* W, int relu_in,
+                      int m, int n, int A) {
+    if (A != 17 || (n != 512 && n != 256) || m <= 0 || gb != gW + (long)A * n || getenv("PPO_NO_WIDE_BWD")) return 0;
+    if ((((uintptr_t)x | (uintptr_t)gx | (uintptr_t)W | (uintptr_t)gW) & 15u) != 0) return 0;
+    ppo::ProfScope ps(PPO_K_GEMM, 4.0 * m * n * A, ppo::gemm_key(3, 1, m, n, A));
+    constexpr int U = 8;
+    int nwg = std::min(512, ppo_divup(m, 16));                // ≥ 16 rows per workgroup
+    const int rows = ppo_divup(ppo_divup(m, nwg), U) * U;
+    nwg = ppo_divup(m, rows);
+    const long stride = ((long)A * n + A + 3) & ~3L;        // slab rows 16-B aligned
+    const size_t lds = sizeof(float) * (size_t)rows * A;
+    PPO_REQUIRE(lds <= 64 * 1024, "phip_out_bwd_wide: rows per workgroup");
+    float* slab = ppo::slab_scratch((size_t)nwg * stride);
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    const bool timed = ppo::take_kernel_events(&e0, &e1);      // one duration: kernel start → reduce end
+    if (n == 512) {
+        if (timed) hipExtLaunchKernelGGL((out_bwd_wide_kernel<17, 2, U>), dim3(nwg), dim3(256), lds, ppo::stream(), e0,
+                                         nullptr, 0, g, x, W, gx, slab, stride, m, rows, relu_in);
+        else hipLaunchKernelGGL((out_bwd_wide_kernel<17, 2, U>), dim3(nwg), dim3(256), lds, ppo::stream(), g, x, W, gx,
+                                slab, stride, m, rows, relu_in);
+    } else {
+        if (timed) hipExtLaunchKernelGGL((out_bwd_wide_kernel<17, 1, U>), dim3(nwg), dim3(256), lds, ppo::stream(), e0,
+                                         nullptr, 0, g, x, W, gx, slab, stride, m, rows, relu_in);
+        else hipLaunchKernelGGL((out_bwd_wide_kernel<17, 1, U>), dim3(nwg), dim3(256), lds, ppo::stream(), g, x, W, gx,
+                                slab, stride, m, rows, relu_in);
+    }
+    PPO_LAUNCH_CHECK();
+    ppo::slab_reduce(slab, gW, (long)A * n + A, stride, nwg, timed ? e1 : nullptr);
+    return 1;
+}
 
 int phip_out_head_supported(int head, int n, int A) {
     if (n != 64 && n != 128 && n != 256 && n != 512 && !(n == 1024 && A == 1)) return 0;

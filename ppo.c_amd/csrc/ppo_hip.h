@@ -133,6 +133,11 @@ void phip_mse(const float* y, const float* t, long count, float* grad, float* d_
 int  phip_out_head_supported(int head, int n, int A);
 /* gemm.hip: 1 when ppo_gemm_tune(·, 1) asked for atomic-free (deterministic) gradient products */
 int  phip_gemm_deterministic(void);
+/* out_head.hip: the backward of a wide output layer (A = 17, n = 512 / 256, fp32) in one pass over the
+ * rows — gx = (g·W) ⊙ 1[x > 0] (relu_in) and gW = gᵀ·x, gb = Σ g through per-workgroup partials;
+ * gb must follow gW in memory (the flat gradient layout); returns 0 when the shape is not taken */
+int  phip_out_bwd_wide(float* gW, float* gb, float* gx, const float* g, const float* x, const float* W, int relu_in,
+                       int m, int n, int A);
 void phip_out_head(int head, int bf16, const void* x, int relu_in, const void* W, const float* b, int m, int n,
                    int A, const float* tgt, const float* log_std, const float* action, const float* adv,
                    const float* old_lp, float eps, float ent_coeff, float* y, void* gx, float* gW, float* gb,

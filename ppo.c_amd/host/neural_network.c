@@ -412,7 +412,11 @@ static void nn_backward_dev_top(NeuralNetwork* nn, const float* d_grad_out, int 
         const int want_gx = i > 0 || want_grad_x0;
         const int relu_in = i > 0 && nn_is_relu(nn, i - 1);
         const unsigned* bits = relu_in && nn->bits_m == m ? act_bits(nn, i) : NULL;   /* this forward's bits */
-        if (use_x3_layer(m, n, l) && phip_x3_supported(2, m, n, l)) {
+        if (i == L - 1 && want_gx && (!relu_in || bits) &&
+            phip_out_bwd_wide(ly->d_grad_weights, ly->d_grad_biases, ly->d_grad_x, g, x, ly->d_weights, relu_in, m, n,
+                              l)) {
+            /* wide output layer (A = 17): grad_x and grad_W in one pass over the rows (out_head.hip) */
+        } else if (use_x3_layer(m, n, l) && phip_x3_supported(2, m, n, l)) {
             phip_x3_bwd_w(ly->d_grad_weights, ly->d_grad_biases, g, x, m, n, l, 1);
             if (want_gx && (!relu_in || bits)) phip_x3_bwd_x(ly->d_grad_x, g, ly->d_weights, bits, m, n, l);
             else if (want_gx) phip_linear_bwd_x_bits(ly->d_grad_x, g, ly->d_weights, ly->d_input, NULL, m, n, l);
