@@ -385,21 +385,95 @@ bool launch_n(const OutArgs& a) {
 // wave-uniform scalar loads, and writes gx = (g·W) ⊙ 1[x > 0]; lanes a < A of wave 0 also sum gb.
 // Each workgroup's gW / gb partial goes to its slab and ppo::slab_reduce sums them in order.  Replaces
 // the paired grad_W + grad_x GEMM launch (x read once for both; HBM ≈ 8·n bytes per row).
-template <int A, int NPT, int U>
-__global__ __launch_bounds__(256) void out_bwd_wide_kernel(const float* __restrict__ g, const float* __restrict__ x,
-                                                           const float* __restrict__ W, float* __restrict__ gx,
-                                                           float* __restrict__ slab, long slab_stride, int m,
-                                                           int rows_per_wg, int relu_in) {
+struct WideArgs {
+    const float* g; const float* x; const float* W; float* gx; float* slab; long slab_stride;
+    int m, rows_per_wg, relu_in;
+    // HEAD: the policy head computed here from μ (the forward's output) — kernels.hip
+    // policy_head_tiled_kernel's per-row arithmetic and its 8 partial sums per column of ∂/∂log σ
+    const float* mu; const float* log_std; const float* action; const float* adv; const float* old_lp;
+    float eps, ent_coeff; float* grad_log_std; float* loss_accum;
+};
+
+// kernels.hip log_prob_row (policy.cu:67-74, double temporaries), on LDS rows
+__device__ __forceinline__ float log_prob_row_p(const float* mu, const float* log_std, const float* a, int A) {
+    const float c = (float)(-0.5 * A * (double)logf((float)(2 * M_PI)));
+    float lp = c;
+    for (int j = 0; j < A; ++j) {
+        const float z = (a[j] - mu[j]) / expf(log_std[j]);
+        lp = (float)((double)lp - ((double)log_std[j] + 0.5 * (double)(z * z)));
+    }
+    return lp;
+}
+
+template <int A, int NPT, int U, bool HEAD>
+__global__ __launch_bounds__(256) void out_bwd_wide_kernel(WideArgs p) {
     constexpr int N = 256 * NPT;
-    extern __shared__ float gs[];                        // this workgroup's rows of g [rows][A]
+    extern __shared__ float gs[];                        // this workgroup's rows of g [rows][A] (+ μ, actions)
+    __shared__ float e2s[32], lss[32], cps[8][32], redl[4];
     const int t = threadIdx.x, k0 = t * NPT;
-    const int r0 = blockIdx.x * rows_per_wg;
-    const int nr = min(m, r0 + rows_per_wg) - r0;
-    for (int e = t; e < nr * A; e += 256) gs[e] = g[(long)r0 * A + e];
+    const int m = p.m;
+    const int r0 = blockIdx.x * p.rows_per_wg;
+    const int nr = min(m, r0 + p.rows_per_wg) - r0;
+    if constexpr (HEAD) {
+        float* mus = gs + p.rows_per_wg * A;
+        float* acts = mus + p.rows_per_wg * A;
+        float* grs = acts + p.rows_per_wg * A;           // ∂L/∂lp per row
+        for (int e = t; e < nr * A; e += 256) {
+            mus[e] = p.mu[(long)r0 * A + e];
+            acts[e] = p.action[(long)r0 * A + e];
+        }
+        if (t < A) {
+            lss[t] = p.log_std[t];
+            e2s[t] = expf(-2 * p.log_std[t]);
+        }
+        __syncthreads();
+        float sv = 0.f;
+        for (int row = t; row < nr; row += 256) {
+            float glp;
+            const float lp = log_prob_row_p(mus + row * A, lss, acts + row * A, A);
+            sv += surrogate(p.adv[r0 + row], lp, p.old_lp[r0 + row], p.eps, m, &glp);
+            grs[row] = glp;
+        }
+        sv = ppo::wave_sum64(sv);
+        if ((t & 63) == 0) redl[t >> 6] = sv;
+        __syncthreads();
+        for (int e = t; e < nr * A; e += 256) {
+            const int row = e / A, j = e - row * A;
+            gs[e] = (acts[e] - mus[e]) * e2s[j] * grs[row];
+        }
+        if (t < 8 * A) {                                 // ∂/∂log σ: 8 partial sums per column
+            const int j = t % A, qq = t / A;
+            float c = 0.f;
+            for (int row = qq; row < nr; row += 8) {
+                const float d = acts[row * A + j] - mus[row * A + j];
+                c += (-1 + d * d * e2s[j]) * grs[row];
+            }
+            cps[qq][j] = c;
+        }
+        __syncthreads();
+        if (t < A) {
+            float v = 0.f;
+            for (int q = 0; q < 8; ++q) v += cps[q][t];
+            if (blockIdx.x == 0) v += -p.ent_coeff;                           // ppo.cu:436-438 (D4)
+            atomicAdd(p.grad_log_std + t, v);
+        }
+        if (t == 0 && p.loss_accum) {
+            const float sl = ((redl[0] + redl[1]) + redl[2]) + redl[3];
+            float contrib = -sl / m;
+            if (blockIdx.x == 0) {
+                float ent = (float)(A * 0.5 * (1 + log(2 * M_PI)));
+                for (int j = 0; j < A; ++j) ent += lss[j];
+                contrib -= p.ent_coeff * ent;
+            }
+            atomicAdd(p.loss_accum, contrib);
+        }
+    } else {
+        for (int e = t; e < nr * A; e += 256) gs[e] = p.g[(long)r0 * A + e];
+    }
     float Wr[A][NPT], acc[A][NPT];
 #pragma unroll
     for (int a = 0; a < A; ++a) {
-        load_cols<NPT>(W + (long)a * N + k0, Wr[a]);
+        load_cols<NPT>(p.W + (long)a * N + k0, Wr[a]);
 #pragma unroll
         for (int q = 0; q < NPT; ++q) acc[a][q] = 0.f;
     }
@@ -408,7 +482,7 @@ __global__ __launch_bounds__(256) void out_bwd_wide_kernel(const float* __restri
         float xv[U][NPT];                                // U rows in flight
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            if (rb + u < nr) load_cols<NPT>(x + (long)(r0 + rb + u) * N + k0, xv[u]);
+            if (rb + u < nr) load_cols<NPT>(p.x + (long)(r0 + rb + u) * N + k0, xv[u]);
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int r = rb + u;
@@ -422,16 +496,16 @@ __global__ __launch_bounds__(256) void out_bwd_wide_kernel(const float* __restri
                 float sacc = 0.f;
 #pragma unroll
                 for (int a = 0; a < A; ++a) sacc += gv[a] * Wr[a][q];
-                o[q] = (!relu_in || xv[u][q] > 0.f) ? sacc : 0.f;
+                o[q] = (!p.relu_in || xv[u][q] > 0.f) ? sacc : 0.f;
             }
-            store_cols<NPT>(gx + (long)(r0 + r) * N + k0, o);
+            store_cols<NPT>(p.gx + (long)(r0 + r) * N + k0, o);
 #pragma unroll
             for (int a = 0; a < A; ++a)
 #pragma unroll
                 for (int q = 0; q < NPT; ++q) acc[a][q] += gv[a] * xv[u][q];
         }
     }
-    float* __restrict__ out = slab + (long)blockIdx.x * slab_stride;
+    float* __restrict__ out = p.slab + (long)blockIdx.x * p.slab_stride;
 #pragma unroll
     for (int a = 0; a < A; ++a) store_cols<NPT>(out + a * N + k0, acc[a]);
     if (t < A) {                                         // gb partial: the rows in order
@@ -445,35 +519,59 @@ __global__ __launch_bounds__(256) void out_bwd_wide_kernel(const float* __restri
 
 extern "C" {
 
-int phip_out_bwd_wide(float* gW, float* gb, float* gx, const float* g, const float* x, const float* W, int relu_in,
-                      int m, int n, int A) {
-    if (A != 17 || (n != 512 && n != 256) || m <= 0 || gb != gW + (long)A * n || getenv("PPO_NO_WIDE_BWD")) return 0;
-    if ((((uintptr_t)x | (uintptr_t)gx | (uintptr_t)W | (uintptr_t)gW) & 15u) != 0) return 0;
+int phip_out_bwd_wide_ok(int m, int n, int A, int head) {
+    if (A != 17 || (n != 512 && n != 256) || m <= 0 || getenv("PPO_NO_WIDE_BWD")) return 0;
+    if (head && getenv("PPO_NO_WIDE_HEAD")) return 0;
+    const int U = 8;
+    const int nwg = std::min(512, ppo_divup(m, 16));
+    const long rows = (long)ppo_divup(ppo_divup(m, nwg), U) * U;
+    return sizeof(float) * rows * (head ? 3 * A + 1 : A) <= 64 * 1024;
+}
+
+static int out_bwd_wide_launch(WideArgs w, float* gW, float* gb, int n, int A, bool head) {
+    const int m = w.m;
+    if (!phip_out_bwd_wide_ok(m, n, A, head) || gb != gW + (long)A * n) return 0;
+    if ((((uintptr_t)w.x | (uintptr_t)w.gx | (uintptr_t)w.W | (uintptr_t)gW) & 15u) != 0) return 0;
     ppo::ProfScope ps(PPO_K_GEMM, 4.0 * m * n * A, ppo::gemm_key(3, 1, m, n, A));
     constexpr int U = 8;
     int nwg = std::min(512, ppo_divup(m, 16));                // ≥ 16 rows per workgroup
     const int rows = ppo_divup(ppo_divup(m, nwg), U) * U;
     nwg = ppo_divup(m, rows);
-    const long stride = ((long)A * n + A + 3) & ~3L;        // slab rows 16-B aligned
-    const size_t lds = sizeof(float) * (size_t)rows * A;
-    PPO_REQUIRE(lds <= 64 * 1024, "phip_out_bwd_wide: rows per workgroup");
-    float* slab = ppo::slab_scratch((size_t)nwg * stride);
+    w.rows_per_wg = rows;
+    w.slab_stride = ((long)A * n + A + 3) & ~3L;              // slab rows 16-B aligned
+    const size_t lds = sizeof(float) * (size_t)rows * (head ? 3 * A + 1 : A);
+    if (lds > 64 * 1024) return 0;                            // (m > 512 · 315 rows: the separate launches)
+    w.slab = ppo::slab_scratch((size_t)nwg * w.slab_stride);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     const bool timed = ppo::take_kernel_events(&e0, &e1);      // one duration: kernel start → reduce end
-    if (n == 512) {
-        if (timed) hipExtLaunchKernelGGL((out_bwd_wide_kernel<17, 2, U>), dim3(nwg), dim3(256), lds, ppo::stream(), e0,
-                                         nullptr, 0, g, x, W, gx, slab, stride, m, rows, relu_in);
-        else hipLaunchKernelGGL((out_bwd_wide_kernel<17, 2, U>), dim3(nwg), dim3(256), lds, ppo::stream(), g, x, W, gx,
-                                slab, stride, m, rows, relu_in);
-    } else {
-        if (timed) hipExtLaunchKernelGGL((out_bwd_wide_kernel<17, 1, U>), dim3(nwg), dim3(256), lds, ppo::stream(), e0,
-                                         nullptr, 0, g, x, W, gx, slab, stride, m, rows, relu_in);
-        else hipLaunchKernelGGL((out_bwd_wide_kernel<17, 1, U>), dim3(nwg), dim3(256), lds, ppo::stream(), g, x, W, gx,
-                                slab, stride, m, rows, relu_in);
-    }
+    auto go = [&](auto kern) {
+        if (timed) hipExtLaunchKernelGGL(kern, dim3(nwg), dim3(256), lds, ppo::stream(), e0, nullptr, 0, w);
+        else hipLaunchKernelGGL(kern, dim3(nwg), dim3(256), lds, ppo::stream(), w);
+    };
+    if (n == 512) head ? go(out_bwd_wide_kernel<17, 2, U, true>) : go(out_bwd_wide_kernel<17, 2, U, false>);
+    else head ? go(out_bwd_wide_kernel<17, 1, U, true>) : go(out_bwd_wide_kernel<17, 1, U, false>);
     PPO_LAUNCH_CHECK();
-    ppo::slab_reduce(slab, gW, (long)A * n + A, stride, nwg, timed ? e1 : nullptr);
+    ppo::slab_reduce(w.slab, gW, (long)A * n + A, w.slab_stride, nwg, timed ? e1 : nullptr);
     return 1;
+}
+
+int phip_out_bwd_wide(float* gW, float* gb, float* gx, const float* g, const float* x, const float* W, int relu_in,
+                      int m, int n, int A) {
+    WideArgs w{};
+    w.g = g; w.x = x; w.W = W; w.gx = gx; w.m = m; w.relu_in = relu_in;
+    return out_bwd_wide_launch(w, gW, gb, n, A, false);
+}
+
+int phip_policy_head_bwd_wide(const float* mu, const float* log_std, const float* action, const float* adv,
+                              const float* old_lp, float eps, float ent_coeff, float* grad_log_std, float* loss_accum,
+                              const float* x, const float* W, int relu_in, float* gW, float* gb, float* gx, int m,
+                              int n, int A) {
+    if (!mu || !log_std || !action || !adv || !old_lp || !grad_log_std) return 0;
+    WideArgs w{};
+    w.x = x; w.W = W; w.gx = gx; w.m = m; w.relu_in = relu_in;
+    w.mu = mu; w.log_std = log_std; w.action = action; w.adv = adv; w.old_lp = old_lp;
+    w.eps = eps; w.ent_coeff = ent_coeff; w.grad_log_std = grad_log_std; w.loss_accum = loss_accum;
+    return out_bwd_wide_launch(w, gW, gb, n, A, true);
 }
 
 int phip_out_head_supported(int head, int n, int A) {

@@ -136,8 +136,16 @@ int  phip_gemm_deterministic(void);
 /* out_head.hip: the backward of a wide output layer (A = 17, n = 512 / 256, fp32) in one pass over the
  * rows — gx = (g·W) ⊙ 1[x > 0] (relu_in) and gW = gᵀ·x, gb = Σ g through per-workgroup partials;
  * gb must follow gW in memory (the flat gradient layout); returns 0 when the shape is not taken */
+/* 1 when the wide pass takes (m rows, width n, A outputs; head: the fused policy head too) */
+int  phip_out_bwd_wide_ok(int m, int n, int A, int head);
 int  phip_out_bwd_wide(float* gW, float* gb, float* gx, const float* g, const float* x, const float* W, int relu_in,
                        int m, int n, int A);
+/* the same pass with the policy head (kernels.hip policy_head_tiled_kernel's arithmetic) computed from μ
+ * first: ∂/∂log σ (+ −c_ent) and the loss accumulated into grad_log_std / loss_accum (atomics) */
+int  phip_policy_head_bwd_wide(const float* mu, const float* log_std, const float* action, const float* adv,
+                               const float* old_lp, float eps, float ent_coeff, float* grad_log_std,
+                               float* loss_accum, const float* x, const float* W, int relu_in, float* gW, float* gb,
+                               float* gx, int m, int n, int A);
 void phip_out_head(int head, int bf16, const void* x, int relu_in, const void* W, const float* b, int m, int n,
                    int A, const float* tgt, const float* log_std, const float* action, const float* adv,
                    const float* old_lp, float eps, float ent_coeff, float* y, void* gx, float* gW, float* gb,

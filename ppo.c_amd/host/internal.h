@@ -57,6 +57,11 @@ void nn_backward_dev_z(NeuralNetwork* nn, const float* d_grad_out, int m, int wa
                        long reduce_extra);
 /* the output layer fused with the loss head (head 0 value / MSE, 1 policy), see neural_network.c */
 int  nn_out_head_ok(const NeuralNetwork* nn, int head);
+int  nn_policy_wide_ok(const NeuralNetwork* nn, int m);
+void nn_policy_wide_step(NeuralNetwork* nn, const float* d_x, const int* d_rows, float* d_xcopy, int m,
+                         int grads_zero, long reduce_extra, const float* log_std, const float* action,
+                         const float* adv, const float* old_lp, float eps, float ent_coeff, float* grad_log_std,
+                         float* loss_accum);
 void nn_out_head_step(NeuralNetwork* nn, int head, const float* d_x, const int* d_rows, float* d_xcopy, int m,
                       int grads_zero, long reduce_extra, const float* tgt, const float* log_std, const float* action,
                       const float* adv, const float* old_lp, float eps, float ent_coeff, float* grad_log_std,

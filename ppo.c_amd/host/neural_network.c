@@ -469,6 +469,36 @@ void nn_out_head_step(NeuralNetwork* nn, int head, const float* d_x, const int* 
     nn_backward_dev_top(nn, ly->d_grad_x, m, 0, 1, reduce_extra, L - 1);
 }
 
+/* The A = 17 policy network (C4): its output layer's backward fused with the policy head
+ * (out_head.hip, phip_policy_head_bwd_wide) — fp32, identity output, at least one hidden layer, the
+ * flat gradient layout (gb after gW), no deterministic-GEMM request (the head's f32 atomics) */
+int nn_policy_wide_ok(const NeuralNetwork* nn, int m) {
+    const int L = nn->num_layers - 1;
+    if (nn->dtype != 0 || L < 2 || nn_is_relu(nn, L - 1) || phip_gemm_deterministic()) return 0;
+    const Layer* ly = &nn->layers[L - 1];
+    if (nn->param_offset[L - 1] % 4 != 0) return 0;                     /* 16-B aligned W / gW */
+    return phip_out_bwd_wide_ok(m, ly->input_size, ly->output_size, 1);
+}
+
+/* forward through every layer, then the policy head + output-layer backward in one pass, then the
+ * hidden layers' backward — the separate path's results (nn_forward_dev_rows → phip_policy_head →
+ * nn_backward_dev_z) up to the order of the output layer's gradient sums */
+void nn_policy_wide_step(NeuralNetwork* nn, const float* d_x, const int* d_rows, float* d_xcopy, int m,
+                         int grads_zero, long reduce_extra, const float* log_std, const float* action,
+                         const float* adv, const float* old_lp, float eps, float ent_coeff, float* grad_log_std,
+                         float* loss_accum) {
+    const int L = nn->num_layers - 1;
+    nn_forward_dev_rows(nn, d_x, d_rows, d_xcopy, m);
+    nn_ensure_grad(nn, m);
+    if (!grads_zero) phip_memset(nn->d_grads, 0, sizeof(float) * (size_t)nn->num_params);
+    Layer* ly = &nn->layers[L - 1];
+    if (!phip_policy_head_bwd_wide(nn->d_output, log_std, action, adv, old_lp, eps, ent_coeff, grad_log_std,
+                                   loss_accum, ly->d_input, ly->d_weights, nn_is_relu(nn, L - 2), ly->d_grad_weights,
+                                   ly->d_grad_biases, ly->d_grad_x, m, ly->input_size, ly->output_size))
+        die("nn_policy_wide_step: the wide head declined a shape nn_policy_wide_ok accepted");
+    nn_backward_dev_top(nn, ly->d_grad_x, m, 0, 1, reduce_extra, L - 1);
+}
+
 /* neural_network.cu:74-105: copies the input into layers[0].d_input first. */
 void forward_propagation_cuda(NeuralNetwork* nn, float* input, int m) {
     nn_ensure_act(nn, m);

@@ -475,7 +475,7 @@ static int ppo_update_tiny(PPO* ppo, PPODev* d, int B, int n_epochs_policy, int 
 typedef struct {
     PPO* ppo;
     PPODev* d;
-    int B, S, A, limit, num_batches, comm, fuse_v, fuse_p;
+    int B, S, A, limit, num_batches, comm, fuse_v, fuse_p, wide_p;
     const int *perms_v, *perms_p;
     const uint64_t *keys_v, *keys_p;
     long nv, np;
@@ -546,6 +546,11 @@ static void policy_step(StepCtx* c, long ip, int* p_zero, int* ls_zero, int tab)
         nn_out_head_step(mu, 1, buf->state_p, d->rows_p, d->states_p, B, *p_zero, c->comm ? align4(A) : -1, NULL,
                          pol->d_log_std, d->actions, d->adv, d->old_lp, ppo->epsilon, ppo->ent_coeff,
                          pol->d_log_std_grad, d->stats + 1);
+    } else if (c->wide_p) { /* A = 17: policy head + output-layer backward in one pass (out_head.hip) */
+        if (!*ls_zero) phip_memset(pol->d_log_std_grad, 0, sizeof(float) * (size_t)A);
+        nn_policy_wide_step(mu, buf->state_p, d->rows_p, d->states_p, B, *p_zero, c->comm ? align4(A) : -1,
+                            pol->d_log_std, d->actions, d->adv, d->old_lp, ppo->epsilon, ppo->ent_coeff,
+                            pol->d_log_std_grad, d->stats + 1);
     } else {
         nn_forward_dev_rows(mu, buf->state_p, d->rows_p, d->states_p, B);
         phip_policy_head(mu->d_output, pol->d_log_std, d->actions, d->adv, d->old_lp, B, A, ppo->epsilon,
@@ -715,8 +720,10 @@ static void ppo_update_body(PPO* ppo, float gamma, int batch_size, int n_epochs_
     const char* serial_env = getenv("PPO_SERIAL");
     const int concurrent = nv > 0 && np > 0 && !(serial_env && *serial_env && *serial_env != '0');
     if (concurrent) phip_side_fork();
-    StepCtx c = {ppo, d, B, S, A, limit, num_batches, comm, nn_out_head_ok(V, 0), nn_out_head_ok(mu, 1),
-                 perms_v, perms_p, keys_v, keys_p, nv, np, NULL, NULL, NULL, NULL, 16, 1, 1};
+    const int fuse_p = nn_out_head_ok(mu, 1);
+    StepCtx c = {ppo, d, B, S, A, limit, num_batches, comm, nn_out_head_ok(V, 0), fuse_p,
+                 !fuse_p && nn_policy_wide_ok(mu, B), perms_v, perms_p, keys_v, keys_p, nv, np, NULL, NULL, NULL,
+                 NULL, 16, 1, 1};
     {
         const char* ge = getenv("PPO_GRAPH_STEPS");
         if (ge && atoi(ge) > 0) c.K = atoi(ge);

@@ -554,10 +554,12 @@ def test_graph_replay_matches_eager(lib, oracle, shuffle_mode, monkeypatch):
 
 
 def test_wide_output_backward_matches_pair(lib, oracle, monkeypatch):
-    """The A = 17 output layer's one-pass backward (out_bwd_wide_kernel: grad_x and grad_W / grad_b from
-    one read of x, per-workgroup partials through the slab reduce) against the paired GEMM launch
-    (PPO_NO_WIDE_BWD=1) from identical state: one policy minibatch of the humanoid config, every policy
-    gradient within the GEMM tolerance (the same products summed in another order)."""
+    """The A = 17 policy head fused with the output layer's one-pass backward (out_bwd_wide_kernel<HEAD>:
+    the head from μ in LDS, then grad_x and grad_W / grad_b from one read of x, per-workgroup partials
+    through the slab reduce) against the separate head launch + paired GEMM launch (PPO_NO_WIDE_BWD=1)
+    from identical state: one policy minibatch of the humanoid config, every policy gradient within the
+    GEMM tolerance (the same products summed in another order), the log σ gradient and the loss sums
+    within reduction rounding."""
     sizes, N = CONFIGS["humanoid"]["sizes"], CONFIGS["humanoid"]["N"]
     out = {}
     for mode in ("1", "0"):
@@ -575,8 +577,10 @@ def test_wide_output_backward_matches_pair(lib, oracle, monkeypatch):
         st = (C.c_double * 7)()
         lib.ppo_read_stats(ppo, st, 7)
         pol = ppo.contents.policy.contents
-        out[mode] = dict(gmu=nn_grads_packed(lib, pol.mu), stats=np.array(st[:4]))
+        out[mode] = dict(gmu=nn_grads_packed(lib, pol.mu), stats=np.array(st[:4]),
+                         gls=ppo_ffi.d2h(lib, pol.d_log_std_grad, F32, sizes[-1]))
         lib.free_ppo(ppo)
     a, b = out["1"], out["0"]
     assert_gemm_close(b["gmu"], a["gmu"], N, "policy grads (wide backward vs paired GEMM)")
+    assert_rel_close(b["gls"], a["gls"], 1e-4, 1e-5 * max(1.0, np.abs(a["gls"]).max()), "log_std grad")
     np.testing.assert_allclose(b["stats"], a["stats"], rtol=1e-5, atol=1e-7)
