@@ -229,6 +229,70 @@ def test_c3_timed_policy_step(lib, oracle, c3):
     assert flips <= mu1.size // 1000
 
 
+# ----------------------------------------------------------------------------- C4: the headline bench update
+C4 = [376, 512, 512, 512, 17]
+
+
+@pytest.fixture(scope="module")
+def c4(lib, oracle):
+    oracle.load(use_openblas=True)
+    oracle.load().ref_blas_threads(16)
+    ppo = bench_ppo(lib, oracle, C4, 256, 4096, seed=4141)
+    yield ppo, 256 * 4096
+    lib.ppo_set_step_limit(ppo, -1, -1)
+    lib.free_ppo(ppo)
+
+
+def test_c4_timed_value_step(lib, oracle, c4):
+    """One value minibatch of the C4 bench update (N = 1,048,576, B = 32768: x3 grids with slab
+    split-K, the fused value head) vs the oracle."""
+    ppo, N = c4
+    B, seed, S = 32768, 73, 376
+    assert lib.ppo_gemm_f32_engine(-1) == 1
+    v0 = nn_params_packed(lib, ppo.contents.V)
+    lib.ppo_set_step_limit(ppo, 1, 0)
+    lib.ppo_update(ppo, 0.99, B, 0, 1, 1, seed)
+    lib.ppo_synchronize()
+    gV, v1 = nn_grads_packed(lib, ppo.contents.V), nn_params_packed(lib, ppo.contents.V)
+    b = ppo.contents.buffer.contents
+    rows = oracle.feistel_perm(N, oracle.splitmix64(seed))[:B]
+    x = _gathered(lib, ppo.contents.V, B, S)
+    np.testing.assert_array_equal(x[:64], ppo_ffi.d2h(lib, b.d_state_p, F32, N * S).reshape(N, S)[rows[:64]])
+    tgt = ppo_ffi.d2h(lib, b.d_adv_target_p, F32, N)[rows]
+    sv = C4[:-1] + [1]
+    g_ref, _ = ref_value_grads(oracle, sv, v0, x, tgt, gpu_relu_masks(lib, ppo.contents.V, x), "C4 value")
+    assert_gemm_close(gV, g_ref, B, "C4 value grads")
+    flips = assert_adam_delta(v1, adam_first_step(v0, g_ref, LR), g_ref, LR, "C4 value params")
+    assert flips <= v1.size // 1000
+
+
+def test_c4_timed_policy_step(lib, oracle, c4):
+    """One policy minibatch of the C4 bench update (A = 17: the policy head fused with the output
+    layer's one-pass backward, out_head.hip) vs the oracle."""
+    ppo, N = c4
+    B, seed, A, S = 32768, 97, 17, 376
+    pol = ppo.contents.policy.contents
+    mu0 = nn_params_packed(lib, pol.mu)
+    ls0 = ppo_ffi.d2h(lib, pol.d_log_std, F32, A)
+    lib.ppo_set_step_limit(ppo, 0, 1)
+    lib.ppo_update(ppo, 0.99, B, 1, 0, 1, seed)
+    lib.ppo_synchronize()
+    gmu, mu1 = nn_grads_packed(lib, pol.mu), nn_params_packed(lib, pol.mu)
+    gls = ppo_ffi.d2h(lib, pol.d_log_std_grad, F32, A)
+    b = ppo.contents.buffer.contents
+    rows = oracle.feistel_perm(N, oracle.splitmix64(seed))[:B]
+    x = _gathered(lib, pol.mu, B, S)
+    a = ppo_ffi.d2h(lib, b.d_action_p, F32, N * A).reshape(N, A)[rows]
+    adv = ppo_ffi.d2h(lib, b.d_advantage_p, F32, N)[rows]
+    old = ppo_ffi.d2h(lib, b.d_logprob_p, F32, N)[rows]
+    g_ref, gls_ref = ref_policy_grads(oracle, C4, mu0, ls0, x, a, adv, old, gpu_relu_masks(lib, pol.mu, x),
+                                      "C4 policy")
+    assert_gemm_close(gmu, g_ref, B, "C4 policy grads")
+    assert_rel_close(gls, gls_ref, 1e-3, 1e-4 * max(1.0, float(np.abs(gls_ref).max())), "C4 log_std grad")
+    flips = assert_adam_delta(mu1, adam_first_step(mu0, g_ref, LR), g_ref, LR, "C4 policy params")
+    assert flips <= mu1.size // 1000
+
+
 # ----------------------------------------------------------------------------- C5: bf16 at the bench shard
 C5 = [1024, 1024, 1024, 1024, 1024, 17]
 ULP = 2.0 ** -8          # bf16 round-to-nearest: relative error ≤ 2^-8 (8 significant bits)
