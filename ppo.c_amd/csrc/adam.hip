@@ -28,9 +28,10 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
 // w16 (bf16 mode): the parameters' bf16 shadow for the first n16 elements, written in the same pass.
 // zero_g: the gradient is cleared once read (ppo_update: the next backward's split-K atomics then
 // accumulate into zeros without a memset launch per minibatch step).
-__global__ void adam_flat_vec_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
-                                     float* __restrict__ v, long n, float step, float b1, float b2, float bc2,
-                                     float scale, __bf16* __restrict__ w16, long n16, int zero_g) {
+__device__ __forceinline__ void adam_vec_body(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
+                                              float* __restrict__ v, long n, float step, float b1, float b2,
+                                              float bc2, float scale, __bf16* __restrict__ w16, long n16,
+                                              int zero_g) {
     typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
     const long n4 = n >> 2;
     for (long i = blockIdx.x * (long)TPB + threadIdx.x; i < n4; i += (long)gridDim.x * TPB) {
@@ -62,6 +63,30 @@ __global__ void adam_flat_vec_kernel(float* __restrict__ p, float* __restrict__ 
         if (zero_g) g[j] = 0.f;
         if (w16 && j < n16) w16[j] = (__bf16)pp;
     }
+}
+
+__global__ void adam_flat_vec_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
+                                     float* __restrict__ v, long n, float step, float b1, float b2, float bc2,
+                                     float scale, __bf16* __restrict__ w16, long n16, int zero_g) {
+    adam_vec_body(p, g, m, v, n, step, b1, b2, bc2, scale, w16, n16, zero_g);
+}
+
+// a second, small flat span in the same launch (the policy step's entropy Adam beside the network's,
+// ppo.cu:440-442 — independent parameters): the last workgroup's first s.n threads, scalar
+struct SideSpan {
+    float* p; float* g; float* m; float* v; int n; float step, bc2, scale; int zero_g;
+};
+__global__ void adam_flat_vec_pair_kernel(float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
+                                          float* __restrict__ v, long n, float step, float b1, float b2, float bc2,
+                                          float scale, __bf16* __restrict__ w16, long n16, int zero_g, SideSpan s) {
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x < s.n) {
+        const int j = threadIdx.x;
+        float pp = s.p[j], mm = s.m[j], vv = s.v[j];
+        adam_elem(pp, s.g[j], mm, vv, s.step, b1, b2, s.bc2, s.scale);
+        s.p[j] = pp; s.m[j] = mm; s.v[j] = vv;
+        if (s.zero_g) s.g[j] = 0.f;
+    }
+    adam_vec_body(p, g, m, v, n, step, b1, b2, bc2, scale, w16, n16, zero_g);
 }
 
 // the flat Adam with its step size / bias correction from the step table (graph replay); which = 0
@@ -173,6 +198,21 @@ void phip_adam_flat_w16(float* p, float* g, float* m, float* v, long n, float lr
         hipLaunchKernelGGL(adam_flat_kernel, dim3(grid_for(n)), dim3(TPB), 0, ppo::stream(), p, g, m, v, n, step,
                            beta1, beta2, bias_correction2, grad_scale);
     }
+    PPO_LAUNCH_CHECK();
+}
+
+void phip_adam_flat_pair(float* p, float* g, float* m, float* v, long n, float lr, float beta1, float beta2,
+                         float bias_correction1, float bias_correction2, float grad_scale, unsigned short* w16,
+                         long n16, int zero_g, float* p2, float* g2, float* m2, float* v2, int n2, float lr2,
+                         float bias_correction1_2, float bias_correction2_2, float grad_scale2, int zero_g2) {
+    PPO_REQUIRE(n > 0 && n2 >= 0 && n2 <= TPB, "phip_adam_flat_pair: spans");
+    PPO_REQUIRE((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15u) == 0 && ((uintptr_t)w16 & 7u) == 0,
+                "phip_adam_flat_pair: the network span must be 16-B aligned");
+    ppo::ProfScope ps(PPO_K_ADAM, 28.0 * (n + n2) + (w16 ? 2.0 * n16 : 0.0) + (zero_g ? 4.0 * n : 0.0));
+    SideSpan s{p2, g2, m2, v2, n2, lr2 / bias_correction1_2, bias_correction2_2, grad_scale2, zero_g2};
+    hipLaunchKernelGGL(adam_flat_vec_pair_kernel, dim3(grid_for((n + 3) / 4)), dim3(TPB), 0, ppo::stream(), p, g, m,
+                       v, n, lr / bias_correction1, beta1, beta2, bias_correction2, grad_scale,
+                       reinterpret_cast<__bf16*>(w16), n16, zero_g, s);
     PPO_LAUNCH_CHECK();
 }
 

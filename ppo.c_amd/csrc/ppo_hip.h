@@ -234,6 +234,12 @@ int  phip_capturing(void);                   /* 1 while a capture is open (profi
 void phip_adam_flat_w16(float* p, float* g, float* m, float* v, long n, float lr, float beta1, float beta2,
                         float bias_correction1, float bias_correction2, float grad_scale, unsigned short* w16,
                         long n16, int zero_g);
+/* the same for a network span (16-B aligned) plus a small second span (≤ 256 floats, any alignment:
+ * the policy step's entropy Adam) with its own step size, in one launch */
+void phip_adam_flat_pair(float* p, float* g, float* m, float* v, long n, float lr, float beta1, float beta2,
+                         float bias_correction1, float bias_correction2, float grad_scale, unsigned short* w16,
+                         long n16, int zero_g, float* p2, float* g2, float* m2, float* v2, int n2, float lr2,
+                         float bias_correction1_2, float bias_correction2_2, float grad_scale2, int zero_g2);
 /* multi-tensor: ptrs/lengths are HOST arrays describing device tensors; m/v are flat */
 void phip_adam_multi(float* const* params, float* const* grads, const int* lengths, int num_tensors,
                      float* m, float* v, float lr, float beta1, float beta2,

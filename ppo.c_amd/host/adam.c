@@ -187,6 +187,29 @@ int adam_update_cuda_w16(Adam* adam, float lr, unsigned short* w16, long n16, in
     return 0;
 }
 
+/* a network's flat Adam (16-B aligned span) and a small flat side Adam (the entropy Adam's log σ) in
+ * one launch; the side's step runs first in the step counters (ppo.cu:440-442 order; the spans are
+ * independent).  Returns bit 0: shadow refreshed, bit 1: network gradients cleared, bit 2: side
+ * gradients cleared; −1 (nothing done) when the pair does not qualify. */
+int adam_update_pair_w16(Adam* adam, float lr, unsigned short* w16, long n16, int zero_g, Adam* side, float lr_side,
+                         int zero_side) {
+    const uintptr_t al = (uintptr_t)adam->weights[0] | (uintptr_t)adam->grad_weights[0] | (uintptr_t)adam->m |
+                         (uintptr_t)adam->v;
+    if (!adam->flat || !side->flat || (al & 15u) || side->span > 256 || side->span < 1 || adam->span < 1 ||
+        adam->beta1 != side->beta1 || adam->beta2 != side->beta2 || ((uintptr_t)w16 & 7u))
+        return -1;
+    float bc1s, bc2s, bc1, bc2;
+    bias_corrections(side, &bc1s, &bc2s);
+    bias_corrections(adam, &bc1, &bc2);
+    nn_note_device_update(adam->weights[0]);
+    nn_note_device_update(side->weights[0]);
+    phip_adam_flat_pair(adam->weights[0], adam->grad_weights[0], adam->m, adam->v, adam->span, lr, adam->beta1,
+                        adam->beta2, bc1, bc2, adam->grad_scale, w16, w16 ? n16 : 0, zero_g, side->weights[0],
+                        side->grad_weights[0], side->m, side->v, (int)side->span, lr_side, bc1s, bc2s,
+                        side->grad_scale, zero_side);
+    return (w16 != NULL) | (zero_g ? 2 : 0) | (zero_side ? 4 : 0);
+}
+
 /* ---------------- checkpoint (adam.cu:172-264 byte layout) ---------------- */
 /* m / v are written packed by tensor (reference order), whatever the padding in HBM. */
 static void moments_to_host(Adam* a, float* m, float* v) {

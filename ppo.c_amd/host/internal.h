@@ -79,6 +79,8 @@ void nn_sync_w16(NeuralNetwork* nn);       /* bf16 mode: refresh the bf16 weight
 void adam_next_step(Adam* a, float lr, float* step, float* bc2);
 /* device Adam that also writes the bf16 shadow w16[0, n16) in the same pass; returns 1 when it did */
 int adam_update_cuda_w16(Adam* adam, float lr, unsigned short* w16, long n16, int zero_g);
+int adam_update_pair_w16(Adam* adam, float lr, unsigned short* w16, long n16, int zero_g, Adam* side, float lr_side,
+                         int zero_side);
 
 /* checkpoint Adam with a known tensor count (n_expected < 0: unknown); rejects mismatches */
 Adam* load_adam_ex(FILE* file, float** weights, float** grad_weights, int* length, int n_expected, bool cuda);

@@ -566,8 +566,22 @@ static void policy_step(StepCtx* c, long ip, int* p_zero, int* ls_zero, int tab)
         *ls_zero = *p_zero = 1;
         return;
     }
-    *ls_zero = ppo->adam_entropy->flat && ppo->adam_entropy->grad_weights[0] == pol->d_log_std_grad &&
-               (adam_update_cuda_w16(ppo->adam_entropy, ppo->lr_policy, NULL, 0, ip + 1 < c->np) & 2);
+    /* both Adams in one launch where they qualify (flat spans, the network's 16-B aligned) */
+    Adam* ap = ppo->adam_policy;
+    const int own = ap->flat && ap->weights[0] == mu->d_params && ap->grad_weights[0] == mu->d_grads;
+    const int fused = mu->dtype == 1 && own;
+    const int ls_own = ppo->adam_entropy->flat && ppo->adam_entropy->grad_weights[0] == pol->d_log_std_grad;
+    const int r = getenv("PPO_NO_ADAM_PAIR") ? -1
+                  : adam_update_pair_w16(ap, ppo->lr_policy, fused ? mu->d_w16 : NULL, mu->num_params,
+                                         ip + 1 < c->np && own, ppo->adam_entropy, ppo->lr_policy,
+                                         ip + 1 < c->np && ls_own);
+    if (r >= 0) {
+        if (!(r & 1) && mu->dtype == 1) nn_sync_w16(mu);
+        *ls_zero = ls_own && (r & 4);
+        *p_zero = (r & 2) != 0;
+        return;
+    }
+    *ls_zero = ls_own && (adam_update_cuda_w16(ppo->adam_entropy, ppo->lr_policy, NULL, 0, ip + 1 < c->np) & 2);
     *p_zero = adam_update_net(ppo->adam_policy, ppo->lr_policy, mu, ip + 1 < c->np);
 }
 
