@@ -777,6 +777,25 @@ __global__ __launch_bounds__(NTH, 1) void gemm_bf16_db_kernel(Args a) {
     epilogue256<OP, BM, BN, TM, TN, NTH, TC>(a, acc, lds, m0, n0, wm, wn, tid, stamp);
 }
 
+// One LDS-DMA piece: 16 B per lane from `g` into the wave's 1 KiB at `l` (global_load_lds_dwordx4).
+// Issued from asm: the compiler's waitcnt pass treats __builtin_amdgcn_global_load_lds as an LDS
+// store of unknown extent and puts `s_waitcnt vmcnt(0)` in front of the next ds_read of ANY image —
+// in the double-buffered loops below the DMA of tile j+2, issued right after the barrier, then had
+// to land before tile j+1's first fragment read, exposing the whole DMA latency once per k-tile.
+// Hidden from that pass, each image is published only by the loops' own `s_waitcnt vmcnt` +
+// barrier (the "memory" clobber keeps the compiler's LDS accesses in program order around it).
+// PPO_G16_BUILTIN_DMA=1 restores the builtin (A/B).
+typedef __attribute__((address_space(3))) void* lds_vptr;
+typedef __attribute__((address_space(1))) void* glb_vptr;
+__device__ __forceinline__ void dma16(glb_vptr g, lds_vptr l) {
+#if defined(PPO_G16_BUILTIN_DMA) && PPO_G16_BUILTIN_DMA
+    __builtin_amdgcn_global_load_lds(g, l, 16, 0, 0);
+#else
+    const unsigned base = __builtin_amdgcn_readfirstlane((unsigned)(unsigned long)l);
+    asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "{m0}"(base) : "memory");
+#endif
+}
+
 // ---------------------------------------------------------------------------
 // LDS-DMA 256×256 tile (forward and grad_x with bf16 operands, K a multiple of 64): each k-tile's A
 // and B images arrive by global_load_lds_dwordx4 (1 KiB per wave-instruction, no VGPR staging, no
@@ -854,11 +873,11 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_dma_kernel(Args a) {
     auto dma = [&](int j, unsigned short* img) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-            __builtin_amdgcn_global_load_lds((g_ptr)(PA + offa[i] + j * BK), (lds_ptr)(img + (4 * w + i) * 512), 16, 0, 0);
+            dma16((g_ptr)(PA + offa[i] + j * BK), (lds_ptr)(img + (4 * w + i) * 512));
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-            __builtin_amdgcn_global_load_lds((g_ptr)(PB + offb[i] + (long)j * kstride_b),
-                                             (lds_ptr)(img + IMG + (4 * w + i) * 512), 16, 0, 0);
+            dma16((g_ptr)(PB + offb[i] + (long)j * kstride_b),
+                  (lds_ptr)(img + IMG + (4 * w + i) * 512));
     };
     // fragment of k-step ks (elements k = 16ks + 8h .. +7) for image row R
     auto frag_k = [&](const unsigned short* img, int R, int ks) {
@@ -994,11 +1013,11 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_dma16_kernel(Args a) {
     auto dma = [&](int j, unsigned short* img) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-            __builtin_amdgcn_global_load_lds((g_ptr)(PA + offa[i] + j * BK), (lds_ptr)(img + (4 * w + i) * 512), 16, 0, 0);
+            dma16((g_ptr)(PA + offa[i] + j * BK), (lds_ptr)(img + (4 * w + i) * 512));
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-            __builtin_amdgcn_global_load_lds((g_ptr)(PB + offb[i] + (long)j * kstride_b),
-                                             (lds_ptr)(img + IMG + (4 * w + i) * 512), 16, 0, 0);
+            dma16((g_ptr)(PB + offb[i] + (long)j * kstride_b),
+                  (lds_ptr)(img + IMG + (4 * w + i) * 512));
     };
     // 16×32 fragment of 32-k step s: row R = block base + (lane & 15), k = 32s + 8(lane >> 4) .. +7
     auto frag_k = [&](const unsigned short* img, int R, int s) {
@@ -1159,11 +1178,11 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_dma_tn_kernel(Args a, float*
     auto dma = [&](int j, unsigned short* img) {
 #pragma unroll
         for (int i = 0; i < PA_; ++i)
-            __builtin_amdgcn_global_load_lds((g_ptr)(PA + offa[i] + j * sa), (lds_ptr)(img + (PA_ * w + i) * 512), 16, 0, 0);
+            dma16((g_ptr)(PA + offa[i] + j * sa), (lds_ptr)(img + (PA_ * w + i) * 512));
 #pragma unroll
         for (int i = 0; i < PB_; ++i)
-            __builtin_amdgcn_global_load_lds((g_ptr)(PB + offb[i] + j * sb),
-                                             (lds_ptr)(img + IMGA + (PB_ * w + i) * 512), 16, 0, 0);
+            dma16((g_ptr)(PB + offb[i] + j * sb),
+                  (lds_ptr)(img + IMGA + (PB_ * w + i) * 512));
     };
     // transposed read of an n-contiguous image of pitch P: lane gets column cbase + (lane & 15),
     // k = 32s + 8(lane >> 4) .. +7
