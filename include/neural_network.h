@@ -94,8 +94,6 @@ typedef struct {
     long   dev_version;     /* bumped by every HBM parameter update */
     long   host_version;    /* dev_version the host mirrors (weights and extra floats) last matched */
     long   host_version_w;  /* dev_version the host weight mirrors last matched (a weights-only sync) */
-    unsigned short* d_wp;   /* x3 engine: the parameters pre-split into three bf16 planes (plane stride num_params) */
-    int    wp_valid;        /* d_wp matches d_params (inside ppo_update, which refreshes it after every Adam) */
 } NeuralNetwork;
 
 typedef struct {

@@ -62,8 +62,6 @@ struct X3Args {
     float* slab;                          // grad_W split-K: per-split partial tiles [splits][M][N] (plain
                                           // stores, summed by slab_reduce_kernel) instead of f32 atomics
     hipEvent_t ev_start, ev_stop;         // explicit dispatch-stamped events (ppo_prof kernel timing)
-    const unsigned short* Bp; long bp_stride;   // BPRE kernels: B (= W) pre-split into three bf16 planes,
-                                                // plane p of element e at Bp[p·bp_stride + e] (W's layout)
 };
 
 // fp32 → bf16 round to nearest even (NaN stays NaN): v_cvt_pk_bf16_f32
@@ -313,18 +311,7 @@ __device__ __forceinline__ void x3_epilogue_out(const X3Args& a, f32x16 (&acc)[T
     else body(std::false_type{});
 }
 
-// One LDS-DMA piece (global_load_lds_dwordx4: 16 B per lane into the wave's 1 KiB at `l`), issued from
-// asm so the compiler's waitcnt pass does not see an LDS store of unknown extent (it would put
-// s_waitcnt vmcnt(0) before the next fragment read); the mainloop publishes each image with its own
-// s_waitcnt vmcnt + barrier.
-typedef __attribute__((address_space(3))) void* lds_vptr;
-typedef __attribute__((address_space(1))) void* glb_vptr;
-__device__ __forceinline__ void x3_dma16(const void* g, void* l) {
-    const unsigned base = __builtin_amdgcn_readfirstlane((unsigned)(unsigned long)(lds_vptr)l);
-    asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"((glb_vptr)g), "{m0}"(base) : "memory");
-}
-
-template <int OP, int BM, int BN, int WARPS_M, int NTH, int OCC, int KG, int ABL = 0, bool BPRE = false>
+template <int OP, int BM, int BN, int WARPS_M, int NTH, int OCC, int KG, int ABL = 0>
 __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     constexpr int NTG = NTH / KG;                                  // threads per k-group
     constexpr int NW = NTG / 64, WARPS_N = NW / WARPS_M;
@@ -377,46 +364,7 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     SA sa;
     SB sb;
     sa.init(a.A, a.lda, OP == OP_NT ? a.ridx : nullptr, m0, a.M, lt);
-    if constexpr (!BPRE) sb.init(a.B, a.ldb, nullptr, n0, a.N, lt);
-    // BPRE: B's three planes arrive by LDS-DMA, already in the image layout (kc_off / mn_off): piece q
-    // (1 KiB, 512 bf16) of the tile's plane block is one wave instruction; each lane's source is the
-    // plane element its 16 B land on (rows clamped into B, k clamped into [0, K): the products of
-    // clamped k meet zeroed A elements)
-    static_assert(!BPRE || (OP != OP_TN && KG == 1), "pre-split B: forward / grad_x");
-    constexpr int NWAVE = NTH / 64;
-    constexpr int PIECES = SB::SIZE / 512, PPW = (PIECES + NWAVE - 1) / NWAVE;
-    static_assert(!BPRE || SB::SIZE % 512 == 0, "B planes: whole 1-KiB pieces");
-    long boff[PPW];
-    int bk[PPW];
-    if constexpr (BPRE) {
-#pragma unroll
-        for (int i = 0; i < PPW; ++i) {
-            const int q = (lt >> 6) + NWAVE * i;
-            const int o = q * 512 + lane * 8;                 // element of the 3-plane block
-            const int p = o / SB::PLANE, e = o % SB::PLANE;
-            if (!B_MN) {                                      // [row][16]: chunk slot cs holds k-chunk cs ^ (row>>3 & 1)
-                const int row = e / BK, c = ((e % BK) >> 3) ^ ((row >> 3) & 1);
-                boff[i] = p * a.bp_stride + (long)min(n0 + row, a.N - 1) * a.ldb;
-                bk[i] = 8 * c;
-            } else {                                          // [k][R]: 16-element segment s holds rows of s ^ sw(k)
-                const int k = e / BN, pos = e % BN;
-                const int row = 16 * ((pos >> 4) ^ SB::sw(k)) + (pos & 15);
-                boff[i] = p * a.bp_stride + min(n0 + row, a.N - 8);
-                bk[i] = k;
-            }
-        }
-    }
-    auto dma_b = [&](unsigned short* img, int k0) {
-#pragma unroll
-        for (int i = 0; i < PPW; ++i) {
-            const int q = (lt >> 6) + NWAVE * i;
-            if (PIECES % NWAVE == 0 || q < PIECES) {
-                const long src = B_MN ? boff[i] + (long)min(k0 + bk[i], a.K - 1) * a.ldb
-                                      : boff[i] + min(k0 + bk[i], a.K - 8);
-                x3_dma16(a.Bp + src, img + SA::SIZE + q * 512);
-            }
-        }
-    };
+    sb.init(a.B, a.ldb, nullptr, n0, a.N, lt);
     const bool do_copy = OP == OP_NT && a.acopy != nullptr && tn == 0;
     // grad_W bias: Σ over this split's k of the A (= g) tile, from the staging registers
     const bool do_bsum = OP == OP_TN && a.gbias != nullptr && tn == 0;
@@ -473,29 +421,14 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     auto stage_b = [&](auto FULLc, unsigned short* img, int k0) {
         constexpr bool FULL = decltype(FULLc)::value;
         if ((ABL & 2) && k0 != kbeg) return;
-        if constexpr (BPRE) dma_b(img, k0);
-        else sb.template store<FULL, (ABL & 64) != 0>(img + SA::SIZE, k0, kend);
+        sb.template store<FULL, (ABL & 64) != 0>(img + SA::SIZE, k0, kend);
     };
     auto load = [&](auto FULLc, int k0) {
         constexpr bool FULL = decltype(FULLc)::value;
         if ((ABL & 8) && k0 != kbeg) return;
         sa.template load<FULL>(k0, kend);
-        if constexpr (!BPRE) sb.template load<FULL>(k0, kend);
+        sb.template load<FULL>(k0, kend);
     };
-    // BPRE: the DMA of the tile staged this iteration has landed (the A loads of the tile after it,
-    // issued later, may still be in flight) before the barrier that publishes it
-    auto dma_wait = [&](bool more) {
-        if constexpr (BPRE) {
-            if (more) {
-                if constexpr (SA::NV == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-                else if constexpr (SA::NV == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-                else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-            } else {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-        }
-    };
-    static_assert(!BPRE || SA::NV == 1 || SA::NV == 2 || SA::NV == 4, "dma_wait: A loads per thread");
     using T = std::true_type;
     using F = std::false_type;
     auto load_t = [&](int j) {
@@ -578,7 +511,6 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
 #ifdef PPO_X3_PRIO
         __builtin_amdgcn_s_setprio(0);
 #endif
-        dma_wait(has3);
         __syncthreads();
     };
     auto mainloop = [&](auto COPYc) {
@@ -588,7 +520,6 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
         if (NK > 0) { load_t(0); stage_a_t(COPYc, cur, 0); stage_b_t(cur, 0); }
         if (NK > 1) { load_t(1); stage_a_t(COPYc, n1, 1); stage_b_t(n1, 1); }
         if (NK > 2) load_t(2);
-        dma_wait(NK > 2);
         __syncthreads();
         if (NK > 0) { rd_a(cur, 2); rd_b(cur, 0); rd_b(cur, 2); rd_a(cur, 0); }
         if (ABL & 32) stamp(1);
@@ -760,7 +691,7 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
 int g_x3_ablate = -1;
 #endif
 
-template <int OP, int BM, int BN, int WARPS_M, int NTH, int OCC, int KG, int ABL = 0, bool BPRE = false>
+template <int OP, int BM, int BN, int WARPS_M, int NTH, int OCC, int KG, int ABL = 0>
 void launch_x3(X3Args a) {
     a.tiles_m = ppo_divup(a.M, BM);
     a.tiles_n = ppo_divup(a.N, BN);
@@ -772,7 +703,7 @@ void launch_x3(X3Args a) {
     using SB = StageX3<BN, OP != OP_NT, NTH / KG>;
     constexpr size_t lds = (size_t)KG * 3 * sizeof(unsigned short) * (SA::SIZE + SB::SIZE);   // 3-stage ring
     static_assert(lds <= 160 * 1024, "gemm_x3: LDS images exceed 160 KiB");
-    auto kern = gemm_x3_kernel<OP, BM, BN, WARPS_M, NTH, OCC, KG, ABL, BPRE>;
+    auto kern = gemm_x3_kernel<OP, BM, BN, WARPS_M, NTH, OCC, KG, ABL>;
     if (lds > 64 * 1024) {
         static bool attr = false;                      // once per instantiation
         if (!attr) {
@@ -834,18 +765,8 @@ constexpr CfgX3 kCfgX3[] = {{256, 256, 1, 1}, {128, 128, 1, 2}, {128, 128, 1, 1}
 int g_force_x3 = -1;
 int g_split_x3 = 0;
 
-template <int OP, bool BPRE = false>
+template <int OP>
 void launch_cfg_x3(int c, const X3Args& a) {
-    if constexpr (BPRE) {
-        static_assert(OP != OP_TN, "pre-split B: forward / grad_x (B = W)");
-        switch (c) {
-            case 0: launch_x3<OP, 256, 256, 4, 512, 2, 1, 0, true>(a); break;
-            case 2: launch_x3<OP, 128, 128, 4, 512, 2, 1, 0, true>(a); break;
-            case 4: launch_x3<OP, 64, 64, 2, 256, 4, 1, 0, true>(a); break;
-            default: launch_x3<OP, 128, 128, 2, 256, 2, 1, 0, true>(a); break;
-        }
-        return;
-    }
 #ifdef PPO_X3_DIAG
     if (g_x3_ablate < 0) {
         const char* e = getenv("PPO_X3_ABLATE");
@@ -895,25 +816,6 @@ int pick_x3(int M, int N, int op) {
 
 inline bool al16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
-// the three-plane split of a contiguous fp32 array (split4, so bit-identical to the kernels' own
-// split at staging): plane p of element e at dst[p·pst + e]
-__global__ __launch_bounds__(256) void split_planes_kernel(unsigned short* __restrict__ dst, long pst,
-                                                           const float* __restrict__ src, long n) {
-    const long n4 = n >> 2;
-    for (long i = blockIdx.x * 256L + threadIdx.x; i < n4; i += (long)gridDim.x * 256) {
-        u32x2 p0, p1, p2;
-        split4(reinterpret_cast<const f32x4*>(src)[i], p0, p1, p2);
-        reinterpret_cast<u32x2*>(dst)[i] = p0;
-        reinterpret_cast<u32x2*>(dst + pst)[i] = p1;
-        reinterpret_cast<u32x2*>(dst + 2 * pst)[i] = p2;
-    }
-}
-
-// W pre-split usable by the BPRE kernels: 16-B aligned planes, 8-element rows and k
-inline bool bpre_ok(const unsigned short* Wp, long stride, int K, int N, int ldb) {
-    return Wp && ((uintptr_t)Wp & 15u) == 0 && stride % 8 == 0 && K % 8 == 0 && N % 8 == 0 && ldb % 8 == 0 && K >= 8;
-}
-
 }  // namespace
 
 namespace ppo {
@@ -958,50 +860,6 @@ int phip_x3_supported(int op, int m, int n, int l) {
     if (op == OP_NT) return n % 4 == 0 && l % 4 == 0;          // K = n; W rows l (k-contiguous)
     if (op == OP_NN) return l % 4 == 0 && n % 4 == 0;          // K = l; W row-contiguous along n
     return n % 4 == 0 && l % 4 == 0;                           // K = m; g rows l, x rows n
-}
-
-// W into three bf16 planes (plane stride `plane_stride` elements), n % 4 == 0, 16-B aligned
-void phip_x3_split_planes(unsigned short* dst, long plane_stride, const float* src, long n) {
-    if (n <= 0) return;
-    PPO_REQUIRE(n % 4 == 0 && plane_stride % 4 == 0 && al16(src) && ((uintptr_t)dst & 7u) == 0,
-                "phip_x3_split_planes: operands");
-    const long g = std::min<long>((n / 4 + 255) / 256, 2048);
-    hipLaunchKernelGGL(split_planes_kernel, dim3((unsigned)g), dim3(256), 0, ppo::stream(), dst, plane_stride, src, n);
-    PPO_LAUNCH_CHECK();
-}
-
-// Wp (optional): W already split into three bf16 planes (phip_x3_split_planes), plane p of element e
-// at Wp[p·wp_stride + e]; the kernel then stages W by LDS-DMA with no split VALU, no VGPR staging and
-// no ds_write (every row tile of the product re-split the same W: 128 times per C4 launch)
-void phip_x3_fwd_p(float* y, const float* x, const int* ridx, float* xcopy, const float* W,
-                   const unsigned short* Wp, long wp_stride, const float* b, int m, int n, int l, int relu,
-                   unsigned* bits) {
-    if (m <= 0 || l <= 0) return;
-    PPO_REQUIRE(y && x && W && n > 0 && n % 4 == 0 && al16(x) && al16(W), "phip_x3_fwd: unsupported operands");
-    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l, ppo::gemm_key(0, 1, m, n, l));
-    X3Args a{};
-    a.A = x; a.lda = n; a.B = W; a.ldb = n; a.C = y; a.ldc = l;
-    a.M = m; a.N = l; a.K = n; a.kchunk = n; a.splits = 1;
-    a.bias = b; a.relu = relu; a.ridx = ridx; a.acopy = ridx ? xcopy : nullptr;
-    a.bits_out = relu ? bits : nullptr; a.wpr = ppo_divup(l, 32);
-    a.Bp = Wp; a.bp_stride = wp_stride;
-    if (bpre_ok(Wp, wp_stride, n, l, n)) launch_cfg_x3<OP_NT, true>(pick_x3(m, l, OP_NT), a);
-    else launch_cfg_x3<OP_NT>(pick_x3(m, l, OP_NT), a);
-}
-
-void phip_x3_bwd_x_p(float* gx, const float* g, const float* W, const unsigned short* Wp, long wp_stride,
-                     const unsigned* bits, int m, int n, int l) {
-    if (m <= 0 || n <= 0) return;
-    PPO_REQUIRE(gx && g && W && l > 0 && l % 4 == 0 && n % 4 == 0 && al16(g) && al16(W),
-                "phip_x3_bwd_x: unsupported operands");
-    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l, ppo::gemm_key(1, 1, m, n, l));
-    X3Args a{};
-    a.A = g; a.lda = l; a.B = W; a.ldb = n; a.C = gx; a.ldc = n;
-    a.M = m; a.N = n; a.K = l; a.kchunk = l; a.splits = 1;
-    a.bits_in = bits; a.wpr = ppo_divup(n, 32);
-    a.Bp = Wp; a.bp_stride = wp_stride;
-    if (bpre_ok(Wp, wp_stride, l, n, n)) launch_cfg_x3<OP_NN, true>(pick_x3(m, n, OP_NN), a);
-    else launch_cfg_x3<OP_NN>(pick_x3(m, n, OP_NN), a);
 }
 
 void phip_x3_fwd(float* y, const float* x, const int* ridx, float* xcopy, const float* W, const float* b, int m,
@@ -1109,11 +967,6 @@ double ppo_bench_gemm_x3(int op, int m, int n, int l, int iters, int cfg, int sp
     phip_fill_uniform(y, (long)sy, 3, -1.f, 1.f);
     phip_fill_uniform(b, (long)std::max(l, n), 4, -0.1f, 0.1f);
     phip_memset(bits, 0xff, 4 * (size_t)m * ppo_divup(std::max(l, n), 32));
-    unsigned short* wp = nullptr;
-    if (op >= 4) {
-        wp = (unsigned short*)phip_malloc(2 * 3 * sw);
-        phip_x3_split_planes(wp, (long)sw, W, (long)sw);
-    }
     const int saved = g_force_x3, saved_split = g_split_x3;
     g_force_x3 = cfg;
     g_split_x3 = splitk_target;
@@ -1121,8 +974,6 @@ double ppo_bench_gemm_x3(int op, int m, int n, int l, int iters, int cfg, int sp
         if (op == 0) phip_x3_fwd(y, x, nullptr, nullptr, W, b, m, n, l, 1, bits);
         else if (op == 3) phip_x3_fwd(y, x, nullptr, nullptr, W, b, m, n, l, 0, nullptr);
         else if (op == 1) phip_x3_bwd_x(x, y, W, bits, m, n, l);
-        else if (op == 4) phip_x3_fwd_p(y, x, nullptr, nullptr, W, wp, (long)sw, b, m, n, l, 1, bits);
-        else if (op == 5) phip_x3_bwd_x_p(x, y, W, wp, (long)sw, bits, m, n, l);
         else phip_x3_bwd_w(gw, b, y, x, m, n, l, 0);
     };
     for (int i = 0; i < 3; ++i) run();
@@ -1139,7 +990,7 @@ double ppo_bench_gemm_x3(int op, int m, int n, int l, int iters, int cfg, int sp
     PPO_CHECK(hipEventDestroy(e1));
     g_force_x3 = saved;
     g_split_x3 = saved_split;
-    phip_free(x); phip_free(W); phip_free(y); phip_free(b); phip_free(gw); phip_free(bits); phip_free(wp);
+    phip_free(x); phip_free(W); phip_free(y); phip_free(b); phip_free(gw); phip_free(bits);
     return 1000.0 * ms / (iters > 0 ? iters : 1);
 }
 

@@ -77,14 +77,6 @@ int  phip_x3_supported(int op, int m, int n, int l);
 void phip_x3_fwd(float* y, const float* x, const int* ridx, float* xcopy, const float* W, const float* b, int m,
                  int n, int l, int relu, unsigned* bits);
 void phip_x3_bwd_x(float* gx, const float* g, const float* W, const unsigned* bits, int m, int n, int l);
-/* the same with W pre-split into three bf16 planes (Wp + p·wp_stride; NULL or unusable: split in the
- * kernel), and the split itself */
-void phip_x3_fwd_p(float* y, const float* x, const int* ridx, float* xcopy, const float* W,
-                   const unsigned short* Wp, long wp_stride, const float* b, int m, int n, int l, int relu,
-                   unsigned* bits);
-void phip_x3_bwd_x_p(float* gx, const float* g, const float* W, const unsigned short* Wp, long wp_stride,
-                     const unsigned* bits, int m, int n, int l);
-void phip_x3_split_planes(unsigned short* dst, long plane_stride, const float* src, long n);
 void phip_x3_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, int n, int l, int zeroed);
 /* dst[i, :] = bf16(src[rows[i], :]) for i < m (S % 4 == 0): layer 0's gather in bf16 mode */
 void phip_gather_rows_bf16(unsigned short* dst, const float* src, const int* rows, int m, int S);

@@ -74,11 +74,6 @@ void nn_host_sync(NeuralNetwork* nn, float* extra); /* before a host-pointer ent
 void nn_sync_extra_snapshot(NeuralNetwork* nn, const float* extra);
 void policy_host_sync(GaussianPolicy* p);
 void nn_sync_w16(NeuralNetwork* nn);       /* bf16 mode: refresh the bf16 weight shadow */
-/* x3 weight planes (fp32 mode, x3 engine): valid from nn_planes_begin to nn_planes_end (ppo_update);
- * nn_planes_refresh re-splits them after a parameter update (no-op when not valid) */
-void nn_planes_begin(NeuralNetwork* nn);
-void nn_planes_refresh(NeuralNetwork* nn);
-void nn_planes_end(NeuralNetwork* nn);
 
 /* adam.c */
 void adam_next_step(Adam* a, float lr, float* step, float* bc2);

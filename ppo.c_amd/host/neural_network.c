@@ -294,31 +294,6 @@ void lin_bwd_w(float* gW, const float* g, const float* x, int m, int n, int l) {
     else phip_linear_bwd_w(gW, NULL, g, x, m, n, l);
 }
 
-/* x3 weight planes: inside ppo_update libppo owns every parameter write, so the parameters are split
- * into three bf16 planes once per Adam step (nn_planes_refresh, one launch) and the forward / grad_x
- * kernels stage W from them by LDS-DMA — instead of every row tile of every product re-splitting
- * the same W (128 times per C4 launch).  Outside the update (the reference API, host pushes) the
- * kernels split W as they stage it.  PPO_X3_NO_WPLANES=1 disables the planes (A/B). */
-static const unsigned short* nn_wplanes(const NeuralNetwork* nn, int i) {
-    return nn->wp_valid ? nn->d_wp + nn->param_offset[i] : NULL;
-}
-
-void nn_planes_begin(NeuralNetwork* nn) {
-    const char* e = getenv("PPO_X3_NO_WPLANES");    /* read per update (tests toggle it) */
-    const int off = e && *e && *e != '0';
-    nn->wp_valid = 0;
-    if (off || nn->dtype != 0 || ppo_gemm_f32_engine(-1) != 1 || nn->num_params % 8) return;
-    if (!nn->d_wp) nn->d_wp = (unsigned short*)phip_malloc(sizeof(unsigned short) * 3 * (size_t)nn->num_params);
-    nn->wp_valid = 1;
-    nn_planes_refresh(nn);
-}
-
-void nn_planes_refresh(NeuralNetwork* nn) {
-    if (nn->wp_valid) phip_x3_split_planes(nn->d_wp, nn->num_params, nn->d_params, nn->num_params);
-}
-
-void nn_planes_end(NeuralNetwork* nn) { nn->wp_valid = 0; }
-
 /* forward through the first `upto` linear layers (fp32 storage; upto = L: the whole network) */
 static void nn_forward_dev_upto(NeuralNetwork* nn, const float* d_x, const int* d_rows, float* d_xcopy, int m,
                                 int upto);
@@ -346,8 +321,7 @@ static void nn_forward_dev_upto(NeuralNetwork* nn, const float* d_x, const int* 
         float* out = nn->layers[i + 1].d_input;
         const int n = ly->input_size, l = ly->output_size;
         if (use_x3_layer(m, n, l) && phip_x3_supported(0, m, n, l)) {
-            phip_x3_fwd_p(out, in, i == 0 ? d_rows : NULL, i == 0 ? d_xcopy : NULL, ly->d_weights, nn_wplanes(nn, i),
-                          nn->num_params, ly->d_biases, m, n,
+            phip_x3_fwd(out, in, i == 0 ? d_rows : NULL, i == 0 ? d_xcopy : NULL, ly->d_weights, ly->d_biases, m, n,
                         l, nn_is_relu(nn, i), act_bits(nn, i + 1));
         } else if (i == 0 && d_rows) {
             phip_linear_fwd_gather(out, in, d_rows, d_xcopy, ly->d_weights, ly->d_biases, m, n, l, nn_is_relu(nn, i),
@@ -444,8 +418,7 @@ static void nn_backward_dev_top(NeuralNetwork* nn, const float* d_grad_out, int 
             /* wide output layer (A = 17): grad_x and grad_W in one pass over the rows (out_head.hip) */
         } else if (use_x3_layer(m, n, l) && phip_x3_supported(2, m, n, l)) {
             phip_x3_bwd_w(ly->d_grad_weights, ly->d_grad_biases, g, x, m, n, l, 1);
-            if (want_gx && (!relu_in || bits))
-                phip_x3_bwd_x_p(ly->d_grad_x, g, ly->d_weights, nn_wplanes(nn, i), nn->num_params, bits, m, n, l);
+            if (want_gx && (!relu_in || bits)) phip_x3_bwd_x(ly->d_grad_x, g, ly->d_weights, bits, m, n, l);
             else if (want_gx) phip_linear_bwd_x_bits(ly->d_grad_x, g, ly->d_weights, ly->d_input, NULL, m, n, l);
         } else if (want_gx && (!relu_in || bits)) {
             phip_linear_bwd_pair(ly->d_grad_weights, ly->d_grad_biases, ly->d_grad_x, g, x, ly->d_weights, bits, m, n,
@@ -634,7 +607,6 @@ void free_neural_network(NeuralNetwork* nn) {
     }
     phip_free(nn->d_act_bits);
     phip_free(nn->d_w16);
-    phip_free(nn->d_wp);
     phip_free(nn->d_tiny_wt);
     phip_free(nn->d_params);
     phip_free(nn->d_grads);

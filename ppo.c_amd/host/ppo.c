@@ -332,7 +332,6 @@ static int adam_update_net(Adam* adam, float lr, NeuralNetwork* nn, int zero_gra
     const int fused = nn->dtype == 1 && own;
     const int r = adam_update_cuda_w16(adam, lr, fused ? nn->d_w16 : NULL, nn->num_params, zero_grads && own);
     if (!(r & 1) && nn->dtype == 1) nn_sync_w16(nn);
-    nn_planes_refresh(nn);
     return (r & 2) != 0;                 /* the network's gradients are zero again */
 }
 
@@ -345,7 +344,6 @@ static void adam_net_tab(Adam* adam, NeuralNetwork* nn, PPODev* d, int ph, int w
                        (unsigned*)(d->ctr + 2 + ph), which, adam->beta1, adam->beta2,
                        adam->grad_scale, fused ? nn->d_w16 : NULL, fused ? nn->num_params : 0, 1);
     nn_note_device_update(adam->weights[0]);
-    if (nn) nn_planes_refresh(nn);
 }
 
 static float* tiny_steps(PPODev* d, int slot, Adam* adam, float lr, int n) {
@@ -579,7 +577,6 @@ static void policy_step(StepCtx* c, long ip, int* p_zero, int* ls_zero, int tab)
                                          ip + 1 < c->np && ls_own);
     if (r >= 0) {
         if (!(r & 1) && mu->dtype == 1) nn_sync_w16(mu);
-        nn_planes_refresh(mu);
         *ls_zero = ls_own && (r & 4);
         *p_zero = (r & 2) != 0;
         return;
@@ -680,11 +677,7 @@ static void ppo_update_body(PPO* ppo, float gamma, int batch_size, int n_epochs_
 void ppo_update(void* vppo, float gamma, int batch_size, int n_epochs_policy, int n_epochs_value, int shuffle_mode,
                 unsigned long long seed) {
     PPO* ppo = (PPO*)vppo;
-    nn_planes_begin(ppo->V);             /* x3 weight planes kept current by every Adam of the update */
-    nn_planes_begin(ppo->policy->mu);
     ppo_update_body(ppo, gamma, batch_size, n_epochs_policy, n_epochs_value, shuffle_mode, seed);
-    nn_planes_end(ppo->V);
-    nn_planes_end(ppo->policy->mu);
     ppo->V->dev_version++;               /* HBM parameters moved (also by the single-workgroup path) */
     ppo->policy->mu->dev_version++;
 }

@@ -43,8 +43,7 @@ class NeuralNetwork(C.Structure):
                 ("bits_m", C.c_int), ("dtype", C.c_int), ("x0_dtype", C.c_int), ("d_w16", C.c_void_p),
                 ("d_tiny_wt", c_float_p), ("tiny_wt_cap", C.c_long),
                 ("h_sync", c_float_p), ("dev_version", C.c_long),
-                ("host_version", C.c_long), ("host_version_w", C.c_long),
-                ("d_wp", C.c_void_p), ("wp_valid", C.c_int)]
+                ("host_version", C.c_long), ("host_version_w", C.c_long)]
 
 
 class GaussianPolicy(C.Structure):
