@@ -1466,6 +1466,8 @@ inline int epl(int t) { return t ? 8 : 4; }
 // PPO_G16_TN=0 keeps the register-staged kernel, PPO_G16_TN_BN=128|256 forces the tile width
 int g_tn_dma = [] { const char* e = getenv("PPO_G16_TN"); return e ? atoi(e) : 1; }();
 int g_tn_bn = [] { const char* e = getenv("PPO_G16_TN_BN"); return e ? atoi(e) : 0; }();
+// workgroup target of the DMA TN split-K grid (PPO_G16_TN_TARGET; default one per CU)
+int g_tn_target = [] { const char* e = getenv("PPO_G16_TN_TARGET"); return e && atoi(e) > 0 ? atoi(e) : 256; }();
 
 bool launch_dma_tn(float* gW, float* gb, const void* g, const void* x, int m, int n, int l, int zeroed) {
     if (g_tn_dma == 0 || dma16_setting() == 0 || g_force16 >= 0) return false;
@@ -1479,7 +1481,7 @@ bool launch_dma_tn(float* gW, float* gb, const void* g, const void* x, int m, in
     a.tiles_m = l / 256;
     a.tiles_n = n / BN;
     const long tiles = (long)a.tiles_m * a.tiles_n;
-    const int target = g_split16 > 0 ? g_split16 : 256;              // one workgroup per CU
+    const int target = g_split16 > 0 ? g_split16 : g_tn_target;
     int splits = (int)std::max<long>(1, target / tiles);
     splits = std::min(splits, std::max(1, m / (4 * 64)));              // ≥ 4 k-tiles per split
     a.kchunk = ppo_divup(ppo_divup(m, splits), 64) * 64;
