@@ -351,8 +351,9 @@ void launch(const OutArgs& a) {
             attr = true;
         }
     }
-    // about 16 rows per wave slot, at most 1024 workgroups
-    int grid = ppo_divup(a.m, SLOTS * 16);
+    // about 16 rows per wave slot (PPO_OUTHEAD_RPS), at most 1024 workgroups
+    static const int rps = [] { const char* e = getenv("PPO_OUTHEAD_RPS"); return e && atoi(e) > 0 ? atoi(e) : 16; }();
+    int grid = ppo_divup(a.m, SLOTS * rps);
     if (grid > 1024) grid = 1024;
     if (grid < 1) grid = 1;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(NTH), lds, ppo::stream(), a);
