@@ -290,7 +290,11 @@ __device__ __forceinline__ void x3_epilogue_out(const X3Args& a, f32x16 (&acc)[T
                     if (OP == OP_NT) {
                         v += bcol[j];
                         if (a.relu) v = v > 0.f ? v : 0.f;
+#ifdef PPO_X3_NTSTORE
+                        if (ok) __builtin_nontemporal_store(v, dst);
+#else
                         if (ok) *dst = v;
+#endif
                         if constexpr (BITS) {
                             const unsigned long long bb = __ballot(ok && v > 0.f);
                             const unsigned half = h ? (unsigned)(bb >> 32) : (unsigned)bb;
@@ -298,7 +302,11 @@ __device__ __forceinline__ void x3_epilogue_out(const X3Args& a, f32x16 (&acc)[T
                         }
                     } else {
                         if (masked && !((mk[(lr0 + dr) * WPT + ((c0 - n0) >> 5)] >> r) & 1u)) v = 0.f;
+#ifdef PPO_X3_NTSTORE
+                        if (ok) __builtin_nontemporal_store(v, dst);
+#else
                         if (ok) *dst = v;
+#endif
                     }
                 }
                 if (BITS && r < 16) {
