@@ -51,6 +51,9 @@ METRIC = "PPO updates/sec + env-steps/sec on 4096×256 synthetic rollout, 1/2/4/
 PEAK_FP32_MFMA_TFLOPS = 157.3          # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 (spec; 155 measured)
 PEAK_BF16_MFMA_TFLOPS = 2500.0         # MI355X_MICROARCH.md: dense bf16 MFMA (spec, no sparsity)
 DTYPE = {"c5": "bf16"}                 # compute precision per config (default fp32)
+# configs whose CONFIGS entry is ONE rank's shard of BASELINE.json's rollout: C5 is 8192 × 512 envs over
+# 8 MI355X (B = 131072 global), i.e. 8192 × 64 envs and B / 8 = 16384 rows per rank per step
+SHARD_OF = {"c5": 8, "c5f32": 8}
 PEAK_HBM_GBPS = 8000.0
 # x3 engine (fp32 mode's default GEMMs): six bf16-MFMA products per fp32 product, so the MFMA bound
 # of the fp32 algorithmic FLOPs is the dense bf16 peak / 6
@@ -108,6 +111,23 @@ def pmc_traffic():
     return d, os.path.relpath(files[-1], ROOT)
 
 
+def cpu_info():
+    """CPU model (/proc/cpuinfo), the machine's logical CPUs and the ones this process may use."""
+    model = platform.machine()
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = os.cpu_count() or 1
+    return model, os.cpu_count() or 1, usable
+
+
 def cpu_baseline(lib, ppo, S, H, A, N, B, sample_envs=16, steps=2):
     """The oracle (plain-C restatement of the reference CPU path, OpenBLAS sgemm, 1 thread) on a bounded
     sample of the same workload; extrapolated to one full update with the update formula."""
@@ -161,16 +181,18 @@ def cpu_baseline(lib, ppo, S, H, A, N, B, sample_envs=16, steps=2):
     r, t_update, sample_s = timed(1)
     # SURVEY §8d also asks for an all-cores run: the same sample with OpenBLAS on every core this
     # process may use (the box's share: OMP_NUM_THREADS; GAE and the element-wise code stay serial C)
-    cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    model, nproc, usable = cpu_info()
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, usable)
     _, t_all, sample_all = timed(cores)
     return {
         "value": N / t_update, "unit": "env-steps/s", "cores": 1, "kind": "port",
         "sample": (f"oracle (C restatement of the reference CPU path, {blas}, 1 thread): GAE over {Ns} "
                    f"transitions + {r['n_v']} value + {r['n_p']} policy minibatches at B={Bs}, "
                    f"extrapolated to a full update (t={t_update:.1f}s); sample took {sample_s:.1f}s"),
-        "cpu": platform.processor() or platform.machine(),
+        "cpu": model, "nproc": nproc, "usable_cpus": usable,
         "all_cores": {"value": N / t_all, "unit": "env-steps/s", "cores": cores,
-                      "sample": f"same sample, OpenBLAS on {cores} threads (t={t_all:.1f}s extrapolated; "
+                      "sample": f"same sample, OpenBLAS on {cores} threads (the process's share: OMP_NUM_THREADS "
+                                f"or min(16, usable CPUs); the machine has {nproc}) (t={t_all:.1f}s extrapolated; "
                                 f"sample took {sample_all:.1f}s)"},
     }
 
@@ -232,6 +254,7 @@ def main():
             raise SystemExit(f"ppo_comm_init (self) failed: {LIB.ppo_last_error().decode()}")
 
     S, H, A, T, E, B = CONFIGS[args.config]
+    shard_of = SHARD_OF.get(args.config, 1)
     split = world if world > 1 else max(1, args.emulate_world)
     if args.weak:
         split = 1
@@ -333,11 +356,17 @@ def main():
         n_sh = min(cap, LIB.ppo_prof_shapes(keys, kms, kl, kw, cap))
         ops = ["forward", "grad_x", "grad_W", "grad_W+grad_x"]
         engines = ["exact-fp32", "x3", "bf16"]
+        issued_sh = (C.c_long * cap)()
+        LIB.ppo_prof_shape_issued(keys, issued_sh, n_sh)
         for i in range(n_sh):
             k = keys[i]
+            avg_ms = kms[i] / kl[i]
+            # the sampled average of the shape × the launches of it the update really issued: one
+            # sampled launch of a rare shape (the 1M-row GAE forward) cannot outweigh a frequent one
             shapes.append({"op": ops[(k >> 60) & 0xF], "engine": engines[(k >> 56) & 0xF], "m": (k >> 32) & 0xFFFFFF,
-                           "n": (k >> 16) & 0xFFFF, "l": k & 0xFFFF, "launches": kl[i], "ms": kms[i],
-                           "avg_us": 1000.0 * kms[i] / kl[i], "tflops": kw[i] / (kms[i] * 1e-3) / 1e12})
+                           "n": (k >> 16) & 0xFFFF, "l": k & 0xFFFF, "sampled_launches": kl[i],
+                           "launches": issued_sh[i], "ms": avg_ms * issued_sh[i], "avg_us": 1000.0 * avg_ms,
+                           "work_per_launch": kw[i] / kl[i], "tflops": kw[i] / (kms[i] * 1e-3) / 1e12})
         shapes.sort(key=lambda d: -d["ms"])
 
     t_update = elapsed / args.steps
@@ -372,12 +401,18 @@ def main():
         "dtype": dtype,
         "data": "synthetic (seeded device generator: obs U(-1,1), actions from the policy, rewards 0.1·N(0,1), "
                 "terminated Bernoulli(1/500), truncated at env-segment ends); random-init weights",
-        "config": {"workload": f"{args.config}: {S}->{'x'.join(map(str, H))}->{A} MLP (policy + value), "
+        "config": {"workload": f"{args.config}: {S}->{'x'.join(map(str, H))}->{A} MLP (policy + value), " + (
+                               f"{T} steps x {E} envs = one rank's shard of the {T}x{E * shard_of} rollout split "
+                               f"over {shard_of} ranks (B/{shard_of}={B} rows per rank per step, global B="
+                               f"{B * shard_of}), measured as one GPU's share of that job"
+                               if shard_of > 1 and split == 1 and world == 1 else
                                f"{T} steps x {E * split} envs" + (f" split over {split} ranks ({E} envs, B/{split}="
                                f"{B} rows per rank per step)" if split > 1 else "") +
                                (" per GPU (weak scaling)" if args.weak else "") +
-                               f", global B={B * (world if args.weak else split)}, 10 value + 4 policy epochs",
-                   "global_batch": B * (world if args.weak else split), "rollout_per_gpu": N,
+                               f", global B={B * (world if args.weak else split)}") + ", 10 value + 4 policy epochs",
+                   "global_batch": B * (world if args.weak else split) * (shard_of if split == 1 and world == 1 else 1),
+                   "rollout_per_gpu": N,
+                   "per_rank_shard_of": shard_of if shard_of > 1 else None,
                    "parallelism": f"dp{world}",
                    "emulated_world": args.emulate_world if (world == 1 and args.emulate_world > 1) else None,
                    "comm": "rccl-self (1-rank rehearsal)" if comm_self else ("rccl" if world > 1 else "none"),
@@ -396,22 +431,27 @@ def main():
     }
     if serial and serial[2][0] and serial[0][0] > 0:
         s_ms, s_work, s_launches = serial[0][0], serial[1][0], serial[2][0]
-        achieved = s_work / (s_ms * 1e-3) / 1e12
+        # the GEMM class over one serial update: Σ_shape issued·work ÷ Σ_shape issued·(sampled average
+        # duration) — the rate a rocprofv3 trace of the same serial update gives (every launch timed)
+        tot_work = sum(sh["launches"] * sh["work_per_launch"] for sh in shapes)
+        tot_ms = sum(sh["ms"] for sh in shapes)
+        achieved = tot_work / (tot_ms * 1e-3) / 1e12 if tot_ms > 0 else s_work / (s_ms * 1e-3) / 1e12
         pmc, traffic_src = pmc_traffic() if args.config == "c4" else ({}, None)   # PMC passes are of c4
         traffic = pmc.get("hbm_bytes_per_launch")
         # dominant kernel = the kernel TEMPLATE (op × engine: one compiled kernel family, e.g. the x3
-        # forward NT) with the most time in the serialised update, over all its shapes: Σ 2mnl ÷ Σ time
+        # grad_W TN) with the most time in the serialised update (each shape's sampled average × its
+        # issued launches), over all its shapes: Σ 2mnl ÷ Σ time; shapes as [m, n, l, launches, avg µs]
         groups = {}
         for sh in shapes:
             g = groups.setdefault((sh["op"], sh["engine"]), {"op": sh["op"], "engine": sh["engine"], "launches": 0,
                                                            "ms": 0.0, "work": 0.0, "bytes": 0.0, "shapes": []})
             g["launches"] += sh["launches"]
             g["ms"] += sh["ms"]
-            g["work"] += sh["tflops"] * 1e12 * sh["ms"] * 1e-3
+            g["work"] += sh["work_per_launch"] * sh["launches"]
             m_, n_, l_ = sh["m"], sh["n"], sh["l"]
             # operands read once, output written once (fp32; grad_W: + its bias-gradient vector)
             g["bytes"] += sh["launches"] * 4 * (m_ * n_ + n_ * l_ + m_ * l_ + (l_ if sh["op"] == "grad_W" else 0))
-            g["shapes"].append([m_, n_, l_, round(sh["avg_us"], 2)])
+            g["shapes"].append([m_, n_, l_, sh["launches"], round(sh["avg_us"], 2)])
         dom = None
         if groups:
             g = max(groups.values(), key=lambda v: v["ms"])
@@ -452,9 +492,10 @@ def main():
                                              "x3": "dense bf16 MFMA spec / 6 (six bf16 products per fp32 product)",
                                              "exact": "fp32 MFMA spec (v_mfma_f32_32x32x2_f32)"}[engine],
                               "fp32_mfma_peak": PEAK_FP32_MFMA_TFLOPS,
-                              "launches": s_launches, "event_stride": args.event_stride,
-                              "avg_launch_us": 1000.0 * s_ms / s_launches,
-                              "algorithmic_flop_per_launch": s_work / s_launches,
+                              "launches": sum(sh["launches"] for sh in shapes), "sampled_launches": s_launches,
+                              "event_stride": args.event_stride,
+                              "avg_launch_us": 1000.0 * tot_ms / max(1, sum(sh["launches"] for sh in shapes)),
+                              "algorithmic_flop_per_launch": tot_work / max(1, sum(sh["launches"] for sh in shapes)),
                               "serial_update_ms": 1000.0 * serial[5],
                               "concurrent_class_tflops": conc, "concurrent_class_frac": conc / peak}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

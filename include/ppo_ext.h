@@ -53,6 +53,16 @@ double ppo_comm_max_f64(double v);
 /* the advantage-statistics combine after the all-gather: `count` device triples (n, mean, M2) in
  * double → one triple (Chan et al. pairwise combine; empty parts skipped).  Synchronises. */
 void ppo_welford_combine(const double* d_parts, int count, double* d_out);
+/* PPO_COMM_LOOPBACK=k (one process standing in for k ranks, tests): the other ranks' contributions,
+ * so rank 0 of a k-rank job whose shards DIFFER runs in one process.  welford: host [(k−1)·3]
+ * (n, mean, M2) triples of ranks 1…k−1, delivered by the all-gather after the local one; limits: host
+ * [k−1] buffer limits for the empty-shard agreement (min over ranks); either may be NULL.  Returns
+ * 0, or −1 outside loopback mode or for count ≠ k − 1. */
+int  ppo_comm_loopback_peers(const double* welford, const int* limits, int count);
+/* an all-reduce of a span inside [d_local_base, d_local_base + n) adds the peers' values at the same
+ * offset from d_peers (device, [k−1][n], rank order) instead of the k-fold identical sum; ≤ 4 spans */
+int  ppo_comm_loopback_peer_grads(const float* d_local_base, const float* d_peers, long n);
+void ppo_comm_loopback_clear(void);                      /* forget every registered peer contribution */
 
 /* ---------------- the PPO update ---------------- */
 enum { PPO_SHUFFLE_HOST_RAND = 0,   /* reference shuffle_buffer: swap(i, rand()%N), host rand() */
@@ -73,6 +83,11 @@ void ppo_update(void* ppo, float gamma, int batch_size, int n_epochs_policy, int
  * out[7]=rows of the last GAE's own V(next_state) forward (those not reused from V(state[t+1])) */
 void ppo_read_stats(void* ppo, double* out, int n);
 void ppo_reset_stats(void* ppo);
+/* the last GAE's state (compute_gae_cuda / ppo_update; synchronises): welford (may be NULL) ← the
+ * (n, mean, M2) triple the normalisation used (global at world > 1; out[3..5] the local triple);
+ * v / v_next (may be NULL) ← the first n values of V(state) and V(next_state) the scan read.
+ * Returns the number of transitions of that GAE. */
+long ppo_gae_state(double* welford, float* v, float* v_next, long n);
 /* Parity testing at full size: cap the value / policy minibatch steps of the following ppo_update
  * calls (−1 = no cap).  GAE, the shuffles and their rand() consumption are unchanged; only the
  * loops stop early (so one step of a 1M-row, B = 32768 update can be checked against the oracle). */
@@ -162,6 +177,10 @@ void ppo_prof_kernel_events(int on);
  * 1 grad_x, 2 grad_W, 3 paired grad_W + grad_x; engine 0 exact fp32, 1 x3, 2 bf16), Σ ms, sampled
  * launches and Σ algorithmic FLOPs.  Returns the number of shapes (fills at most cap).  Synchronises. */
 int  ppo_prof_shapes(long long* keys, double* ms, long* launches, double* work, int cap);
+/* per GEMM shape key (as ppo_prof_shapes returns them): launches issued while profiling was enabled,
+ * sampled or not — so a sampled average can be weighted by how often the shape really runs.
+ * Returns how many of the n keys were seen. */
+int  ppo_prof_shape_issued(const long long* keys, long* issued, int n);
 /* per class: launches issued while profiling was enabled (sampled or not) */
 void ppo_prof_counts(long* out_total);
 /* per class: Σ algorithmic work of every launch issued while profiling was enabled */

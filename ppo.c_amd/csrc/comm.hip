@@ -18,6 +18,10 @@
 // 1/k, the Welford all-gather + Chan combine, the limit agreement, the comm stream); the all-reduce
 // is the exact k-fold sum of identical buffers (×k on the comm stream) and the all-gather
 // replicates the local block k times.  For k a power of two an update must equal the 1-GPU update.
+// Disagreeing ranks (tests): ppo_comm_loopback_peers() supplies ranks 1…k−1's Welford triples and
+// buffer limits, ppo_comm_loopback_peer_grads() their gradient buffers — the all-gather then
+// delivers [own, peers…], the min runs over [own, peers…] and an all-reduce over a registered span
+// adds the peers' values, so rank 0 of a k-rank job with different shards runs in one process.
 #include "dev.h"
 #include "../../include/ppo_ext.h"
 
@@ -35,16 +39,30 @@ __global__ void scale_kernel(float* __restrict__ x, long n, float s) {
         x[i] *= s;
 }
 
-__global__ void replicate_kernel(const double* __restrict__ src, double* __restrict__ dst, long n, int k) {
+// loopback all-gather: block 0 = the local block; blocks 1…k−1 = the registered peers' blocks
+// (peer == nullptr: replicas of the local block)
+__global__ void gather_loopback_kernel(const double* __restrict__ src, const double* __restrict__ peer,
+                                       double* __restrict__ dst, long n, int k) {
     for (long i = blockIdx.x * 256L + threadIdx.x; i < n * k; i += (long)gridDim.x * 256)
-        dst[i] = src[i % n];
+        dst[i] = (i < n || !peer) ? src[i % n] : peer[i - n];
 }
-// loopback stand-in of an integer min all-reduce: lane r < k holds rank r's (identical) value
-__global__ void min_i32_loopback_kernel(int* __restrict__ x, int k) {
+// loopback all-reduce over a registered span: x += Σ_{r=1}^{k−1} peer[r−1]  (rank order, as RCCL's
+// two-rank sum; for k = 2 one add, commutative: rank 0's result of a real two-rank all-reduce)
+__global__ void add_peers_kernel(float* __restrict__ x, const float* __restrict__ peer, long n, long stride,
+                                 int peers) {
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+        float s = x[i];
+        for (int r = 0; r < peers; ++r) s += peer[r * stride + i];
+        x[i] = s;
+    }
+}
+// loopback stand-in of an integer min all-reduce: x[0] = the local value, x[1…k−1] the peers'
+// (peers == 0: every rank holds the local value)
+__global__ void min_i32_loopback_kernel(int* __restrict__ x, int k, int peers) {
     const int r = threadIdx.x;
     int v = x[0];
     __syncthreads();
-    if (r < k && r < 64) x[r] = v;
+    if (!peers && r < k && r < 64) x[r] = v;
     __syncthreads();
     if (r == 0) {
         int m = x[0];
@@ -52,6 +70,14 @@ __global__ void min_i32_loopback_kernel(int* __restrict__ x, int k) {
         x[0] = m;
     }
 }
+// registered peer contributions (ppo_comm_loopback_peers / _peer_grads)
+double* g_peer_welford = nullptr;            // device [(k−1)·3] or null
+long g_peer_welford_n = 0;
+int g_peer_limits[64];
+int g_peer_limits_set = 0;
+struct PeerSpan { const float* base; const float* peer; long n; };
+PeerSpan g_peer_spans[4];
+int g_peer_nspans = 0;
 hipStream_t g_comm_stream = nullptr;
 constexpr int kEvents = 16;                  // ring: a wait captures the record at enqueue time
 hipEvent_t g_ready[kEvents], g_done[kEvents];
@@ -79,6 +105,24 @@ hipStream_t comm_enter(int* slot) {
 void comm_leave(int slot) {
     PPO_CHECK(hipEventRecord(g_done[slot], g_comm_stream));
     PPO_CHECK(hipStreamWaitEvent(ppo::stream(), g_done[slot], 0));
+}
+
+// the loopback all-reduce on the comm stream: a span inside a registered peer span adds the peers'
+// values at the same offset (disagreeing ranks); anything else is the k-fold sum of identical ranks
+void loopback_allreduce(hipStream_t cs, float* d_buf, long n) {
+    int grid = ppo_divup(n, 256);
+    if (grid > 2048) grid = 2048;
+    for (int i = 0; i < g_peer_nspans; ++i) {
+        const PeerSpan& p = g_peer_spans[i];
+        if (d_buf >= p.base && d_buf + n <= p.base + p.n) {
+            hipLaunchKernelGGL(add_peers_kernel, dim3(grid), dim3(256), 0, cs, d_buf, p.peer + (d_buf - p.base), n,
+                               p.n, g_loopback - 1);
+            PPO_LAUNCH_CHECK();
+            return;
+        }
+    }
+    hipLaunchKernelGGL(scale_kernel, dim3(grid), dim3(256), 0, cs, d_buf, n, (float)g_loopback);
+    PPO_LAUNCH_CHECK();
 }
 
 void nccl_check(ncclResult_t r, const char* what, int line) {
@@ -140,6 +184,7 @@ void ppo_comm_finalize(void) {
         phip_sync();
         PPO_CHECK(hipStreamSynchronize(g_comm_stream));
         g_loopback = 0;
+        ppo_comm_loopback_clear();
     }
     if (g_comm) {
         phip_sync();
@@ -161,10 +206,7 @@ void phip_allreduce_sum_f32(float* d_buf, long n) {
     int slot;
     hipStream_t cs = comm_enter(&slot);
     if (g_loopback) {                          // k identical ranks: the sum is k·x
-        int grid = ppo_divup(n, 256);
-        if (grid > 2048) grid = 2048;
-        hipLaunchKernelGGL(scale_kernel, dim3(grid), dim3(256), 0, cs, d_buf, n, (float)g_loopback);
-        PPO_LAUNCH_CHECK();
+        loopback_allreduce(cs, d_buf, n);
         comm_leave(slot);
         return;
     }
@@ -188,10 +230,7 @@ void phip_allreduce_sum_f32_async(float* d_buf, long n) {
     int slot;
     hipStream_t cs = comm_enter(&slot);
     if (g_loopback) {
-        int grid = ppo_divup(n, 256);
-        if (grid > 2048) grid = 2048;
-        hipLaunchKernelGGL(scale_kernel, dim3(grid), dim3(256), 0, cs, d_buf, n, (float)g_loopback);
-        PPO_LAUNCH_CHECK();
+        loopback_allreduce(cs, d_buf, n);
     } else {
         nccl_check(ncclAllReduce(d_buf, d_buf, (size_t)n, ncclFloat32, ncclSum, g_comm, cs), "ncclAllReduce",
                    __LINE__);
@@ -214,8 +253,11 @@ void phip_allgather_f64(const double* d_send, double* d_recv, long n_per_rank) {
     ppo::ProfScope ps(PPO_K_COMM, 8.0 * n_per_rank * g_world);
     int slot;
     hipStream_t cs = comm_enter(&slot);
-    if (g_loopback) {                          // every rank holds the same block
-        hipLaunchKernelGGL(replicate_kernel, dim3(1), dim3(256), 0, cs, d_send, d_recv, n_per_rank, g_loopback);
+    if (g_loopback) {                          // [own block, peers' blocks] (or k replicas of the own block)
+        const double* peer = g_peer_welford && g_peer_welford_n == n_per_rank * (g_loopback - 1) ? g_peer_welford
+                                                                                               : nullptr;
+        hipLaunchKernelGGL(gather_loopback_kernel, dim3(1), dim3(256), 0, cs, d_send, peer, d_recv, n_per_rank,
+                           g_loopback);
         PPO_LAUNCH_CHECK();
         comm_leave(slot);
         return;
@@ -253,11 +295,15 @@ void ppo_comm_barrier(void) {
 int phip_comm_min_i32(int v) {
     if (!g_comm && !g_loopback) return v;      // world 1
     if (!g_i32) g_i32 = (int*)phip_malloc(sizeof(int) * 64);
-    phip_h2d(g_i32, &v, sizeof(int));
+    int x[64];
+    x[0] = v;
+    const int peers = g_loopback && g_peer_limits_set ? g_loopback - 1 : 0;
+    for (int r = 0; r < peers && r < 63; ++r) x[r + 1] = g_peer_limits[r];
+    phip_h2d(g_i32, x, sizeof(int) * (size_t)(1 + (peers < 63 ? peers : 63)));
     int slot;
     hipStream_t cs = comm_enter(&slot);
-    if (g_loopback) {                          // k identical ranks: replicate, then the min over the k copies
-        hipLaunchKernelGGL(min_i32_loopback_kernel, dim3(1), dim3(64), 0, cs, g_i32, g_loopback);
+    if (g_loopback) {                          // min over [own, peers…] (or over k copies of the own value)
+        hipLaunchKernelGGL(min_i32_loopback_kernel, dim3(1), dim3(64), 0, cs, g_i32, g_loopback, peers);
         PPO_LAUNCH_CHECK();
     } else {
         nccl_check(ncclAllReduce(g_i32, g_i32, 1, ncclInt32, ncclMin, g_comm, cs), "ncclAllReduce(min)", __LINE__);
@@ -266,6 +312,43 @@ int phip_comm_min_i32(int v) {
     int out = v;
     phip_d2h(&out, g_i32, sizeof(int));
     return out;
+}
+
+void ppo_comm_loopback_clear(void) {
+    if (g_peer_welford) { phip_sync(); phip_free(g_peer_welford); }
+    g_peer_welford = nullptr;
+    g_peer_welford_n = 0;
+    g_peer_limits_set = 0;
+    g_peer_nspans = 0;
+}
+
+int ppo_comm_loopback_peers(const double* welford, const int* limits, int count) {
+    if (g_loopback < 2 || count != g_loopback - 1 || count > 63) {
+        phip_record_error("ppo_comm_loopback_peers: needs PPO_COMM_LOOPBACK=k and count = k - 1 (< 64)");
+        return -1;
+    }
+    if (welford) {
+        if (!g_peer_welford || g_peer_welford_n != 3L * count) {
+            phip_free(g_peer_welford);
+            g_peer_welford = (double*)phip_malloc(sizeof(double) * 3 * (size_t)count);
+            g_peer_welford_n = 3L * count;
+        }
+        phip_h2d(g_peer_welford, welford, sizeof(double) * 3 * (size_t)count);
+    }
+    if (limits) {
+        for (int r = 0; r < count; ++r) g_peer_limits[r] = limits[r];
+        g_peer_limits_set = 1;
+    }
+    return 0;
+}
+
+int ppo_comm_loopback_peer_grads(const float* d_local_base, const float* d_peers, long n) {
+    if (g_loopback < 2 || !d_local_base || !d_peers || n <= 0 || g_peer_nspans >= 4) {
+        phip_record_error("ppo_comm_loopback_peer_grads: needs PPO_COMM_LOOPBACK=k, device spans, at most 4");
+        return -1;
+    }
+    g_peer_spans[g_peer_nspans++] = PeerSpan{d_local_base, d_peers, n};
+    return 0;
 }
 
 }  // extern "C"

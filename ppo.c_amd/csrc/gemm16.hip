@@ -777,6 +777,15 @@ __global__ __launch_bounds__(NTH, 1) void gemm_bf16_db_kernel(Args a) {
     epilogue256<OP, BM, BN, TM, TN, NTH, TC>(a, acc, lds, m0, n0, wm, wn, tid, stamp);
 }
 
+// s_waitcnt vmcnt(N) with N a compile-time count of this wave's outstanding vector-memory operations
+// (the prologue waits below: "all but the pieces of the second image have landed", so N = the 1-KiB
+// pieces one wave issues per k-tile — derived from the tile constants, never a literal)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    static_assert(N >= 0 && N <= 63, "vmcnt immediate");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
 // One LDS-DMA piece: 16 B per lane from `g` into the wave's 1 KiB at `l` (global_load_lds_dwordx4).
 // Issued from asm: the compiler's waitcnt pass treats __builtin_amdgcn_global_load_lds as an LDS
 // store of unknown extent and puts `s_waitcnt vmcnt(0)` in front of the next ds_read of ANY image —
@@ -820,6 +829,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_dma_kernel(Args a) {
     constexpr int WM = 64, WN = 128, TM = 2, TN = 4;
     constexpr bool B_MN = OP == OP_NN;
     constexpr int IMG = BM * BK;                       // elements per operand image (32 KiB)
+    static_assert(IMG / 512 / 8 == 4, "dma(): 4 + 4 one-KiB pieces per wave per k-tile (the prologue wait)");
     constexpr int BUF = 2 * IMG;
     extern __shared__ __attribute__((aligned(16))) unsigned short lds[];     // max(2·BUF, C image)
     typedef __attribute__((address_space(3))) void* lds_ptr;
@@ -931,7 +941,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_dma_kernel(Args a) {
     dma(0, buf0);
     if (nk > 1) {
         dma(1, buf1);
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");     // tile 0's eight pieces (this wave's) landed
+        wait_vmcnt<4 + 4>();                                  // tile 0's 4 + 4 pieces (this wave's) landed
     } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -973,6 +983,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_dma16_kernel(Args a) {
     constexpr int WM = 64, WN = 128, TM = 4, TN = 8;           // 16×16 blocks per wave
     constexpr bool B_MN = OP == OP_NN;
     constexpr int IMG = BM * BK;
+    static_assert(IMG / 512 / 8 == 4, "dma(): 4 + 4 one-KiB pieces per wave per k-tile (the prologue wait)");
     constexpr int BUF = 2 * IMG;
     extern __shared__ __attribute__((aligned(16))) unsigned short lds[];     // max(2·BUF, C image)
     typedef __attribute__((address_space(3))) void* lds_ptr;
@@ -1063,7 +1074,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_dma16_kernel(Args a) {
     dma(0, buf0);
     if (nk > 1) {
         dma(1, buf1);
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        wait_vmcnt<4 + 4>();                                  // the 4 + 4 pieces per wave of dma() above
     } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -1245,8 +1256,7 @@ __global__ __launch_bounds__(512, 1) void gemm_bf16_dma_tn_kernel(Args a, float*
     dma(0, buf0);
     if (nk > 1) {
         dma(1, buf1);
-        if constexpr (BN == 256) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // tile 0's pieces landed
-        else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        wait_vmcnt<PA_ + PB_>();                              // tile 0's pieces (this wave's) landed
     } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }

@@ -77,6 +77,7 @@ static bool                  g_prof_kattach = false;      // GEMM scopes timed b
 static int                   g_pending = -1;              // slot awaiting a PPO_TIMED_LAUNCH
 struct ShapeStat { long long key; double ms; long launches; double work; };
 static std::vector<ShapeStat> g_shapes;
+static std::vector<std::pair<long long, long>> g_shape_issued;   // every launch per shape, sampled or not
 static int                   g_prof_stride = 1;
 static long                  g_issued[PPO_K_COUNT];
 static double                g_issued_work[PPO_K_COUNT];   // algorithmic work of every issued launch
@@ -144,6 +145,12 @@ static int g_capturing = 0;                  // a hipGraph capture is open on li
 int phip_prof_begin_key(int cls, double work, long long key) {
     if (!g_prof_on || g_capturing) return -1;
     g_issued_work[cls] += work;
+    if (key) {
+        bool found = false;
+        for (auto& x : g_shape_issued)
+            if (x.first == key) { x.second++; found = true; break; }
+        if (!found) g_shape_issued.emplace_back(key, 1L);
+    }
     if (g_issued[cls]++ % g_prof_stride != 0) return -1;
     if (g_slots.size() >= (1u << 16)) harvest();
     const int ext = g_prof_kattach && cls == PPO_K_GEMM ? 1 : 0;
@@ -316,9 +323,20 @@ int ppo_prof_shapes(long long* keys, double* ms, long* launches, double* work, i
     return n;
 }
 
+int ppo_prof_shape_issued(const long long* keys, long* issued, int n) {
+    int found = 0;
+    for (int i = 0; i < n; i++) {
+        issued[i] = 0;
+        for (auto& x : g_shape_issued)
+            if (x.first == keys[i]) { issued[i] = x.second; found++; break; }
+    }
+    return found;
+}
+
 void ppo_prof_reset(void) {
     harvest();
     g_shapes.clear();
+    g_shape_issued.clear();
     for (int k = 0; k < PPO_K_COUNT; k++) { g_ms[k] = 0; g_work[k] = 0; g_launches[k] = 0; g_issued[k] = 0; g_issued_work[k] = 0; }
 }
 

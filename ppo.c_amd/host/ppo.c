@@ -57,6 +57,7 @@ static double* g_welford_all = NULL;
 static int g_welford_world = 0;
 static float* g_adv_stats = NULL; /* (mean, std) as used for normalisation */
 static long g_gae_own_rows = 0;   /* rows of the last GAE's own V(next_state) forward */
+static long g_gae_n = 0;          /* transitions of the last GAE */
 
 static uint64_t splitmix64(uint64_t z) {
     z += 0x9E3779B97F4A7C15ULL;
@@ -209,6 +210,7 @@ static int gae_full_forwards(void) {
 void ppo_gae_device(NeuralNetwork* V, TrajectoryBuffer* b, float gamma, float lambda) {
     const int n = b->full ? b->capacity : b->idx;
     g_gae_own_rows = 0;                     /* an empty buffer reports no own-row forward */
+    g_gae_n = n;
     ensure_gae_ws(n);
     if (n > 0 && gae_full_forwards()) {     /* the reference's two full forwards (ppo.cu:333-336) */
         nn_forward_dev(V, b->next_state_p, n);
@@ -236,6 +238,23 @@ void ppo_gae_device(NeuralNetwork* V, TrajectoryBuffer* b, float gamma, float la
         phip_welford_combine(g_welford_all, world, g_welford);
     }
     phip_normalize(b->advantage_p, n, g_welford, g_adv_stats);
+}
+
+long ppo_gae_state(double* welford, float* v, float* v_next, long n) {
+    phip_sync();
+    if (n > g_gae_n) n = g_gae_n;
+    if (welford) {
+        double w[6] = {0, 0, 0, 0, 0, 0};
+        if (g_welford) phip_d2h(w, g_welford, 3 * sizeof(double));
+        if (phip_comm_world() > 1 && g_welford_all)
+            phip_d2h(w + 3, g_welford_all + 3 * (size_t)phip_comm_rank(), 3 * sizeof(double));
+        else
+            memcpy(w + 3, w, 3 * sizeof(double));
+        memcpy(welford, w, sizeof(w));
+    }
+    if (v && n > 0) phip_d2h(v, g_v, sizeof(float) * (size_t)n);
+    if (v_next && n > 0) phip_d2h(v_next, g_vn, sizeof(float) * (size_t)n);
+    return g_gae_n;
 }
 
 /* device buffer (after buffer_to_device); `horizon` is unused: the scan is exact (D7) */
@@ -602,12 +621,17 @@ static int step_graphs_ok(const StepCtx* c) {
                              (uintptr_t)a->v;
         if (!a->flat || (al & 15u)) return 0;
     }
-    if (ppo->adam_V->weights[0] != ppo->V->d_params || ppo->adam_policy->weights[0] != ppo->policy->mu->d_params ||
+    /* the table Adam always clears the gradient it read (the captured steps run their backward with
+     * the gradients already zero), so every Adam must own its network's gradient span, as `own` in
+     * adam_update_net requires on the eager path */
+    if (ppo->adam_V->weights[0] != ppo->V->d_params || ppo->adam_V->grad_weights[0] != ppo->V->d_grads ||
+        ppo->adam_policy->weights[0] != ppo->policy->mu->d_params ||
+        ppo->adam_policy->grad_weights[0] != ppo->policy->mu->d_grads ||
         ppo->adam_entropy->grad_weights[0] != ppo->policy->d_log_std_grad)
         return 0;
-    if ((ppo->V->dtype == 1 && ppo->V->num_params > ppo->adam_V->span) ||
-        (ppo->policy->mu->dtype == 1 && ppo->policy->mu->num_params > ppo->adam_policy->span))
-        return 0;
+    /* only the combination tests/test_gpu_update.py replays against eager launches: fp32 networks with
+     * the fused output heads (value A = 1, policy A <= 6) */
+    if (ppo->V->dtype != 0 || ppo->policy->mu->dtype != 0 || !c->fuse_v || !c->fuse_p) return 0;
     return 1;
 }
 
@@ -615,7 +639,7 @@ static int step_graphs_ok(const StepCtx* c) {
  * and the Adam step sizes in the reference's step order (advancing the host Adam step counters as
  * the eager path does) — uploaded, the counter reset, and one step captured as a graph */
 static void* capture_graph(StepCtx* c, int ph, int steps) {
-    if (phip_graph_begin() != 0) die("ppo_update: graph capture could not start");
+    if (phip_graph_begin() != 0) return NULL;
     for (int s = 0; s < steps; s++) {
         if (ph) {
             int pz = 1, lz = 1;
@@ -624,9 +648,7 @@ static void* capture_graph(StepCtx* c, int ph, int steps) {
             (void)value_step(c, 1, 1, 1);
         }
     }
-    void* exec = phip_graph_end();
-    if (!exec) die("ppo_update: graph capture failed");
-    return exec;
+    return phip_graph_end();
 }
 
 static void capture_steps(StepCtx* c, int ph) {
@@ -647,6 +669,9 @@ static void capture_steps(StepCtx* c, int ph) {
     if (!d->ctr) d->ctr = (int*)phip_malloc(sizeof(int) * 4);
     const int* perms = ph ? c->perms_p : c->perms_v;
     const uint64_t* keys = ph ? c->keys_p : c->keys_v;
+    /* the table advances the host Adam step counters as the eager steps would; kept to roll back if
+     * the capture fails (the phase then runs every step eagerly) */
+    const int t_v = ppo->adam_V->time_step, t_p = ppo->adam_policy->time_step, t_e = ppo->adam_entropy->time_step;
     for (long t = 0; t < n; t++) {
         const long i = t + 1;
         const int j = (int)(i / c->num_batches), k = (int)(i % c->num_batches);
@@ -667,7 +692,18 @@ static void capture_steps(StepCtx* c, int ph) {
     phip_memset(d->ctr + 2 + ph, 0, sizeof(int));
     const int K = (int)(n < c->K ? n : c->K);
     void* gk = capture_graph(c, ph, K);
-    void* g1 = K > 1 ? capture_graph(c, ph, 1) : NULL;
+    void* g1 = gk && K > 1 ? capture_graph(c, ph, 1) : NULL;
+    if (!gk || (K > 1 && !g1)) {
+        /* an opt-in speed feature must not end a training run: warn, drop the graphs, replay nothing */
+        fprintf(stderr, "libppo: warning: graph capture of the %s steps failed (%s); running them eagerly\n",
+                ph ? "policy" : "value", ppo_last_error());
+        phip_graph_destroy(gk);
+        phip_graph_destroy(g1);
+        ppo->adam_V->time_step = t_v;
+        ppo->adam_policy->time_step = t_p;
+        ppo->adam_entropy->time_step = t_e;
+        return;
+    }
     if (ph) { c->gp = gk; c->gp1 = g1; c->Kp = K; } else { c->gv = gk; c->gv1 = g1; c->Kv = K; }
 }
 

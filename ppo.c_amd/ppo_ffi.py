@@ -132,6 +132,10 @@ _SIGS = {
     "ppo_comm_finalize": (None, []),
     "ppo_comm_allreduce_f32": (None, [_P, C.c_long]),
     "ppo_welford_combine": (None, [_P, C.c_int, _P]),
+    "ppo_comm_loopback_peers": (C.c_int, [_P, _P, C.c_int]),
+    "ppo_comm_loopback_peer_grads": (C.c_int, [_P, _P, C.c_long]),
+    "ppo_comm_loopback_clear": (None, []),
+    "ppo_gae_state": (C.c_long, [_P, _P, _P, C.c_long]),
     "ppo_comm_barrier": (None, []),
     "ppo_comm_max_f64": (C.c_double, [C.c_double]),
     "ppo_update": (None, [_P, C.c_float, C.c_int, C.c_int, C.c_int, C.c_int, C.c_ulonglong]),
@@ -147,6 +151,7 @@ _SIGS = {
                                   C.c_int]),
     "ppo_prof_read": (None, [C.POINTER(C.c_double), C.POINTER(C.c_double), c_long_p]),
     "ppo_prof_counts": (None, [c_long_p]),
+    "ppo_prof_shape_issued": (C.c_int, [C.POINTER(C.c_longlong), c_long_p, C.c_int]),
     "ppo_prof_issued_work": (None, [C.POINTER(C.c_double)]),
     # mat_mul.h
     "mat_mul": (None, [_P, _P, _P, _P, C.c_int, C.c_int, C.c_int]),

@@ -1,4 +1,4 @@
-"""Index work bit-exactly, the timed C4 configuration, and the world > 1 code paths on one GPU.
+"""Index work bit-exactly and the world > 1 code paths on one GPU.
 
 * shuffle_buffer / shuffle_buffer_cuda (trajectory_buffer.cu:126-166) against ref_shuffle after the
   same srand — assert_array_equal on every index;
@@ -7,9 +7,8 @@
 * the minibatch gather fused into the layer-0 GEMM: the rows a value / policy step actually trained
   on (the gathered copy the GEMM leaves, NeuralNetwork.d_x0) equal the buffer rows the reference's
   get_batch would pick — host rand() permutation and libppo's device Feistel permutation;
-* the bench's exact C4 configuration (N = 1,048,576 from ppo_fill_synthetic, B = 32768, 376 → 3×512
-  → 17, the x3 engine with its production split-K grids): one value and one policy minibatch
-  against the oracle on the same rows — every gradient and the Adam delta;
+* (the bench's exact C4 configuration is pinned in test_gpu_production.py, its data-parallel shards
+  in test_gpu_dp_shards.py);
 * PPO_COMM_LOOPBACK=k (k identical ranks in one process): grad_scale 1/k, the Welford all-gather +
   combine, the empty-shard agreement and the comm stream reproduce the one-GPU update;
 * the Welford combine on unequal triples against the numpy Chan combine.
@@ -21,9 +20,8 @@ import pytest
 
 import ppo_ffi
 from gpu_internal import set_host_buffer
-from helpers import (F32, assert_gemm_close, assert_rel_close, gpu_relu_masks, nn_grads_packed, nn_params_packed,
-                     oracle_grads_with_masks)
-from test_gpu_update import adam_first_step, assert_adam_delta, load_buffer, make_ppo, policy_state, synthetic_buffer
+from helpers import F32, nn_params_packed
+from test_gpu_update import load_buffer, make_ppo, policy_state, synthetic_buffer
 
 pytestmark = pytest.mark.gpu
 
@@ -146,89 +144,6 @@ def test_fused_gather_rows(lib, oracle, shuffle_mode, B):
         np.testing.assert_array_equal(_gathered_rows(lib, net, B, sizes[0]), buf["state"][rows], err_msg=phase)
     lib.ppo_set_step_limit(ppo, -1, -1)
     lib.free_ppo(ppo)
-
-
-# ----------------------------------------------------------------------------- the timed configuration
-C4 = [376, 512, 512, 512, 17]
-
-
-@pytest.fixture(scope="module")
-def c4(lib, oracle):
-    """The bench's C4 state: 256 envs × 4096 steps from ppo_fill_synthetic (bench.py's generator)."""
-    oracle.load(use_openblas=True)
-    oracle.load().ref_blas_threads(16)
-    N = 256 * 4096
-    ppo = make_ppo(lib, oracle, C4, N, seed=4242)
-    lib.ppo_fill_synthetic(ppo, 256, 4096, 4242, 1.0 / 500)
-    lib.ppo_synchronize()
-    yield ppo, N
-    lib.ppo_set_step_limit(ppo, -1, -1)
-    lib.free_ppo(ppo)
-
-
-def _dev_rows(lib, ptr, rows, width, total):
-    full = ppo_ffi.d2h(lib, ptr, F32, total * width).reshape(total, width)
-    return full[rows]
-
-
-def test_c4_timed_value_step(lib, oracle, c4):
-    """One value minibatch of the bench's C4 update (B = 32768, x3 engine, production split-K) vs the oracle."""
-    ppo, N = c4
-    B, seed = 32768, 77
-    assert lib.ppo_gemm_f32_engine(-1) == 1
-    v0 = nn_params_packed(lib, ppo.contents.V)
-    lib.ppo_set_step_limit(ppo, 1, 0)
-    lib.ppo_update(ppo, 0.99, B, 0, 1, 1, seed)
-    lib.ppo_synchronize()
-    gV = nn_grads_packed(lib, ppo.contents.V)
-    v1 = nn_params_packed(lib, ppo.contents.V)
-    b = ppo.contents.buffer.contents
-    rows = oracle.feistel_perm(N, oracle.splitmix64(seed))[:B]
-    x = _dev_rows(lib, b.d_state_p, rows, 376, N)
-    np.testing.assert_array_equal(_gathered_rows(lib, ppo.contents.V, B, 376), x)
-    tgt = ppo_ffi.d2h(lib, b.d_adv_target_p, F32, N)[rows]
-    sv = C4[:-1] + [1]
-    acts = oracle.mlp_forward(sv, RELU(sv), v0, x)
-    y = oracle.mlp_layer_outputs(sv, acts, B)[-1].ravel()
-    _, g = oracle.mse(y, tgt)
-    g_ref, nflip = oracle_grads_with_masks(oracle, sv, RELU(sv), v0, x, g.reshape(-1, 1),
-                                           gpu_relu_masks(lib, ppo.contents.V, x), "C4 value", max_flips=256)
-    assert_gemm_close(gV, g_ref, B, "C4 value grads")
-    flips = assert_adam_delta(v1, adam_first_step(v0, g_ref, 3e-4), g_ref, 3e-4, "C4 value params")
-    assert flips <= v1.size // 1000
-
-
-def test_c4_timed_policy_step(lib, oracle, c4):
-    """One policy minibatch of the bench's C4 update vs the oracle (clipped surrogate, A = 17)."""
-    ppo, N = c4
-    B, seed, A = 32768, 91, 17
-    pol = ppo.contents.policy.contents
-    mu0 = nn_params_packed(lib, pol.mu)
-    ls0 = ppo_ffi.d2h(lib, pol.d_log_std, F32, A)
-    lib.ppo_set_step_limit(ppo, 0, 1)
-    lib.ppo_update(ppo, 0.99, B, 1, 0, 1, seed)
-    lib.ppo_synchronize()
-    gmu = nn_grads_packed(lib, pol.mu)
-    gls = ppo_ffi.d2h(lib, pol.d_log_std_grad, F32, A)
-    mu1 = nn_params_packed(lib, pol.mu)
-    b = ppo.contents.buffer.contents
-    rows = oracle.feistel_perm(N, oracle.splitmix64(seed))[:B]
-    x = _dev_rows(lib, b.d_state_p, rows, 376, N)
-    np.testing.assert_array_equal(_gathered_rows(lib, pol.mu, B, 376), x)
-    a = _dev_rows(lib, b.d_action_p, rows, A, N)
-    adv = ppo_ffi.d2h(lib, b.d_advantage_p, F32, N)[rows]
-    old = ppo_ffi.d2h(lib, b.d_logprob_p, F32, N)[rows]
-    acts = oracle.mlp_forward(C4, RELU(C4), mu0, x)
-    mu = oracle.mlp_layer_outputs(C4, acts, B)[-1]
-    lp = oracle.log_prob(mu, ls0, a)
-    _, glp, gent = oracle.policy_loss_and_grad(adv, lp, old, oracle.entropy(ls0), 0.0, 0.2)
-    gmu_out, gls_ref = oracle.log_prob_backwards(mu, ls0, a, glp)
-    g_ref, _ = oracle_grads_with_masks(oracle, C4, RELU(C4), mu0, x, gmu_out, gpu_relu_masks(lib, pol.mu, x),
-                                       "C4 policy", max_flips=256)
-    assert_gemm_close(gmu, g_ref, B, "C4 policy grads")
-    assert_rel_close(gls, gls_ref + gent, 1e-3, 1e-4 * max(1.0, float(np.abs(gls_ref).max())), "C4 log_std grad")
-    flips = assert_adam_delta(mu1, adam_first_step(mu0, g_ref, 3e-4), g_ref, 3e-4, "C4 policy params")
-    assert flips <= mu1.size // 1000
 
 
 # ----------------------------------------------------------------------------- world > 1 on one GPU

@@ -14,15 +14,24 @@ oracle (reference ppo.cu:391-447 per minibatch; mat_mul.cu:132-217 for every pro
   whole gradient against the fp32 oracle (3e-2·max|ref|, SURVEY §8c's bf16 bound), Adam on the
   gradient it read; the bf16 gathered layer-0 copy equals bf16(state[rows]) bit for bit.
 
+GAE at every production size (round 4): the device GAE (V(state) forward over the whole buffer, the
+V(next_state) reuse with its own-row forward, the scan, the Welford statistics and the normalisation)
+against the oracle's GAE — the reference's two full V forwards (OpenBLAS, 16 threads) and its
+recursion (ref_gae) — at C3 (N = 262,144), C4 (N = 1,048,576) and the C5 shard (N = 524,288; bf16 V:
+the scan teacher-forced on the GPU's own V values, V itself within the bf16 bound).  The step tests
+then take their targets and advantages from the ORACLE's GAE, so no link of the production chain
+compares the GPU with its own output.
+
 Inputs are bench.py's own: ppo_fill_synthetic (seeded device generator) after create_ppo from srand.
 """
+import hashlib
 import ctypes as C
 
 import numpy as np
 import pytest
 
 import ppo_ffi
-from helpers import (F32, assert_gemm_close, assert_rel_close, gpu_relu_masks, nn_grads_packed, nn_params_packed,
+from helpers import (F32, assert_gemm_close, assert_normalised_close, assert_rel_close, gpu_relu_masks, nn_grads_packed, nn_params_packed,
                      oracle_grads_with_masks)
 from test_gpu_bf16 import bf16, unpack
 from test_gpu_update import adam_first_step, assert_adam_delta, make_ppo, policy_state
@@ -43,6 +52,53 @@ def device_buffer(lib, ppo, N, S, A):
                 logprob=ppo_ffi.d2h(lib, b.d_logprob_p, F32, N),
                 terminated=ppo_ffi.d2h(lib, b.d_terminated_p, np.uint8, N),
                 truncated=ppo_ffi.d2h(lib, b.d_truncated_p, np.uint8, N))
+
+
+_GAE_CACHE = {}
+
+
+def oracle_gae(lib, oracle, ppo, sizes, N):
+    """The oracle's GAE over the device buffer with the network's CURRENT V parameters (reference
+    compute_gae, ppo.cu:326-369: V over every next_state and state row, then the recursion):
+    (normalised advantages, targets), cached per (buffer, V parameters)."""
+    v0 = nn_params_packed(lib, ppo.contents.V)
+    b = ppo.contents.buffer.contents
+    key = (ctypes_addr(b.d_state_p), N, hashlib.sha1(v0.tobytes()).hexdigest())
+    if key not in _GAE_CACHE:
+        _GAE_CACHE.clear()
+        buf = device_buffer(lib, ppo, N, sizes[0], sizes[-1])
+        A = sizes[-1]
+        ref = oracle.ppo_update(sizes, RELU(sizes), np.zeros(oracle.mlp_num_params(sizes), F32), np.zeros(A, F32), v0,
+                                buf, batch_size=1, n_epochs_policy=0, n_epochs_value=0, max_value_steps=0,
+                                max_policy_steps=0)
+        _GAE_CACHE[key] = (ref["advantage"], ref["adv_target"], ref["adv_mean"], ref["adv_std"])
+    return _GAE_CACHE[key]
+
+
+def ctypes_addr(p):
+    return C.cast(p, C.c_void_p).value
+
+
+def gpu_gae(lib, ppo, N):
+    """Run the device GAE alone (ppo_update capped at zero minibatch steps) and read its outputs."""
+    lib.ppo_set_step_limit(ppo, 0, 0)
+    lib.ppo_update(ppo, 0.99, 64, 0, 0, 1, 1)
+    lib.ppo_synchronize()
+    b = ppo.contents.buffer.contents
+    return ppo_ffi.d2h(lib, b.d_advantage_p, F32, N), ppo_ffi.d2h(lib, b.d_adv_target_p, F32, N)
+
+
+def assert_gae_pinned(lib, oracle, ppo, sizes, N, what):
+    """Device GAE vs the oracle's: targets 1e-5 relative + 1e-5·max|target|, normalised advantages
+    1e-4 relative + 1e-4 absolute of the exact statistics (helpers.assert_normalised_close)."""
+    adv_ref, tgt_ref, mean_ref, std_ref = oracle_gae(lib, oracle, ppo, sizes, N)
+    adv, tgt = gpu_gae(lib, ppo, N)
+    e_t = np.abs(tgt.astype(np.float64) - tgt_ref)
+    e_a = np.abs(adv.astype(np.float64) - adv_ref)
+    print(f"{what}: targets max err {e_t.max():.3g} (max|t| {np.abs(tgt_ref).max():.3g}), "
+          f"advantages max err {e_a.max():.3g}")
+    assert_rel_close(tgt, tgt_ref, 1e-5, 1e-5 * float(np.abs(tgt_ref).max()), f"{what} adv_target")
+    assert_normalised_close(adv, adv_ref, mean_ref, std_ref, f"{what} normalised advantage")
 
 
 def bench_ppo(lib, oracle, sizes, E, T, seed, dtype=0):
@@ -180,26 +236,10 @@ def _gathered(lib, nn_ptr, B, S):
     return ppo_ffi.d2h(lib, nn.d_x0, F32, B * S).reshape(B, S)
 
 
-def test_c3_timed_value_step(lib, oracle, c3):
-    """One value minibatch of the C3 bench update (N = 262,144, B = 8192, x3 grids, fused head) vs the oracle."""
+def test_c3_gae_vs_oracle(lib, oracle, c3):
+    """C3's device GAE (N = 262,144: x3 V forward, V(next_state) reuse, scan, statistics) vs the oracle."""
     ppo, N = c3
-    B, seed = 8192, 71
-    assert lib.ppo_gemm_f32_engine(-1) == 1
-    v0 = nn_params_packed(lib, ppo.contents.V)
-    lib.ppo_set_step_limit(ppo, 1, 0)
-    lib.ppo_update(ppo, 0.99, B, 0, 1, 1, seed)
-    lib.ppo_synchronize()
-    gV, v1 = nn_grads_packed(lib, ppo.contents.V), nn_params_packed(lib, ppo.contents.V)
-    b = ppo.contents.buffer.contents
-    rows = oracle.feistel_perm(N, oracle.splitmix64(seed))[:B]
-    x = ppo_ffi.d2h(lib, b.d_state_p, F32, N * 17).reshape(N, 17)[rows]
-    np.testing.assert_array_equal(_gathered(lib, ppo.contents.V, B, 17), x)
-    tgt = ppo_ffi.d2h(lib, b.d_adv_target_p, F32, N)[rows]
-    sv = C3[:-1] + [1]
-    g_ref, _ = ref_value_grads(oracle, sv, v0, x, tgt, gpu_relu_masks(lib, ppo.contents.V, x), "C3 value")
-    assert_gemm_close(gV, g_ref, B, "C3 value grads")
-    flips = assert_adam_delta(v1, adam_first_step(v0, g_ref, LR), g_ref, LR, "C3 value params")
-    assert flips <= v1.size // 1000
+    assert_gae_pinned(lib, oracle, ppo, C3, N, "C3 GAE")
 
 
 def test_c3_timed_policy_step(lib, oracle, c3):
@@ -209,6 +249,7 @@ def test_c3_timed_policy_step(lib, oracle, c3):
     pol = ppo.contents.policy.contents
     mu0 = nn_params_packed(lib, pol.mu)
     ls0 = ppo_ffi.d2h(lib, pol.d_log_std, F32, A)
+    adv_all, _, _, _ = oracle_gae(lib, oracle, ppo, C3, N)
     lib.ppo_set_step_limit(ppo, 0, 1)
     lib.ppo_update(ppo, 0.99, B, 1, 0, 1, seed)
     lib.ppo_synchronize()
@@ -219,7 +260,7 @@ def test_c3_timed_policy_step(lib, oracle, c3):
     x = ppo_ffi.d2h(lib, b.d_state_p, F32, N * 17).reshape(N, 17)[rows]
     np.testing.assert_array_equal(_gathered(lib, pol.mu, B, 17), x)
     a = ppo_ffi.d2h(lib, b.d_action_p, F32, N * A).reshape(N, A)[rows]
-    adv = ppo_ffi.d2h(lib, b.d_advantage_p, F32, N)[rows]
+    adv = adv_all[rows]                                         # the oracle's normalised advantages
     old = ppo_ffi.d2h(lib, b.d_logprob_p, F32, N)[rows]
     g_ref, gls_ref = ref_policy_grads(oracle, C3, mu0, ls0, x, a, adv, old, gpu_relu_masks(lib, pol.mu, x),
                                       "C3 policy")
@@ -227,6 +268,29 @@ def test_c3_timed_policy_step(lib, oracle, c3):
     assert_rel_close(gls, gls_ref, 1e-3, 1e-4 * max(1.0, float(np.abs(gls_ref).max())), "C3 log_std grad")
     flips = assert_adam_delta(mu1, adam_first_step(mu0, g_ref, LR), g_ref, LR, "C3 policy params")
     assert flips <= mu1.size // 1000
+
+
+def test_c3_timed_value_step(lib, oracle, c3):
+    """One value minibatch of the C3 bench update (N = 262,144, B = 8192, x3 grids, fused head) vs the oracle."""
+    ppo, N = c3
+    B, seed = 8192, 71
+    assert lib.ppo_gemm_f32_engine(-1) == 1
+    v0 = nn_params_packed(lib, ppo.contents.V)
+    _, tgt_all, _, _ = oracle_gae(lib, oracle, ppo, C3, N)
+    lib.ppo_set_step_limit(ppo, 1, 0)
+    lib.ppo_update(ppo, 0.99, B, 0, 1, 1, seed)
+    lib.ppo_synchronize()
+    gV, v1 = nn_grads_packed(lib, ppo.contents.V), nn_params_packed(lib, ppo.contents.V)
+    b = ppo.contents.buffer.contents
+    rows = oracle.feistel_perm(N, oracle.splitmix64(seed))[:B]
+    x = ppo_ffi.d2h(lib, b.d_state_p, F32, N * 17).reshape(N, 17)[rows]
+    np.testing.assert_array_equal(_gathered(lib, ppo.contents.V, B, 17), x)
+    tgt = tgt_all[rows]                                         # the oracle's GAE targets
+    sv = C3[:-1] + [1]
+    g_ref, _ = ref_value_grads(oracle, sv, v0, x, tgt, gpu_relu_masks(lib, ppo.contents.V, x), "C3 value")
+    assert_gemm_close(gV, g_ref, B, "C3 value grads")
+    flips = assert_adam_delta(v1, adam_first_step(v0, g_ref, LR), g_ref, LR, "C3 value params")
+    assert flips <= v1.size // 1000
 
 
 # ----------------------------------------------------------------------------- C4: the headline bench update
@@ -243,27 +307,15 @@ def c4(lib, oracle):
     lib.free_ppo(ppo)
 
 
-def test_c4_timed_value_step(lib, oracle, c4):
-    """One value minibatch of the C4 bench update (N = 1,048,576, B = 32768: x3 grids with slab
-    split-K, the fused value head) vs the oracle."""
+def test_c4_gae_vs_oracle(lib, oracle, c4):
+    """The bench's C4 GAE at N = 1,048,576 (the V(state) forward over the whole buffer, the 2,368-row
+    own V(next_state) forward, 512 scan workgroups and their carries, the Welford combine) vs the
+    oracle's two full V forwards and recursion."""
     ppo, N = c4
-    B, seed, S = 32768, 73, 376
-    assert lib.ppo_gemm_f32_engine(-1) == 1
-    v0 = nn_params_packed(lib, ppo.contents.V)
-    lib.ppo_set_step_limit(ppo, 1, 0)
-    lib.ppo_update(ppo, 0.99, B, 0, 1, 1, seed)
-    lib.ppo_synchronize()
-    gV, v1 = nn_grads_packed(lib, ppo.contents.V), nn_params_packed(lib, ppo.contents.V)
-    b = ppo.contents.buffer.contents
-    rows = oracle.feistel_perm(N, oracle.splitmix64(seed))[:B]
-    x = _gathered(lib, ppo.contents.V, B, S)
-    np.testing.assert_array_equal(x[:64], ppo_ffi.d2h(lib, b.d_state_p, F32, N * S).reshape(N, S)[rows[:64]])
-    tgt = ppo_ffi.d2h(lib, b.d_adv_target_p, F32, N)[rows]
-    sv = C4[:-1] + [1]
-    g_ref, _ = ref_value_grads(oracle, sv, v0, x, tgt, gpu_relu_masks(lib, ppo.contents.V, x), "C4 value")
-    assert_gemm_close(gV, g_ref, B, "C4 value grads")
-    flips = assert_adam_delta(v1, adam_first_step(v0, g_ref, LR), g_ref, LR, "C4 value params")
-    assert flips <= v1.size // 1000
+    assert_gae_pinned(lib, oracle, ppo, C4, N, "C4 GAE")
+    st = (C.c_double * 8)()
+    lib.ppo_read_stats(ppo, st, 8)
+    assert 0 < st[7] < N // 100                    # the reuse ran: only episode ends got their own forward
 
 
 def test_c4_timed_policy_step(lib, oracle, c4):
@@ -274,6 +326,7 @@ def test_c4_timed_policy_step(lib, oracle, c4):
     pol = ppo.contents.policy.contents
     mu0 = nn_params_packed(lib, pol.mu)
     ls0 = ppo_ffi.d2h(lib, pol.d_log_std, F32, A)
+    adv_all, _, _, _ = oracle_gae(lib, oracle, ppo, C4, N)
     lib.ppo_set_step_limit(ppo, 0, 1)
     lib.ppo_update(ppo, 0.99, B, 1, 0, 1, seed)
     lib.ppo_synchronize()
@@ -283,7 +336,7 @@ def test_c4_timed_policy_step(lib, oracle, c4):
     rows = oracle.feistel_perm(N, oracle.splitmix64(seed))[:B]
     x = _gathered(lib, pol.mu, B, S)
     a = ppo_ffi.d2h(lib, b.d_action_p, F32, N * A).reshape(N, A)[rows]
-    adv = ppo_ffi.d2h(lib, b.d_advantage_p, F32, N)[rows]
+    adv = adv_all[rows]                                         # the oracle's normalised advantages
     old = ppo_ffi.d2h(lib, b.d_logprob_p, F32, N)[rows]
     g_ref, gls_ref = ref_policy_grads(oracle, C4, mu0, ls0, x, a, adv, old, gpu_relu_masks(lib, pol.mu, x),
                                       "C4 policy")
@@ -291,6 +344,30 @@ def test_c4_timed_policy_step(lib, oracle, c4):
     assert_rel_close(gls, gls_ref, 1e-3, 1e-4 * max(1.0, float(np.abs(gls_ref).max())), "C4 log_std grad")
     flips = assert_adam_delta(mu1, adam_first_step(mu0, g_ref, LR), g_ref, LR, "C4 policy params")
     assert flips <= mu1.size // 1000
+
+
+def test_c4_timed_value_step(lib, oracle, c4):
+    """One value minibatch of the C4 bench update (N = 1,048,576, B = 32768: x3 grids with slab
+    split-K, the fused value head) vs the oracle."""
+    ppo, N = c4
+    B, seed, S = 32768, 73, 376
+    assert lib.ppo_gemm_f32_engine(-1) == 1
+    v0 = nn_params_packed(lib, ppo.contents.V)
+    _, tgt_all, _, _ = oracle_gae(lib, oracle, ppo, C4, N)
+    lib.ppo_set_step_limit(ppo, 1, 0)
+    lib.ppo_update(ppo, 0.99, B, 0, 1, 1, seed)
+    lib.ppo_synchronize()
+    gV, v1 = nn_grads_packed(lib, ppo.contents.V), nn_params_packed(lib, ppo.contents.V)
+    b = ppo.contents.buffer.contents
+    rows = oracle.feistel_perm(N, oracle.splitmix64(seed))[:B]
+    x = _gathered(lib, ppo.contents.V, B, S)
+    np.testing.assert_array_equal(x[:64], ppo_ffi.d2h(lib, b.d_state_p, F32, N * S).reshape(N, S)[rows[:64]])
+    tgt = tgt_all[rows]                                         # the oracle's GAE targets
+    sv = C4[:-1] + [1]
+    g_ref, _ = ref_value_grads(oracle, sv, v0, x, tgt, gpu_relu_masks(lib, ppo.contents.V, x), "C4 value")
+    assert_gemm_close(gV, g_ref, B, "C4 value grads")
+    flips = assert_adam_delta(v1, adam_first_step(v0, g_ref, LR), g_ref, LR, "C4 value params")
+    assert flips <= v1.size // 1000
 
 
 # ----------------------------------------------------------------------------- C5: bf16 at the bench shard
@@ -415,33 +492,37 @@ def _gathered_bf16(lib, nn_ptr, B, S):
     return _bf16_dev(lib, nn_ptr.contents.d_x0, B, S)
 
 
-def test_c5_bf16_timed_value_step(lib, oracle, c5):
-    """One bf16 value minibatch at the bench's C5 shard (N = 524,288, B = 16384, fused bf16 value head):
-    every kernel teacher-forced against the bf16 rounding model, the whole gradient against the fp32
-    oracle (3e-2·max|ref|), Adam on the gradient it read."""
-    ppo, N, state = c5
-    B, seed = 16384, 57
-    V = ppo.contents.V
-    v0 = nn_params_packed(lib, V)
-    lib.ppo_set_step_limit(ppo, 1, 0)
-    lib.ppo_update(ppo, 0.99, B, 0, 1, 1, seed)
-    lib.ppo_synchronize()
-    v1 = nn_params_packed(lib, V)
+def test_c5_bf16_gae(lib, oracle, c5):
+    """The C5 shard's GAE (N = 524,288) in bf16 mode: V runs on the bf16 GEMMs, so (1) the scan,
+    statistics and normalisation are pinned on the GPU's own V(state) / V(next_state) values
+    (ppo_gae_state) against ref_gae at the fp32 tolerances, and (2) V itself against the oracle's fp32
+    forward within the bf16 bound 3e-2·max|V|, the targets / advantages likewise."""
+    ppo, N, _ = c5
+    adv, tgt = gpu_gae(lib, ppo, N)
+    w = np.zeros(6)
+    v, vn = np.empty(N, F32), np.empty(N, F32)
+    assert lib.ppo_gae_state(w.ctypes.data, v.ctypes.data, vn.ctypes.data, N) == N
     b = ppo.contents.buffer.contents
-    rows = oracle.feistel_perm(N, oracle.splitmix64(seed))[:B]
-    x = state[rows]
-    np.testing.assert_array_equal(_gathered_bf16(lib, V, B, 1024), bf16(x))      # the gather, bit for bit
-    tgt = ppo_ffi.d2h(lib, b.d_adv_target_p, F32, N)[rows]
-    sv = C5[:-1] + [1]
-    y = ppo_ffi.d2h(lib, V.contents.d_output, F32, B)
-    gtop = (2 * (y.astype(np.float64) - tgt) / B).reshape(-1, 1)
-    gV = check_bf16_layers(lib, V, sv, v0, x, gtop, True, "C5 value")
-    g_ref, _ = ref_value_grads(oracle, sv, v0, x, tgt, None, "C5 value")
-    close(gV, g_ref, 3e-2, "C5 value grads vs fp32 oracle")
-    # Adam (element-wise fp32) on the gradient it read — a bf16-level gradient difference would move
-    # Adam's first step lr·g/(|g| + ε) where |g| is near ε
-    flips = assert_adam_delta(v1, adam_first_step(v0, gV, LR), gV, LR, "C5 value params")
-    assert flips <= v1.size // 1000
+    r = ppo_ffi.d2h(lib, b.d_reward_p, F32, N)
+    term = ppo_ffi.d2h(lib, b.d_terminated_p, np.uint8, N)
+    trunc = ppo_ffi.d2h(lib, b.d_truncated_p, np.uint8, N)
+    adv_tf, tgt_tf, mean_tf, std_tf = oracle.gae(v, vn, r, term, trunc, 0.99, 0.95)
+    assert_rel_close(tgt, tgt_tf, 1e-5, 1e-5 * float(np.abs(tgt_tf).max()), "C5 targets (scan on the GPU's V)")
+    assert_normalised_close(adv, adv_tf, mean_tf, std_tf, "C5 advantages (scan on the GPU's V)")
+    raw = tgt_tf.astype(np.float64) - v                             # the exact statistics of the scan's A
+    assert w[0] == N and abs(w[1] - raw.mean()) <= 1e-5 * raw.std()
+    assert abs(np.sqrt(w[2] / w[0]) - raw.std()) <= 1e-5 * raw.std()
+    sv, m = C5[:-1] + [1], 32768                                 # V on the first 32768 rows, fp32 oracle
+    x = ppo_ffi.d2h(lib, b.d_state_p, F32, m * 1024).reshape(m, 1024)
+    v0 = nn_params_packed(lib, ppo.contents.V)
+    v_ref = oracle.mlp_layer_outputs(sv, oracle.mlp_forward(sv, RELU(sv), v0, x), m)[-1].ravel()
+    print(f"C5 bf16 V vs fp32 oracle: max err {np.abs(v[:m] - v_ref).max():.3g} (max|V| {np.abs(v_ref).max():.3g})")
+    close(v[:m], v_ref, 3e-2, "C5 V(state) vs fp32 oracle")
+    adv_ref, tgt_ref, _, _ = oracle_gae(lib, oracle, ppo, C5, N)
+    for got, ref, what in ((tgt, tgt_ref, "targets"), (adv, adv_ref, "advantages")):
+        err = float(np.abs(got.astype(np.float64) - ref).max())
+        print(f"C5 bf16 GAE {what} vs fp32 oracle: max err {err:.3g} (max|ref| {np.abs(ref).max():.3g})")
+        close(got, ref, 3e-2, f"C5 {what} vs fp32 oracle")
 
 
 def test_c5_bf16_timed_policy_step(lib, oracle, c5):
@@ -451,6 +532,7 @@ def test_c5_bf16_timed_policy_step(lib, oracle, c5):
     pol = ppo.contents.policy.contents
     mu0 = nn_params_packed(lib, pol.mu)
     ls0 = ppo_ffi.d2h(lib, pol.d_log_std, F32, A)
+    adv_ref_all, _, _, _ = oracle_gae(lib, oracle, ppo, C5, N)
     lib.ppo_set_step_limit(ppo, 0, 1)
     lib.ppo_update(ppo, 0.99, B, 1, 0, 1, seed)
     lib.ppo_synchronize()
@@ -470,8 +552,38 @@ def test_c5_bf16_timed_policy_step(lib, oracle, c5):
     gtop, gls_head = oracle.log_prob_backwards(y, ls0, a, glp)
     assert_rel_close(gls, gls_head + gent, 1e-3, 1e-4 * max(1.0, float(np.abs(gls_head).max())), "C5 log_std grad")
     gmu = check_bf16_layers(lib, pol.mu, C5, mu0, x, gtop, True, "C5 policy")
-    g_ref, gls_ref = ref_policy_grads(oracle, C5, mu0, ls0, x, a, adv, old, None, "C5 policy")
+    g_ref, gls_ref = ref_policy_grads(oracle, C5, mu0, ls0, x, a, adv_ref_all[rows], old, None, "C5 policy")
     close(gmu, g_ref, 3e-2, "C5 policy grads vs fp32 oracle")
     close(gls, gls_ref, 3e-2, "C5 log_std grad vs fp32 oracle")
     flips = assert_adam_delta(mu1, adam_first_step(mu0, gmu, LR), gmu, LR, "C5 policy params")
     assert flips <= mu1.size // 1000
+def test_c5_bf16_timed_value_step(lib, oracle, c5):
+    """One bf16 value minibatch at the bench's C5 shard (N = 524,288, B = 16384, fused bf16 value head):
+    every kernel teacher-forced against the bf16 rounding model, the whole gradient against the fp32
+    oracle (3e-2·max|ref|), Adam on the gradient it read."""
+    ppo, N, state = c5
+    B, seed = 16384, 57
+    V = ppo.contents.V
+    v0 = nn_params_packed(lib, V)
+    _, tgt_ref_all, _, _ = oracle_gae(lib, oracle, ppo, C5, N)
+    lib.ppo_set_step_limit(ppo, 1, 0)
+    lib.ppo_update(ppo, 0.99, B, 0, 1, 1, seed)
+    lib.ppo_synchronize()
+    v1 = nn_params_packed(lib, V)
+    b = ppo.contents.buffer.contents
+    rows = oracle.feistel_perm(N, oracle.splitmix64(seed))[:B]
+    x = state[rows]
+    np.testing.assert_array_equal(_gathered_bf16(lib, V, B, 1024), bf16(x))      # the gather, bit for bit
+    tgt = ppo_ffi.d2h(lib, b.d_adv_target_p, F32, N)[rows]
+    sv = C5[:-1] + [1]
+    y = ppo_ffi.d2h(lib, V.contents.d_output, F32, B)
+    gtop = (2 * (y.astype(np.float64) - tgt) / B).reshape(-1, 1)
+    gV = check_bf16_layers(lib, V, sv, v0, x, gtop, True, "C5 value")
+    g_ref, _ = ref_value_grads(oracle, sv, v0, x, tgt_ref_all[rows], None, "C5 value")   # fp32 oracle GAE
+    close(gV, g_ref, 3e-2, "C5 value grads vs fp32 oracle")
+    # Adam (element-wise fp32) on the gradient it read — a bf16-level gradient difference would move
+    # Adam's first step lr·g/(|g| + ε) where |g| is near ε
+    flips = assert_adam_delta(v1, adam_first_step(v0, gV, LR), gV, LR, "C5 value params")
+    assert flips <= v1.size // 1000
+
+

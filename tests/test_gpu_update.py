@@ -312,7 +312,7 @@ def test_concurrent_value_policy_loops(lib, oracle, shuffle_mode, monkeypatch):
     for k in ("mu", "ls"):        # the log σ-gradient's atomics may flip an Adam step of a tiny gradient
         err = np.abs(a[k] - b[k])  # (a 1-ulp log σ difference reaches every μ gradient: measured 0.2-1.04 %
         assert err.max() <= 2 * 3e-4, (k, err.max())           # of μ elements beyond 1e-6 run to run)
-        assert (err > 1e-6).mean() < 0.05, (k, (err > 1e-6).mean())
+        assert (err > 1e-6).mean() < 0.02, (k, (err > 1e-6).mean())
 
 
 def test_comm_stream_rehearsal(lib, oracle, monkeypatch):
@@ -513,8 +513,10 @@ def test_graph_replay_matches_eager(lib, oracle, shuffle_mode, monkeypatch):
     """Graph replay of minibatch steps (PPO_GRAPH=1, B = 64: steps 1 … n−2 of each phase replay captured
     16-step graphs whose gather / Adam arguments come from the device step table) against the eager
     launches from identical state: the same minibatch order (host rand() permutations and the
-    device Feistel order), the same Adam step counts and sizes, so parameters and loss sums agree to
-    the rounding of the fused heads' per-workgroup f32 atomics."""
+    device Feistel order), the same Adam step counts and sizes, so the value network agrees bit for bit
+    and the policy to the rounding of the fused head's log σ f32 atomics.  Graph replay is only enabled
+    for this combination (fp32, fused value and A ≤ 6 policy heads: step_graphs_ok); the A = 17 wide head
+    and the unfused path run eagerly even with PPO_GRAPH=1 (checked below)."""
     sizes, N, B = [17, 256, 256, 6], 4096, 64
     out = {}
     for mode in ("eager", "graph"):
@@ -544,13 +546,49 @@ def test_graph_replay_matches_eager(lib, oracle, shuffle_mode, monkeypatch):
     assert a["next_rand"] == b["next_rand"]
     assert a["stats"][1] == b["stats"][1] and a["stats"][3] == b["stats"][3]
     np.testing.assert_allclose(b["stats"], a["stats"], rtol=1e-4, atol=1e-6)
+    # the value loop: the same gather rows, GEMMs, fused head (one workgroup at B = 64: no cross-workgroup
+    # atomics) and Adam arithmetic with the same host-computed step sizes — bit for bit
+    np.testing.assert_array_equal(a["v"], b["v"])
     lr, n_steps = 3e-4, 2 * N // B
-    for key in ("v", "mu", "ls"):
+    for key in ("mu", "ls"):
         err = np.abs(a[key].astype(np.float64) - b[key])
         assert err.max() <= 2 * lr * n_steps, (key, err.max())
         assert (err <= 0.1 * lr).mean() >= 0.99, (key, (err <= 0.1 * lr).mean())
     # the last value minibatch ran eagerly in both: its gradients are there to read
     assert np.abs(b["gv"]).max() > 0
+
+
+@pytest.mark.parametrize("case", ["wide_head", "unfused"])
+def test_graph_replay_declines_untested_paths(lib, oracle, case, monkeypatch):
+    """PPO_GRAPH=1 with the A = 17 wide policy head or PPO_OUT_HEAD=0 (separate head launches): no graph
+    is captured (step_graphs_ok), every step runs eagerly — bit-identical to the same run without
+    PPO_GRAPH (split-K off: no atomics anywhere but the log σ sums, which the policy bound covers)."""
+    sizes = [376, 512, 512, 17] if case == "wide_head" else [17, 256, 256, 6]
+    N, B = 2048, 64
+    lib.ppo_gemm_tune(-1, 1)
+    out = {}
+    try:
+        for mode in ("eager", "graph"):
+            if case == "unfused":
+                monkeypatch.setenv("PPO_OUT_HEAD", "0")
+            if mode == "graph":
+                monkeypatch.setenv("PPO_GRAPH", "1")
+            else:
+                monkeypatch.delenv("PPO_GRAPH", raising=False)
+            monkeypatch.setenv("PPO_SERIAL", "1")
+            ppo = make_ppo(lib, oracle, sizes, N, init_std=0.7)
+            mu0, ls0 = policy_state(lib, ppo)
+            buf = synthetic_buffer(oracle, sizes, mu0, ls0, N, seed=45, n_envs=4)
+            load_buffer(lib, ppo, buf)
+            lib.ppo_update(ppo, 0.99, B, 1, 1, 1, 78)
+            lib.ppo_synchronize()
+            out[mode] = dict(v=nn_params_packed(lib, ppo.contents.V), mu=policy_state(lib, ppo)[0])
+            lib.free_ppo(ppo)
+    finally:
+        lib.ppo_gemm_tune(-1, 0)
+    np.testing.assert_array_equal(out["eager"]["v"], out["graph"]["v"])
+    err = np.abs(out["eager"]["mu"] - out["graph"]["mu"])
+    assert err.max() <= 2 * 3e-4 and (err > 1e-6).mean() < 0.02
 
 
 def test_wide_output_backward_matches_pair(lib, oracle, monkeypatch):
