@@ -348,7 +348,10 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     const int kend = min(a.K, kbeg + a.kchunk);
 
     const int tid = threadIdx.x, lane = tid & 63;
-    const int grp = KG > 1 ? tid / NTG : 0;                        // wave-uniform
+    // wave-uniform, and the compiler must know it: otherwise the k-tile count, the k offsets and the
+    // ring slot of a k-group are per-lane values — VGPR loop control (exec-masked back edge), 64-bit
+    // v_mad per global load and VALU ring-slot addresses in every grad_W iteration
+    const int grp = KG > 1 ? __builtin_amdgcn_readfirstlane(tid / NTG) : 0;
     const int lt = KG > 1 ? tid % NTG : tid;
     const int w = lt >> 6;
     const int wm = w / WARPS_N, wn = w % WARPS_N;
@@ -373,7 +376,10 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     SB sb;
     sa.init(a.A, a.lda, OP == OP_NT ? a.ridx : nullptr, m0, a.M, lt);
     sb.init(a.B, a.ldb, nullptr, n0, a.N, lt);
-    const bool do_copy = OP == OP_NT && a.acopy != nullptr && tn == 0;
+    // the fused gather's copy of A's rows: every column tile of a row block stages the same rows, so
+    // they share the copy — column tile tn writes the k-tiles with index ≡ tn (mod tiles_n) (one
+    // workgroup writing all of it finished its tile ≈ a copy later than the others in a one-round grid)
+    const bool do_copy = OP == OP_NT && a.acopy != nullptr;
     // grad_W bias: Σ over this split's k of the A (= g) tile, from the staging registers
     const bool do_bsum = OP == OP_TN && a.gbias != nullptr && tn == 0;
     f32x4 bs[SA::NV];
@@ -416,12 +422,17 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     unsigned short* const ring = lds + (KG > 1 ? grp * NS * BUF : 0);
 
     // split + LDS store of the staged tile at k0 (FULL: no k tail); COPY: also the gathered rows
+    // COPY (forward, fused gather): also the gathered rows; BSUM (grad_W of a bias): also Σ g — both
+    // compile-time, so the mainloop of the workgroups that do neither carries no dead VALU
     auto stage_a = [&](auto FULLc, auto COPYc, unsigned short* img, int k0) {
-        constexpr bool FULL = decltype(FULLc)::value, COPY = decltype(COPYc)::value;
+        constexpr bool FULL = decltype(FULLc)::value, COPY = OP == OP_NT && decltype(COPYc)::value;
+        constexpr bool BSUM = OP == OP_TN && decltype(COPYc)::value;
         if ((ABL & 2) && k0 != kbeg) return;
-        if (COPY) sa.copy_out(a.acopy, a.K, m0, a.M, k0, kend);
+        if constexpr (COPY) {
+            if (((k0 - kbeg) / BK) % a.tiles_n == tn) sa.copy_out(a.acopy, a.K, m0, a.M, k0, kend);
+        }
         sa.template store<FULL, (ABL & 64) != 0>(img, k0, kend);
-        if (do_bsum) {
+        if constexpr (BSUM) {
 #pragma unroll
             for (int q = 0; q < SA::NV; ++q) bs[q] += sa.v[q];
         }
@@ -531,9 +542,22 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
         __syncthreads();
         if (NK > 0) { rd_a(cur, 2); rd_b(cur, 0); rd_b(cur, 2); rd_a(cur, 0); }
         if (ABL & 32) stamp(1);
-        // steady state: tiles j+2 and j+3 exist and are full
+        // steady state: tiles j+2 and j+3 exist and are full.  grad_W's loop is unrolled by the ring
+        // length, so every ring slot's fragment / staging addresses are loop-invariant registers (no
+        // per-iteration slot arithmetic: 130 → 92 VALU per k-tile); the 256×256 kernels have no
+        // registers for three slots' addresses (the unrolled form spills)
         const int steady = NK - 3 - tail;
         int j = 0;
+        if constexpr (KG > 1) {
+            unsigned short* const s0 = cur;
+            unsigned short* const s1 = n1;
+            unsigned short* const s2 = n2;
+            for (; j + 3 <= steady; j += 3) {
+                iter(T{}, COPYc, j, s0, s1, s2);
+                iter(T{}, COPYc, j + 1, s1, s2, s0);
+                iter(T{}, COPYc, j + 2, s2, s0, s1);
+            }
+        }
         for (; j < steady; ++j) {
             iter(T{}, COPYc, j, cur, n1, n2);
             unsigned short* t = cur; cur = n1; n1 = n2; n2 = t;
@@ -546,7 +570,7 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
 #ifdef PPO_X3_PRIO2
     if ((tid >> 6) >= NTH / 128) __builtin_amdgcn_s_setprio(1);   // the second-dispatched half wins VALU arbitration
 #endif
-    if (do_copy) mainloop(T{});
+    if (do_copy || do_bsum) mainloop(T{});                          // (COPYc: the gather copy / Σ g)
     else mainloop(F{});
 #ifdef PPO_X3_PRIO2
     __builtin_amdgcn_s_setprio(0);
@@ -768,8 +792,11 @@ int g_x3_atomics = -1;                   // PPO_X3_ATOMICS=1: split-K partials b
 // waves of 32×64, 3 = 128×128 over two k-groups of 4 waves of 64×64, one workgroup per CU (grad_W),
 // 4 = 64×64 over 4 waves of 32×32, four workgroups per CU (small outputs: C3's 8192×256 minibatch
 // products have 32 tiles of 256×256 — an eighth of the CUs — but 512 of 64×64)
+// 5 = 256×128 over 8 waves of 64×64, one workgroup per CU (two rounds at C4: the first round's store
+// tail drains under the second round's mainloop)
 struct CfgX3 { int bm, bn, kg, slots_per_cu; };
-constexpr CfgX3 kCfgX3[] = {{256, 256, 1, 1}, {128, 128, 1, 2}, {128, 128, 1, 1}, {128, 128, 2, 1}, {64, 64, 1, 4}};
+constexpr CfgX3 kCfgX3[] = {{256, 256, 1, 1}, {128, 128, 1, 2}, {128, 128, 1, 1}, {128, 128, 2, 1}, {64, 64, 1, 4},
+                            {256, 128, 1, 1}};
 int g_force_x3 = -1;
 int g_split_x3 = 0;
 
@@ -802,6 +829,7 @@ void launch_cfg_x3(int c, const X3Args& a) {
         case 0: launch_x3<OP, 256, 256, 4, 512, 2, 1>(a); break;
         case 2: launch_x3<OP, 128, 128, 4, 512, 2, 1>(a); break;
         case 4: launch_x3<OP, 64, 64, 2, 256, 4, 1>(a); break;
+        case 5: launch_x3<OP, 256, 128, 4, 512, 2, 1>(a); break;
         case 3:
             if constexpr (OP == OP_TN) { launch_x3<OP, 128, 128, 2, 512, 2, 2>(a); break; }
             [[fallthrough]];

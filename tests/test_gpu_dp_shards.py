@@ -23,8 +23,8 @@ import numpy as np
 import pytest
 
 import ppo_ffi
-from helpers import (F32, assert_gemm_close, assert_normalised_close, assert_rel_close, gpu_relu_masks, nn_params_packed,
-                     oracle_grads_with_masks)
+from helpers import (F32, assert_gemm_close, assert_normalised_close, assert_rel_close, gpu_relu_masks, nn_grads_packed,
+                     nn_params_packed, oracle_grads_with_masks)
 from test_gpu_production import RELU, device_buffer
 from test_gpu_update import adam_first_step, assert_adam_delta, make_ppo, policy_state
 
@@ -45,11 +45,12 @@ def _gathered(lib, nn_ptr, B, S):
 
 
 def _mu_span(pol):
-    """μ's flat gradient span including the log σ gradient behind it (the policy's top bucket)."""
+    """μ's flat gradient span including the log σ gradient behind it: the policy's top all-reduce
+    bucket carries align4(A) floats there (ppo.c policy_step), so the span ends at the padded end."""
     mu = pol.mu.contents
     off = (_addr(pol.d_log_std_grad) - _addr(mu.d_grads)) // 4
     assert off >= mu.num_params
-    return off + pol.action_size, off
+    return off + (pol.action_size + 3) // 4 * 4, off
 
 
 def _read_rank(lib, ppo, Bs, S, A, rows_v, rows_p, buf):
@@ -59,8 +60,11 @@ def _read_rank(lib, ppo, Bs, S, A, rows_v, rows_p, buf):
     xv, xp = buf["state"][rows_v], buf["state"][rows_p]
     np.testing.assert_array_equal(_gathered(lib, ppo.contents.V, Bs, S), xv)
     np.testing.assert_array_equal(_gathered(lib, pol.mu, Bs, S), xp)
+    # gV / gmu_span: the flat (16-B padded) gradient buffers the all-reduce runs over; gV_packed /
+    # gmu_packed: the reference's packed [W0, b0, W1, b1, …] order for the comparisons
     return dict(gV=ppo_ffi.d2h(lib, ppo.contents.V.contents.d_grads, F32, ppo.contents.V.contents.num_params),
                 gmu_span=ppo_ffi.d2h(lib, pol.mu.contents.d_grads, F32, n_mu), ls_off=ls_off,
+                gV_packed=nn_grads_packed(lib, ppo.contents.V), gmu_packed=nn_grads_packed(lib, pol.mu),
                 mV=gpu_relu_masks(lib, ppo.contents.V, xv), mmu=gpu_relu_masks(lib, pol.mu, xp),
                 v1=nn_params_packed(lib, ppo.contents.V), mu1=nn_params_packed(lib, pol.mu),
                 adv=ppo_ffi.d2h(lib, ppo.contents.buffer.contents.d_advantage_p, F32, buf["reward"].size))
@@ -160,8 +164,8 @@ def test_two_rank_shards_vs_global_minibatch(lib, oracle, monkeypatch, cfg):
     assert w_glob[0] == 2 * Ns
     # normalised with the GLOBAL statistics (the exact statistics of the union's advantages: the
     # oracle's fp32 running sums drift at N ≳ 1e5, helpers.assert_normalised_close)
-    A = adv_u.astype(np.float64) * (np.float64(ref["adv_std"]) + 1e-8) + ref["adv_mean"]
-    adv_exact = (A - A.mean()) / (A.std() + 1e-8)
+    raw_u = adv_u.astype(np.float64) * (np.float64(ref["adv_std"]) + 1e-8) + ref["adv_mean"]
+    adv_exact = (raw_u - raw_u.mean()) / (raw_u.std() + 1e-8)
     for r, rr in ((0, r0), (1, r1)):
         assert_rel_close(rr["adv"], adv_exact[r * Ns:(r + 1) * Ns], 1e-4, 1e-4, f"{cfg} rank {r} advantages")
     assert_normalised_close(np.concatenate([r0["adv"], r1["adv"]]), adv_u, ref["adv_mean"], ref["adv_std"],
@@ -176,7 +180,7 @@ def test_two_rank_shards_vs_global_minibatch(lib, oracle, monkeypatch, cfg):
     _, g = oracle.mse(y, tgt)
     gV_ref, _ = oracle_grads_with_masks(oracle, sv, RELU(sv), v0, x, g.reshape(-1, 1), _cat_masks(r0["mV"], r1["mV"]),
                                         f"{cfg} value", max_flips=256)
-    gV = r0["gV"] / 2
+    gV = r0["gV_packed"] / 2
     assert_gemm_close(gV, gV_ref, B, f"{cfg} all-reduced value gradient")
     flips = assert_adam_delta(r0["v1"], adam_first_step(v0, gV_ref, LR), gV_ref, LR, f"{cfg} value params")
     assert flips <= v0.size // 1000
@@ -194,11 +198,11 @@ def test_two_rank_shards_vs_global_minibatch(lib, oracle, monkeypatch, cfg):
     gmu_ref, _ = oracle_grads_with_masks(oracle, sizes, RELU(sizes), mu0, x, gmu_out,
                                          _cat_masks(r0["mmu"], r1["mmu"]), f"{cfg} policy", max_flips=256)
     n_mu = mu0.size
-    gmu = r0["gmu_span"][:n_mu] / 2
+    gmu = r0["gmu_packed"] / 2
     gls = r0["gmu_span"][r0["ls_off"]:r0["ls_off"] + A] / 2
     assert_gemm_close(gmu, gmu_ref, B, f"{cfg} all-reduced policy gradient")
     assert_rel_close(gls, gls_ref + gent, 1e-3, 1e-4 * max(1.0, float(np.abs(gls_ref).max())), f"{cfg} log σ grad")
     flips = assert_adam_delta(r0["mu1"], adam_first_step(mu0, gmu_ref, LR), gmu_ref, LR, f"{cfg} policy params")
     assert flips <= n_mu // 1000
     # the two ranks' local gradients really differ (the test is not self-similar)
-    assert np.abs(r0["gV"] - 2 * g1V).max() > 1e-3 * np.abs(gV_ref).max()
+    assert np.abs(r0["gV_packed"] - r1["gV_packed"]).max() > 1e-3 * np.abs(gV_ref).max()

@@ -19,8 +19,9 @@ V(next_state) reuse with its own-row forward, the scan, the Welford statistics a
 against the oracle's GAE — the reference's two full V forwards (OpenBLAS, 16 threads) and its
 recursion (ref_gae) — at C3 (N = 262,144), C4 (N = 1,048,576) and the C5 shard (N = 524,288; bf16 V:
 the scan teacher-forced on the GPU's own V values, V itself within the bf16 bound).  The step tests
-then take their targets and advantages from the ORACLE's GAE, so no link of the production chain
-compares the GPU with its own output.
+of C3 and C4 then take their targets and advantages from the ORACLE's GAE, so no link of the fp32
+production chain compares the GPU with its own output (C5's bf16 steps are compared given the
+advantages they trained on, which test_c5_bf16_gae pins).
 
 Inputs are bench.py's own: ppo_fill_synthetic (seeded device generator) after create_ppo from srand.
 """
@@ -532,7 +533,6 @@ def test_c5_bf16_timed_policy_step(lib, oracle, c5):
     pol = ppo.contents.policy.contents
     mu0 = nn_params_packed(lib, pol.mu)
     ls0 = ppo_ffi.d2h(lib, pol.d_log_std, F32, A)
-    adv_ref_all, _, _, _ = oracle_gae(lib, oracle, ppo, C5, N)
     lib.ppo_set_step_limit(ppo, 0, 1)
     lib.ppo_update(ppo, 0.99, B, 1, 0, 1, seed)
     lib.ppo_synchronize()
@@ -552,9 +552,23 @@ def test_c5_bf16_timed_policy_step(lib, oracle, c5):
     gtop, gls_head = oracle.log_prob_backwards(y, ls0, a, glp)
     assert_rel_close(gls, gls_head + gent, 1e-3, 1e-4 * max(1.0, float(np.abs(gls_head).max())), "C5 log_std grad")
     gmu = check_bf16_layers(lib, pol.mu, C5, mu0, x, gtop, True, "C5 policy")
-    g_ref, gls_ref = ref_policy_grads(oracle, C5, mu0, ls0, x, a, adv_ref_all[rows], old, None, "C5 policy")
+    # the GPU's advantages: in bf16 mode the GAE's V forward is bf16 too, so the fp32 oracle's advantages
+    # differ by the bf16 bound (test_c5_bf16_gae pins them: V against the fp32 oracle, the scan on the
+    # GPU's own V at the fp32 tolerances) — the step is compared given the advantages it trained on
+    g_ref, gls_ref = ref_policy_grads(oracle, C5, mu0, ls0, x, a, adv, old, None, "C5 policy")
     close(gmu, g_ref, 3e-2, "C5 policy grads vs fp32 oracle")
-    close(gls, gls_ref, 3e-2, "C5 log_std grad vs fp32 oracle")
+    # ∂L/∂logσ_a = Σ_rows (−1 + z²)·∂L/∂lp with z = (a − μ)/σ: a sum of 16384 terms that cancel
+    # (|Σ| ≪ Σ|terms|), each moved by the bf16 network's μ (≈ 2^-8 relative) — bounded by 3e-2·max|ref|
+    # plus 2^-7·Σ|terms| per action dimension (the terms from the fp32 oracle's forward)
+    mu_ref = oracle.mlp_layer_outputs(C5, oracle.mlp_forward(C5, RELU(C5), mu0, x), B)[-1]
+    _, glp_ref, _ = oracle.policy_loss_and_grad(adv, oracle.log_prob(mu_ref, ls0, a), old, oracle.entropy(ls0), 0.0,
+                                                0.2)
+    z = (a.astype(np.float64) - mu_ref) * np.exp(-ls0.astype(np.float64))
+    sum_abs = (np.abs(-1.0 + z * z) * np.abs(glp_ref.astype(np.float64))[:, None]).sum(axis=0)
+    err = np.abs(gls.astype(np.float64) - gls_ref)
+    tol = 3e-2 * float(np.abs(gls_ref).max()) + 2.0 ** -7 * sum_abs
+    print(f"C5 log_std grad vs fp32 oracle: max err {err.max():.3g}, worst err/tol {float((err / tol).max()):.3f}")
+    assert (err <= tol).all(), "C5 log_std grad vs fp32 oracle"
     flips = assert_adam_delta(mu1, adam_first_step(mu0, gmu, LR), gmu, LR, "C5 policy params")
     assert flips <= mu1.size // 1000
 def test_c5_bf16_timed_value_step(lib, oracle, c5):
@@ -565,7 +579,6 @@ def test_c5_bf16_timed_value_step(lib, oracle, c5):
     B, seed = 16384, 57
     V = ppo.contents.V
     v0 = nn_params_packed(lib, V)
-    _, tgt_ref_all, _, _ = oracle_gae(lib, oracle, ppo, C5, N)
     lib.ppo_set_step_limit(ppo, 1, 0)
     lib.ppo_update(ppo, 0.99, B, 0, 1, 1, seed)
     lib.ppo_synchronize()
@@ -579,7 +592,7 @@ def test_c5_bf16_timed_value_step(lib, oracle, c5):
     y = ppo_ffi.d2h(lib, V.contents.d_output, F32, B)
     gtop = (2 * (y.astype(np.float64) - tgt) / B).reshape(-1, 1)
     gV = check_bf16_layers(lib, V, sv, v0, x, gtop, True, "C5 value")
-    g_ref, _ = ref_value_grads(oracle, sv, v0, x, tgt_ref_all[rows], None, "C5 value")   # fp32 oracle GAE
+    g_ref, _ = ref_value_grads(oracle, sv, v0, x, tgt, None, "C5 value")   # targets: see the policy step
     close(gV, g_ref, 3e-2, "C5 value grads vs fp32 oracle")
     # Adam (element-wise fp32) on the gradient it read — a bf16-level gradient difference would move
     # Adam's first step lr·g/(|g| + ε) where |g| is near ε

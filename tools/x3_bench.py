@@ -31,7 +31,7 @@ def main():
             for s in map(int, args.splits.split(",")):
                 if op != 2 and s:
                     continue
-                if c >= 0 and op == 2 and c not in (1, 3, 4):
+                if c >= 0 and op == 2 and c not in (1, 3, 4, 5):
                     continue
                 us = lib.ppo_bench_gemm_x3(op, m, n, l, args.iters if m < 1 << 20 else 5, c, s)
                 tf = 2.0 * m * n * l / (us * 1e-6) / 1e12
