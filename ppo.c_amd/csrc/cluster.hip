@@ -1,0 +1,670 @@
+// cluster.hip — a whole phase of minibatch steps at the reference's B = 64 for mid-size networks
+// (S → H → H → O with H = 256, config C3), in ONE launch of NWG = H/32 cooperating workgroups.
+//
+// At B = 64 the multi-launch loop is a chain of ≈ 9 dependent small kernels per step (≈ 36 µs per
+// step at C3, profiles/r03_graph_replay.txt) and one workgroup (tiny.hip) cannot hold a 256-wide
+// network's Adam state or run its ≈ 27 MFLOP per step fast enough.  Here workgroup c owns the 32
+// hidden units [32c, 32c+32) of both hidden layers: rows of W0 and W1, their biases, and the
+// matching input columns of the output layer W2; its parameters live in LDS and their Adam moments in
+// VGPRs for the whole phase.  Per step (reference ppo.cu:395-443, arithmetic as in tiny.hip):
+//   gather (every workgroup, the same 64 rows)           → x [64 × S]
+//   h1[:, own] = relu(x·W0[own]ᵀ + b0)                   → published (X1)       — barrier A
+//   h1 = every workgroup's columns;  h2[:, own] = relu(h1·W1[own]ᵀ + b1)
+//   y partial = h2[:, own]·W2[:, own]ᵀ                   → published (Y)        — barrier B
+//   y = Σ partials + b2 (fixed order);  head (MSE or clipped surrogate) — every workgroup, identically
+//   gW2[:, own], gb2, g2 = (g3·W2[:, own]) ⊙ 1[h2 > 0];  g1 partial = g2·W1[own, :] → published (G1)
+//   gW1[own] = g2ᵀ·h1 with Adam fused into its epilogue                        — barrier C
+//   g1[:, own] = Σ partials ⊙ 1[h1 > 0];  gW0[own] = g1ᵀ·x;  Adam of the rest
+// Three barriers per step.  Hand-offs (MI355X_MICROARCH.md § inter-workgroup visibility, the first
+// row of the sc1 table): every published byte is stored write-through (sc1, 16-B buffer stores),
+// every storing wave drains (s_waitcnt vmcnt(0)) before the workgroup barrier, ONE lane per workgroup
+// adds to one monotonic counter (agent scope), ONE lane polls it with sc1 loads + s_sleep, the other
+// waves wait at the workgroup barrier, and every load of published bytes is an sc1 load.  Spins are
+// bounded: a timeout sets the host-visible error word and every workgroup leaves.  b2 and log σ are
+// replicated: every workgroup computes their gradients from the same values in the same order and
+// applies the same Adam step (bit-identical copies).  GEMMs: v_mfma_f32_16x16x4_f32 (exact fp32).
+#include "dev.h"
+
+#include <cmath>
+#include <cstdlib>
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int TPB = 512, NWAVE = TPB / 64;
+constexpr int BB = 64;            // minibatch rows
+constexpr int HC = 32;            // hidden units per workgroup
+constexpr int HCP = 36;           // pitch of [64][HC] arrays (4·odd: conflict-free strided MFMA reads)
+constexpr int OMAX = 16;          // output width
+constexpr int OPP = 20;           // pitch of [64][OMAX] arrays
+
+struct Feistel { uint32_t k[4]; uint32_t half, mask, n; };
+
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+    return x;
+}
+// identical to buffer.hip's feistel_index (restated in oracle/ref_cpu.c: ref_feistel_index)
+__device__ __forceinline__ uint32_t feistel_index(uint32_t i, const Feistel& f) {
+    uint32_t x = i;
+    do {
+        uint32_t L = x >> f.half, R = x & f.mask;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const uint32_t nl = R;
+            R = L ^ (mix32(R ^ f.k[r]) & f.mask);
+            L = nl;
+        }
+        x = (L << f.half) | R;
+    } while (x >= f.n);
+    return x;
+}
+
+struct ClArgs {
+    int S, O, policy, SP;                     // SP: pitch of x and W0 rows in LDS (4·odd ≥ S)
+    float *params, *grads, *m, *v;            // the network's flat buffers and Adam moments
+    long woff[3], boff[3];
+    float *log_std, *log_std_grad, *m_ls, *v_ls;
+    const float *state, *action, *logprob, *adv, *adv_target;
+    int limit, num_batches, n_epochs, total_steps;
+    const int* perms;
+    Feistel fk[16];
+    const float *steps, *steps_ls;            // per step {lr/bc1, bc2}
+    float b1, b2, eps, ent_coeff;
+    float* stats;
+    float *X1, *Y, *G1;                       // published: h1 [64][H], y partials [NWG][64][OMAX], g1 partials [NWG][64][H]
+    unsigned* ctr;                            // barrier arrivals (zeroed before the launch)
+    unsigned* err;                            // host-visible error word (0 = fine)
+    int active_stride;                        // workgroup b works iff b % active_stride == 0 (same-XCD bias)
+};
+
+// ---- hand-off primitives (sc1: write-through stores, L1-bypassing loads) ----
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, long floats) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, (int)(floats * 4), 0x00020000);
+}
+__device__ __forceinline__ void st16_sc1(__amdgpu_buffer_rsrc_t r, int off_floats, f32x4 v) {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off_floats * 4, 0, 16);
+}
+__device__ __forceinline__ f32x4 ld16_sc1(__amdgpu_buffer_rsrc_t r, int off_floats) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off_floats * 4, 0, 16));
+}
+
+// the workgroup's published stores are complete (every wave drained), then one arrival; wait until
+// all `nwg` workgroups have arrived for barrier number `n` (counting from 0 within the launch).
+// Returns false on timeout (error word set), uniformly for the workgroup.
+__device__ __forceinline__ bool cluster_barrier(const ClArgs& a, unsigned n, int nwg, int* flag_lds) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(a.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned target = (unsigned)nwg * (n + 1);
+        unsigned spins = 0;
+        int ok = 1;
+        while (__hip_atomic_load(a.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > (1u << 22) ||
+                __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
+                __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                ok = 0;
+                break;
+            }
+        }
+        *flag_lds = ok;
+    }
+    __syncthreads();
+    return *flag_lds != 0;
+}
+
+// One 16×16 output tile: acc(i, j) = Σ_k A(i, k)·B(k, j), A(i, k) = A[i·as_i + k·as_k],
+// B(k, j) = B[k·bs_k + j·bs_j] (pointers at the tile's origin, LDS).  Lane (c = l&15, q = l>>4)
+// loads A(c, k0+q), B(k0+q, c) and receives acc rows 4q..4q+3 of column c.  K ≥ 1; a k-tail
+// (K % 4) is zeroed.  Eight MFMAs' operands are loaded before their MFMAs issue.
+__device__ __forceinline__ f32x4 mm_tile(const float* A, int as_i, int as_k, const float* B, int bs_k, int bs_j,
+                                         int K) {
+    const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    const float* Ar = A + c * as_i;
+    const float* Bc = B + c * bs_j;
+    for (int k0 = 0; k0 < K; k0 += 32) {
+        float av[8], bv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int k = min(k0 + 4 * u + q, K - 1);
+            av[u] = Ar[k * as_k];
+            bv[u] = Bc[k * bs_k];
+        }
+        asm("" : "+v"(av[0]), "+v"(av[1]), "+v"(av[2]), "+v"(av[3]), "+v"(av[4]), "+v"(av[5]), "+v"(av[6]),
+                 "+v"(av[7]), "+v"(bv[0]), "+v"(bv[1]), "+v"(bv[2]), "+v"(bv[3]), "+v"(bv[4]), "+v"(bv[5]),
+                 "+v"(bv[6]), "+v"(bv[7]));
+        const int nu = K - k0 >= 32 ? 8 : (K - k0 + 3) >> 2;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const bool kin = k0 + 4 * u + q < K;
+            if (u < nu) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(kin ? av[u] : 0.f, kin ? bv[u] : 0.f, acc, 0, 0, 0);
+        }
+    }
+    return acc;
+}
+
+__device__ __forceinline__ float log_prob_row(const float* mu, const float* log_std, const float* a, int A) {
+    const float cst = (float)(-0.5 * A * (double)logf((float)(2 * M_PI)));
+    float lp = cst;
+    for (int j = 0; j < A; ++j) {
+        const float z = (a[j] - mu[j]) / expf(log_std[j]);
+        lp = (float)((double)lp - ((double)log_std[j] + 0.5 * (double)(z * z)));
+    }
+    return lp;
+}
+
+__device__ __forceinline__ float surrogate(float adv, float lp, float old_lp, float eps, int m, float* grad) {
+    const float ratio = (float)exp((double)(lp - old_lp));
+    const int adv_pos = adv > 0;
+    const int ratio_pos = ratio > 1 + eps;
+    const int ratio_neg = ratio < 1 - eps;
+    *grad = -(adv_pos * !ratio_pos + !adv_pos * !ratio_neg) * adv * ratio / m;
+    return adv * (adv_pos * (ratio_pos * (1 + eps) + !ratio_pos * ratio) +
+                  !adv_pos * (ratio_neg * (1 - eps) + !ratio_neg * ratio));
+}
+
+// adam.cu:53-74 / tiny.hip adam_elem
+__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, float step, float b1, float b2,
+                                          float bc2) {
+    m = b1 * m + (1 - b1) * g;
+    v = b2 * v + (1 - b2) * (g * g);
+    const float denom = (float)((double)sqrtf(v / bc2) + 1e-8);
+    p -= step * m / denom;
+}
+
+// LDS layout (floats) for hidden width H
+template <int H>
+struct Lay {
+    static constexpr int HP = H + 4;                  // pitch of [64][H] and [HC][H] (4·odd)
+    static constexpr int SPMAX = 20;                  // S ≤ 20 (SP = 4·odd ≤ 20)
+    static constexpr int x = 0;                       // [64][SP]
+    static constexpr int rows = x + BB * SPMAX;       // int [64]
+    static constexpr int tgt = rows + BB;             // [64] value target / policy advantage
+    static constexpr int olp = tgt + BB;              // [64] old log-prob
+    static constexpr int act = olp + BB;              // [64][OMAX] actions
+    static constexpr int W0 = act + BB * OMAX;        // [HC][SP]
+    static constexpr int b0 = W0 + HC * SPMAX;        // [HC]
+    static constexpr int W1 = b0 + HC;                // [HC][HP]
+    static constexpr int b1 = W1 + HC * HP;           // [HC]
+    static constexpr int W2 = b1 + HC;                // [OMAX][HCP] own input columns of the output layer
+    static constexpr int b2 = W2 + OMAX * HCP;        // [OMAX] (replicated)
+    static constexpr int ls = b2 + OMAX;              // [OMAX] log σ (replicated)
+    static constexpr int h1 = ls + OMAX;              // [64][HP]
+    static constexpr int h2 = h1 + BB * HP;           // [64][HCP] own columns
+    static constexpr int yo = h2 + BB * HCP;          // [64][OPP] y / μ, then (in place) ∂L/∂y
+    static constexpr int g2 = yo + BB * OPP;          // [64][HCP]
+    static constexpr int g1 = g2 + BB * HCP;          // [64][HCP]
+    static constexpr int gW0 = g1 + BB * HCP;         // [HC][SP]
+    static constexpr int gb0 = gW0 + HC * SPMAX;      // [HC]
+    static constexpr int gb1 = gb0 + HC;              // [HC]
+    static constexpr int gW2 = gb1 + HC;              // [OMAX][HCP]
+    static constexpr int gb2 = gW2 + OMAX * HCP;      // [OMAX]
+    static constexpr int gls = gb2 + OMAX;            // [OMAX]
+    static constexpr int glr = gls + OMAX;            // [64][OMAX] per-row log σ terms (ordered sum)
+    static constexpr int red = glr + BB * OMAX;       // [NWAVE] loss partials
+    static constexpr int flag = red + NWAVE;          // int: barrier result
+    static constexpr int TOTAL = flag + 4;
+};
+
+// the small parameters of a workgroup (everything but its W1 rows), enumerated e = 0 … nsmall−1:
+// W0 rows [HC][S], b0 [HC], b1 [HC], W2 columns [O][HC], b2 [O] (replicated), log σ [O] (policy,
+// replicated; its Adam uses the entropy step sizes)
+struct Small { int lds_p, lds_g; long gflat; int kind; };   // kind 0 network, 1 log σ, 2 replicated net
+
+template <int H>
+__device__ __forceinline__ Small small_elem(const ClArgs& a, int e, int c0) {
+    using L = Lay<H>;
+    const int S = a.S, O = a.O;
+    if (e < HC * S) { const int j = e / S, s = e % S;
+        return {L::W0 + j * a.SP + s, L::gW0 + j * a.SP + s, a.woff[0] + (long)(c0 + j) * S + s, 0}; }
+    e -= HC * S;
+    if (e < HC) return {L::b0 + e, L::gb0 + e, a.boff[0] + c0 + e, 0};
+    e -= HC;
+    if (e < HC) return {L::b1 + e, L::gb1 + e, a.boff[1] + c0 + e, 0};
+    e -= HC;
+    if (e < O * HC) { const int o = e / HC, j = e % HC;
+        return {L::W2 + o * HCP + j, L::gW2 + o * HCP + j, a.woff[2] + (long)o * H + c0 + j, 0}; }
+    e -= O * HC;
+    if (e < O) return {L::b2 + e, L::gb2 + e, a.boff[2] + e, 2};
+    e -= O;
+    return {L::ls + e, L::gls + e, e, 1};
+}
+
+constexpr int SMALL_SLOTS = 4;        // ≤ 4·512 small parameters per workgroup
+
+template <int H>
+__global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
+    constexpr int NWG = H / HC;
+    using L = Lay<H>;
+    constexpr int HP = L::HP;
+    if ((int)blockIdx.x % a.active_stride) return;
+    const int cw = (int)blockIdx.x / a.active_stride;            // this workgroup's unit block
+    const int c0 = cw * HC;
+    extern __shared__ float lds[];
+    int* rows = reinterpret_cast<int*>(lds + L::rows);
+    int* flag = reinterpret_cast<int*>(lds + L::flag);
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int c = lane & 15, q = lane >> 4;
+    const int S = a.S, O = a.O, SP = a.SP, A = a.O;
+    const int nsmall = HC * S + 2 * HC + O * HC + O + (a.policy ? A : 0);
+    const auto rX1 = rsrc(a.X1, (long)BB * H);
+    const auto rY = rsrc(a.Y, (long)NWG * BB * OMAX);
+    const auto rG1 = rsrc(a.G1, (long)NWG * BB * H);
+
+    // ---- phase start: own parameters → LDS, Adam moments → VGPRs ----
+    for (int e = tid; e < HC * H; e += TPB) {
+        const int j = e / H, k = e % H;
+        lds[L::W1 + j * HP + k] = a.params[a.woff[1] + (long)(c0 + j) * H + k];
+    }
+    for (int e = tid; e < OMAX * HCP; e += TPB) lds[L::W2 + e] = 0.f;       // rows o ≥ O stay zero
+    for (int e = tid; e < OMAX; e += TPB) { lds[L::b2 + e] = 0.f; lds[L::ls + e] = 0.f; }
+    __syncthreads();
+    float sm[SMALL_SLOTS], sv[SMALL_SLOTS];
+#pragma unroll
+    for (int u = 0; u < SMALL_SLOTS; ++u) {
+        const int e = tid + u * TPB;
+        sm[u] = sv[u] = 0.f;
+        if (e < nsmall) {
+            const Small s = small_elem<H>(a, e, c0);
+            if (s.kind == 1) { lds[s.lds_p] = a.log_std[s.gflat]; sm[u] = a.m_ls[s.gflat]; sv[u] = a.v_ls[s.gflat]; }
+            else { lds[s.lds_p] = a.params[s.gflat]; sm[u] = a.m[s.gflat]; sv[u] = a.v[s.gflat]; }
+        }
+    }
+    // W1 rows' moments: the elements this lane's gW1 tiles hold (tiles t = w + 8u: rows 16(t/16) + 4q + e,
+    // column 16(t%16) + c)
+    constexpr int T1 = (HC / 16) * (H / 16) / NWAVE;              // gW1 tiles per wave
+    float m1[T1][4], v1[T1][4];
+#pragma unroll
+    for (int u = 0; u < T1; ++u) {
+        const int t = w + NWAVE * u, tj = t / (H / 16), tk = t % (H / 16);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+            const long g = a.woff[1] + (long)(c0 + 16 * tj + 4 * q + e) * H + 16 * tk + c;
+            m1[u][e] = a.m[g];
+            v1[u][e] = a.v[g];
+        }
+    }
+    __syncthreads();
+
+    unsigned nbar = 0;
+    int step = 0;
+    bool ok = true;
+    for (int ep = 0; ep < a.n_epochs && ok; ++ep) {
+        for (int kb = 0; kb < a.num_batches && step < a.total_steps && ok; ++kb, ++step) {
+            // ---- gather (trajectory_buffer.cu:168-200) ----
+            if (tid < BB) {
+                const int list = (int)(((long)kb * BB + tid) % a.limit);
+                const int src = a.perms ? a.perms[(long)ep * a.limit + list]
+                                        : (int)feistel_index((uint32_t)list, a.fk[ep & 15]);
+                rows[tid] = src;
+                if (a.policy) {
+                    lds[L::tgt + tid] = a.adv[src];
+                    lds[L::olp + tid] = a.logprob[src];
+                } else {
+                    lds[L::tgt + tid] = a.adv_target[src];
+                }
+            }
+            __syncthreads();
+            for (int e = tid; e < BB * S; e += TPB) {
+                const int i = e / S, s = e % S;
+                lds[L::x + i * SP + s] = a.state[(long)rows[i] * S + s];
+            }
+            if (a.policy)
+                for (int e = tid; e < BB * A; e += TPB) {
+                    const int i = e / A, j = e % A;
+                    lds[L::act + i * OMAX + j] = a.action[(long)rows[i] * A + j];
+                }
+            __syncthreads();
+
+            // ---- layer 0, own units: h1ᵀ[j][b] = Σ_s W0[j][s]·x[b][s] + b0[j]  (2 × 4 tiles, one per wave)
+            {
+                const int tj = w / 4, tb = w % 4;
+                const f32x4 acc = mm_tile(lds + L::W0 + 16 * tj * SP, SP, 1, lds + L::x + 16 * tb * SP, 1, SP, S);
+                const int b = 16 * tb + c, j = 16 * tj + 4 * q;
+                f32x4 hv;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float v = acc[e] + lds[L::b0 + j + e];
+                    hv[e] = v > 0.f ? v : 0.f;                           // neural_network.cu:74-105 (ReLU)
+                }
+                *reinterpret_cast<f32x4*>(lds + L::h1 + b * HP + c0 + j) = hv;
+                st16_sc1(rX1, b * H + c0 + j, hv);                       // publish
+            }
+            ok = cluster_barrier(a, nbar++, NWG, flag);                  // A: every h1 column published
+            if (!ok) break;
+            // every other workgroup's h1 columns (sc1 loads)
+            for (int e = tid; e < BB * (H / 4); e += TPB) {
+                const int b = e / (H / 4), k = 4 * (e % (H / 4));
+                if (k >= c0 && k < c0 + HC) continue;
+                *reinterpret_cast<f32x4*>(lds + L::h1 + b * HP + k) = ld16_sc1(rX1, b * H + k);
+            }
+            __syncthreads();
+
+            // ---- layer 1, own units: h2[b][j] = relu(Σ_k h1[b][k]·W1[j][k] + b1[j])  (4 × 2 tiles)
+            {
+                const int tb = w / 2, tj = w % 2;
+                const f32x4 acc = mm_tile(lds + L::h1 + 16 * tb * HP, HP, 1, lds + L::W1 + 16 * tj * HP, 1, HP, H);
+                const int j = 16 * tj + c;
+                const float bj = lds[L::b1 + j];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float v = acc[e] + bj;
+                    lds[L::h2 + (16 * tb + 4 * q + e) * HCP + j] = v > 0.f ? v : 0.f;
+                }
+            }
+            __syncthreads();
+            // ---- output layer, own input columns: yᵀ[o][b] = Σ_j W2[o][j]·h2[b][j]  (4 tiles, waves 0-3)
+            if (w < 4) {
+                const f32x4 acc = mm_tile(lds + L::W2, HCP, 1, lds + L::h2 + 16 * w * HCP, 1, HCP, HC);
+                st16_sc1(rY, (cw * BB + 16 * w + c) * OMAX + 4 * q, acc);     // publish Y[cw][b][4q..4q+3]
+            }
+            ok = cluster_barrier(a, nbar++, NWG, flag);                  // B: every y partial published
+            if (!ok) break;
+            // ---- y = Σ_c partials (fixed order) + b2; the head, identically in every workgroup ----
+            if (tid < BB * (OMAX / 4)) {
+                const int b = tid / (OMAX / 4), oq = 4 * (tid % (OMAX / 4));
+                f32x4 s = ld16_sc1(rY, b * OMAX + oq);
+                for (int cc = 1; cc < NWG; ++cc) s += ld16_sc1(rY, (cc * BB + b) * OMAX + oq);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) lds[L::yo + b * OPP + oq + e] = s[e] + lds[L::b2 + oq + e];
+            }
+            __syncthreads();
+            float part = 0.f;
+            if (tid < BB) {
+                const int i = tid;
+                float* yo = lds + L::yo + i * OPP;
+                if (!a.policy) {                                         // loss.cu:5-23
+                    const float y = yo[0], t = lds[L::tgt + i];
+                    const float d = t - y;
+                    part = d * d;
+                    yo[0] = 2 * (y - t) / (float)BB;
+                } else {                                                 // ppo.cu:82-107, policy.cu:67-111
+                    float g;
+                    const float* ls = lds + L::ls;
+                    const float* ac = lds + L::act + i * OMAX;
+                    const float lp = log_prob_row(yo, ls, ac, A);
+                    part = surrogate(lds[L::tgt + i], lp, lds[L::olp + i], a.eps, BB, &g);
+                    for (int j = 0; j < A; ++j) {
+                        const float e2 = expf(-2 * ls[j]);
+                        const float d = ac[j] - yo[j];
+                        lds[L::glr + i * OMAX + j] = (-1 + d * d * e2) * g;
+                        yo[j] = d * e2 * g;
+                    }
+                }
+                for (int j = O; j < OMAX; ++j) yo[j] = 0.f;              // padded outputs carry no gradient
+                for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+            }
+            __syncthreads();
+            if (tid == 0 && cw == 0) {                                   // the loss sums (once)
+                if (!a.policy) {
+                    atomicAdd(a.stats + 0, part * (1.0f / (float)BB));
+                } else {
+                    float ent = (float)(A * 0.5 * (1 + log(2 * M_PI)));
+                    for (int j = 0; j < A; ++j) ent += lds[L::ls + j];
+                    atomicAdd(a.stats + 1, -part / BB - a.ent_coeff * ent);
+                }
+            }
+            // replicated gradients in a fixed order: gb2[o] = Σ_b g3[b][o]; log σ: Σ_b row terms − c_ent
+            if (tid < O) {
+                float s = 0.f;
+                for (int b = 0; b < BB; ++b) s += lds[L::yo + b * OPP + tid];
+                lds[L::gb2 + tid] = s;
+                if (a.policy) {
+                    float t = 0.f;
+                    for (int b = 0; b < BB; ++b) t += lds[L::glr + b * OMAX + tid];
+                    lds[L::gls + tid] = t + -a.ent_coeff;                // ppo.cu:436-438
+                }
+            }
+            // ---- output layer backward, own columns: gW2[o][j] = Σ_b g3[b][o]·h2[b][j]  (2 tiles)
+            if (w < 2) {
+                const f32x4 acc = mm_tile(lds + L::yo, 1, OPP, lds + L::h2 + 16 * w, HCP, 1, BB);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) lds[L::gW2 + (4 * q + e) * HCP + 16 * w + c] = acc[e];
+            }
+            // g2[b][j] = (Σ_o g3[b][o]·W2[o][j]) ⊙ 1[h2[b][j] > 0]  (4 × 2 tiles)
+            {
+                const int tb = w / 2, tj = w % 2;
+                const f32x4 acc = mm_tile(lds + L::yo + 16 * tb * OPP, OPP, 1, lds + L::W2 + 16 * tj, HCP, 1, O);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int b = 16 * tb + 4 * q + e, j = 16 * tj + c;
+                    lds[L::g2 + b * HCP + j] = lds[L::h2 + b * HCP + j] > 0.f ? acc[e] : 0.f;
+                }
+            }
+            __syncthreads();
+            // ---- g1 partial: P[b][k] = Σ_j g2[b][j]·W1[j][k], computed as Pᵀ tiles (4 consecutive k per
+            // lane → 16-B publishes): Pᵀ[k][b] = Σ_j W1[j][k]·g2[b][j]  (16 × 4 tiles, 8 per wave)
+            for (int t = w; t < (H / 16) * (BB / 16); t += NWAVE) {
+                const int tk = t / (BB / 16), tb = t % (BB / 16);
+                const f32x4 acc = mm_tile(lds + L::W1 + 16 * tk, 1, HP, lds + L::g2 + 16 * tb * HCP, 1, HCP, HC);
+                st16_sc1(rG1, (cw * BB + 16 * tb + c) * H + 16 * tk + 4 * q, acc);
+            }
+            // bias gradient of layer 1 (fixed order)
+            if (tid < HC) {
+                float s = 0.f;
+                for (int b = 0; b < BB; ++b) s += lds[L::g2 + b * HCP + tid];
+                lds[L::gb1 + tid] = s;
+            }
+            __syncthreads();                                             // every wave done reading W1
+            // ---- gW1[j][k] = Σ_b g2[b][j]·h1[b][k] with Adam fused (the lane holds these elements'
+            // moments); the last step also writes the gradient out (callers may read it)
+            {
+                const float st = a.steps[2 * step], bc2 = a.steps[2 * step + 1];
+#pragma unroll
+                for (int u = 0; u < T1; ++u) {
+                    const int t = w + NWAVE * u, tj = t / (H / 16), tk = t % (H / 16);
+                    const f32x4 acc = mm_tile(lds + L::g2 + 16 * tj, 1, HCP, lds + L::h1 + 16 * tk, HP, 1, BB);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        float* p = lds + L::W1 + (16 * tj + 4 * q + e) * HP + 16 * tk + c;
+                        float pv = *p;
+                        adam_elem(pv, acc[e], m1[u][e], v1[u][e], st, a.b1, a.b2, bc2);
+                        *p = pv;
+                    }
+                }
+            }
+            ok = cluster_barrier(a, nbar++, NWG, flag);                  // C: every g1 partial published
+            if (!ok) break;
+            // ---- g1[b][j] = Σ_c partials (fixed order) ⊙ 1[h1 > 0], own units ----
+            {
+                const int b = tid / (HC / 4), jq = 4 * (tid % (HC / 4));      // 64 × 8 float4 = 512 threads
+                f32x4 s = ld16_sc1(rG1, b * H + c0 + jq);
+                for (int cc = 1; cc < NWG; ++cc) s += ld16_sc1(rG1, (cc * BB + b) * H + c0 + jq);
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                    lds[L::g1 + b * HCP + jq + e] = lds[L::h1 + b * HP + c0 + jq + e] > 0.f ? s[e] : 0.f;
+            }
+            __syncthreads();
+            // ---- layer 0 backward, own rows: gW0[j][s] = Σ_b g1[b][j]·x[b][s] (2 × ⌈S/16⌉ tiles), gb0 ----
+            {
+                const int ts = (S + 15) / 16;
+                for (int t = w; t < 2 * ts; t += NWAVE) {
+                    const int tj = t / ts, tsb = t % ts;
+                    const f32x4 acc = mm_tile(lds + L::g1 + 16 * tj, 1, HCP, lds + L::x + 16 * tsb, SP, 1, BB);
+                    const int s = 16 * tsb + c;
+                    if (s < S) {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) lds[L::gW0 + (16 * tj + 4 * q + e) * SP + s] = acc[e];
+                    }
+                }
+                if (tid >= TPB - HC) {
+                    const int j = tid - (TPB - HC);
+                    float s = 0.f;
+                    for (int b = 0; b < BB; ++b) s += lds[L::g1 + b * HCP + j];
+                    lds[L::gb0 + j] = s;
+                }
+            }
+            __syncthreads();
+            // ---- Adam of the small parameters: log σ with the entropy step sizes (ppo.cu:440-442), the
+            // network's with its own; the last step writes the gradients out ----
+            {
+                const float st = a.steps[2 * step], bc2 = a.steps[2 * step + 1];
+                const float st_ls = a.policy ? a.steps_ls[2 * step] : 0.f;
+                const float bc2_ls = a.policy ? a.steps_ls[2 * step + 1] : 1.f;
+#pragma unroll
+                for (int u = 0; u < SMALL_SLOTS; ++u) {
+                    const int e = tid + u * TPB;
+                    if (e < nsmall) {
+                        const Small s = small_elem<H>(a, e, c0);
+                        float pv = lds[s.lds_p];
+                        const float g = lds[s.lds_g];
+                        if (s.kind == 1) adam_elem(pv, g, sm[u], sv[u], st_ls, a.b1, a.b2, bc2_ls);
+                        else adam_elem(pv, g, sm[u], sv[u], st, a.b1, a.b2, bc2);
+                        lds[s.lds_p] = pv;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    if (!ok) return;
+    // ---- phase end.  Addresses are recomputed from opaque copies: the compiler would otherwise keep
+    // every 64-bit address of the phase-start loads live across the whole step loop (spills) ----
+    int tid_e = tid, c0_e = c0;
+    asm volatile("" : "+v"(tid_e), "+s"(c0_e));
+    // the last step's gradients (callers may read them, as after the multi-launch loop): the small
+    // ones are still in LDS; gW1 is recomputed from the last step's g2 and h1, which are too
+    if (step > 0) {
+        for (int e = tid_e; e < nsmall; e += TPB) {
+            const Small s = small_elem<H>(a, e, c0_e);
+            if (s.kind != 0 && cw != 0) continue;
+            if (s.kind == 1) a.log_std_grad[s.gflat] = lds[s.lds_g];
+            else a.grads[s.gflat] = lds[s.lds_g];
+        }
+        for (int t = (tid_e >> 6); t < (HC / 16) * (H / 16); t += NWAVE) {
+            const int tj = t / (H / 16), tk = t % (H / 16);
+            const int ln = tid_e & 63, cc = ln & 15, qq = ln >> 4;
+            const f32x4 acc = mm_tile(lds + L::g2 + 16 * tj, 1, HCP, lds + L::h1 + 16 * tk, HP, 1, BB);
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+                a.grads[a.woff[1] + (long)(c0_e + 16 * tj + 4 * qq + e) * H + 16 * tk + cc] = acc[e];
+        }
+    }
+    for (int e = tid_e; e < HC * H; e += TPB) {
+        const int j = e / H, k = e % H;
+        a.params[a.woff[1] + (long)(c0_e + j) * H + k] = lds[L::W1 + j * HP + k];
+    }
+    {
+        const int we = tid_e >> 6, ln = tid_e & 63, cc = ln & 15, qq = ln >> 4;
+#pragma unroll
+        for (int u = 0; u < T1; ++u) {
+            const int t = we + NWAVE * u, tj = t / (H / 16), tk = t % (H / 16);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const long g = a.woff[1] + (long)(c0_e + 16 * tj + 4 * qq + e) * H + 16 * tk + cc;
+                a.m[g] = m1[u][e];
+                a.v[g] = v1[u][e];
+            }
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < SMALL_SLOTS; ++u) {
+        const int e = tid_e + u * TPB;
+        if (e < nsmall) {
+            const Small s = small_elem<H>(a, e, c0_e);
+            if (s.kind != 0 && cw != 0) continue;
+            if (s.kind == 1) { a.log_std[s.gflat] = lds[s.lds_p]; a.m_ls[s.gflat] = sm[u]; a.v_ls[s.gflat] = sv[u]; }
+            else { a.params[s.gflat] = lds[s.lds_p]; a.m[s.gflat] = sm[u]; a.v[s.gflat] = sv[u]; }
+        }
+    }
+}
+
+// per-stream workspace (the value and policy phases run concurrently on two streams)
+struct Ws { float *X1, *Y, *G1; unsigned* ctr; long cap; };
+Ws g_ws[2] = {};
+unsigned* g_err = nullptr;            // host-mapped error word
+
+}  // namespace
+
+extern "C" {
+
+// host-visible error of the last cluster phases (nonzero: a barrier timed out — a workgroup of the
+// launch was never resident or a device fault stopped one); cleared by reading
+int phip_cluster_error(void) {
+    if (!g_err) return 0;
+    const unsigned e = __atomic_load_n(g_err, __ATOMIC_ACQUIRE);
+    return e != 0u;
+}
+
+// Returns 0 when launched (or, with n_epochs = 0, when the shape fits); −1 when the network or the
+// minibatch does not fit this path (the caller falls back).
+int phip_cluster_update(const PhipTinyNet* net, const PhipTinyPhase* ph) {
+    if (getenv("PPO_NO_CLUSTER")) return -1;
+    if (net->L != 3 || ph->B != BB || ph->n_epochs > 16) return -1;
+    const int S = net->sizes[0], H = net->sizes[1], O = net->sizes[3];
+    if (H != 256 || net->sizes[2] != H || S < 1 || S > 20 || O < 1 || O > OMAX) return -1;
+    if (!net->relu[0] || !net->relu[1] || net->relu[2]) return -1;
+    if (ph->policy && (!net->log_std || !net->m_ls)) return -1;
+    using Ly = Lay<256>;
+    constexpr size_t bytes = sizeof(float) * (size_t)Ly::TOTAL;
+    static_assert(bytes <= 160 * 1024, "cluster: LDS");
+    if (ph->n_epochs <= 0 || ph->num_batches <= 0) return 0;     // fit check only
+    ClArgs a{};
+    a.S = S; a.O = O; a.policy = ph->policy;
+    a.SP = ((S + 3) / 4) * 4;
+    if (((a.SP / 4) & 1) == 0) a.SP += 4;                         // 4·odd (conflict-free strided reads)
+    a.params = net->params; a.grads = net->grads; a.m = net->m; a.v = net->v;
+    for (int l = 0; l < 3; ++l) { a.woff[l] = net->woff[l]; a.boff[l] = net->boff[l]; }
+    a.log_std = net->log_std; a.log_std_grad = net->log_std_grad; a.m_ls = net->m_ls; a.v_ls = net->v_ls;
+    a.state = ph->state; a.action = ph->action; a.logprob = ph->logprob; a.adv = ph->adv; a.adv_target = ph->adv_target;
+    a.limit = ph->limit; a.num_batches = ph->num_batches; a.n_epochs = ph->n_epochs;
+    a.total_steps = ph->n_epochs * ph->num_batches;
+    if (ph->max_steps > 0 && ph->max_steps < a.total_steps) a.total_steps = (int)ph->max_steps;
+    a.perms = ph->perms;
+    for (int e = 0; e < ph->n_epochs && !ph->perms; ++e) {
+        Feistel& f = a.fk[e];
+        int bits = 2;
+        while ((1ULL << bits) < (unsigned long long)ph->limit) bits++;
+        f.half = (uint32_t)((bits + 1) / 2);
+        f.mask = (1u << f.half) - 1u;
+        f.n = (uint32_t)ph->limit;
+        for (int r = 0; r < 4; ++r) f.k[r] = ph->feistel_k[4 * e + r];
+    }
+    a.steps = ph->steps; a.steps_ls = ph->steps_ls;
+    a.b1 = ph->b1; a.b2 = ph->b2; a.eps = ph->eps; a.ent_coeff = ph->ent_coeff;
+    a.stats = ph->stats;
+    constexpr int NWG = 256 / HC;
+    Ws& ws = g_ws[phip_side_active() ? 1 : 0];
+    const long need = (long)BB * 256 + (long)NWG * BB * OMAX + (long)NWG * BB * 256;
+    if (ws.cap < need) {
+        phip_free(ws.X1);
+        phip_free(ws.ctr);
+        ws.X1 = (float*)phip_malloc(sizeof(float) * (size_t)need);
+        ws.ctr = (unsigned*)phip_malloc(64);
+        ws.cap = need;
+    }
+    ws.Y = ws.X1 + (long)BB * 256;
+    ws.G1 = ws.Y + (long)NWG * BB * OMAX;
+    if (!g_err) {
+        PPO_CHECK(hipHostMalloc((void**)&g_err, 64, hipHostMallocMapped | hipHostMallocCoherent));
+        *g_err = 0u;
+    }
+    if (*g_err) {
+        phip_record_error("cluster phase: a barrier timed out in an earlier launch");
+        return -2;
+    }
+    unsigned* d_err = nullptr;
+    PPO_CHECK(hipHostGetDevicePointer((void**)&d_err, g_err, 0));
+    a.X1 = ws.X1; a.Y = ws.Y; a.G1 = ws.G1; a.ctr = ws.ctr; a.err = d_err;
+    // one workgroup in every 8: blocks b and b + 8 are dealt to one XCD (observed, MI355X_MICROARCH.md
+    // § Workgroup dispatch) — same-XCD hand-offs are faster; correctness never depends on it
+    a.active_stride = 8;
+    auto kfn = cluster_phase_kernel<256>;
+    static bool attr = false;
+    if (!attr) {
+        PPO_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+        attr = true;
+    }
+    PPO_CHECK(hipMemsetAsync(ws.ctr, 0, 64, ppo::stream()));
+    ppo::ProfScope ps(PPO_K_OTHER, 0.0);
+    hipLaunchKernelGGL(kfn, dim3(NWG * a.active_stride), dim3(TPB), bytes, ppo::stream(), a);
+    PPO_LAUNCH_CHECK();
+    return 0;
+}
+
+}  // extern "C"

@@ -117,6 +117,10 @@ typedef struct {
 /* runs every minibatch step of the phase in one workgroup; returns −1 (nothing launched) when the
  * network or minibatch does not fit */
 int phip_tiny_update(const PhipTinyNet* net, const PhipTinyPhase* ph);
+/* the same phase for S → 256 → 256 → O networks (S ≤ 20, O ≤ 16) at B = 64 on 8 cooperating
+ * workgroups (cluster.hip; net->wt unused); −1 when it does not fit, −2 after an earlier timeout */
+int phip_cluster_update(const PhipTinyNet* net, const PhipTinyPhase* ph);
+int phip_cluster_error(void);          /* nonzero: a cluster barrier timed out */
 
 /* ---------------- element-wise / heads (kernels.hip) ---------------- */
 void phip_relu(float* x, long count);

@@ -313,12 +313,18 @@ static const int* next_perm(PPO* ppo, PPODev* d, int shuffle_mode, uint64_t* key
 /* small networks: every minibatch step of a phase in one workgroup    */
 /* (csrc/tiny.hip); same arithmetic, rand() order and Adam step counts  */
 /* ------------------------------------------------------------------ */
-static int tiny_net(NeuralNetwork* nn, Adam* adam, PhipTinyNet* t) {
+/* max_w: widest layer the kernel takes (128 for the single-workgroup kernel; the multi-workgroup
+ * cluster kernel checks its own shapes) */
+static int tiny_net(NeuralNetwork* nn, Adam* adam, PhipTinyNet* t, int max_w) {
     const int L = nn->num_layers - 1;
-    if (nn->dtype != 0 || L < 1 || L > 8 || !adam->flat || adam->weights[0] != nn->d_params) return -1;
+    if (nn->dtype != 0 || L < 1 || L > 8 || !adam->flat || adam->weights[0] != nn->d_params ||
+        adam->grad_weights[0] != nn->d_grads)
+        return -1;
+    for (int i = 0; i < L; i++)
+        if (nn->layers[i].input_size > max_w || nn->layers[i].output_size > max_w) return -1;
     long nw = 0;
     for (int i = 0; i < L; i++) nw += (long)nn->layers[i].input_size * nn->layers[i].output_size;
-    if (nw > nn->tiny_wt_cap) {
+    if (max_w <= 128 && nw > nn->tiny_wt_cap) {
         phip_free(nn->d_tiny_wt);
         nn->d_tiny_wt = (float*)phip_malloc(sizeof(float) * (size_t)nw);
         nn->tiny_wt_cap = nw;
@@ -330,7 +336,6 @@ static int tiny_net(NeuralNetwork* nn, Adam* adam, PhipTinyNet* t) {
         t->relu[i] = nn_is_relu(nn, i);
         t->woff[i] = nn->param_offset[i];
         t->boff[i] = nn->bias_offset[i];
-        if (nn->layers[i].input_size > 128 || nn->layers[i].output_size > 128) return -1;
     }
     if (t->sizes[L] > 32) return -1;
     t->params = nn->d_params;
@@ -416,8 +421,16 @@ static int ppo_update_tiny(PPO* ppo, PPODev* d, int B, int n_epochs_policy, int 
     const int num_batches = buf->capacity / B;
     if (getenv("PPO_NO_TINY") || phip_comm_world() > 1 || n_epochs_value > 16 || n_epochs_policy > 16) return -1;
     PhipTinyNet nv, np;
-    if (tiny_net(ppo->V, ppo->adam_V, &nv) || tiny_net(ppo->policy->mu, ppo->adam_policy, &np)) return -1;
-    if (!ppo->adam_entropy->flat) return -1;
+    /* one workgroup per phase for networks ≤ 128 wide; otherwise the cluster kernel (S → 256 → 256 → O
+     * at B = 64, cluster.hip) when it takes the shape */
+    int cluster = 0;
+    if (tiny_net(ppo->V, ppo->adam_V, &nv, 128) || tiny_net(ppo->policy->mu, ppo->adam_policy, &np, 128)) {
+        if (tiny_net(ppo->V, ppo->adam_V, &nv, 1 << 20) || tiny_net(ppo->policy->mu, ppo->adam_policy, &np, 1 << 20))
+            return -1;
+        cluster = 1;
+    }
+    int (*phase_fn)(const PhipTinyNet*, const PhipTinyPhase*) = cluster ? phip_cluster_update : phip_tiny_update;
+    if (!ppo->adam_entropy->flat || ppo->adam_entropy->grad_weights[0] != ppo->policy->d_log_std_grad) return -1;
     GaussianPolicy* pol = ppo->policy;
     np.log_std = pol->d_log_std;
     np.log_std_grad = pol->d_log_std_grad;
@@ -435,10 +448,10 @@ static int ppo_update_tiny(PPO* ppo, PPODev* d, int B, int n_epochs_policy, int 
         PhipTinyNet probe = nv;
         PhipTinyPhase pp = ph;
         pp.n_epochs = 0;
-        if (phip_tiny_update(&probe, &pp) != 0) return -1;
+        if (phase_fn(&probe, &pp) != 0) return -1;
         probe = np;
         pp.policy = 1;
-        if (phip_tiny_update(&probe, &pp) != 0) return -1;
+        if (phase_fn(&probe, &pp) != 0) return -1;
     }
     /* both phases' permutations and Adam step tables first, in the reference's order (value
      * epochs' shuffles, then the policy's); then the two single-workgroup phases run concurrently
@@ -475,12 +488,12 @@ static int ppo_update_tiny(PPO* ppo, PPODev* d, int B, int n_epochs_policy, int 
     const int concurrent = run_v && run_p && !(serial_env && *serial_env && *serial_env != '0');
     if (concurrent) phip_side_fork();
     if (run_v) {
-        if (phip_tiny_update(&nv, &pv) != 0) die("ppo_update: tiny value phase failed to launch");
+        if (phase_fn(&nv, &pv) != 0) die("ppo_update: single-launch value phase failed to launch");
         d->n_v += cap_v;
     }
     if (run_p) {
         if (concurrent) phip_side_use(1);
-        if (phip_tiny_update(&np, &pp) != 0) die("ppo_update: tiny policy phase failed to launch");
+        if (phase_fn(&np, &pp) != 0) die("ppo_update: single-launch policy phase failed to launch");
         if (concurrent) phip_side_use(0);
         d->n_p += cap_p;
     }
@@ -721,6 +734,7 @@ void ppo_update(void* vppo, float gamma, int batch_size, int n_epochs_policy, in
 static void ppo_update_body(PPO* ppo, float gamma, int batch_size, int n_epochs_policy, int n_epochs_value,
                             int shuffle_mode, unsigned long long seed) {
     TrajectoryBuffer* buf = ppo->buffer;
+    if (phip_cluster_error()) die("ppo_update: a multi-workgroup phase (cluster.hip) timed out at a barrier");
     if (!buf->on_device) die("ppo_update: buffer must be device-resident (buffer_to_device / ppo_fill_synthetic)");
     if (batch_size <= 0) die("ppo_update: batch_size must be positive");
     PPODev* d = dev_ws(ppo, batch_size);

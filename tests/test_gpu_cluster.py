@@ -1,0 +1,132 @@
+"""The multi-workgroup single-launch phase (csrc/cluster.hip) for S → 256 → 256 → O networks at the
+reference's B = 64 (config C3's networks, main.c:34's minibatch) against the multi-launch loop and the
+oracle (reference ppo.cu:395-443).
+
+ppo_update takes it by itself for these shapes at B = 64 on one GPU; PPO_NO_CLUSTER=1 forces the
+multi-launch loop.  From identical state both must give the same minibatch gradients (stated fp32 GEMM
+tolerance), the same Adam step counts and host rand() consumption, and over many steps the same
+parameter motion; against the oracle, single steps element by element and the first 16 + 16 steps of
+an update (the bounds of test_short_update_elementwise).
+"""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+import ppo_ffi
+from helpers import F32, assert_gemm_close, assert_rel_close, nn_grads_packed, nn_params_packed
+
+pytestmark = pytest.mark.gpu
+
+LIBC = C.CDLL("libc.so.6")
+C3 = [17, 256, 256, 6]
+RELU = lambda sizes: [1] * (len(sizes) - 2) + [0]  # noqa: E731
+LR = 3e-4
+
+
+def run(lib, sizes, N, B, n_pol, n_val, shuffle, cluster, seed=21, limit=None, ent=0.01):
+    if cluster:
+        os.environ.pop("PPO_NO_CLUSTER", None)
+    else:
+        os.environ["PPO_NO_CLUSTER"] = "1"
+    try:
+        LIBC.srand(seed)
+        acts = ["relu"] * (len(sizes) - 2) + ["none"]
+        ppo = lib.create_ppo(ppo_ffi.c_strings(acts), ppo_ffi.c_ints(sizes), len(sizes), N, 3e-4, 3e-4, 0.95, 0.2,
+                             ent, 1.0, True)
+        E = max(1, N // 256)
+        lib.ppo_fill_synthetic(ppo, E, N // E, 17, 1.0 / 200)
+        pol = ppo.contents.policy.contents
+        v0 = nn_params_packed(lib, ppo.contents.V)
+        mu0 = nn_params_packed(lib, pol.mu)
+        ls0 = ppo_ffi.d2h(lib, pol.d_log_std, F32, pol.action_size)
+        b = ppo.contents.buffer.contents
+        buf = dict(state=ppo_ffi.d2h(lib, b.d_state_p, F32, N * sizes[0]).reshape(N, sizes[0]),
+                   next_state=ppo_ffi.d2h(lib, b.d_next_state_p, F32, N * sizes[0]).reshape(N, sizes[0]),
+                   action=ppo_ffi.d2h(lib, b.d_action_p, F32, N * sizes[-1]).reshape(N, sizes[-1]),
+                   reward=ppo_ffi.d2h(lib, b.d_reward_p, F32, N), logprob=ppo_ffi.d2h(lib, b.d_logprob_p, F32, N),
+                   terminated=ppo_ffi.d2h(lib, b.d_terminated_p, np.uint8, N),
+                   truncated=ppo_ffi.d2h(lib, b.d_truncated_p, np.uint8, N))
+        if limit:
+            lib.ppo_set_step_limit(ppo, limit[0], limit[1])
+        lib.ppo_reset_stats(ppo)
+        LIBC.srand(seed + 1)
+        lib.ppo_update(ppo, 0.99, B, n_pol, n_val, shuffle, 9)
+        lib.ppo_synchronize()
+        assert lib.ppo_last_error() in (b"", None), lib.ppo_last_error()
+        stats = (C.c_double * 7)()
+        lib.ppo_read_stats(ppo, stats, 7)
+        out = dict(stats=np.array(stats[:4]), next_rand=LIBC.rand(), v0=v0, mu0=mu0, ls0=ls0, buf=buf,
+                   v=nn_params_packed(lib, ppo.contents.V), gv=nn_grads_packed(lib, ppo.contents.V),
+                   mu=nn_params_packed(lib, pol.mu), gmu=nn_grads_packed(lib, pol.mu),
+                   ls=ppo_ffi.d2h(lib, pol.d_log_std, F32, pol.action_size),
+                   gls=ppo_ffi.d2h(lib, pol.d_log_std_grad, F32, pol.action_size),
+                   multi=ppo.contents.V.contents.bits_m == B or pol.mu.contents.bits_m == B,
+                   t=(ppo.contents.adam_V.contents.time_step, ppo.contents.adam_policy.contents.time_step,
+                      ppo.contents.adam_entropy.contents.time_step))
+        lib.ppo_set_step_limit(ppo, -1, -1)
+        lib.free_ppo(ppo)
+        return out
+    finally:
+        os.environ.pop("PPO_NO_CLUSTER", None)
+
+
+@pytest.mark.parametrize("shuffle", [0, 1])
+def test_cluster_single_steps_match_multilaunch(lib, oracle, shuffle):
+    """one value step, then one policy step (C3 networks, B = 64): the same gradients and Adam deltas"""
+    N, B = 4096, 64
+    for n_pol, n_val in ((0, 1), (1, 0)):
+        a = run(lib, C3, N, B, n_pol, n_val, shuffle, cluster=True)
+        b = run(lib, C3, N, B, n_pol, n_val, shuffle, cluster=False)
+        assert not a["multi"] and b["multi"], "the cluster path did not run (or the fallback did not)"
+        assert a["t"] == b["t"] == (n_val, n_pol, n_pol)
+        assert a["next_rand"] == b["next_rand"], "host rand() stream consumed differently"
+        np.testing.assert_allclose(a["stats"], b["stats"], rtol=2e-4, atol=1e-6)
+        assert_gemm_close(a["gv"], b["gv"], B, "value grads")
+        assert_gemm_close(a["gmu"], b["gmu"], B, "policy grads")
+        if n_pol:
+            assert_rel_close(a["gls"], b["gls"], 1e-4, 1e-6, "log σ grad")
+        for k in ("v", "mu", "ls"):
+            err = np.abs(a[k] - b[k])
+            assert err.max() <= 2 * LR * 1.0001 + 1e-7, (k, err.max())
+            assert (err > 1e-6).mean() < 0.01, (k, (err > 1e-6).mean())
+
+
+def test_cluster_first_steps_vs_oracle(lib, oracle):
+    """the first 16 value and 16 policy steps of a C3-network update at B = 64 on the cluster path
+    against the oracle's update of the same buffer, element by element (≥ 99 % within 0.1·lr)"""
+    oracle.load(use_openblas=True)
+    N, B, n = 16384, 64, 16
+    a = run(lib, C3, N, B, 1, 1, 1, cluster=True, limit=(n, n), ent=0.0)
+    assert not a["multi"]
+    ref = oracle.ppo_update(C3, RELU(C3), a["mu0"], a["ls0"], a["v0"], a["buf"], batch_size=B, n_epochs_policy=1,
+                            n_epochs_value=1, shuffle_mode=1, seed=9, max_value_steps=n, max_policy_steps=n)
+    assert a["t"] == (ref["t_v"], ref["t_mu"], ref["t_ent"]) == (n, n, n)
+    for got, want, what in ((a["v"], ref["v"], "V"), (a["mu"], ref["mu"], "mu"), (a["ls"], ref["log_std"], "log_std")):
+        err = np.abs(got.astype(np.float64) - want)
+        q = float((err <= 0.1 * LR).mean())
+        print(f"cluster C3 {what}: max err {err.max() / LR:.4f} lr, {100 * q:.3f} % within 0.1 lr")
+        assert err.max() <= 2 * LR * n, f"{what}: max err {err.max()}"
+        assert q >= 0.99, f"{what}: only {q * 100:.2f} % within 0.1·lr"
+    np.testing.assert_allclose(a["stats"][0], ref["sum_v_loss"], rtol=1e-3)
+    np.testing.assert_allclose(a["stats"][2], ref["sum_policy_loss"], rtol=1e-3, atol=1e-5)
+
+
+@pytest.mark.parametrize("shuffle", [0, 1])
+def test_cluster_full_update_matches_multilaunch(lib, oracle, shuffle):
+    """a whole update (10 value + 4 policy epochs of 64-row minibatches over 16,384 transitions:
+    2560 + 1024 steps) on both paths: step counts, rand() use, losses and parameter motion"""
+    N, B = 16384, 64
+    a = run(lib, C3, N, B, 4, 10, shuffle, cluster=True)
+    b = run(lib, C3, N, B, 4, 10, shuffle, cluster=False)
+    assert not a["multi"] and b["multi"]
+    assert a["t"] == b["t"] == (2560, 1024, 1024)
+    assert a["next_rand"] == b["next_rand"]
+    assert abs(a["stats"][0] - b["stats"][0]) <= 0.02 * abs(b["stats"][0])
+    assert abs(a["stats"][2] - b["stats"][2]) <= 0.05 * abs(b["stats"][2]) + 1e-3
+    for k, k0 in (("v", "v0"), ("mu", "mu0")):
+        da, db = a[k] - a[k0], b[k] - b[k0]
+        cos = float(da @ db / (np.linalg.norm(da) * np.linalg.norm(db)))
+        assert cos > 0.95, (k, cos)
+        assert abs(np.linalg.norm(da) / np.linalg.norm(db) - 1) < 0.1, k
