@@ -76,9 +76,9 @@ def run(lib, sizes, N, B, n_pol, n_val, shuffle, cluster, seed=21, limit=None, e
 def test_cluster_single_steps_match_multilaunch(lib, oracle, shuffle):
     """one value step, then one policy step (C3 networks, B = 64): the same gradients and Adam deltas"""
     N, B = 4096, 64
-    for n_pol, n_val in ((0, 1), (1, 0)):
-        a = run(lib, C3, N, B, n_pol, n_val, shuffle, cluster=True)
-        b = run(lib, C3, N, B, n_pol, n_val, shuffle, cluster=False)
+    for n_pol, n_val in ((0, 1), (1, 0)):                  # one epoch each, capped at one step
+        a = run(lib, C3, N, B, n_pol, n_val, shuffle, cluster=True, limit=(n_val, n_pol))
+        b = run(lib, C3, N, B, n_pol, n_val, shuffle, cluster=False, limit=(n_val, n_pol))
         assert not a["multi"] and b["multi"], "the cluster path did not run (or the fallback did not)"
         assert a["t"] == b["t"] == (n_val, n_pol, n_pol)
         assert a["next_rand"] == b["next_rand"], "host rand() stream consumed differently"
