@@ -78,6 +78,8 @@ struct ClArgs {
     unsigned* ctr;                            // barrier arrivals (zeroed before the launch)
     unsigned* err;                            // host-visible error word (0 = fine)
     int active_stride;                        // workgroup b works iff b % active_stride == 0 (same-XCD bias)
+    unsigned long long* stamps;               // diagnostics (PPO_CLUSTER_STAMPS): wall clock per phase,
+                                              // workgroup 0, steps 0..63, 12 slots
 };
 
 // ---- hand-off primitives (sc1: write-through stores, L1-bypassing loads) ----
@@ -237,6 +239,11 @@ __device__ __forceinline__ Small small_elem(const ClArgs& a, int e, int c0) {
 
 constexpr int SMALL_SLOTS = 4;        // ≤ 4·512 small parameters per workgroup
 
+#define CL_STAMP(slot)                                                                          \
+    do {                                                                                        \
+        if (a.stamps && cw == 0 && tid == 0 && step < 64) a.stamps[step * 12 + (slot)] = wall_clock64(); \
+    } while (0)
+
 template <int H>
 __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
     constexpr int NWG = H / HC;
@@ -296,6 +303,7 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
     bool ok = true;
     for (int ep = 0; ep < a.n_epochs && ok; ++ep) {
         for (int kb = 0; kb < a.num_batches && step < a.total_steps && ok; ++kb, ++step) {
+            CL_STAMP(0);
             // ---- gather (trajectory_buffer.cu:168-200) ----
             if (tid < BB) {
                 const int list = (int)(((long)kb * BB + tid) % a.limit);
@@ -321,6 +329,7 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
                 }
             __syncthreads();
 
+            CL_STAMP(1);
             // ---- layer 0, own units: h1ᵀ[j][b] = Σ_s W0[j][s]·x[b][s] + b0[j]  (2 × 4 tiles, one per wave)
             {
                 const int tj = w / 4, tb = w % 4;
@@ -335,8 +344,10 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
                 *reinterpret_cast<f32x4*>(lds + L::h1 + b * HP + c0 + j) = hv;
                 st16_sc1(rX1, b * H + c0 + j, hv);                       // publish
             }
+            CL_STAMP(2);
             ok = cluster_barrier(a, nbar++, NWG, flag);                  // A: every h1 column published
             if (!ok) break;
+            CL_STAMP(3);
             // every other workgroup's h1 columns (sc1 loads)
             for (int e = tid; e < BB * (H / 4); e += TPB) {
                 const int b = e / (H / 4), k = 4 * (e % (H / 4));
@@ -345,6 +356,7 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
             }
             __syncthreads();
 
+            CL_STAMP(4);
             // ---- layer 1, own units: h2[b][j] = relu(Σ_k h1[b][k]·W1[j][k] + b1[j])  (4 × 2 tiles)
             {
                 const int tb = w / 2, tj = w % 2;
@@ -363,8 +375,10 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
                 const f32x4 acc = mm_tile(lds + L::W2, HCP, 1, lds + L::h2 + 16 * w * HCP, 1, HCP, HC);
                 st16_sc1(rY, (cw * BB + 16 * w + c) * OMAX + 4 * q, acc);     // publish Y[cw][b][4q..4q+3]
             }
+            CL_STAMP(5);
             ok = cluster_barrier(a, nbar++, NWG, flag);                  // B: every y partial published
             if (!ok) break;
+            CL_STAMP(6);
             // ---- y = Σ_c partials (fixed order) + b2; the head, identically in every workgroup ----
             if (tid < BB * (OMAX / 4)) {
                 const int b = tid / (OMAX / 4), oq = 4 * (tid % (OMAX / 4));
@@ -437,6 +451,7 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
                 }
             }
             __syncthreads();
+            CL_STAMP(7);
             // ---- g1 partial: P[b][k] = Σ_j g2[b][j]·W1[j][k], computed as Pᵀ tiles (4 consecutive k per
             // lane → 16-B publishes): Pᵀ[k][b] = Σ_j W1[j][k]·g2[b][j]  (16 × 4 tiles, 8 per wave)
             for (int t = w; t < (H / 16) * (BB / 16); t += NWAVE) {
@@ -468,8 +483,10 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
                     }
                 }
             }
+            CL_STAMP(8);
             ok = cluster_barrier(a, nbar++, NWG, flag);                  // C: every g1 partial published
             if (!ok) break;
+            CL_STAMP(9);
             // ---- g1[b][j] = Σ_c partials (fixed order) ⊙ 1[h1 > 0], own units ----
             {
                 const int b = tid / (HC / 4), jq = 4 * (tid % (HC / 4));      // 64 × 8 float4 = 512 threads
@@ -500,6 +517,7 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
                 }
             }
             __syncthreads();
+            CL_STAMP(10);
             // ---- Adam of the small parameters: log σ with the entropy step sizes (ppo.cu:440-442), the
             // network's with its own; the last step writes the gradients out ----
             {
@@ -520,6 +538,7 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
                 }
             }
             __syncthreads();
+            CL_STAMP(11);
         }
     }
     if (!ok) return;
@@ -654,6 +673,12 @@ int phip_cluster_update(const PhipTinyNet* net, const PhipTinyPhase* ph) {
     // one workgroup in every 8: blocks b and b + 8 are dealt to one XCD (observed, MI355X_MICROARCH.md
     // § Workgroup dispatch) — same-XCD hand-offs are faster; correctness never depends on it
     a.active_stride = 8;
+    static unsigned long long* stamps = nullptr;
+    const bool want_stamps = getenv("PPO_CLUSTER_STAMPS") != nullptr;
+    if (want_stamps) {
+        if (!stamps) stamps = (unsigned long long*)phip_malloc(sizeof(unsigned long long) * 64 * 12);
+        a.stamps = stamps;
+    }
     auto kfn = cluster_phase_kernel<256>;
     static bool attr = false;
     if (!attr) {
@@ -664,6 +689,25 @@ int phip_cluster_update(const PhipTinyNet* net, const PhipTinyPhase* ph) {
     ppo::ProfScope ps(PPO_K_OTHER, 0.0);
     hipLaunchKernelGGL(kfn, dim3(NWG * a.active_stride), dim3(TPB), bytes, ppo::stream(), a);
     PPO_LAUNCH_CHECK();
+    if (want_stamps && a.total_steps >= 64) {               // diagnostics: mean µs per sub-phase, steps 1..63
+        unsigned long long h[64 * 12];
+        phip_d2h(h, stamps, sizeof(h));
+        int dev = 0, khz = 0;
+        PPO_CHECK(hipGetDevice(&dev));
+        PPO_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+        const double mhz = khz > 0 ? khz / 1000.0 : 100.0;
+        static const char* names[12] = {"gather", "L0", "barrier A", "h1 load", "L1+Y", "barrier B", "head+bwd",
+                                        "G1+gW1 adam", "barrier C", "g1+gW0", "adam", "step->next"};
+        double acc[12] = {0};
+        for (int st = 1; st < 63; ++st)
+            for (int k = 0; k < 12; ++k) {
+                const unsigned long long t0 = h[st * 12 + k], t1 = k < 11 ? h[st * 12 + k + 1] : h[(st + 1) * 12];
+                acc[k] += (double)(t1 - t0) / mhz;
+            }
+        fprintf(stderr, "cluster %s step (us):", ph->policy ? "policy" : "value");
+        for (int k = 0; k < 12; ++k) fprintf(stderr, " %s %.2f", names[k], acc[k] / 62);
+        fprintf(stderr, "\n");
+    }
     return 0;
 }
 
