@@ -93,14 +93,19 @@ __device__ __forceinline__ f32x4 ld16_sc1(__amdgpu_buffer_rsrc_t r, int off_floa
     return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off_floats * 4, 0, 16));
 }
 
-// the workgroup's published stores are complete (every wave drained), then one arrival; wait until
-// all `nwg` workgroups have arrived for barrier number `n` (counting from 0 within the launch).
-// Returns false on timeout (error word set), uniformly for the workgroup.
-__device__ __forceinline__ bool cluster_barrier(const ClArgs& a, unsigned n, int nwg, int* flag_lds) {
+// Arrival: the workgroup's published stores are complete (every wave drained, then a workgroup
+// barrier), then ONE lane adds to the monotonic counter.  Work that publishes nothing may run between
+// cluster_arrive and cluster_wait (it overlaps the other workgroups' arrival skew).
+__device__ __forceinline__ void cluster_arrive(const ClArgs& a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(a.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Wait until all `nwg` workgroups have arrived for barrier number `n` (counting from 0 within the
+// launch): the arriving lane polls (sc1 loads + s_sleep), the other waves wait at the workgroup
+// barrier it then joins.  Returns false on timeout (error word set), uniformly for the workgroup.
+__device__ __forceinline__ bool cluster_wait(const ClArgs& a, unsigned n, int nwg, int* flag_lds) {
     if (threadIdx.x == 0) {
-        __hip_atomic_fetch_add(a.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned target = (unsigned)nwg * (n + 1);
         unsigned spins = 0;
         int ok = 1;
@@ -117,6 +122,25 @@ __device__ __forceinline__ bool cluster_barrier(const ClArgs& a, unsigned n, int
     }
     __syncthreads();
     return *flag_lds != 0;
+}
+
+// Σ_b M[b][col] over the 64 minibatch rows for columns [0, NC) by ONE wave, in a fixed order: lane
+// (col = lane / P, part = lane % P) adds rows part·R … part·R + R − 1 in order, then the P parts are
+// combined by xor shuffles (commutative pairs: every lane of a column, and every workgroup, gets the
+// same bits).  out[col] = sum + add for col < ncols.
+template <int NC>
+__device__ __forceinline__ void colsum64(const float* M, int pitch, int ncols, float add, float* out) {
+    constexpr int P = 64 / NC, R = 64 / P;
+    const int lane = threadIdx.x & 63, col = lane / P, part = lane % P;
+    float v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[r] = M[(part * R + r) * pitch + col];
+    float s = 0.f;
+#pragma unroll
+    for (int r = 0; r < R; ++r) s += v[r];
+#pragma unroll
+    for (int o = 1; o < P; o <<= 1) s += __shfl_xor(s, o, 64);
+    if (part == 0 && col < ncols) out[col] = s + add;
 }
 
 // One 16×16 output tile: acc(i, j) = Σ_k A(i, k)·B(k, j), A(i, k) = A[i·as_i + k·as_k],
@@ -345,14 +369,23 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
                 st16_sc1(rX1, b * H + c0 + j, hv);                       // publish
             }
             CL_STAMP(2);
-            ok = cluster_barrier(a, nbar++, NWG, flag);                  // A: every h1 column published
+            cluster_arrive(a);
+            ok = cluster_wait(a, nbar++, NWG, flag);                     // A: every h1 column published
             if (!ok) break;
             CL_STAMP(3);
-            // every other workgroup's h1 columns (sc1 loads)
-            for (int e = tid; e < BB * (H / 4); e += TPB) {
-                const int b = e / (H / 4), k = 4 * (e % (H / 4));
-                if (k >= c0 && k < c0 + HC) continue;
-                *reinterpret_cast<f32x4*>(lds + L::h1 + b * HP + k) = ld16_sc1(rX1, b * H + k);
+            // every other workgroup's h1 columns (sc1 loads): lane → column quad 4·lane, rows w + 8u,
+            // all eight loads in flight before the LDS writes
+            {
+                static_assert(H == 4 * 64 && BB == 8 * NWAVE, "h1 gather mapping");
+                const int k = 4 * lane;
+                if (k < c0 || k >= c0 + HC) {
+                    f32x4 hv[BB / NWAVE];
+#pragma unroll
+                    for (int u = 0; u < BB / NWAVE; ++u) hv[u] = ld16_sc1(rX1, (w + NWAVE * u) * H + k);
+#pragma unroll
+                    for (int u = 0; u < BB / NWAVE; ++u)
+                        *reinterpret_cast<f32x4*>(lds + L::h1 + (w + NWAVE * u) * HP + k) = hv[u];
+                }
             }
             __syncthreads();
 
@@ -376,7 +409,8 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
                 st16_sc1(rY, (cw * BB + 16 * w + c) * OMAX + 4 * q, acc);     // publish Y[cw][b][4q..4q+3]
             }
             CL_STAMP(5);
-            ok = cluster_barrier(a, nbar++, NWG, flag);                  // B: every y partial published
+            cluster_arrive(a);
+            ok = cluster_wait(a, nbar++, NWG, flag);                     // B: every y partial published
             if (!ok) break;
             CL_STAMP(6);
             // ---- y = Σ_c partials (fixed order) + b2; the head, identically in every workgroup ----
@@ -424,16 +458,9 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
                 }
             }
             // replicated gradients in a fixed order: gb2[o] = Σ_b g3[b][o]; log σ: Σ_b row terms − c_ent
-            if (tid < O) {
-                float s = 0.f;
-                for (int b = 0; b < BB; ++b) s += lds[L::yo + b * OPP + tid];
-                lds[L::gb2 + tid] = s;
-                if (a.policy) {
-                    float t = 0.f;
-                    for (int b = 0; b < BB; ++b) t += lds[L::glr + b * OMAX + tid];
-                    lds[L::gls + tid] = t + -a.ent_coeff;                // ppo.cu:436-438
-                }
-            }
+            // (ppo.cu:436-438); waves 7 and 6 (the tiles below keep waves 0-1 longest)
+            if (w == NWAVE - 1) colsum64<OMAX>(lds + L::yo, OPP, O, 0.f, lds + L::gb2);
+            if (w == NWAVE - 2 && a.policy) colsum64<OMAX>(lds + L::glr, OMAX, A, -a.ent_coeff, lds + L::gls);
             // ---- output layer backward, own columns: gW2[o][j] = Σ_b g3[b][o]·h2[b][j]  (2 tiles)
             if (w < 2) {
                 const f32x4 acc = mm_tile(lds + L::yo, 1, OPP, lds + L::h2 + 16 * w, HCP, 1, BB);
@@ -460,14 +487,10 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
                 st16_sc1(rG1, (cw * BB + 16 * tb + c) * H + 16 * tk + 4 * q, acc);
             }
             // bias gradient of layer 1 (fixed order)
-            if (tid < HC) {
-                float s = 0.f;
-                for (int b = 0; b < BB; ++b) s += lds[L::g2 + b * HCP + tid];
-                lds[L::gb1 + tid] = s;
-            }
-            __syncthreads();                                             // every wave done reading W1
+            if (w == NWAVE - 1) colsum64<HC>(lds + L::g2, HCP, HC, 0.f, lds + L::gb1);
+            cluster_arrive(a);                                           // (its barrier: every wave done reading W1)
             // ---- gW1[j][k] = Σ_b g2[b][j]·h1[b][k] with Adam fused (the lane holds these elements'
-            // moments); the last step also writes the gradient out (callers may read it)
+            // moments), overlapping the other workgroups' arrivals ----
             {
                 const float st = a.steps[2 * step], bc2 = a.steps[2 * step + 1];
 #pragma unroll
@@ -484,7 +507,7 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
                 }
             }
             CL_STAMP(8);
-            ok = cluster_barrier(a, nbar++, NWG, flag);                  // C: every g1 partial published
+            ok = cluster_wait(a, nbar++, NWG, flag);                     // C: every g1 partial published
             if (!ok) break;
             CL_STAMP(9);
             // ---- g1[b][j] = Σ_c partials (fixed order) ⊙ 1[h1 > 0], own units ----
@@ -509,12 +532,7 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
                         for (int e = 0; e < 4; ++e) lds[L::gW0 + (16 * tj + 4 * q + e) * SP + s] = acc[e];
                     }
                 }
-                if (tid >= TPB - HC) {
-                    const int j = tid - (TPB - HC);
-                    float s = 0.f;
-                    for (int b = 0; b < BB; ++b) s += lds[L::g1 + b * HCP + j];
-                    lds[L::gb0 + j] = s;
-                }
+                if (w == NWAVE - 1) colsum64<HC>(lds + L::g1, HCP, HC, 0.f, lds + L::gb0);
             }
             __syncthreads();
             CL_STAMP(10);
