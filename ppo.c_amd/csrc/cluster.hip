@@ -35,8 +35,6 @@ typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int TPB = 512, NWAVE = TPB / 64;
 constexpr int BB = 64;            // minibatch rows
-constexpr int HC = 32;            // hidden units per workgroup
-constexpr int HCP = 36;           // pitch of [64][HC] arrays (4·odd: conflict-free strided MFMA reads)
 constexpr int OMAX = 16;          // output width
 constexpr int OPP = 20;           // pitch of [64][OMAX] arrays
 
@@ -203,17 +201,22 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
     p -= step * m / denom;
 }
 
-// LDS layout (floats) for hidden width H
-template <int H>
+// LDS layout (floats) for hidden width H, HC hidden units per workgroup
+template <int H, int HC>
 struct Lay {
     static constexpr int HP = H + 4;                  // pitch of [64][H] and [HC][H] (4·odd)
+    static constexpr int HCP = HC + 4;                // pitch of [64][HC] arrays (4·odd: conflict-free strided reads)
+    static constexpr int NT1 = 4 * (HC / 16);         // layer-1 output tiles; split over K when < NWAVE
+    static constexpr int KS1 = NWAVE / NT1;
     static constexpr int SPMAX = 20;                  // S ≤ 20 (SP = 4·odd ≤ 20)
-    static constexpr int x = 0;                       // [64][SP]
-    static constexpr int rows = x + BB * SPMAX;       // int [64]
-    static constexpr int tgt = rows + BB;             // [64] value target / policy advantage
-    static constexpr int olp = tgt + BB;              // [64] old log-prob
-    static constexpr int act = olp + BB;              // [64][OMAX] actions
-    static constexpr int W0 = act + BB * OMAX;        // [HC][SP]
+    // the minibatch's rows, double-buffered (step s uses buffer s & 1; step s + 1's gather runs inside
+    // step s's barrier waits)
+    static constexpr int x = 0;                       // [2][64][SP]
+    static constexpr int rows = x + 2 * BB * SPMAX;   // int [64]
+    static constexpr int tgt = rows + BB;             // [2][64] value target / policy advantage
+    static constexpr int olp = tgt + 2 * BB;          // [2][64] old log-prob
+    static constexpr int act = olp + 2 * BB;          // [2][64][OMAX] actions
+    static constexpr int W0 = act + 2 * BB * OMAX;    // [HC][SP]
     static constexpr int b0 = W0 + HC * SPMAX;        // [HC]
     static constexpr int W1 = b0 + HC;                // [HC][HP]
     static constexpr int b1 = W1 + HC * HP;           // [HC]
@@ -234,7 +237,9 @@ struct Lay {
     static constexpr int glr = gls + OMAX;            // [64][OMAX] per-row log σ terms (ordered sum)
     static constexpr int red = glr + BB * OMAX;       // [NWAVE] loss partials
     static constexpr int flag = red + NWAVE;          // int: barrier result
-    static constexpr int TOTAL = flag + 4;
+    static constexpr int l1s = flag + 4;              // [4·256] upper halves: layer-1 K partials (KS1 = 2), Y and
+                                                      // G1 partial sums
+    static constexpr int TOTAL = l1s + 4 * 256;
 };
 
 // the small parameters of a workgroup (everything but its W1 rows), enumerated e = 0 … nsmall−1:
@@ -242,9 +247,10 @@ struct Lay {
 // replicated; its Adam uses the entropy step sizes)
 struct Small { int lds_p, lds_g; long gflat; int kind; };   // kind 0 network, 1 log σ, 2 replicated net
 
-template <int H>
+template <int H, int HC>
 __device__ __forceinline__ Small small_elem(const ClArgs& a, int e, int c0) {
-    using L = Lay<H>;
+    using L = Lay<H, HC>;
+    constexpr int HCP = L::HCP;
     const int S = a.S, O = a.O;
     if (e < HC * S) { const int j = e / S, s = e % S;
         return {L::W0 + j * a.SP + s, L::gW0 + j * a.SP + s, a.woff[0] + (long)(c0 + j) * S + s, 0}; }
@@ -261,23 +267,77 @@ __device__ __forceinline__ Small small_elem(const ClArgs& a, int e, int c0) {
     return {L::ls + e, L::gls + e, e, 1};
 }
 
-constexpr int SMALL_SLOTS = 4;        // ≤ 4·512 small parameters per workgroup
+// row i of step (ep, kb)'s minibatch (trajectory_buffer.cu:168-200): epoch ep's permutation of the
+// `limit` stored rows at list position kb·64 + i (mod limit)
+__device__ __forceinline__ int gather_src(const ClArgs& a, int ep, int kb, int i) {
+    const int list = (int)(((long)kb * BB + i) % a.limit);
+    return a.perms ? a.perms[(long)ep * a.limit + list] : (int)feistel_index((uint32_t)list, a.fk[ep & 15]);
+}
+// gather, part 1 (threads 0-63): the row indices → rows[], the per-row scalars → buffer `buf`
+template <class L>
+__device__ __forceinline__ void gather_rows(const ClArgs& a, float* lds, int ep, int kb, int buf) {
+    const int i = threadIdx.x;
+    if (i < BB) {
+        const int src = gather_src(a, ep, kb, i);
+        reinterpret_cast<int*>(lds + L::rows)[i] = src;
+        if (a.policy) {
+            const float ad = a.adv[src], lp = a.logprob[src];
+            lds[L::tgt + buf * BB + i] = ad;
+            lds[L::olp + buf * BB + i] = lp;
+        } else {
+            lds[L::tgt + buf * BB + i] = a.adv_target[src];
+        }
+    }
+}
+// gather, part 2 (every thread, behind a workgroup barrier after part 1): the rows' states (and
+// actions) → buffer `buf`, every load in flight before the LDS writes
+template <class L>
+__device__ __forceinline__ void gather_cols(const ClArgs& a, float* lds, int buf) {
+    constexpr int XU = (BB * L::SPMAX + TPB - 1) / TPB, AU = (BB * OMAX + TPB - 1) / TPB;
+    const int* rows = reinterpret_cast<const int*>(lds + L::rows);
+    const int tid = threadIdx.x, S = a.S, A = a.O;
+    float xv[XU], av[AU];
+#pragma unroll
+    for (int u = 0; u < XU; ++u) {
+        const int e = tid + u * TPB;
+        xv[u] = e < BB * S ? a.state[(long)rows[e / S] * S + e % S] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < AU; ++u) {
+        const int e = tid + u * TPB;
+        av[u] = a.policy && e < BB * A ? a.action[(long)rows[e / A] * A + e % A] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < XU; ++u) {
+        const int e = tid + u * TPB;
+        if (e < BB * S) lds[L::x + buf * BB * L::SPMAX + (e / S) * a.SP + e % S] = xv[u];
+    }
+#pragma unroll
+    for (int u = 0; u < AU; ++u) {
+        const int e = tid + u * TPB;
+        if (a.policy && e < BB * A) lds[L::act + buf * BB * OMAX + (e / A) * OMAX + e % A] = av[u];
+    }
+}
+
+// small parameters per workgroup ≤ HC·(S + 2 + O) + 2·O with S ≤ 20, O ≤ 16: slots per thread
+template <int HC>
+constexpr int small_slots() { return (HC * (20 + 2 + 16) + 32 + TPB - 1) / TPB; }
 
 #define CL_STAMP(slot)                                                                          \
     do {                                                                                        \
         if (a.stamps && cw == 0 && tid == 0 && step < 64) a.stamps[step * 12 + (slot)] = wall_clock64(); \
     } while (0)
 
-template <int H>
+template <int H, int HC>
 __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
     constexpr int NWG = H / HC;
-    using L = Lay<H>;
-    constexpr int HP = L::HP;
+    using L = Lay<H, HC>;
+    constexpr int HP = L::HP, HCP = L::HCP;
+    constexpr int SMALL_SLOTS = small_slots<HC>();
     if ((int)blockIdx.x % a.active_stride) return;
     const int cw = (int)blockIdx.x / a.active_stride;            // this workgroup's unit block
     const int c0 = cw * HC;
     extern __shared__ float lds[];
-    int* rows = reinterpret_cast<int*>(lds + L::rows);
     int* flag = reinterpret_cast<int*>(lds + L::flag);
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int c = lane & 15, q = lane >> 4;
@@ -301,7 +361,7 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
         const int e = tid + u * TPB;
         sm[u] = sv[u] = 0.f;
         if (e < nsmall) {
-            const Small s = small_elem<H>(a, e, c0);
+            const Small s = small_elem<H, HC>(a, e, c0);
             if (s.kind == 1) { lds[s.lds_p] = a.log_std[s.gflat]; sm[u] = a.m_ls[s.gflat]; sv[u] = a.v_ls[s.gflat]; }
             else { lds[s.lds_p] = a.params[s.gflat]; sm[u] = a.m[s.gflat]; sv[u] = a.v[s.gflat]; }
         }
@@ -320,6 +380,10 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
             v1[u][e] = a.v[g];
         }
     }
+    // the first step's minibatch
+    gather_rows<L>(a, lds, 0, 0, 0);
+    __syncthreads();
+    gather_cols<L>(a, lds, 0);
     __syncthreads();
 
     unsigned nbar = 0;
@@ -328,36 +392,16 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
     for (int ep = 0; ep < a.n_epochs && ok; ++ep) {
         for (int kb = 0; kb < a.num_batches && step < a.total_steps && ok; ++kb, ++step) {
             CL_STAMP(0);
-            // ---- gather (trajectory_buffer.cu:168-200) ----
-            if (tid < BB) {
-                const int list = (int)(((long)kb * BB + tid) % a.limit);
-                const int src = a.perms ? a.perms[(long)ep * a.limit + list]
-                                        : (int)feistel_index((uint32_t)list, a.fk[ep & 15]);
-                rows[tid] = src;
-                if (a.policy) {
-                    lds[L::tgt + tid] = a.adv[src];
-                    lds[L::olp + tid] = a.logprob[src];
-                } else {
-                    lds[L::tgt + tid] = a.adv_target[src];
-                }
-            }
-            __syncthreads();
-            for (int e = tid; e < BB * S; e += TPB) {
-                const int i = e / S, s = e % S;
-                lds[L::x + i * SP + s] = a.state[(long)rows[i] * S + s];
-            }
-            if (a.policy)
-                for (int e = tid; e < BB * A; e += TPB) {
-                    const int i = e / A, j = e % A;
-                    lds[L::act + i * OMAX + j] = a.action[(long)rows[i] * A + j];
-                }
-            __syncthreads();
-
+            const int cur = step & 1;
+            const int xc = L::x + cur * BB * L::SPMAX, tc = L::tgt + cur * BB, oc = L::olp + cur * BB,
+                      acb = L::act + cur * BB * OMAX;
+            const bool has_next = step + 1 < a.total_steps;
+            const int kb_n = kb + 1 < a.num_batches ? kb + 1 : 0, ep_n = kb + 1 < a.num_batches ? ep : ep + 1;
             CL_STAMP(1);
-            // ---- layer 0, own units: h1ᵀ[j][b] = Σ_s W0[j][s]·x[b][s] + b0[j]  (2 × 4 tiles, one per wave)
-            {
+            // ---- layer 0, own units: h1ᵀ[j][b] = Σ_s W0[j][s]·x[b][s] + b0[j]  (HC/16 × 4 tiles, one per wave)
+            if (w < 4 * (HC / 16)) {
                 const int tj = w / 4, tb = w % 4;
-                const f32x4 acc = mm_tile(lds + L::W0 + 16 * tj * SP, SP, 1, lds + L::x + 16 * tb * SP, 1, SP, S);
+                const f32x4 acc = mm_tile(lds + L::W0 + 16 * tj * SP, SP, 1, lds + xc + 16 * tb * SP, 1, SP, S);
                 const int b = 16 * tb + c, j = 16 * tj + 4 * q;
                 f32x4 hv;
 #pragma unroll
@@ -370,6 +414,7 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
             }
             CL_STAMP(2);
             cluster_arrive(a);
+            if (has_next) gather_rows<L>(a, lds, ep_n, kb_n, cur ^ 1);   // the next minibatch, part 1
             ok = cluster_wait(a, nbar++, NWG, flag);                     // A: every h1 column published
             if (!ok) break;
             CL_STAMP(3);
@@ -390,16 +435,28 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
             __syncthreads();
 
             CL_STAMP(4);
-            // ---- layer 1, own units: h2[b][j] = relu(Σ_k h1[b][k]·W1[j][k] + b1[j])  (4 × 2 tiles)
+            // ---- layer 1, own units: h2[b][j] = relu(Σ_k h1[b][k]·W1[j][k] + b1[j])  (4 × HC/16 tiles; with
+            // fewer tiles than waves, K is split in two and the upper half's partial added through LDS)
             {
-                const int tb = w / 2, tj = w % 2;
-                const f32x4 acc = mm_tile(lds + L::h1 + 16 * tb * HP, HP, 1, lds + L::W1 + 16 * tj * HP, 1, HP, H);
-                const int j = 16 * tj + c;
-                const float bj = lds[L::b1 + j];
+                constexpr int NT = L::NT1, KS = L::KS1, KL = H / KS;
+                const int t = w % NT, ks = w / NT;
+                const int tb = t / (HC / 16), tj = t % (HC / 16);
+                f32x4 acc = mm_tile(lds + L::h1 + 16 * tb * HP + ks * KL, HP, 1, lds + L::W1 + 16 * tj * HP + ks * KL, 1,
+                                    HP, KL);
+                if constexpr (KS > 1) {
+                    static_assert(KS == 2, "layer-1 K split");
+                    if (ks == 1) *reinterpret_cast<f32x4*>(lds + L::l1s + (t * 64 + lane) * 4) = acc;
+                    __syncthreads();
+                    if (ks == 0) acc += *reinterpret_cast<const f32x4*>(lds + L::l1s + (t * 64 + lane) * 4);
+                }
+                if (ks == 0) {
+                    const int j = 16 * tj + c;
+                    const float bj = lds[L::b1 + j];
 #pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const float v = acc[e] + bj;
-                    lds[L::h2 + (16 * tb + 4 * q + e) * HCP + j] = v > 0.f ? v : 0.f;
+                    for (int e = 0; e < 4; ++e) {
+                        const float v = acc[e] + bj;
+                        lds[L::h2 + (16 * tb + 4 * q + e) * HCP + j] = v > 0.f ? v : 0.f;
+                    }
                 }
             }
             __syncthreads();
@@ -410,16 +467,29 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
             }
             CL_STAMP(5);
             cluster_arrive(a);
+            if (has_next) gather_cols<L>(a, lds, cur ^ 1);               // the next minibatch, part 2
             ok = cluster_wait(a, nbar++, NWG, flag);                     // B: every y partial published
             if (!ok) break;
             CL_STAMP(6);
             // ---- y = Σ_c partials (fixed order) + b2; the head, identically in every workgroup ----
-            if (tid < BB * (OMAX / 4)) {
-                const int b = tid / (OMAX / 4), oq = 4 * (tid % (OMAX / 4));
-                f32x4 s = ld16_sc1(rY, b * OMAX + oq);
-                for (int cc = 1; cc < NWG; ++cc) s += ld16_sc1(rY, (cc * BB + b) * OMAX + oq);
+            // (256 float4 sums: threads 256-511 add partials NWG/2 … NWG−1 and hand them over through LDS)
+            {
+                static_assert(BB * (OMAX / 4) * 2 == TPB && NWG % 2 == 0, "y sum mapping");
+                const int it = tid % (BB * (OMAX / 4)), half = tid / (BB * (OMAX / 4));
+                const int b = it / (OMAX / 4), oq = 4 * (it % (OMAX / 4));
+                f32x4 v[NWG / 2];
 #pragma unroll
-                for (int e = 0; e < 4; ++e) lds[L::yo + b * OPP + oq + e] = s[e] + lds[L::b2 + oq + e];
+                for (int cc = 0; cc < NWG / 2; ++cc) v[cc] = ld16_sc1(rY, ((half * (NWG / 2) + cc) * BB + b) * OMAX + oq);
+                f32x4 s = v[0];
+#pragma unroll
+                for (int cc = 1; cc < NWG / 2; ++cc) s += v[cc];
+                if (half) *reinterpret_cast<f32x4*>(lds + L::l1s + 4 * it) = s;
+                __syncthreads();
+                if (!half) {
+                    s += *reinterpret_cast<const f32x4*>(lds + L::l1s + 4 * it);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) lds[L::yo + b * OPP + oq + e] = s[e] + lds[L::b2 + oq + e];
+                }
             }
             __syncthreads();
             float part = 0.f;
@@ -427,16 +497,16 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
                 const int i = tid;
                 float* yo = lds + L::yo + i * OPP;
                 if (!a.policy) {                                         // loss.cu:5-23
-                    const float y = yo[0], t = lds[L::tgt + i];
+                    const float y = yo[0], t = lds[tc + i];
                     const float d = t - y;
                     part = d * d;
                     yo[0] = 2 * (y - t) / (float)BB;
                 } else {                                                 // ppo.cu:82-107, policy.cu:67-111
                     float g;
                     const float* ls = lds + L::ls;
-                    const float* ac = lds + L::act + i * OMAX;
+                    const float* ac = lds + acb + i * OMAX;
                     const float lp = log_prob_row(yo, ls, ac, A);
-                    part = surrogate(lds[L::tgt + i], lp, lds[L::olp + i], a.eps, BB, &g);
+                    part = surrogate(lds[tc + i], lp, lds[oc + i], a.eps, BB, &g);
                     for (int j = 0; j < A; ++j) {
                         const float e2 = expf(-2 * ls[j]);
                         const float d = ac[j] - yo[j];
@@ -461,15 +531,15 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
             // (ppo.cu:436-438); waves 7 and 6 (the tiles below keep waves 0-1 longest)
             if (w == NWAVE - 1) colsum64<OMAX>(lds + L::yo, OPP, O, 0.f, lds + L::gb2);
             if (w == NWAVE - 2 && a.policy) colsum64<OMAX>(lds + L::glr, OMAX, A, -a.ent_coeff, lds + L::gls);
-            // ---- output layer backward, own columns: gW2[o][j] = Σ_b g3[b][o]·h2[b][j]  (2 tiles)
-            if (w < 2) {
+            // ---- output layer backward, own columns: gW2[o][j] = Σ_b g3[b][o]·h2[b][j]  (HC/16 tiles)
+            if (w < HC / 16) {
                 const f32x4 acc = mm_tile(lds + L::yo, 1, OPP, lds + L::h2 + 16 * w, HCP, 1, BB);
 #pragma unroll
                 for (int e = 0; e < 4; ++e) lds[L::gW2 + (4 * q + e) * HCP + 16 * w + c] = acc[e];
             }
-            // g2[b][j] = (Σ_o g3[b][o]·W2[o][j]) ⊙ 1[h2[b][j] > 0]  (4 × 2 tiles)
-            {
-                const int tb = w / 2, tj = w % 2;
+            // g2[b][j] = (Σ_o g3[b][o]·W2[o][j]) ⊙ 1[h2[b][j] > 0]  (4 × HC/16 tiles)
+            if (w < 4 * (HC / 16)) {
+                const int tb = w / (HC / 16), tj = w % (HC / 16);
                 const f32x4 acc = mm_tile(lds + L::yo + 16 * tb * OPP, OPP, 1, lds + L::W2 + 16 * tj, HCP, 1, O);
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
@@ -511,21 +581,33 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
             if (!ok) break;
             CL_STAMP(9);
             // ---- g1[b][j] = Σ_c partials (fixed order) ⊙ 1[h1 > 0], own units ----
+            // (64 × HC/4 float4 sums; threads 256-511 add partials NWG/2 … NWG−1 and hand them over)
             {
-                const int b = tid / (HC / 4), jq = 4 * (tid % (HC / 4));      // 64 × 8 float4 = 512 threads
-                f32x4 s = ld16_sc1(rG1, b * H + c0 + jq);
-                for (int cc = 1; cc < NWG; ++cc) s += ld16_sc1(rG1, (cc * BB + b) * H + c0 + jq);
+                static_assert(BB * (HC / 4) * 2 == TPB && NWG % 2 == 0, "g1 sum mapping");
+                const int it = tid % (BB * (HC / 4)), half = tid / (BB * (HC / 4));
+                const int b = it / (HC / 4), jq = 4 * (it % (HC / 4));
+                f32x4 v[NWG / 2];
 #pragma unroll
-                for (int e = 0; e < 4; ++e)
-                    lds[L::g1 + b * HCP + jq + e] = lds[L::h1 + b * HP + c0 + jq + e] > 0.f ? s[e] : 0.f;
+                for (int cc = 0; cc < NWG / 2; ++cc) v[cc] = ld16_sc1(rG1, ((half * (NWG / 2) + cc) * BB + b) * H + c0 + jq);
+                f32x4 s = v[0];
+#pragma unroll
+                for (int cc = 1; cc < NWG / 2; ++cc) s += v[cc];
+                if (half) *reinterpret_cast<f32x4*>(lds + L::l1s + 4 * it) = s;
+                __syncthreads();
+                if (!half) {
+                    s += *reinterpret_cast<const f32x4*>(lds + L::l1s + 4 * it);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        lds[L::g1 + b * HCP + jq + e] = lds[L::h1 + b * HP + c0 + jq + e] > 0.f ? s[e] : 0.f;
+                }
             }
             __syncthreads();
-            // ---- layer 0 backward, own rows: gW0[j][s] = Σ_b g1[b][j]·x[b][s] (2 × ⌈S/16⌉ tiles), gb0 ----
+            // ---- layer 0 backward, own rows: gW0[j][s] = Σ_b g1[b][j]·x[b][s] (HC/16 × ⌈S/16⌉ tiles), gb0 ----
             {
                 const int ts = (S + 15) / 16;
-                for (int t = w; t < 2 * ts; t += NWAVE) {
+                for (int t = w; t < (HC / 16) * ts; t += NWAVE) {
                     const int tj = t / ts, tsb = t % ts;
-                    const f32x4 acc = mm_tile(lds + L::g1 + 16 * tj, 1, HCP, lds + L::x + 16 * tsb, SP, 1, BB);
+                    const f32x4 acc = mm_tile(lds + L::g1 + 16 * tj, 1, HCP, lds + xc + 16 * tsb, SP, 1, BB);
                     const int s = 16 * tsb + c;
                     if (s < S) {
 #pragma unroll
@@ -546,7 +628,7 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
                 for (int u = 0; u < SMALL_SLOTS; ++u) {
                     const int e = tid + u * TPB;
                     if (e < nsmall) {
-                        const Small s = small_elem<H>(a, e, c0);
+                        const Small s = small_elem<H, HC>(a, e, c0);
                         float pv = lds[s.lds_p];
                         const float g = lds[s.lds_g];
                         if (s.kind == 1) adam_elem(pv, g, sm[u], sv[u], st_ls, a.b1, a.b2, bc2_ls);
@@ -568,7 +650,7 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
     // ones are still in LDS; gW1 is recomputed from the last step's g2 and h1, which are too
     if (step > 0) {
         for (int e = tid_e; e < nsmall; e += TPB) {
-            const Small s = small_elem<H>(a, e, c0_e);
+            const Small s = small_elem<H, HC>(a, e, c0_e);
             if (s.kind != 0 && cw != 0) continue;
             if (s.kind == 1) a.log_std_grad[s.gflat] = lds[s.lds_g];
             else a.grads[s.gflat] = lds[s.lds_g];
@@ -603,7 +685,7 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
     for (int u = 0; u < SMALL_SLOTS; ++u) {
         const int e = tid_e + u * TPB;
         if (e < nsmall) {
-            const Small s = small_elem<H>(a, e, c0_e);
+            const Small s = small_elem<H, HC>(a, e, c0_e);
             if (s.kind != 0 && cw != 0) continue;
             if (s.kind == 1) { a.log_std[s.gflat] = lds[s.lds_p]; a.m_ls[s.gflat] = sm[u]; a.v_ls[s.gflat] = sv[u]; }
             else { a.params[s.gflat] = lds[s.lds_p]; a.m[s.gflat] = sm[u]; a.v[s.gflat] = sv[u]; }
@@ -637,8 +719,8 @@ int phip_cluster_update(const PhipTinyNet* net, const PhipTinyPhase* ph) {
     if (H != 256 || net->sizes[2] != H || S < 1 || S > 20 || O < 1 || O > OMAX) return -1;
     if (!net->relu[0] || !net->relu[1] || net->relu[2]) return -1;
     if (ph->policy && (!net->log_std || !net->m_ls)) return -1;
-    using Ly = Lay<256>;
-    constexpr size_t bytes = sizeof(float) * (size_t)Ly::TOTAL;
+    constexpr int HC = 16, NWG = 256 / HC;                         // 16 workgroups of 16 hidden units
+    constexpr size_t bytes = sizeof(float) * (size_t)Lay<256, HC>::TOTAL;
     static_assert(bytes <= 160 * 1024, "cluster: LDS");
     if (ph->n_epochs <= 0 || ph->num_batches <= 0) return 0;     // fit check only
     ClArgs a{};
@@ -665,7 +747,6 @@ int phip_cluster_update(const PhipTinyNet* net, const PhipTinyPhase* ph) {
     a.steps = ph->steps; a.steps_ls = ph->steps_ls;
     a.b1 = ph->b1; a.b2 = ph->b2; a.eps = ph->eps; a.ent_coeff = ph->ent_coeff;
     a.stats = ph->stats;
-    constexpr int NWG = 256 / HC;
     Ws& ws = g_ws[phip_side_active() ? 1 : 0];
     const long need = (long)BB * 256 + (long)NWG * BB * OMAX + (long)NWG * BB * 256;
     if (ws.cap < need) {
@@ -688,16 +769,22 @@ int phip_cluster_update(const PhipTinyNet* net, const PhipTinyPhase* ph) {
     unsigned* d_err = nullptr;
     PPO_CHECK(hipHostGetDevicePointer((void**)&d_err, g_err, 0));
     a.X1 = ws.X1; a.Y = ws.Y; a.G1 = ws.G1; a.ctr = ws.ctr; a.err = d_err;
-    // one workgroup in every 8: blocks b and b + 8 are dealt to one XCD (observed, MI355X_MICROARCH.md
-    // § Workgroup dispatch) — same-XCD hand-offs are faster; correctness never depends on it
-    a.active_stride = 8;
+    // one workgroup in every `active_stride`: blocks b and b + 8 are dealt to one XCD (observed,
+    // MI355X_MICROARCH.md § Workgroup dispatch), so stride 8 puts the phase on one XCD, 4 on two, 1 on
+    // all eight; correctness never depends on it (PPO_CLUSTER_STRIDE overrides; 1, 2, 4 or 8)
+    // (value phase — the longer — on one XCD, policy on two: 16 + 8 ≤ 32 CUs wherever they land)
+    a.active_stride = ph->policy ? 4 : 8;
+    if (const char* st = getenv("PPO_CLUSTER_STRIDE")) {
+        const int v = atoi(st);
+        if (v == 1 || v == 2 || v == 4 || v == 8) a.active_stride = v;
+    }
     static unsigned long long* stamps = nullptr;
     const bool want_stamps = getenv("PPO_CLUSTER_STAMPS") != nullptr;
     if (want_stamps) {
         if (!stamps) stamps = (unsigned long long*)phip_malloc(sizeof(unsigned long long) * 64 * 12);
         a.stamps = stamps;
     }
-    auto kfn = cluster_phase_kernel<256>;
+    auto kfn = cluster_phase_kernel<256, HC>;
     static bool attr = false;
     if (!attr) {
         PPO_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
