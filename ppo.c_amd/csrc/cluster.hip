@@ -23,42 +23,16 @@
 // bounded: a timeout sets the host-visible error word and every workgroup leaves.  b2 and log σ are
 // replicated: every workgroup computes their gradients from the same values in the same order and
 // applies the same Adam step (bit-identical copies).  GEMMs: v_mfma_f32_16x16x4_f32 (exact fp32).
-#include "dev.h"
+#include "cluster_common.h"
 
 #include <cmath>
 #include <cstdlib>
 
 namespace {
+using namespace clu;
 
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-
-constexpr int TPB = 512, NWAVE = TPB / 64;
-constexpr int BB = 64;            // minibatch rows
 constexpr int OMAX = 16;          // output width
 constexpr int OPP = 20;           // pitch of [64][OMAX] arrays
-
-struct Feistel { uint32_t k[4]; uint32_t half, mask, n; };
-
-__device__ __forceinline__ uint32_t mix32(uint32_t x) {
-    x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
-    return x;
-}
-// identical to buffer.hip's feistel_index (restated in oracle/ref_cpu.c: ref_feistel_index)
-__device__ __forceinline__ uint32_t feistel_index(uint32_t i, const Feistel& f) {
-    uint32_t x = i;
-    do {
-        uint32_t L = x >> f.half, R = x & f.mask;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const uint32_t nl = R;
-            R = L ^ (mix32(R ^ f.k[r]) & f.mask);
-            L = nl;
-        }
-        x = (L << f.half) | R;
-    } while (x >= f.n);
-    return x;
-}
 
 struct ClArgs {
     int S, O, policy, SP;                     // SP: pitch of x and W0 rows in LDS (4·odd ≥ S)
@@ -79,127 +53,6 @@ struct ClArgs {
     unsigned long long* stamps;               // diagnostics (PPO_CLUSTER_STAMPS): wall clock per phase,
                                               // workgroup 0, steps 0..63, 12 slots
 };
-
-// ---- hand-off primitives (sc1: write-through stores, L1-bypassing loads) ----
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const float* p, long floats) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, (int)(floats * 4), 0x00020000);
-}
-__device__ __forceinline__ void st16_sc1(__amdgpu_buffer_rsrc_t r, int off_floats, f32x4 v) {
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off_floats * 4, 0, 16);
-}
-__device__ __forceinline__ f32x4 ld16_sc1(__amdgpu_buffer_rsrc_t r, int off_floats) {
-    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, off_floats * 4, 0, 16));
-}
-
-// Arrival: the workgroup's published stores are complete (every wave drained, then a workgroup
-// barrier), then ONE lane adds to the monotonic counter.  Work that publishes nothing may run between
-// cluster_arrive and cluster_wait (it overlaps the other workgroups' arrival skew).
-__device__ __forceinline__ void cluster_arrive(const ClArgs& a) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(a.ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// Wait until all `nwg` workgroups have arrived for barrier number `n` (counting from 0 within the
-// launch): the arriving lane polls (sc1 loads + s_sleep), the other waves wait at the workgroup
-// barrier it then joins.  Returns false on timeout (error word set), uniformly for the workgroup.
-__device__ __forceinline__ bool cluster_wait(const ClArgs& a, unsigned n, int nwg, int* flag_lds) {
-    if (threadIdx.x == 0) {
-        const unsigned target = (unsigned)nwg * (n + 1);
-        unsigned spins = 0;
-        int ok = 1;
-        while (__hip_atomic_load(a.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-            __builtin_amdgcn_s_sleep(1);
-            if (++spins > (1u << 22) ||
-                __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
-                __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                ok = 0;
-                break;
-            }
-        }
-        *flag_lds = ok;
-    }
-    __syncthreads();
-    return *flag_lds != 0;
-}
-
-// Σ_b M[b][col] over the 64 minibatch rows for columns [0, NC) by ONE wave, in a fixed order: lane
-// (col = lane / P, part = lane % P) adds rows part·R … part·R + R − 1 in order, then the P parts are
-// combined by xor shuffles (commutative pairs: every lane of a column, and every workgroup, gets the
-// same bits).  out[col] = sum + add for col < ncols.
-template <int NC>
-__device__ __forceinline__ void colsum64(const float* M, int pitch, int ncols, float add, float* out) {
-    constexpr int P = 64 / NC, R = 64 / P;
-    const int lane = threadIdx.x & 63, col = lane / P, part = lane % P;
-    float v[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) v[r] = M[(part * R + r) * pitch + col];
-    float s = 0.f;
-#pragma unroll
-    for (int r = 0; r < R; ++r) s += v[r];
-#pragma unroll
-    for (int o = 1; o < P; o <<= 1) s += __shfl_xor(s, o, 64);
-    if (part == 0 && col < ncols) out[col] = s + add;
-}
-
-// One 16×16 output tile: acc(i, j) = Σ_k A(i, k)·B(k, j), A(i, k) = A[i·as_i + k·as_k],
-// B(k, j) = B[k·bs_k + j·bs_j] (pointers at the tile's origin, LDS).  Lane (c = l&15, q = l>>4)
-// loads A(c, k0+q), B(k0+q, c) and receives acc rows 4q..4q+3 of column c.  K ≥ 1; a k-tail
-// (K % 4) is zeroed.  Eight MFMAs' operands are loaded before their MFMAs issue.
-__device__ __forceinline__ f32x4 mm_tile(const float* A, int as_i, int as_k, const float* B, int bs_k, int bs_j,
-                                         int K) {
-    const int lane = threadIdx.x & 63, c = lane & 15, q = lane >> 4;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    const float* Ar = A + c * as_i;
-    const float* Bc = B + c * bs_j;
-    for (int k0 = 0; k0 < K; k0 += 32) {
-        float av[8], bv[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int k = min(k0 + 4 * u + q, K - 1);
-            av[u] = Ar[k * as_k];
-            bv[u] = Bc[k * bs_k];
-        }
-        asm("" : "+v"(av[0]), "+v"(av[1]), "+v"(av[2]), "+v"(av[3]), "+v"(av[4]), "+v"(av[5]), "+v"(av[6]),
-                 "+v"(av[7]), "+v"(bv[0]), "+v"(bv[1]), "+v"(bv[2]), "+v"(bv[3]), "+v"(bv[4]), "+v"(bv[5]),
-                 "+v"(bv[6]), "+v"(bv[7]));
-        const int nu = K - k0 >= 32 ? 8 : (K - k0 + 3) >> 2;
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const bool kin = k0 + 4 * u + q < K;
-            if (u < nu) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(kin ? av[u] : 0.f, kin ? bv[u] : 0.f, acc, 0, 0, 0);
-        }
-    }
-    return acc;
-}
-
-__device__ __forceinline__ float log_prob_row(const float* mu, const float* log_std, const float* a, int A) {
-    const float cst = (float)(-0.5 * A * (double)logf((float)(2 * M_PI)));
-    float lp = cst;
-    for (int j = 0; j < A; ++j) {
-        const float z = (a[j] - mu[j]) / expf(log_std[j]);
-        lp = (float)((double)lp - ((double)log_std[j] + 0.5 * (double)(z * z)));
-    }
-    return lp;
-}
-
-__device__ __forceinline__ float surrogate(float adv, float lp, float old_lp, float eps, int m, float* grad) {
-    const float ratio = (float)exp((double)(lp - old_lp));
-    const int adv_pos = adv > 0;
-    const int ratio_pos = ratio > 1 + eps;
-    const int ratio_neg = ratio < 1 - eps;
-    *grad = -(adv_pos * !ratio_pos + !adv_pos * !ratio_neg) * adv * ratio / m;
-    return adv * (adv_pos * (ratio_pos * (1 + eps) + !ratio_pos * ratio) +
-                  !adv_pos * (ratio_neg * (1 - eps) + !ratio_neg * ratio));
-}
-
-// adam.cu:53-74 / tiny.hip adam_elem
-__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, float step, float b1, float b2,
-                                          float bc2) {
-    m = b1 * m + (1 - b1) * g;
-    v = b2 * v + (1 - b2) * (g * g);
-    const float denom = (float)((double)sqrtf(v / bc2) + 1e-8);
-    p -= step * m / denom;
-}
 
 // LDS layout (floats) for hidden width H, HC hidden units per workgroup
 template <int H, int HC>
@@ -413,9 +266,9 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
                 st16_sc1(rX1, b * H + c0 + j, hv);                       // publish
             }
             CL_STAMP(2);
-            cluster_arrive(a);
+            cluster_arrive(a.ctr);
             if (has_next) gather_rows<L>(a, lds, ep_n, kb_n, cur ^ 1);   // the next minibatch, part 1
-            ok = cluster_wait(a, nbar++, NWG, flag);                     // A: every h1 column published
+            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag);                     // A: every h1 column published
             if (!ok) break;
             CL_STAMP(3);
             // every other workgroup's h1 columns (sc1 loads): lane → column quad 4·lane, rows w + 8u,
@@ -466,9 +319,9 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
                 st16_sc1(rY, (cw * BB + 16 * w + c) * OMAX + 4 * q, acc);     // publish Y[cw][b][4q..4q+3]
             }
             CL_STAMP(5);
-            cluster_arrive(a);
+            cluster_arrive(a.ctr);
             if (has_next) gather_cols<L>(a, lds, cur ^ 1);               // the next minibatch, part 2
-            ok = cluster_wait(a, nbar++, NWG, flag);                     // B: every y partial published
+            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag);                     // B: every y partial published
             if (!ok) break;
             CL_STAMP(6);
             // ---- y = Σ_c partials (fixed order) + b2; the head, identically in every workgroup ----
@@ -558,7 +411,7 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
             }
             // bias gradient of layer 1 (fixed order)
             if (w == NWAVE - 1) colsum64<HC>(lds + L::g2, HCP, HC, 0.f, lds + L::gb1);
-            cluster_arrive(a);                                           // (its barrier: every wave done reading W1)
+            cluster_arrive(a.ctr);                                           // (its barrier: every wave done reading W1)
             // ---- gW1[j][k] = Σ_b g2[b][j]·h1[b][k] with Adam fused (the lane holds these elements'
             // moments), overlapping the other workgroups' arrivals ----
             {
@@ -577,7 +430,7 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
                 }
             }
             CL_STAMP(8);
-            ok = cluster_wait(a, nbar++, NWG, flag);                     // C: every g1 partial published
+            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag);                     // C: every g1 partial published
             if (!ok) break;
             CL_STAMP(9);
             // ---- g1[b][j] = Σ_c partials (fixed order) ⊙ 1[h1 > 0], own units ----
@@ -712,8 +565,25 @@ int phip_cluster_error(void) {
 
 // Returns 0 when launched (or, with n_epochs = 0, when the shape fits); −1 when the network or the
 // minibatch does not fit this path (the caller falls back).
+// the device pointer of the host-mapped error word shared by the cluster kernels (allocated on first
+// use); NULL, with the error recorded, when an earlier launch left it set
+unsigned* phip_cluster_err_dev(void) {
+    if (!g_err) {
+        PPO_CHECK(hipHostMalloc((void**)&g_err, 64, hipHostMallocMapped | hipHostMallocCoherent));
+        *g_err = 0u;
+    }
+    if (*g_err) {
+        phip_record_error("cluster phase: a barrier timed out in an earlier launch");
+        return nullptr;
+    }
+    unsigned* d_err = nullptr;
+    PPO_CHECK(hipHostGetDevicePointer((void**)&d_err, g_err, 0));
+    return d_err;
+}
+
 int phip_cluster_update(const PhipTinyNet* net, const PhipTinyPhase* ph) {
     if (getenv("PPO_NO_CLUSTER")) return -1;
+    if (net->L == 4) return phip_cluster_deep_update(net, ph);       // S → 512 × 3 → O (cluster_deep.hip)
     if (net->L != 3 || ph->B != BB || ph->n_epochs > 16) return -1;
     const int S = net->sizes[0], H = net->sizes[1], O = net->sizes[3];
     if (H != 256 || net->sizes[2] != H || S < 1 || S > 20 || O < 1 || O > OMAX) return -1;
@@ -758,16 +628,8 @@ int phip_cluster_update(const PhipTinyNet* net, const PhipTinyPhase* ph) {
     }
     ws.Y = ws.X1 + (long)BB * 256;
     ws.G1 = ws.Y + (long)NWG * BB * OMAX;
-    if (!g_err) {
-        PPO_CHECK(hipHostMalloc((void**)&g_err, 64, hipHostMallocMapped | hipHostMallocCoherent));
-        *g_err = 0u;
-    }
-    if (*g_err) {
-        phip_record_error("cluster phase: a barrier timed out in an earlier launch");
-        return -2;
-    }
-    unsigned* d_err = nullptr;
-    PPO_CHECK(hipHostGetDevicePointer((void**)&d_err, g_err, 0));
+    unsigned* d_err = phip_cluster_err_dev();
+    if (!d_err) return -2;
     a.X1 = ws.X1; a.Y = ws.Y; a.G1 = ws.G1; a.ctr = ws.ctr; a.err = d_err;
     // one workgroup in every `active_stride`: blocks b and b + 8 are dealt to one XCD (observed,
     // MI355X_MICROARCH.md § Workgroup dispatch), so stride 8 puts the phase on one XCD, 4 on two, 1 on

@@ -121,6 +121,10 @@ int phip_tiny_update(const PhipTinyNet* net, const PhipTinyPhase* ph);
  * workgroups (cluster.hip; net->wt unused); −1 when it does not fit, −2 after an earlier timeout */
 int phip_cluster_update(const PhipTinyNet* net, const PhipTinyPhase* ph);
 int phip_cluster_error(void);          /* nonzero: a cluster barrier timed out */
+/* S → 512 → 512 → 512 → O (S ≤ 380, S % 4 = 0, O ≤ 20) at B = 64 on 32 cooperating workgroups
+ * (cluster_deep.hip); phip_cluster_update dispatches 4-layer networks here */
+int phip_cluster_deep_update(const PhipTinyNet* net, const PhipTinyPhase* ph);
+unsigned* phip_cluster_err_dev(void);  /* device pointer of the shared error word (NULL: already set) */
 
 /* ---------------- element-wise / heads (kernels.hip) ---------------- */
 void phip_relu(float* x, long count);

@@ -1,6 +1,6 @@
-"""The multi-workgroup single-launch phase (csrc/cluster.hip) for S → 256 → 256 → O networks at the
-reference's B = 64 (config C3's networks, main.c:34's minibatch) against the multi-launch loop and the
-oracle (reference ppo.cu:395-443).
+"""The multi-workgroup single-launch phases at the reference's B = 64 (main.c:34's minibatch) against
+the multi-launch loop and the oracle (reference ppo.cu:395-443): csrc/cluster.hip for S → 256 → 256 →
+O networks (config C3's) and csrc/cluster_deep.hip for S → 512 → 512 → 512 → O (config C4's).
 
 ppo_update takes it by itself for these shapes at B = 64 on one GPU; PPO_NO_CLUSTER=1 forces the
 multi-launch loop.  From identical state both must give the same minibatch gradients (stated fp32 GEMM
@@ -21,6 +21,8 @@ pytestmark = pytest.mark.gpu
 
 LIBC = C.CDLL("libc.so.6")
 C3 = [17, 256, 256, 6]
+C4 = [376, 512, 512, 512, 17]
+NETS = pytest.mark.parametrize("sizes", [C3, C4], ids=["c3", "c4"])
 RELU = lambda sizes: [1] * (len(sizes) - 2) + [0]  # noqa: E731
 LR = 3e-4
 
@@ -72,13 +74,14 @@ def run(lib, sizes, N, B, n_pol, n_val, shuffle, cluster, seed=21, limit=None, e
         os.environ.pop("PPO_NO_CLUSTER", None)
 
 
+@NETS
 @pytest.mark.parametrize("shuffle", [0, 1])
-def test_cluster_single_steps_match_multilaunch(lib, oracle, shuffle):
-    """one value step, then one policy step (C3 networks, B = 64): the same gradients and Adam deltas"""
+def test_cluster_single_steps_match_multilaunch(lib, oracle, shuffle, sizes):
+    """one value step, then one policy step (B = 64): the same gradients and Adam deltas"""
     N, B = 4096, 64
     for n_pol, n_val in ((0, 1), (1, 0)):                  # one epoch each, capped at one step
-        a = run(lib, C3, N, B, n_pol, n_val, shuffle, cluster=True, limit=(n_val, n_pol))
-        b = run(lib, C3, N, B, n_pol, n_val, shuffle, cluster=False, limit=(n_val, n_pol))
+        a = run(lib, sizes, N, B, n_pol, n_val, shuffle, cluster=True, limit=(n_val, n_pol))
+        b = run(lib, sizes, N, B, n_pol, n_val, shuffle, cluster=False, limit=(n_val, n_pol))
         assert not a["multi"] and b["multi"], "the cluster path did not run (or the fallback did not)"
         assert a["t"] == b["t"] == (n_val, n_pol, n_pol)
         assert a["next_rand"] == b["next_rand"], "host rand() stream consumed differently"
@@ -93,33 +96,35 @@ def test_cluster_single_steps_match_multilaunch(lib, oracle, shuffle):
             assert (err > 1e-6).mean() < 0.01, (k, (err > 1e-6).mean())
 
 
-def test_cluster_first_steps_vs_oracle(lib, oracle):
-    """the first 16 value and 16 policy steps of a C3-network update at B = 64 on the cluster path
-    against the oracle's update of the same buffer, element by element (≥ 99 % within 0.1·lr)"""
+@NETS
+def test_cluster_first_steps_vs_oracle(lib, oracle, sizes):
+    """the first 16 value and 16 policy steps of an update at B = 64 on the cluster path against the
+    oracle's update of the same buffer, element by element (≥ 99 % within 0.1·lr)"""
     oracle.load(use_openblas=True)
     N, B, n = 16384, 64, 16
-    a = run(lib, C3, N, B, 1, 1, 1, cluster=True, limit=(n, n), ent=0.0)
+    a = run(lib, sizes, N, B, 1, 1, 1, cluster=True, limit=(n, n), ent=0.0)
     assert not a["multi"]
-    ref = oracle.ppo_update(C3, RELU(C3), a["mu0"], a["ls0"], a["v0"], a["buf"], batch_size=B, n_epochs_policy=1,
+    ref = oracle.ppo_update(sizes, RELU(sizes), a["mu0"], a["ls0"], a["v0"], a["buf"], batch_size=B, n_epochs_policy=1,
                             n_epochs_value=1, shuffle_mode=1, seed=9, max_value_steps=n, max_policy_steps=n)
     assert a["t"] == (ref["t_v"], ref["t_mu"], ref["t_ent"]) == (n, n, n)
     for got, want, what in ((a["v"], ref["v"], "V"), (a["mu"], ref["mu"], "mu"), (a["ls"], ref["log_std"], "log_std")):
         err = np.abs(got.astype(np.float64) - want)
         q = float((err <= 0.1 * LR).mean())
-        print(f"cluster C3 {what}: max err {err.max() / LR:.4f} lr, {100 * q:.3f} % within 0.1 lr")
+        print(f"cluster {sizes} {what}: max err {err.max() / LR:.4f} lr, {100 * q:.3f} % within 0.1 lr")
         assert err.max() <= 2 * LR * n, f"{what}: max err {err.max()}"
         assert q >= 0.99, f"{what}: only {q * 100:.2f} % within 0.1·lr"
     np.testing.assert_allclose(a["stats"][0], ref["sum_v_loss"], rtol=1e-3)
     np.testing.assert_allclose(a["stats"][2], ref["sum_policy_loss"], rtol=1e-3, atol=1e-5)
 
 
+@NETS
 @pytest.mark.parametrize("shuffle", [0, 1])
-def test_cluster_full_update_matches_multilaunch(lib, oracle, shuffle):
+def test_cluster_full_update_matches_multilaunch(lib, oracle, shuffle, sizes):
     """a whole update (10 value + 4 policy epochs of 64-row minibatches over 16,384 transitions:
     2560 + 1024 steps) on both paths: step counts, rand() use, losses and parameter motion"""
     N, B = 16384, 64
-    a = run(lib, C3, N, B, 4, 10, shuffle, cluster=True)
-    b = run(lib, C3, N, B, 4, 10, shuffle, cluster=False)
+    a = run(lib, sizes, N, B, 4, 10, shuffle, cluster=True)
+    b = run(lib, sizes, N, B, 4, 10, shuffle, cluster=False)
     assert not a["multi"] and b["multi"]
     assert a["t"] == b["t"] == (2560, 1024, 1024)
     assert a["next_rand"] == b["next_rand"]
