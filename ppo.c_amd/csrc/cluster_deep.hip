@@ -11,13 +11,14 @@
 //   h1[:, own] = relu(x·W0[own]ᵀ + b0)                         → X1            barrier A
 //   h2[:, own] = relu(h1·W1[own]ᵀ + b1)                        → X2            barrier B
 //   h3[:, own] = relu(h2·W2[own]ᵀ + b2);  y partial = h3[:, own]·W3[:, own]ᵀ → Y   barrier C
-//   rows 2c, 2c+1: y = Σ partials (fixed order) + b3, the head → G3 (∂L/∂y, log σ row terms, loss)  D
+//   policy: rows 2c, 2c+1: y = Σ partials (fixed order) + b3, the head → G3 (∂L/∂y, log σ terms, loss) D
+//   value (O = 1): every workgroup reduces all 64 rows' partials and runs the head itself (no D)
 //   gW3[:, own], gb3, g3 = (∂L/∂y·W3[:, own]) ⊙ 1[h3 > 0];  P2 = g3·W2[own, :] → Pa               E
 //     (gW2[own] = g3ᵀ·h2 with Adam fused, inside E's wait)
 //   g2[:, own] = Σ P2 partials ⊙ 1[h2 > 0];  P1 = g2·W1[own, :] → Pb                              F
 //     (gW1[own] = g2ᵀ·h1 with Adam fused, inside F's wait)
 //   g1[:, own] = Σ P1 partials ⊙ 1[h1 > 0];  gW0[own] = g1ᵀ·x with Adam fused;  Adam of the rest
-// Six barriers per step (cluster_common.h: sc1 hand-offs, split arrive / wait).  b3 and log σ are
+// Six barriers per policy step, five per value step (cluster_common.h: sc1 hand-offs, split arrive / wait).  b3 and log σ are
 // replicated: every workgroup reads the same ∂L/∂y rows and reduces them in the same order.  Buffer
 // reuse across steps is safe by the barrier order, except X1, which the F gap of step s reads while a
 // workgroup past F may already publish step s + 1's h1: X1 is double-buffered by step parity.
@@ -401,7 +402,8 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
                 const int to = w >> 2, tb = w & 3;
                 if (16 * to < O) {
                     const f32x4 acc = mm_tile(lds + L::W3 + 16 * to * HCP, HCP, 1, lds + L::h3 + 16 * tb * HCP, 1, HCP, HC, tid);
-                    if (16 * to + 4 * q < OP) st16_sc1(rY, (cw * BB + 16 * tb + c) * OP + 16 * to + 4 * q, acc);
+                    if (16 * to + 4 * q < (a.policy ? OP : 4))
+                        st16_sc1(rY, (cw * BB + 16 * tb + c) * OP + 16 * to + 4 * q, acc);
                 }
             }
             CD_STAMP(5);
@@ -409,6 +411,32 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
             ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag);          // C: y partials published
             if (!ok) break;
             CD_STAMP(6);
+            if (!a.policy) {
+                // ---- the value head, replicated: every workgroup reduces all 64 rows' partials (one
+                // float4 each) in the same order — no ∂L/∂y hand-off (loss.cu:5-23) ----
+                {
+                    const int b = tid >> 3, pg = tid & 7;
+                    f32x4 v[NWG / 8];
+#pragma unroll
+                    for (int u = 0; u < NWG / 8; ++u) v[u] = ld16_sc1(rY, ((pg * (NWG / 8) + u) * BB + b) * OP);
+                    float s = v[0][0];
+#pragma unroll
+                    for (int u = 1; u < NWG / 8; ++u) s += v[u][0];
+                    lds[L::scr + tid] = s;
+                }
+                __syncthreads();
+                if (tid < BB) {
+                    float y = lds[L::scr + 8 * tid];
+                    for (int pg = 1; pg < 8; ++pg) y += lds[L::scr + 8 * tid + pg];
+                    y += lds[L::b3];
+                    const float t = lds[tc + tid], d = t - y;
+                    lds[L::lossr + tid] = d * d;
+                    lds[L::g3 + tid * GOP] = 2 * (y - t) / (float)BB;
+                }
+                __syncthreads();
+                CD_STAMP(7);
+                CD_STAMP(8);
+            } else {
             // ---- the head of rows 2cw, 2cw + 1: y = Σ_p partials (fixed order) + b3 ----
             {
                 constexpr int QN = OP / 4, IT = RPW * QN;                // 10 float4 sums of 32 partials
@@ -475,6 +503,7 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
                 else lds[L::lossr + r] = v[0];
             }
             __syncthreads();
+            }
             // replicated sums in a fixed order: gb3[o] = Σ_b g3[b][o]; log σ: Σ_b row terms − c_ent
             // (ppo.cu:436-438); the loss sum once (workgroup 0)
             if (w == NWAVE - 1) colsum64<32>(lds + L::g3, GOP, O, 0.f, lds + L::gb3, tid);
