@@ -126,11 +126,12 @@ __device__ __forceinline__ int gather_src(const ClArgs& a, int ep, int kb, int i
     const int list = (int)(((long)kb * BB + i) % a.limit);
     return a.perms ? a.perms[(long)ep * a.limit + list] : (int)feistel_index((uint32_t)list, a.fk[ep & 15]);
 }
-// gather, part 1 (threads 0-63): the row indices → rows[], the per-row scalars → buffer `buf`
+// gather, part 1 (wave 1 — wave 0's first lane polls the barriers this runs beside): the row indices
+// → rows[], the per-row scalars → buffer `buf`
 template <class L>
 __device__ __forceinline__ void gather_rows(const ClArgs& a, float* lds, int ep, int kb, int buf) {
-    const int i = threadIdx.x;
-    if (i < BB) {
+    const int i = (int)threadIdx.x - 64;
+    if (i >= 0 && i < BB) {
         const int src = gather_src(a, ep, kb, i);
         reinterpret_cast<int*>(lds + L::rows)[i] = src;
         if (a.policy) {
@@ -142,32 +143,34 @@ __device__ __forceinline__ void gather_rows(const ClArgs& a, float* lds, int ep,
         }
     }
 }
-// gather, part 2 (every thread, behind a workgroup barrier after part 1): the rows' states (and
+// gather, part 2 (waves 1-7, behind a workgroup barrier after part 1): the rows' states (and
 // actions) → buffer `buf`, every load in flight before the LDS writes
 template <class L>
 __device__ __forceinline__ void gather_cols(const ClArgs& a, float* lds, int buf) {
-    constexpr int XU = (BB * L::SPMAX + TPB - 1) / TPB, AU = (BB * OMAX + TPB - 1) / TPB;
+    if (threadIdx.x < 64) return;
+    constexpr int NT = TPB - 64;
+    constexpr int XU = (BB * L::SPMAX + NT - 1) / NT, AU = (BB * OMAX + NT - 1) / NT;
     const int* rows = reinterpret_cast<const int*>(lds + L::rows);
-    const int tid = threadIdx.x, S = a.S, A = a.O;
+    const int tid = (int)threadIdx.x - 64, S = a.S, A = a.O;
     float xv[XU], av[AU];
 #pragma unroll
     for (int u = 0; u < XU; ++u) {
-        const int e = tid + u * TPB;
+        const int e = tid + u * NT;
         xv[u] = e < BB * S ? a.state[(long)rows[e / S] * S + e % S] : 0.f;
     }
 #pragma unroll
     for (int u = 0; u < AU; ++u) {
-        const int e = tid + u * TPB;
+        const int e = tid + u * NT;
         av[u] = a.policy && e < BB * A ? a.action[(long)rows[e / A] * A + e % A] : 0.f;
     }
 #pragma unroll
     for (int u = 0; u < XU; ++u) {
-        const int e = tid + u * TPB;
+        const int e = tid + u * NT;
         if (e < BB * S) lds[L::x + buf * BB * L::SPMAX + (e / S) * a.SP + e % S] = xv[u];
     }
 #pragma unroll
     for (int u = 0; u < AU; ++u) {
-        const int e = tid + u * TPB;
+        const int e = tid + u * NT;
         if (a.policy && e < BB * A) lds[L::act + buf * BB * OMAX + (e / A) * OMAX + e % A] = av[u];
     }
 }

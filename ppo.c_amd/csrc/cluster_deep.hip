@@ -41,9 +41,6 @@ constexpr int T12 = (H / 16) / NWAVE;                // gW1 / gW2 tiles per wave
 constexpr int T0 = (SPMAX + 15) / 16 / NWAVE;        // gW0 tiles per wave (3)
 constexpr int RPW = BB / NWG;                        // head rows per workgroup (2)
 constexpr int NSTAMP = 16;
-#ifndef FWD_G
-#define FWD_G 4                                      // forward k-groups of 16 in flight per lane
-#endif
 static_assert(T12 * NWAVE * 16 == H && T0 * NWAVE * 16 >= SPMAX && RPW * NWG == BB, "tile counts");
 
 struct DArgs {
@@ -119,10 +116,11 @@ __device__ __forceinline__ int gather_src(const DArgs& a, int ep, int kb, int i)
     const int list = (int)(((long)kb * BB + i) % a.limit);
     return a.perms ? a.perms[(long)ep * a.limit + list] : (int)feistel_index((uint32_t)list, a.fk[ep & 15]);
 }
-// the minibatch of step (ep, kb) (trajectory_buffer.cu:168-200): row indices and per-row scalars
+// the minibatch of step (ep, kb) (trajectory_buffer.cu:168-200): row indices and per-row scalars, by
+// wave 1 (wave 0's first lane polls the barriers this runs beside)
 __device__ __forceinline__ void gather_rows(const DArgs& a, float* lds, int ep, int kb, int buf) {
-    const int i = threadIdx.x;
-    if (i < BB) {
+    const int i = (int)threadIdx.x - 64;
+    if (i >= 0 && i < BB) {
         const int src = gather_src(a, ep, kb, i);
         reinterpret_cast<int*>(lds + L::rows)[buf * BB + i] = src;
         if (a.policy) {
@@ -134,21 +132,21 @@ __device__ __forceinline__ void gather_rows(const DArgs& a, float* lds, int ep, 
         }
     }
 }
-// the policy's action rows (behind a workgroup barrier after gather_rows)
+// the policy's action rows (behind a workgroup barrier after gather_rows), by waves 1-7
 __device__ __forceinline__ void gather_act(const DArgs& a, float* lds, int buf) {
-    if (!a.policy) return;
+    if (!a.policy || threadIdx.x < 64) return;
     const int* rows = reinterpret_cast<const int*>(lds + L::rows) + buf * BB;
-    const int A = a.O;
-    constexpr int U = (BB * OP + TPB - 1) / TPB;
+    const int A = a.O, t = (int)threadIdx.x - 64;
+    constexpr int NT = TPB - 64, U = (BB * OP + NT - 1) / NT;
     float v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-        const int e = threadIdx.x + u * TPB;
+        const int e = t + u * NT;
         v[u] = e < BB * A ? a.action[(long)rows[e / A] * A + e % A] : 0.f;
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-        const int e = threadIdx.x + u * TPB;
+        const int e = t + u * NT;
         if (e < BB * A) lds[L::act + buf * BB * OP + (e / A) * OP + e % A] = v[u];
     }
 }
@@ -156,75 +154,85 @@ __device__ __forceinline__ void gather_act(const DArgs& a, float* lds, int buf) 
 // Forward tile: acc(j, b) = Σ_{k ∈ [k0, k1)} W[j][k]·X[b][k] for one 16 × 16 block, lane (c, q) holding
 // the weight row c (LDS, Wr) and the activation row c (HBM, ldx(k) = 4 values at k).  k runs in groups
 // of 16: lane q takes k = 16u + 4q + i for the group's MFMA i — both operands alike, so the sum covers
-// every k once (in a different association order than mm_tile's).  k0, k1 multiples of 4.
-template <int FG, class LoadX>
+// every k once (in a different association order than mm_tile's).  k0, k1 multiples of 4,
+// k1 − k0 ≤ 16·NG: every activation load of the range is in flight before the first MFMA (one
+// memory latency per tile), the weights are read from LDS group by group.
+template <int NG, class LoadX>
 __device__ __forceinline__ f32x4 fwd_tile(int tid, const float* Wr, int k0, int k1, LoadX ldx) {
     const int q = (tid & 63) >> 4;
+    f32x4 xv[NG];
+#pragma unroll
+    for (int u = 0; u < NG; ++u) {
+        const int k = k0 + 16 * u + 4 * q;
+        xv[u] = k < k1 ? ldx(k) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int g0 = k0; g0 < k1; g0 += 16 * FG) {
-        f32x4 xv[FG], wv[FG];
 #pragma unroll
-        for (int u = 0; u < FG; ++u) {
-            const int k = g0 + 16 * u + 4 * q;
-            const bool in = k < k1;
-            xv[u] = in ? ldx(k) : f32x4{0.f, 0.f, 0.f, 0.f};
-            wv[u] = in ? *reinterpret_cast<const f32x4*>(Wr + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int u = 0; u < NG; ++u) {
+        if (k0 + 16 * u < k1) {
+            const int k = k0 + 16 * u + 4 * q;
+            const f32x4 wv = k < k1 ? *reinterpret_cast<const f32x4*>(Wr + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[i], xv[u][i], acc, 0, 0, 0);
         }
+    }
+    return acc;
+}
+
+// Weight-gradient tiles with Adam fused.  The lane's wave owns tiles t = 0 … T−1 at columns
+// col = 16(w + 8t) + c (< ncols), rows j = 4q + e: gW[j][col] = Σ_b G[b][j]·X[b][col] over the 64 rows
+// (lane (c, q) holds G[b][c] from LDS and X[b][col] = ldb(b, col) for b = 4u + q).  load(): every X
+// operand of the T tiles and the moments (HBM, row j at g0 + j·ld) in flight at once; apply(): the
+// MFMAs, Adam on the LDS parameters (row j at W + j·pp), the moments written back, and on the last
+// step of the phase the gradient too (callers may read it, as after the multi-launch loop).
+template <int T>
+struct GwTiles {
+    float bv[T][16], mm[T][4], vv[T][4];
+    template <class LoadB>
+    __device__ __forceinline__ void load(int tid, const DArgs& a, long g0, long ld, int ncols, LoadB ldb) {
+        const int lane = tid & 63, c = lane & 15, q = lane >> 4, w = tid >> 6;
 #pragma unroll
-        for (int u = 0; u < FG; ++u) {
-            if (g0 + 16 * u < k1) {
+        for (int t = 0; t < T; ++t) {
+            const int col = 16 * (w + NWAVE * t) + c;
+            const bool in = col < ncols;
 #pragma unroll
-                for (int i = 0; i < 4; ++i) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[u][i], xv[u][i], acc, 0, 0, 0);
+            for (int u = 0; u < 16; ++u) bv[t][u] = in ? ldb(4 * u + q, col) : 0.f;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                mm[t][e] = in ? a.m[g0 + (4 * q + e) * ld + col] : 0.f;
+                vv[t][e] = in ? a.v[g0 + (4 * q + e) * ld + col] : 0.f;
             }
         }
     }
-    return acc;
-}
-
-// Weight-gradient tile: acc(j, k) = Σ_b G[b][j]·X[b][k] over the 64 rows: lane (c, q) holds G[b][c]
-// (LDS, pitch HCP) and X[b][k0 + c] (ldb(b), one float) for b = 4u + q.  Rows j = 4q + e of column c.
-template <class LoadB>
-__device__ __forceinline__ f32x4 gw_tile(int tid, const float* G, LoadB ldb) {
-    const int lane = tid & 63, c = lane & 15, q = lane >> 4;
-    float av[16], bv[16];
+    __device__ __forceinline__ void apply(int tid, const DArgs& a, const float* G, float* W, int pp, long g0, long ld,
+                                          int ncols, float st, float bc2, bool last) {
+        const int lane = tid & 63, c = lane & 15, q = lane >> 4, w = tid >> 6;
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
-        const int b = 4 * u + q;
-        bv[u] = ldb(b);
-        av[u] = G[b * HCP + c];
-    }
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        for (int t = 0; t < T; ++t) {
+            if (16 * (w + NWAVE * t) >= ncols) continue;                    // wave-uniform
+            const int col = 16 * (w + NWAVE * t) + c;
+            float av[16];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u], acc, 0, 0, 0);
-    return acc;
-}
-
-// A weight-gradient tile with Adam fused: the lane's four elements are rows 4q + e of column c
-// (p: LDS parameter of row 4q, pitch pp; g: the flat index of that element, row stride ld — ld = 0
-// marks a column past the layer's width: nothing is updated).  The moments are read from and written
-// back to HBM around the tile's MFMAs (their loads in flight under them); the last step of the phase
-// also writes the gradient out (callers may read it, as after the multi-launch loop).
-template <class LoadB>
-__device__ __forceinline__ void adam_tile(int tid, const DArgs& a, float* p, int pp, long g, long ld, float st,
-                                          float bc2, bool last, LoadB ldb, const float* lds) {
-    float mm[4], vv[4];
-    if (ld) {
+            for (int u = 0; u < 16; ++u) av[u] = G[(4 * u + q) * HCP + c];
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int e = 0; e < 4; ++e) { mm[e] = a.m[g + e * ld]; vv[e] = a.v[g + e * ld]; }
-    }
-    const f32x4 acc = gw_tile(tid, lds + L::gh, ldb);
-    if (ld) {
+            for (int u = 0; u < 16; ++u) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[t][u], acc, 0, 0, 0);
+            if (col < ncols) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            float pv = p[e * pp];
-            adam_elem(pv, acc[e], mm[e], vv[e], st, a.b1, a.b2, bc2);
-            p[e * pp] = pv;
-            a.m[g + e * ld] = mm[e];
-            a.v[g + e * ld] = vv[e];
-            if (last) a.grads[g + e * ld] = acc[e];
+                for (int e = 0; e < 4; ++e) {
+                    float* p = W + (4 * q + e) * pp + col;
+                    float pv = *p;
+                    adam_elem(pv, acc[e], mm[t][e], vv[t][e], st, a.b1, a.b2, bc2);
+                    *p = pv;
+                    const long gi = g0 + (4 * q + e) * ld + col;
+                    a.m[gi] = mm[t][e];
+                    a.v[gi] = vv[t][e];
+                    if (last) a.grads[gi] = acc[e];
+                }
+            }
         }
     }
-}
+};
 
 // K-split epilogue: waves 4-7 hand their partial to waves 0-3 (tile w & 3) through LDS, then the
 // owners return the sum.  Every thread reaches the barrier.
@@ -336,7 +344,7 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
             {
                 const int tb = w & 3, ks = w >> 2, kh = ((S / 4 + 1) / 2) * 4;
                 const float* xr = a.state + (long)rows[16 * tb + c] * S;
-                f32x4 acc = fwd_tile<FWD_G>(tid, lds + L::W0 + c * SPMAX, ks ? kh : 0, ks ? S : kh,
+                f32x4 acc = fwd_tile<16>(tid, lds + L::W0 + c * SPMAX, ks ? kh : 0, ks ? S : kh,
                                      [&](int k) { return *reinterpret_cast<const f32x4*>(xr + k); });
                 acc = ksplit_sum(tid, acc, lds);
                 if (w < 4) {
@@ -360,7 +368,7 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
             // ---- layer 1: h2ᵀ[j][b] = Σ_k W1[j][k]·h1[b][k] ----
             {
                 const int tb = w & 3, ks = w >> 2, b = 16 * tb + c;
-                f32x4 acc = fwd_tile<FWD_G>(tid, lds + L::W1 + c * HP, ks * (H / 2), (ks + 1) * (H / 2),
+                f32x4 acc = fwd_tile<16>(tid, lds + L::W1 + c * HP, ks * (H / 2), (ks + 1) * (H / 2),
                                      [&](int k) { return ld16_sc1(rX1, x1o + b * H + k); });
                 acc = ksplit_sum(tid, acc, lds);
                 if (w < 4) {
@@ -383,7 +391,7 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
             // ---- layer 2: h3ᵀ[j][b] = Σ_k W2[j][k]·h2[b][k] (own columns stay in LDS) ----
             {
                 const int tb = w & 3, ks = w >> 2, b = 16 * tb + c;
-                f32x4 acc = fwd_tile<FWD_G>(tid, lds + L::W2 + c * HP, ks * (H / 2), (ks + 1) * (H / 2),
+                f32x4 acc = fwd_tile<16>(tid, lds + L::W2 + c * HP, ks * (H / 2), (ks + 1) * (H / 2),
                                      [&](int k) { return ld16_sc1(rX2, b * H + k); });
                 acc = ksplit_sum(tid, acc, lds);
                 if (w < 4) {
@@ -542,11 +550,11 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
             CD_STAMP(9);
             cluster_arrive(a.ctr);                                       // (its barrier: W2 reads done)
             // gW2[j][k] = Σ_b g3h[b][j]·h2[b][k] with Adam fused, inside E's wait
-#pragma unroll
-            for (int u = 0; u < T12; ++u) {
-                const int k = 16 * (w + NWAVE * u) + c;
-                adam_tile(tid, a, lds + L::W2 + 4 * q * HP + k, HP, a.woff[2] + (long)(c0 + 4 * q) * H + k, H, st, bc2, last,
-                          [&](int b) { return ld4_sc1(rX2, b * H + k); }, lds);
+            {
+                GwTiles<T12> gt;
+                const long g0 = a.woff[2] + (long)c0 * H;
+                gt.load(tid, a, g0, H, H, [&](int b, int k) { return ld4_sc1(rX2, b * H + k); });
+                gt.apply(tid, a, lds + L::gh, lds + L::W2, HP, g0, H, H, st, bc2, last);
             }
             CD_STAMP(10);
             ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag);          // E: P2 published
@@ -559,11 +567,11 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
             if (w == NWAVE - 1) colsum64<HC>(lds + L::gh, HCP, HC, 0.f, lds + L::gb1, tid);
             CD_STAMP(12);
             cluster_arrive(a.ctr);
-#pragma unroll
-            for (int u = 0; u < T12; ++u) {
-                const int k = 16 * (w + NWAVE * u) + c;
-                adam_tile(tid, a, lds + L::W1 + 4 * q * HP + k, HP, a.woff[1] + (long)(c0 + 4 * q) * H + k, H, st, bc2, last,
-                          [&](int b) { return ld4_sc1(rX1, x1o + b * H + k); }, lds);
+            {
+                GwTiles<T12> gt;
+                const long g0 = a.woff[1] + (long)c0 * H;
+                gt.load(tid, a, g0, H, H, [&](int b, int k) { return ld4_sc1(rX1, x1o + b * H + k); });
+                gt.apply(tid, a, lds + L::gh, lds + L::W1, HP, g0, H, H, st, bc2, last);
             }
             CD_STAMP(13);
             ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag);          // F: P1 published
@@ -571,15 +579,14 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
             CD_STAMP(14);
             // ---- layer 0 backward: g1h = Σ P1 ⊙ 1[h1 > 0]; gW0[j][s] = Σ_b g1h[b][j]·x[b][s] with Adam
             // fused; gb0 ----
-            reduce_partials(tid, rPb, c0, lds + L::h1, lds);
-            __syncthreads();
-#pragma unroll
-            for (int u = 0; u < T0; ++u) {
-                const int s = 16 * (w + NWAVE * u) + c;
-                if (16 * (w + NWAVE * u) < S)
-                    adam_tile(tid, a, lds + L::W0 + 4 * q * SPMAX + s, SPMAX, a.woff[0] + (long)(c0 + 4 * q) * S + s,
-                              s < S ? S : 0, st, bc2, last,
-                              [&](int b) { return s < S ? a.state[(long)rows[b] * S + s] : 0.f; }, lds);
+            {
+                // the state operands and W0's moments in flight under the ∂L/∂h1 reduction
+                GwTiles<T0> gt;
+                const long g0 = a.woff[0] + (long)c0 * S;
+                gt.load(tid, a, g0, S, S, [&](int b, int s) { return a.state[(long)rows[b] * S + s]; });
+                reduce_partials(tid, rPb, c0, lds + L::h1, lds);
+                __syncthreads();
+                gt.apply(tid, a, lds + L::gh, lds + L::W0, SPMAX, g0, S, S, st, bc2, last);
             }
             if (w == NWAVE - 1) colsum64<HC>(lds + L::gh, HCP, HC, 0.f, lds + L::gb0, tid);
             __syncthreads();

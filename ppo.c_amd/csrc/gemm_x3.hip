@@ -843,7 +843,10 @@ void launch_cfg_x3(int c, const X3Args& a) {
 // 128×128 at two per CU (4 waves of 64×64) vs 28.0 µs on 8 waves of 32×64; 16384 rows 50.4 vs 47.9
 int pick_x3(int M, int N, int op) {
     if (g_force_x3 >= 0) return g_force_x3;
-    if (op == OP_TN) return 3;
+    if (op == OP_TN) {
+        static const int tn = [] { const char* e = getenv("PPO_X3_TN_CFG"); return e ? atoi(e) : 3; }();
+        return tn == 5 ? 5 : 3;                              // PPO_X3_TN_CFG=5: 256×128 slabs (A/B)
+    }
     auto tiles = [&](int c) { return (long)ppo_divup(M, kCfgX3[c].bm) * ppo_divup(N, kCfgX3[c].bn); };
     if (tiles(0) >= 256) return 0;
     if (tiles(2) >= 256) return 2;
