@@ -41,6 +41,10 @@ constexpr int T12 = (H / 16) / NWAVE;                // gW1 / gW2 tiles per wave
 constexpr int T0 = (SPMAX + 15) / 16 / NWAVE;        // gW0 tiles per wave (3)
 constexpr int RPW = BB / NWG;                        // head rows per workgroup (2)
 constexpr int NSTAMP = 16;
+#ifndef CLU_FWD_NG
+#define CLU_FWD_NG 4                                 // forward k-groups of 16 in flight per lane (16 — a whole
+                                                     // K half — measured slower: 5.7 vs 4.9 µs per layer)
+#endif
 static_assert(T12 * NWAVE * 16 == H && T0 * NWAVE * 16 >= SPMAX && RPW * NWG == BB, "tile counts");
 
 struct DArgs {
@@ -154,26 +158,28 @@ __device__ __forceinline__ void gather_act(const DArgs& a, float* lds, int buf) 
 // Forward tile: acc(j, b) = Σ_{k ∈ [k0, k1)} W[j][k]·X[b][k] for one 16 × 16 block, lane (c, q) holding
 // the weight row c (LDS, Wr) and the activation row c (HBM, ldx(k) = 4 values at k).  k runs in groups
 // of 16: lane q takes k = 16u + 4q + i for the group's MFMA i — both operands alike, so the sum covers
-// every k once (in a different association order than mm_tile's).  k0, k1 multiples of 4,
-// k1 − k0 ≤ 16·NG: every activation load of the range is in flight before the first MFMA (one
-// memory latency per tile), the weights are read from LDS group by group.
+// every k once (in a different association order than mm_tile's).  k0, k1 multiples of 4.  NG groups'
+// activation loads are in flight before their MFMAs (NG = 16: a whole K half, one memory latency per
+// tile); the weights are read from LDS group by group.
 template <int NG, class LoadX>
 __device__ __forceinline__ f32x4 fwd_tile(int tid, const float* Wr, int k0, int k1, LoadX ldx) {
     const int q = (tid & 63) >> 4;
-    f32x4 xv[NG];
-#pragma unroll
-    for (int u = 0; u < NG; ++u) {
-        const int k = k0 + 16 * u + 4 * q;
-        xv[u] = k < k1 ? ldx(k) : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int g0 = k0; g0 < k1; g0 += 16 * NG) {
+        f32x4 xv[NG];
 #pragma unroll
-    for (int u = 0; u < NG; ++u) {
-        if (k0 + 16 * u < k1) {
-            const int k = k0 + 16 * u + 4 * q;
-            const f32x4 wv = k < k1 ? *reinterpret_cast<const f32x4*>(Wr + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int u = 0; u < NG; ++u) {
+            const int k = g0 + 16 * u + 4 * q;
+            xv[u] = k < k1 ? ldx(k) : f32x4{0.f, 0.f, 0.f, 0.f};
+        }
 #pragma unroll
-            for (int i = 0; i < 4; ++i) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[i], xv[u][i], acc, 0, 0, 0);
+        for (int u = 0; u < NG; ++u) {
+            if (g0 + 16 * u < k1) {
+                const int k = g0 + 16 * u + 4 * q;
+                const f32x4 wv = k < k1 ? *reinterpret_cast<const f32x4*>(Wr + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int i = 0; i < 4; ++i) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[i], xv[u][i], acc, 0, 0, 0);
+            }
         }
     }
     return acc;
@@ -189,11 +195,11 @@ template <int T>
 struct GwTiles {
     float bv[T][16], mm[T][4], vv[T][4];
     template <class LoadB>
-    __device__ __forceinline__ void load(int tid, const DArgs& a, long g0, long ld, int ncols, LoadB ldb) {
+    __device__ __forceinline__ void load(int tid, const DArgs& a, long g0, long ld, int ncols, LoadB ldb, int t0 = 0) {
         const int lane = tid & 63, c = lane & 15, q = lane >> 4, w = tid >> 6;
 #pragma unroll
         for (int t = 0; t < T; ++t) {
-            const int col = 16 * (w + NWAVE * t) + c;
+            const int col = 16 * (w + NWAVE * (t0 + t)) + c;
             const bool in = col < ncols;
 #pragma unroll
             for (int u = 0; u < 16; ++u) bv[t][u] = in ? ldb(4 * u + q, col) : 0.f;
@@ -205,12 +211,12 @@ struct GwTiles {
         }
     }
     __device__ __forceinline__ void apply(int tid, const DArgs& a, const float* G, float* W, int pp, long g0, long ld,
-                                          int ncols, float st, float bc2, bool last) {
+                                          int ncols, float st, float bc2, bool last, int t0 = 0) {
         const int lane = tid & 63, c = lane & 15, q = lane >> 4, w = tid >> 6;
 #pragma unroll
         for (int t = 0; t < T; ++t) {
-            if (16 * (w + NWAVE * t) >= ncols) continue;                    // wave-uniform
-            const int col = 16 * (w + NWAVE * t) + c;
+            if (16 * (w + NWAVE * (t0 + t)) >= ncols) continue;             // wave-uniform
+            const int col = 16 * (w + NWAVE * (t0 + t)) + c;
             float av[16];
 #pragma unroll
             for (int u = 0; u < 16; ++u) av[u] = G[(4 * u + q) * HCP + c];
@@ -321,6 +327,7 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
     __syncthreads();
 
     unsigned nbar = 0;
+    f32x4 pf = {0.f, 0.f, 0.f, 0.f};                             // the next minibatch's state rows, prefetched
     int step = 0;
     bool ok = true;
     for (int ep = 0; ep < a.n_epochs && ok; ++ep) {
@@ -331,6 +338,9 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
             asm volatile("" : "+v"(tid));
             const int lane = tid & 63, w = tid >> 6, c = lane & 15, q = lane >> 4;
             CD_STAMP(0);
+#ifndef CLU_NO_PREFETCH
+            asm volatile("" ::"v"(pf));                                  // (the prefetch has landed)
+#endif
             const int cur = step & 1;
             const int* rows = reinterpret_cast<const int*>(lds + L::rows) + cur * BB;
             const int tc = L::tgt + cur * BB, oc = L::olp + cur * BB, acb = L::act + cur * BB * OP;
@@ -344,7 +354,7 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
             {
                 const int tb = w & 3, ks = w >> 2, kh = ((S / 4 + 1) / 2) * 4;
                 const float* xr = a.state + (long)rows[16 * tb + c] * S;
-                f32x4 acc = fwd_tile<16>(tid, lds + L::W0 + c * SPMAX, ks ? kh : 0, ks ? S : kh,
+                f32x4 acc = fwd_tile<CLU_FWD_NG>(tid, lds + L::W0 + c * SPMAX, ks ? kh : 0, ks ? S : kh,
                                      [&](int k) { return *reinterpret_cast<const f32x4*>(xr + k); });
                 acc = ksplit_sum(tid, acc, lds);
                 if (w < 4) {
@@ -368,7 +378,7 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
             // ---- layer 1: h2ᵀ[j][b] = Σ_k W1[j][k]·h1[b][k] ----
             {
                 const int tb = w & 3, ks = w >> 2, b = 16 * tb + c;
-                f32x4 acc = fwd_tile<16>(tid, lds + L::W1 + c * HP, ks * (H / 2), (ks + 1) * (H / 2),
+                f32x4 acc = fwd_tile<CLU_FWD_NG>(tid, lds + L::W1 + c * HP, ks * (H / 2), (ks + 1) * (H / 2),
                                      [&](int k) { return ld16_sc1(rX1, x1o + b * H + k); });
                 acc = ksplit_sum(tid, acc, lds);
                 if (w < 4) {
@@ -385,13 +395,22 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
             CD_STAMP(3);
             cluster_arrive(a.ctr);
             if (has_next) gather_act(a, lds, cur ^ 1);                   // the next minibatch, part 2
+#ifndef CLU_NO_PREFETCH
+            // rows 2cw, 2cw + 1 of the next minibatch from HBM into the caches (each workgroup two, so
+            // every row is fetched once before the 32 workgroups read all of them at the next layer 0)
+            if (has_next && tid < 2 * (S / 4)) {
+                const int* rn = reinterpret_cast<const int*>(lds + L::rows) + (cur ^ 1) * BB;
+                const int r = tid / (S / 4), k = 4 * (tid % (S / 4));
+                pf = *reinterpret_cast<const f32x4*>(a.state + (long)rn[RPW * cw + r] * S + k);
+            }
+#endif
             ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag);          // B: h2 published
             if (!ok) break;
             CD_STAMP(4);
             // ---- layer 2: h3ᵀ[j][b] = Σ_k W2[j][k]·h2[b][k] (own columns stay in LDS) ----
             {
                 const int tb = w & 3, ks = w >> 2, b = 16 * tb + c;
-                f32x4 acc = fwd_tile<16>(tid, lds + L::W2 + c * HP, ks * (H / 2), (ks + 1) * (H / 2),
+                f32x4 acc = fwd_tile<CLU_FWD_NG>(tid, lds + L::W2 + c * HP, ks * (H / 2), (ks + 1) * (H / 2),
                                      [&](int k) { return ld16_sc1(rX2, b * H + k); });
                 acc = ksplit_sum(tid, acc, lds);
                 if (w < 4) {
@@ -550,11 +569,13 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
             CD_STAMP(9);
             cluster_arrive(a.ctr);                                       // (its barrier: W2 reads done)
             // gW2[j][k] = Σ_b g3h[b][j]·h2[b][k] with Adam fused, inside E's wait
-            {
-                GwTiles<T12> gt;
+            // (one tile's loads at a time: all four tiles' in flight measured slower, 7.9 vs 6.7 µs)
+#pragma unroll 1
+            for (int t = 0; t < T12; ++t) {
+                GwTiles<1> gt;
                 const long g0 = a.woff[2] + (long)c0 * H;
-                gt.load(tid, a, g0, H, H, [&](int b, int k) { return ld4_sc1(rX2, b * H + k); });
-                gt.apply(tid, a, lds + L::gh, lds + L::W2, HP, g0, H, H, st, bc2, last);
+                gt.load(tid, a, g0, H, H, [&](int b, int k) { return ld4_sc1(rX2, b * H + k); }, t);
+                gt.apply(tid, a, lds + L::gh, lds + L::W2, HP, g0, H, H, st, bc2, last, t);
             }
             CD_STAMP(10);
             ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag);          // E: P2 published
@@ -567,11 +588,12 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
             if (w == NWAVE - 1) colsum64<HC>(lds + L::gh, HCP, HC, 0.f, lds + L::gb1, tid);
             CD_STAMP(12);
             cluster_arrive(a.ctr);
-            {
-                GwTiles<T12> gt;
+#pragma unroll 1
+            for (int t = 0; t < T12; ++t) {
+                GwTiles<1> gt;
                 const long g0 = a.woff[1] + (long)c0 * H;
-                gt.load(tid, a, g0, H, H, [&](int b, int k) { return ld4_sc1(rX1, x1o + b * H + k); });
-                gt.apply(tid, a, lds + L::gh, lds + L::W1, HP, g0, H, H, st, bc2, last);
+                gt.load(tid, a, g0, H, H, [&](int b, int k) { return ld4_sc1(rX1, x1o + b * H + k); }, t);
+                gt.apply(tid, a, lds + L::gh, lds + L::W1, HP, g0, H, H, st, bc2, last, t);
             }
             CD_STAMP(13);
             ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag);          // F: P1 published
