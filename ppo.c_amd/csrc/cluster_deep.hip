@@ -41,6 +41,9 @@ constexpr int T12 = (H / 16) / NWAVE;                // gW1 / gW2 tiles per wave
 constexpr int T0 = (SPMAX + 15) / 16 / NWAVE;        // gW0 tiles per wave (3)
 constexpr int RPW = BB / NWG;                        // head rows per workgroup (2)
 constexpr int NSTAMP = 16;
+#ifndef CLU_GW_PRE
+#define CLU_GW_PRE 1                                 // weight-gradient tiles whose operands load under the P partial
+#endif
 #ifndef CLU_FWD_NG
 #define CLU_FWD_NG 4                                 // forward k-groups of 16 in flight per lane (16 — a whole
                                                      // K half — measured slower: 5.7 vs 4.9 µs per layer)
@@ -563,37 +566,51 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
                 }
             }
             __syncthreads();
-            // ---- layer 2 backward: P2 = g3h·W2[own, :] → Pa; gb2 ----
-            publish_partial(tid, rPa, cw, lds + L::W2, lds);
-            if (w == NWAVE - 1) colsum64<HC>(lds + L::gh, HCP, HC, 0.f, lds + L::gb2, tid);
-            CD_STAMP(9);
-            cluster_arrive(a.ctr);                                       // (its barrier: W2 reads done)
-            // gW2[j][k] = Σ_b g3h[b][j]·h2[b][k] with Adam fused, inside E's wait
-            // (one tile's loads at a time: all four tiles' in flight measured slower, 7.9 vs 6.7 µs)
-#pragma unroll 1
-            for (int t = 0; t < T12; ++t) {
-                GwTiles<1> gt;
+            // ---- layer 2 backward: P2 = g3h·W2[own, :] → Pa; gb2; then gW2[j][k] = Σ_b g3h[b][j]·h2[b][k]
+            // with Adam fused, inside E's wait — the first CLU_GW_PRE tiles' operands (h2, moments) in
+            // flight under P2, the rest one tile's loads at a time (all four tiles' at once measured
+            // slower: 7.9 vs 6.7 µs) ----
+            {
                 const long g0 = a.woff[2] + (long)c0 * H;
-                gt.load(tid, a, g0, H, H, [&](int b, int k) { return ld4_sc1(rX2, b * H + k); }, t);
-                gt.apply(tid, a, lds + L::gh, lds + L::W2, HP, g0, H, H, st, bc2, last, t);
+                auto ldx2 = [&](int b, int k) { return ld4_sc1(rX2, b * H + k); };
+                GwTiles<CLU_GW_PRE> pre;
+                pre.load(tid, a, g0, H, H, ldx2, 0);
+                publish_partial(tid, rPa, cw, lds + L::W2, lds);
+                if (w == NWAVE - 1) colsum64<HC>(lds + L::gh, HCP, HC, 0.f, lds + L::gb2, tid);
+                CD_STAMP(9);
+                cluster_arrive(a.ctr);                                   // (its barrier: W2 reads done)
+                pre.apply(tid, a, lds + L::gh, lds + L::W2, HP, g0, H, H, st, bc2, last, 0);
+#pragma unroll 1
+                for (int t = CLU_GW_PRE; t < T12; ++t) {
+                    GwTiles<1> gt;
+                    gt.load(tid, a, g0, H, H, ldx2, t);
+                    gt.apply(tid, a, lds + L::gh, lds + L::W2, HP, g0, H, H, st, bc2, last, t);
+                }
             }
             CD_STAMP(10);
             ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag);          // E: P2 published
             if (!ok) break;
             CD_STAMP(11);
-            // ---- layer 1 backward: g2h = Σ P2 ⊙ 1[h2 > 0]; P1 = g2h·W1[own, :] → Pb; gb1 ----
-            reduce_partials(tid, rPa, c0, lds + L::h2, lds);
-            __syncthreads();
-            publish_partial(tid, rPb, cw, lds + L::W1, lds);
-            if (w == NWAVE - 1) colsum64<HC>(lds + L::gh, HCP, HC, 0.f, lds + L::gb1, tid);
-            CD_STAMP(12);
-            cluster_arrive(a.ctr);
-#pragma unroll 1
-            for (int t = 0; t < T12; ++t) {
-                GwTiles<1> gt;
+            // ---- layer 1 backward: g2h = Σ P2 ⊙ 1[h2 > 0]; P1 = g2h·W1[own, :] → Pb; gb1; gW1 as gW2 (its
+            // first tiles' operands in flight under the reduction and P1) ----
+            {
                 const long g0 = a.woff[1] + (long)c0 * H;
-                gt.load(tid, a, g0, H, H, [&](int b, int k) { return ld4_sc1(rX1, x1o + b * H + k); }, t);
-                gt.apply(tid, a, lds + L::gh, lds + L::W1, HP, g0, H, H, st, bc2, last, t);
+                auto ldx1 = [&](int b, int k) { return ld4_sc1(rX1, x1o + b * H + k); };
+                GwTiles<CLU_GW_PRE> pre;
+                pre.load(tid, a, g0, H, H, ldx1, 0);
+                reduce_partials(tid, rPa, c0, lds + L::h2, lds);
+                __syncthreads();
+                publish_partial(tid, rPb, cw, lds + L::W1, lds);
+                if (w == NWAVE - 1) colsum64<HC>(lds + L::gh, HCP, HC, 0.f, lds + L::gb1, tid);
+                CD_STAMP(12);
+                cluster_arrive(a.ctr);
+                pre.apply(tid, a, lds + L::gh, lds + L::W1, HP, g0, H, H, st, bc2, last, 0);
+#pragma unroll 1
+                for (int t = CLU_GW_PRE; t < T12; ++t) {
+                    GwTiles<1> gt;
+                    gt.load(tid, a, g0, H, H, ldx1, t);
+                    gt.apply(tid, a, lds + L::gh, lds + L::W1, HP, g0, H, H, st, bc2, last, t);
+                }
             }
             CD_STAMP(13);
             ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag);          // F: P1 published
