@@ -9,7 +9,8 @@ import sys
 def row(name, gpus, path, note=""):
     if not os.path.exists(path):
         return f"| {name} | {gpus} | — | — | — | — | — | — | — |"
-    d = json.load(open(path))
+    lines = [ln for ln in open(path) if ln.startswith("{")]     # RCCL may print a banner first
+    d = json.loads(lines[-1])
     ms = d["ms_per_step"]
     rf = d.get("roofline", {})
     cb = d.get("cpu_baseline") or {}
