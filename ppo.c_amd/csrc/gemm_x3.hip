@@ -945,7 +945,8 @@ void phip_x3_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, 
     // C3's 256×256 gradient measured 23.5 -> 20.7 µs but sum each output over longer fp32 chains:
     // not adopted)
     const int kq = BK * kCfgX3[c].kg;                       // a split's k range: whole k-tiles per group
-    const int target = g_split_x3 > 0 ? g_split_x3 : 256 * kCfgX3[c].slots_per_cu;
+    static const int env_target = [] { const char* e = getenv("PPO_X3_SPLIT_TARGET"); return e ? atoi(e) : 0; }();
+    const int target = g_split_x3 > 0 ? g_split_x3 : env_target > 0 ? env_target : 256 * kCfgX3[c].slots_per_cu;
     int splits = (int)(target / tiles);
     const int max_splits = m / (8 * kq) > 0 ? m / (8 * kq) : 1;
     splits = std::max(1, std::min(splits, max_splits));
