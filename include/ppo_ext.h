@@ -146,6 +146,9 @@ int    ppo_gemm_f32_engine(int engine);
 /* bf16 mode's LDS-DMA GEMM kernel (forward / grad_x with bf16 operands, gemm16.hip): on = 1 / 0
  * sets, −1 queries; returns the previous setting (initially PPO_G16_DMA, else on) */
 int    ppo_gemm16_dma(int on);
+/* bf16 mode's LDS-DMA grad_W tile width: 128 (256 × 128 tiles, default) or 256 (256 × 256, for
+ * n % 256 = 0); other values query; returns the previous width */
+int    ppo_gemm16_tn_width(int bn);
 /* x3 engine tuning: force a tile configuration (−1 = automatic) and the grad_W split-K workgroup
  * target (0 = automatic, < 0 keeps); returns the number of configurations */
 int    ppo_gemm_x3_tune(int force_cfg, int splitk_target);

@@ -1473,9 +1473,12 @@ inline bool al16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 inline int epl(int t) { return t ? 8 : 4; }
 
 // grad_W on the LDS-DMA TN tile (bf16 g and x): l a multiple of 256, n of 128, the batch of 64;
-// PPO_G16_TN=0 keeps the register-staged kernel, PPO_G16_TN_BN=128|256 forces the tile width
+// PPO_G16_TN=0 keeps the register-staged kernel, PPO_G16_TN_BN=128|256 (or ppo_gemm16_tn_width)
+// sets the tile width — 256 × 128 by default: at C5 (1024-wide layers, 16384 rows) its 32 tiles × 8
+// splits beat 16 tiles of 256 × 256 × 16 splits in the update, 235.5 vs 244.0 ms
+// (profiles/r04_c5_gradw_tile_ab.txt): half the split-partial bytes for the slab reduce
 int g_tn_dma = [] { const char* e = getenv("PPO_G16_TN"); return e ? atoi(e) : 1; }();
-int g_tn_bn = [] { const char* e = getenv("PPO_G16_TN_BN"); return e ? atoi(e) : 0; }();
+int g_tn_bn = [] { const char* e = getenv("PPO_G16_TN_BN"); return e && (atoi(e) == 128 || atoi(e) == 256) ? atoi(e) : 128; }();
 // workgroup target of the DMA TN split-K grid (PPO_G16_TN_TARGET; default one per CU)
 int g_tn_target = [] { const char* e = getenv("PPO_G16_TN_TARGET"); return e && atoi(e) > 0 ? atoi(e) : 256; }();
 
@@ -1483,7 +1486,7 @@ bool launch_dma_tn(float* gW, float* gb, const void* g, const void* x, int m, in
     if (g_tn_dma == 0 || dma16_setting() == 0 || g_force16 >= 0) return false;
     if (l % 256 != 0 || n % 128 != 0 || m % 64 != 0 || !al16(g) || !al16(x) || !al16(gW)) return false;
     if ((long)m * l >= (1L << 31) || (long)m * n >= (1L << 31)) return false;
-    const int BN = g_tn_bn == 128 || g_tn_bn == 256 ? g_tn_bn : (n % 256 == 0 ? 256 : 128);
+    const int BN = g_tn_bn == 256 && n % 256 == 0 ? 256 : 128;
     if (n % BN != 0) return false;
     Args a{};
     a.A = g; a.lda = l; a.B = x; a.ldb = n; a.C = gW; a.ldc = n;
@@ -1675,6 +1678,12 @@ int ppo_g16_stamps(unsigned long long* out, int n) {
 int ppo_gemm16_dma(int on) {
     const int old = dma16_setting();
     if (on == 0 || on == 1) g_dma16 = on;
+    return old;
+}
+
+int ppo_gemm16_tn_width(int bn) {
+    const int old = g_tn_bn;
+    if (bn == 128 || bn == 256) g_tn_bn = bn;
     return old;
 }
 

@@ -108,6 +108,7 @@ _SIGS = {
     "ppo_bench_gemm16": (C.c_double, [C.c_int] * 7),
     "ppo_gemm_f32_engine": (C.c_int, [C.c_int]),
     "ppo_gemm16_dma": (C.c_int, [C.c_int]),
+    "ppo_gemm16_tn_width": (C.c_int, [C.c_int]),
     "ppo_gemm_x3_tune": (C.c_int, [C.c_int, C.c_int]),
     "ppo_bench_gemm_x3": (C.c_double, [C.c_int] * 7),
     "ppo_x3_stamps": (C.c_int, [C.POINTER(C.c_ulonglong), C.c_int]),

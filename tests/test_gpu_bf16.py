@@ -207,7 +207,7 @@ def test_bf16_dma_matches_register_staged(lib, sizes, m):
 def test_bf16_dma_tn_grad_w(lib, oracle, sizes, m):
     """grad_W on the LDS-DMA TN tile (gemm_bf16_dma_tn_kernel: both operands by hardware-transposed
     reads, split partials summed by the slab reduce, bias from the g image) — the automatic choice
-    for bf16 g and x with l % 256 = 0, n % 128 = 0 (256- and 128-wide tiles here) — against the bf16
+    for bf16 g and x with l % 256 = 0, n % 128 = 0 (256 × 128 tiles by default, 256 × 256 selectable) — against the bf16
     emulation (2e-3·max|ref|, the file's bar, up to 2048 rows) and against the register-staged kernel (DMA off): the
     same rounded products, summed in another order (1e-4·max|ref|)."""
     rng = np.random.default_rng(sum(sizes) + m)
@@ -222,16 +222,20 @@ def test_bf16_dma_tn_grad_w(lib, oracle, sizes, m):
     dx, dgo = dev(lib, x), dev(lib, gout)
     out = {}
     old = lib.ppo_gemm16_dma(-1)
+    old_w = lib.ppo_gemm16_tn_width(0)
     try:
         lib.ppo_gemm16_tune(-1)
-        for on in (1, 0):
+        for on, width in ((1, 128), (1, 256), (0, 128)):         # both DMA tile widths, then DMA off
             lib.ppo_gemm16_dma(on)
+            lib.ppo_gemm16_tn_width(width)
             lib.forward_propagation_cuda(nn, dx.ptr, m)
             lib.backward_propagation_cuda(nn, dgo.ptr, m)
-            out[on] = nn_grads_packed(lib, nn)
+            out[(on, width)] = nn_grads_packed(lib, nn)
     finally:
         lib.ppo_gemm16_dma(old)
+        lib.ppo_gemm16_tn_width(old_w)
         lib.free_neural_network(nn)
-    if m <= 2048:      # deeper / longer: hidden bf16 rounding flips compound against the emulation
-        close(out[1], g_emu, 2e-3, "grads (DMA TN) vs bf16 emulation")
-    close(out[1], out[0], 1e-4, "grads, DMA TN vs register-staged")
+    for width in (128, 256):
+        if m <= 2048:  # deeper / longer: hidden bf16 rounding flips compound against the emulation
+            close(out[(1, width)], g_emu, 2e-3, f"grads (DMA TN, {width}-wide) vs bf16 emulation")
+        close(out[(1, width)], out[(0, 128)], 1e-4, f"grads, DMA TN {width}-wide vs register-staged")
