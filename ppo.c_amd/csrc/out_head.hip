@@ -395,12 +395,14 @@ struct WideArgs {
     float eps, ent_coeff; float* grad_log_std; float* loss_accum;
 };
 
-// kernels.hip log_prob_row (policy.cu:67-74, double temporaries), on LDS rows
-__device__ __forceinline__ float log_prob_row_p(const float* mu, const float* log_std, const float* a, int A) {
+// kernels.hip log_prob_row (policy.cu:67-74, double temporaries), on LDS rows; es[j] = expf(log_std[j])
+// computed once per workgroup (the same value the per-element expf gave)
+__device__ __forceinline__ float log_prob_row_p(const float* mu, const float* log_std, const float* es, const float* a,
+                                                int A) {
     const float c = (float)(-0.5 * A * (double)logf((float)(2 * M_PI)));
     float lp = c;
     for (int j = 0; j < A; ++j) {
-        const float z = (a[j] - mu[j]) / expf(log_std[j]);
+        const float z = (a[j] - mu[j]) / es[j];
         lp = (float)((double)lp - ((double)log_std[j] + 0.5 * (double)(z * z)));
     }
     return lp;
@@ -410,15 +412,27 @@ template <int A, int NPT, int U, bool HEAD>
 __global__ __launch_bounds__(256) void out_bwd_wide_kernel(WideArgs p) {
     constexpr int N = 256 * NPT;
     extern __shared__ float gs[];                        // this workgroup's rows of g [rows][A] (+ μ, actions)
-    __shared__ float e2s[32], lss[32], cps[8][32], redl[4];
+    __shared__ float e2s[32], lss[32], ess[32], cps[8][32], redl[4];
     const int t = threadIdx.x, k0 = t * NPT;
     const int m = p.m;
     const int r0 = blockIdx.x * p.rows_per_wg;
     const int nr = min(m, r0 + p.rows_per_wg) - r0;
+    // the weights and the first U rows' x in flight before the head (they do not depend on it)
+    float Wr[A][NPT], acc[A][NPT], xpre[U][NPT];
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+        load_cols<NPT>(p.W + (long)a * N + k0, Wr[a]);
+#pragma unroll
+        for (int q = 0; q < NPT; ++q) acc[a][q] = 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        if (u < nr) load_cols<NPT>(p.x + (long)(r0 + u) * N + k0, xpre[u]);
     if constexpr (HEAD) {
         float* mus = gs + p.rows_per_wg * A;
         float* acts = mus + p.rows_per_wg * A;
         float* grs = acts + p.rows_per_wg * A;           // ∂L/∂lp per row
+        const float adv0 = t < nr ? p.adv[r0 + t] : 0.f, olp0 = t < nr ? p.old_lp[r0 + t] : 0.f;   // first row's
         for (int e = t; e < nr * A; e += 256) {
             mus[e] = p.mu[(long)r0 * A + e];
             acts[e] = p.action[(long)r0 * A + e];
@@ -426,13 +440,15 @@ __global__ __launch_bounds__(256) void out_bwd_wide_kernel(WideArgs p) {
         if (t < A) {
             lss[t] = p.log_std[t];
             e2s[t] = expf(-2 * p.log_std[t]);
+            ess[t] = expf(p.log_std[t]);
         }
         __syncthreads();
         float sv = 0.f;
         for (int row = t; row < nr; row += 256) {
             float glp;
-            const float lp = log_prob_row_p(mus + row * A, lss, acts + row * A, A);
-            sv += surrogate(p.adv[r0 + row], lp, p.old_lp[r0 + row], p.eps, m, &glp);
+            const float lp = log_prob_row_p(mus + row * A, lss, ess, acts + row * A, A);
+            const float ad = row == t ? adv0 : p.adv[r0 + row], ol = row == t ? olp0 : p.old_lp[r0 + row];
+            sv += surrogate(ad, lp, ol, p.eps, m, &glp);
             grs[row] = glp;
         }
         sv = ppo::wave_sum64(sv);
@@ -471,19 +487,19 @@ __global__ __launch_bounds__(256) void out_bwd_wide_kernel(WideArgs p) {
     } else {
         for (int e = t; e < nr * A; e += 256) gs[e] = p.g[(long)r0 * A + e];
     }
-    float Wr[A][NPT], acc[A][NPT];
-#pragma unroll
-    for (int a = 0; a < A; ++a) {
-        load_cols<NPT>(p.W + (long)a * N + k0, Wr[a]);
-#pragma unroll
-        for (int q = 0; q < NPT; ++q) acc[a][q] = 0.f;
-    }
     __syncthreads();
     for (int rb = 0; rb < nr; rb += U) {
         float xv[U][NPT];                                // U rows in flight
+        if (rb == 0) {
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (rb + u < nr) load_cols<NPT>(p.x + (long)(r0 + rb + u) * N + k0, xv[u]);
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int q = 0; q < NPT; ++q) xv[u][q] = xpre[u][q];
+        } else {
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (rb + u < nr) load_cols<NPT>(p.x + (long)(r0 + rb + u) * N + k0, xv[u]);
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int r = rb + u;
@@ -491,19 +507,22 @@ __global__ __launch_bounds__(256) void out_bwd_wide_kernel(WideArgs p) {
             float gv[A];
 #pragma unroll
             for (int a = 0; a < A; ++a) gv[a] = gs[r * A + a];   // uniform address: LDS broadcast
+            // fused multiply-adds (this file is built with -ffp-contract=off): the two 17-term products
+            // are GEMM-shaped sums, held to the GEMM tolerance; packed they are one v_pk_fma_f32 per
+            // term and column pair instead of a v_pk_mul + v_pk_add (the loop was VALU-bound)
             float o[NPT];
 #pragma unroll
             for (int q = 0; q < NPT; ++q) {
                 float sacc = 0.f;
 #pragma unroll
-                for (int a = 0; a < A; ++a) sacc += gv[a] * Wr[a][q];
+                for (int a = 0; a < A; ++a) sacc = __builtin_fmaf(gv[a], Wr[a][q], sacc);
                 o[q] = (!p.relu_in || xv[u][q] > 0.f) ? sacc : 0.f;
             }
             store_cols<NPT>(p.gx + (long)(r0 + r) * N + k0, o);
 #pragma unroll
             for (int a = 0; a < A; ++a)
 #pragma unroll
-                for (int q = 0; q < NPT; ++q) acc[a][q] += gv[a] * xv[u][q];
+                for (int q = 0; q < NPT; ++q) acc[a][q] = __builtin_fmaf(gv[a], xv[u][q], acc[a][q]);
         }
     }
     float* __restrict__ out = p.slab + (long)blockIdx.x * p.slab_stride;
@@ -520,11 +539,17 @@ __global__ __launch_bounds__(256) void out_bwd_wide_kernel(WideArgs p) {
 
 extern "C" {
 
+// workgroups of the one-pass wide backward (PPO_WIDE_NWG, default 512: ≥ 16 rows each)
+static int wide_nwg_cap() {
+    static const int cap = [] { const char* e = getenv("PPO_WIDE_NWG"); return e && atoi(e) >= 64 ? atoi(e) : 512; }();
+    return cap;
+}
+
 int phip_out_bwd_wide_ok(int m, int n, int A, int head) {
     if (A != 17 || (n != 512 && n != 256) || m <= 0 || getenv("PPO_NO_WIDE_BWD")) return 0;
     if (head && getenv("PPO_NO_WIDE_HEAD")) return 0;
     const int U = 8;
-    const int nwg = std::min(512, ppo_divup(m, 16));
+    const int nwg = std::min(wide_nwg_cap(), ppo_divup(m, 16));
     const long rows = (long)ppo_divup(ppo_divup(m, nwg), U) * U;
     return sizeof(float) * rows * (head ? 3 * A + 1 : A) <= 64 * 1024;
 }
@@ -535,7 +560,7 @@ static int out_bwd_wide_launch(WideArgs w, float* gW, float* gb, int n, int A, b
     if ((((uintptr_t)w.x | (uintptr_t)w.gx | (uintptr_t)w.W | (uintptr_t)gW) & 15u) != 0) return 0;
     ppo::ProfScope ps(PPO_K_GEMM, 4.0 * m * n * A, ppo::gemm_key(3, 1, m, n, A));
     constexpr int U = 8;
-    int nwg = std::min(512, ppo_divup(m, 16));                // ≥ 16 rows per workgroup
+    int nwg = std::min(wide_nwg_cap(), ppo_divup(m, 16));     // ≥ 16 rows per workgroup
     const int rows = ppo_divup(ppo_divup(m, nwg), U) * U;
     nwg = ppo_divup(m, rows);
     w.rows_per_wg = rows;
