@@ -243,6 +243,20 @@ struct GwTiles {
     }
 };
 
+// Adam of the thread's small parameter (log σ with the entropy step sizes, ppo.cu:440-442): the b0
+// elements when b0 is set, the others otherwise
+__device__ __forceinline__ void small_adam(const DArgs& a, float* lds, int tid, int c0, int nsmall, float& sm, float& sv,
+                                           int step, float st, float bc2, bool b0) {
+    if (tid >= nsmall) return;
+    const Small s = small_elem(a, tid, c0);
+    if ((s.lds_p >= L::b0 && s.lds_p < L::b0 + HC) != b0) return;
+    float pv = lds[s.lds_p];
+    const float g = lds[s.lds_g];
+    if (s.kind == 1) adam_elem(pv, g, sm, sv, a.steps_ls[2 * step], a.b1, a.b2, a.steps_ls[2 * step + 1]);
+    else adam_elem(pv, g, sm, sv, st, a.b1, a.b2, bc2);
+    lds[s.lds_p] = pv;
+}
+
 // K-split epilogue: waves 4-7 hand their partial to waves 0-3 (tile w & 3) through LDS, then the
 // owners return the sum.  Every thread reaches the barrier.
 __device__ __forceinline__ f32x4 ksplit_sum(int tid, f32x4 acc, float* lds) {
@@ -612,6 +626,9 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
                     gt.apply(tid, a, lds + L::gh, lds + L::W1, HP, g0, H, H, st, bc2, last, t);
                 }
             }
+            // Adam of the small parameters whose gradients are complete (all but b0: W3's columns, b1,
+            // b2, the replicated b3 and log σ — none is read again this step)
+            small_adam(a, lds, tid, c0, nsmall, sm, sv, step, st, bc2, false);
             CD_STAMP(13);
             ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag);          // F: P1 published
             if (!ok) break;
@@ -629,15 +646,8 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
             }
             if (w == NWAVE - 1) colsum64<HC>(lds + L::gh, HCP, HC, 0.f, lds + L::gb0, tid);
             __syncthreads();
-            // ---- Adam of the small parameters (log σ with the entropy step sizes, ppo.cu:440-442) ----
-            if (tid < nsmall) {
-                const Small s = small_elem(a, tid, c0);
-                float pv = lds[s.lds_p];
-                const float g = lds[s.lds_g];
-                if (s.kind == 1) adam_elem(pv, g, sm, sv, a.steps_ls[2 * step], a.b1, a.b2, a.steps_ls[2 * step + 1]);
-                else adam_elem(pv, g, sm, sv, st, a.b1, a.b2, bc2);
-                lds[s.lds_p] = pv;
-            }
+            // ---- Adam of b0 (the rest of the small parameters stepped inside F's wait) ----
+            small_adam(a, lds, tid, c0, nsmall, sm, sv, step, st, bc2, true);
             __syncthreads();
             CD_STAMP(15);
         }
