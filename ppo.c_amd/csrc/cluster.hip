@@ -271,7 +271,7 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
             CL_STAMP(2);
             cluster_arrive(a.ctr);
             if (has_next) gather_rows<L>(a, lds, ep_n, kb_n, cur ^ 1);   // the next minibatch, part 1
-            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag);                     // A: every h1 column published
+            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag, cw);                     // A: every h1 column published
             if (!ok) break;
             CL_STAMP(3);
             // every other workgroup's h1 columns (sc1 loads): lane → column quad 4·lane, rows w + 8u,
@@ -324,7 +324,7 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
             CL_STAMP(5);
             cluster_arrive(a.ctr);
             if (has_next) gather_cols<L>(a, lds, cur ^ 1);               // the next minibatch, part 2
-            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag);                     // B: every y partial published
+            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag, cw);                     // B: every y partial published
             if (!ok) break;
             CL_STAMP(6);
             // ---- y = Σ_c partials (fixed order) + b2; the head, identically in every workgroup ----
@@ -433,7 +433,7 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
                 }
             }
             CL_STAMP(8);
-            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag);                     // C: every g1 partial published
+            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag, cw);                     // C: every g1 partial published
             if (!ok) break;
             CL_STAMP(9);
             // ---- g1[b][j] = Σ_c partials (fixed order) ⊙ 1[h1 > 0], own units ----
@@ -626,7 +626,7 @@ int phip_cluster_update(const PhipTinyNet* net, const PhipTinyPhase* ph) {
         phip_free(ws.X1);
         phip_free(ws.ctr);
         ws.X1 = (float*)phip_malloc(sizeof(float) * (size_t)need);
-        ws.ctr = (unsigned*)phip_malloc(64);
+        ws.ctr = (unsigned*)phip_malloc(128 * CLU_REPL);      // counter replicas
         ws.cap = need;
     }
     ws.Y = ws.X1 + (long)BB * 256;
@@ -655,7 +655,7 @@ int phip_cluster_update(const PhipTinyNet* net, const PhipTinyPhase* ph) {
         PPO_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
         attr = true;
     }
-    PPO_CHECK(hipMemsetAsync(ws.ctr, 0, 64, ppo::stream()));
+    PPO_CHECK(hipMemsetAsync(ws.ctr, 0, 128 * CLU_REPL, ppo::stream()));
     ppo::ProfScope ps(PPO_K_OTHER, 0.0);
     hipLaunchKernelGGL(kfn, dim3(NWG * a.active_stride), dim3(TPB), bytes, ppo::stream(), a);
     PPO_LAUNCH_CHECK();

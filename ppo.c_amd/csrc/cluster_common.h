@@ -8,6 +8,9 @@
 #include <cmath>
 #include <cstdint>
 
+#ifndef CLU_REPL
+#define CLU_REPL 8                                   // barrier counter replicas (128-B lines; ≤ 64)
+#endif
 #ifndef CLU_SLEEP
 #define CLU_SLEEP 4                                  // s_sleep between barrier polls (× 64 clocks): 32 pollers
                                                      // at 1 slowed every barrier (C4 value step 75 → 69 µs at 4)
@@ -57,19 +60,25 @@ __device__ __forceinline__ float ld4_sc1(__amdgpu_buffer_rsrc_t r, int off_float
     return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off_floats * 4, 0, 16));
 }
 
+// The arrival counter is kept in CLU_REPL replicas, each on a 128-B line of its own (ctr + 32·r;
+// MI355X_MICROARCH.md's replicated-counter row): every workgroup adds to every replica with ONE wave
+// instruction (lanes 0 … CLU_REPL−1, one replica each) and polls only its own replica, so the polls of
+// 32 workgroups spread over CLU_REPL lines instead of loading the line every arrival lands on.
 // Arrival: the workgroup's published stores are complete (every wave drained, then a workgroup
-// barrier), then ONE lane adds to the monotonic counter.  Work that publishes nothing may run between
-// cluster_arrive and cluster_wait (it overlaps the other workgroups' arrival skew).
+// barrier), then the adds.  Work that publishes nothing may run between cluster_arrive and
+// cluster_wait (it overlaps the other workgroups' arrival skew).
 __device__ __forceinline__ void cluster_arrive(unsigned* ctr) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x < CLU_REPL)
+        __hip_atomic_fetch_add(ctr + 32 * threadIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // Wait until all `nwg` workgroups have arrived for barrier number `n` (counting from 0 within the
-// launch): the arriving lane polls (sc1 loads + s_sleep), the other waves wait at the workgroup
-// barrier it then joins.  Returns false on timeout (error word set), uniformly for the workgroup.
-__device__ __forceinline__ bool cluster_wait(unsigned* ctr, unsigned* err, unsigned n, int nwg, int* flag_lds) {
+// launch; `rank` = the workgroup's index in the phase, picks its replica): the arriving lane polls
+// (sc1 loads + s_sleep), the other waves wait at the workgroup barrier it then joins.  Returns false on timeout (error word set), uniformly for the workgroup.
+__device__ __forceinline__ bool cluster_wait(unsigned* ctr, unsigned* err, unsigned n, int nwg, int* flag_lds, int rank) {
     if (threadIdx.x == 0) {
+        ctr += 32 * (rank % CLU_REPL);                           // this workgroup's replica
         const unsigned target = (unsigned)nwg * (n + 1);
         unsigned spins = 0;
         int ok = 1;

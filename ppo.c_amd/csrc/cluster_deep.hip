@@ -389,7 +389,7 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
             CD_STAMP(1);
             cluster_arrive(a.ctr);
             if (has_next) gather_rows(a, lds, ep_n, kb_n, cur ^ 1);     // the next minibatch, part 1
-            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag);          // A: h1 published
+            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag, cw);          // A: h1 published
             if (!ok) break;
             CD_STAMP(2);
             // ---- layer 1: h2ᵀ[j][b] = Σ_k W1[j][k]·h1[b][k] ----
@@ -421,7 +421,7 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
                 pf = *reinterpret_cast<const f32x4*>(a.state + (long)rn[RPW * cw + r] * S + k);
             }
 #endif
-            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag);          // B: h2 published
+            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag, cw);          // B: h2 published
             if (!ok) break;
             CD_STAMP(4);
             // ---- layer 2: h3ᵀ[j][b] = Σ_k W2[j][k]·h2[b][k] (own columns stay in LDS) ----
@@ -452,7 +452,7 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
             }
             CD_STAMP(5);
             cluster_arrive(a.ctr);
-            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag);          // C: y partials published
+            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag, cw);          // C: y partials published
             if (!ok) break;
             CD_STAMP(6);
             if (!a.policy) {
@@ -535,7 +535,7 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
             }
             CD_STAMP(7);
             cluster_arrive(a.ctr);
-            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag);          // D: every row's ∂L/∂y published
+            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag, cw);          // D: every row's ∂L/∂y published
             if (!ok) break;
             CD_STAMP(8);
             // ---- ∂L/∂y of all rows → LDS ----
@@ -602,7 +602,7 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
                 }
             }
             CD_STAMP(10);
-            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag);          // E: P2 published
+            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag, cw);          // E: P2 published
             if (!ok) break;
             CD_STAMP(11);
             // ---- layer 1 backward: g2h = Σ P2 ⊙ 1[h2 > 0]; P1 = g2h·W1[own, :] → Pb; gb1; gW1 as gW2 (its
@@ -630,7 +630,7 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
             // b2, the replicated b3 and log σ — none is read again this step)
             small_adam(a, lds, tid, c0, nsmall, sm, sv, step, st, bc2, false);
             CD_STAMP(13);
-            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag);          // F: P1 published
+            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag, cw);          // F: P1 published
             if (!ok) break;
             CD_STAMP(14);
             // ---- layer 0 backward: g1h = Σ P1 ⊙ 1[h1 > 0]; gW0[j][s] = Σ_b g1h[b][j]·x[b][s] with Adam
@@ -731,7 +731,7 @@ int phip_cluster_deep_update(const PhipTinyNet* net, const PhipTinyPhase* ph) {
         phip_free(ws.base);
         phip_free(ws.ctr);
         ws.base = (float*)phip_malloc(sizeof(float) * (size_t)need);
-        ws.ctr = (unsigned*)phip_malloc(64);
+        ws.ctr = (unsigned*)phip_malloc(128 * CLU_REPL);      // counter replicas
         ws.cap = need;
     }
     a.X1 = ws.base; a.X2 = a.X1 + nX1; a.Y = a.X2 + nX2; a.G3 = a.Y + nY; a.Pa = a.G3 + nG3; a.Pb = a.Pa + nP;
@@ -755,7 +755,7 @@ int phip_cluster_deep_update(const PhipTinyNet* net, const PhipTinyPhase* ph) {
                                       (int)bytes));
         attr = true;
     }
-    PPO_CHECK(hipMemsetAsync(ws.ctr, 0, 64, ppo::stream()));
+    PPO_CHECK(hipMemsetAsync(ws.ctr, 0, 128 * CLU_REPL, ppo::stream()));
     ppo::ProfScope ps(PPO_K_OTHER, 0.0);
     hipLaunchKernelGGL(cluster_deep_kernel, dim3(NWG * a.active_stride), dim3(TPB), bytes, ppo::stream(), a);
     PPO_LAUNCH_CHECK();
