@@ -156,6 +156,10 @@ __device__ __forceinline__ void store_cols(float* __restrict__ p, const float (&
 // T: storage of x, W and gx — float (fp32 mode) or unsigned short (bf16 mode: x and gx bf16, W the
 // bf16 parameter shadow, and the head gradient rounded to bf16 before its products, as the separate
 // bf16 GEMMs round the fp32 operand they stage)
+#ifndef OUTHEAD_PF
+#define OUTHEAD_PF 4                                 // rows in flight per wave (one wave per row)
+#endif
+
 template <int NPL, int A, int HEAD, int WPR, typename T>
 __global__ __launch_bounds__(NTH) void out_head_kernel(OutArgs p) {
     constexpr bool B16 = sizeof(T) == 2;
@@ -198,7 +202,7 @@ __global__ __launch_bounds__(NTH) void out_head_kernel(OutArgs p) {
     // rows in flight per wave: PF rows' slices are loaded ahead (a ring of registers, statically
     // indexed by unrolling PF rows per iteration); one wave per row keeps up to PF·NPL loads in
     // flight instead of one row's (3.5 -> ≈5 TB/s of x read + gx written at C4's value head)
-    constexpr int PF = WPR == 1 ? 4 : 1;
+    constexpr int PF = WPR == 1 ? OUTHEAD_PF : 1;
     float xr[PF][NPL];
     const int first = blockIdx.x * SLOTS + slot;
 #pragma unroll
