@@ -1,5 +1,6 @@
 """Shared helpers for the parity tests (numpy <-> libppo device memory, tolerances)."""
 import ctypes as C
+import os
 
 import numpy as np
 
@@ -25,6 +26,10 @@ def gemm_tol(ref, K):
 def assert_gemm_close(got, ref, K, what=""):
     err = float(np.abs(got - ref).max(initial=0.0))
     tol = gemm_tol(ref, K)
+    report = os.environ.get("PPO_TOL_REPORT")          # optional: log the margin (err / tol) per check
+    if report:
+        with open(report, "a") as f:
+            f.write(f"{err / tol:.5f}\t{err:.3e}\t{tol:.3e}\tK={K}\t{os.environ.get('PYTEST_CURRENT_TEST', '').split(' ')[0]}\t{what}\n")
     assert err <= tol, f"{what}: max |err| {err:.3g} > tol {tol:.3g} (K={K})"
 
 
