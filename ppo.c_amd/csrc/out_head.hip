@@ -35,14 +35,16 @@ constexpr int NW = NTH / 64;
 
 __device__ __forceinline__ float wsum(float v) { return ppo::wave_sum64(v); }   // DPP rows + scalar reads
 
-// policy.cu:67-74 with the reference's double temporaries (kernels.hip log_prob_row)
+// policy.cu:67-74 with the reference's double temporaries (kernels.hip log_prob_row); es[j] =
+// expf(log_std[j]), computed once per wave (the same value the per-element expf gave)
 template <int A>
-__device__ __forceinline__ float log_prob_row(const float (&mu)[A], const float* log_std, const float (&a)[A]) {
+__device__ __forceinline__ float log_prob_row(const float (&mu)[A], const float (&log_std)[A], const float (&es)[A],
+                                              const float (&a)[A]) {
     const float c = (float)(-0.5 * A * (double)logf((float)(2 * M_PI)));
     float lp = c;
 #pragma unroll
     for (int j = 0; j < A; ++j) {
-        const float z = (a[j] - mu[j]) / expf(log_std[j]);
+        const float z = (a[j] - mu[j]) / es[j];
         lp = (float)((double)lp - ((double)log_std[j] + 0.5 * (double)(z * z)));
     }
     return lp;
@@ -178,7 +180,7 @@ __global__ __launch_bounds__(NTH) void out_head_kernel(OutArgs p) {
     const int c0 = (part * 64 + lane) * NPL;
     const int m = p.m;
 
-    float Wr[A][NPL], bias[A], e2[A], ls[A];
+    float Wr[A][NPL], bias[A], e2[A], ls[A], es[A];
 #pragma unroll
     for (int a = 0; a < A; ++a) {
         load_cols<NPL>(Wp + (long)a * N + c0, Wr[a]);
@@ -186,6 +188,7 @@ __global__ __launch_bounds__(NTH) void out_head_kernel(OutArgs p) {
         if (HEAD == 1) {
             ls[a] = p.log_std[a];
             e2[a] = expf(-2 * ls[a]);
+            es[a] = expf(ls[a]);
         }
     }
     float gWacc[A][NPL], gbacc[A], glsacc[A];
@@ -256,7 +259,7 @@ __global__ __launch_bounds__(NTH) void out_head_kernel(OutArgs p) {
             float act[A];
 #pragma unroll
             for (int a = 0; a < A; ++a) act[a] = p.action[(long)row * A + a];
-            const float lp = log_prob_row<A>(yv, p.log_std, act);
+            const float lp = log_prob_row<A>(yv, ls, es, act);
             float glp;
             const float sv = surrogate(p.adv[row], lp, p.old_lp[row], p.eps, m, &glp);
             if (owner) loss += sv;
