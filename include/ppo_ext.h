@@ -73,14 +73,17 @@ enum { PPO_SHUFFLE_HOST_RAND = 0,   /* reference shuffle_buffer: swap(i, rand()%
  * epochs of ⌊limit/batch_size⌋ minibatches (reference ppo.cu:487-533).  With
  * ppo_comm_world() > 1 every rank holds its own env shard; gradients are
  * all-reduced (mean over the global minibatch) and advantage statistics are
- * global.  Asynchronous: nothing is read back to the host. */
+ * global.  Asynchronous: nothing is read back to the host — except after the multi-workgroup
+ * B = 64 phases (cluster.hip), which synchronise once at the end to check their grid barriers
+ * (a timeout ends the process with status 1: the phase's state is incomplete). */
 void ppo_update(void* ppo, float gamma, int batch_size, int n_epochs_policy, int n_epochs_value,
                 int shuffle_mode, unsigned long long seed);
 
 /* stats accumulated by ppo_update since the last reset (synchronises):
  * out[0]=Σ value loss, out[1]=#value steps, out[2]=Σ policy loss,
  * out[3]=#policy steps, out[4]=entropy, out[5]=advantage mean, out[6]=advantage std,
- * out[7]=rows of the last GAE's own V(next_state) forward (those not reused from V(state[t+1])) */
+ * out[7]=rows of the last GAE's own V(next_state) forward (those not reused from V(state[t+1])),
+ * out[8]=minibatch steps replayed from captured graphs (PPO_GRAPH=1) */
 void ppo_read_stats(void* ppo, double* out, int n);
 void ppo_reset_stats(void* ppo);
 /* the last GAE's state (compute_gae_cuda / ppo_update; synchronises): welford (may be NULL) ← the

@@ -86,6 +86,13 @@ def load(use_openblas=False):
     return _lib
 
 
+def blas_mode(mode):
+    """Chaos-floor perturbation of the oracle's products (ref_cpu.c): 0 = the oracle proper,
+    1 = split-K halves, 2 = double-precision products rounded once to fp32.  Needs OpenBLAS."""
+    if load(use_openblas=True).ref_blas_mode(int(mode)) != 0:
+        raise RuntimeError(f"oracle: blas mode {mode} unavailable")
+
+
 def _p(a):
     return a.ctypes.data_as(C.c_void_p)
 

@@ -34,8 +34,18 @@ typedef void (*sgemm64_fn)(int order, int ta, int tb, int64_t M, int64_t N, int6
                            const float* A, int64_t lda, const float* B, int64_t ldb, float beta,
                            float* C, int64_t ldc);
 typedef void (*setthreads_fn)(int);
+typedef void (*dgemm64_fn)(int order, int ta, int tb, int64_t M, int64_t N, int64_t K, double alpha,
+                           const double* A, int64_t lda, const double* B, int64_t ldb, double beta,
+                           double* C, int64_t ldc);
 static sgemm64_fn g_sgemm = NULL;
+static dgemm64_fn g_dgemm = NULL;
 static setthreads_fn g_setthreads = NULL;
+/* Perturbation modes (chaos-floor measurements only, tools/chaos_floor.py; 0 = the oracle proper):
+ * 1 = every product's K range summed as two halves (sgemm over the first half, then β = 1 over the
+ *     second: a split-K re-association of the same fp32 arithmetic);
+ * 2 = products evaluated in double (dgemm on widened operands), rounded once to fp32 on store
+ *     (β·C added in double) — the most accurate fp32-output BLAS. */
+static int g_blas_mode = 0;
 
 int ref_blas_load(const char* path) {
     if (!path || !*path) return 0;
@@ -43,6 +53,8 @@ int ref_blas_load(const char* path) {
     if (!h) return 0;
     g_sgemm = (sgemm64_fn)dlsym(h, "scipy_cblas_sgemm64_");
     if (!g_sgemm) g_sgemm = (sgemm64_fn)dlsym(h, "cblas_sgemm64_");
+    g_dgemm = (dgemm64_fn)dlsym(h, "scipy_cblas_dgemm64_");
+    if (!g_dgemm) g_dgemm = (dgemm64_fn)dlsym(h, "cblas_dgemm64_");
     g_setthreads = (setthreads_fn)dlsym(h, "scipy_openblas_set_num_threads64_");
     if (!g_setthreads) g_setthreads = (setthreads_fn)dlsym(h, "openblas_set_num_threads");
     if (g_setthreads) g_setthreads(1);       /* main.c:18 pins OpenBLAS to one thread */
@@ -50,10 +62,53 @@ int ref_blas_load(const char* path) {
 }
 void ref_blas_threads(int n) { if (g_setthreads) g_setthreads(n); }
 const char* ref_blas_name(void) { return g_sgemm ? "openblas(scipy_openblas64_)" : "blocked-C"; }
+int ref_blas_mode(int mode) {
+    if (mode == 2 && !g_dgemm) return -1;
+    if (mode < 0 || mode > 2 || (mode && !g_sgemm)) return -1;
+    g_blas_mode = mode;
+    return 0;
+}
+
+static void sgemm_rm(int ta, int tb, int M, int N, int K, float alpha, const float* A, int lda,
+                     const float* B, int ldb, float beta, float* C, int ldc);
+
+/* mode 2: C = round_f32(α·op(A)·op(B) + β·C) with every operation in double */
+static void sgemm_rm_wide(int ta, int tb, int M, int N, int K, float alpha, const float* A, int lda,
+                          const float* B, int ldb, float beta, float* C, int ldc) {
+    const long ar = ta ? K : M, ac = ta ? M : K, br = tb ? N : K, bc = tb ? K : N;
+    double* a = (double*)malloc(sizeof(double) * (size_t)(ar * ac));
+    double* b = (double*)malloc(sizeof(double) * (size_t)(br * bc));
+    double* c = (double*)malloc(sizeof(double) * (size_t)M * N);
+    for (long i = 0; i < ar; i++)
+        for (long j = 0; j < ac; j++) a[i * ac + j] = A[i * lda + j];
+    for (long i = 0; i < br; i++)
+        for (long j = 0; j < bc; j++) b[i * bc + j] = B[i * ldb + j];
+    for (long i = 0; i < M; i++)
+        for (long j = 0; j < N; j++) c[i * N + j] = (double)C[i * ldc + j];
+    g_dgemm(101, ta ? 112 : 111, tb ? 112 : 111, M, N, K, alpha, a, ac, b, bc, beta, c, N);
+    for (long i = 0; i < M; i++)
+        for (long j = 0; j < N; j++) C[i * ldc + j] = (float)c[i * N + j];
+    free(a);
+    free(b);
+    free(c);
+}
 
 /* Row-major C[M,N] = alpha·op(A)·op(B) + beta·C, op = transpose if t != 0. */
 static void sgemm_rm(int ta, int tb, int M, int N, int K, float alpha, const float* A, int lda,
                      const float* B, int ldb, float beta, float* C, int ldc) {
+    if (g_blas_mode == 2) {
+        sgemm_rm_wide(ta, tb, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc);
+        return;
+    }
+    if (g_blas_mode == 1 && K >= 2) {
+        /* the first ⌊K/2⌋ terms, then the rest accumulated on top */
+        const int k1 = K / 2;
+        const float* A2 = ta ? A + (size_t)k1 * lda : A + k1;
+        const float* B2 = tb ? B + k1 : B + (size_t)k1 * ldb;
+        g_sgemm(101, ta ? 112 : 111, tb ? 112 : 111, M, N, k1, alpha, A, lda, B, ldb, beta, C, ldc);
+        g_sgemm(101, ta ? 112 : 111, tb ? 112 : 111, M, N, K - k1, alpha, A2, lda, B2, ldb, 1.0f, C, ldc);
+        return;
+    }
     if (g_sgemm) {   /* CblasRowMajor=101, NoTrans=111, Trans=112 */
         g_sgemm(101, ta ? 112 : 111, tb ? 112 : 111, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc);
         return;

@@ -30,6 +30,9 @@ extern "C" {
 int  ref_blas_load(const char* openblas_path);   /* 1 if OpenBLAS sgemm was bound */
 void ref_blas_threads(int n);
 const char* ref_blas_name(void);
+/* chaos-floor perturbations of the product arithmetic (0 = oracle proper, 1 = split-K halves,
+ * 2 = double-precision products rounded once); -1 if unavailable */
+int  ref_blas_mode(int mode);
 
 /* ---- ops (mat_mul.cu:39-80, activation_function.cu:5-15, loss.cu:5-23) ---- */
 void  ref_mat_mul(float* out, const float* x, const float* W, const float* b, int m, int n, int l);

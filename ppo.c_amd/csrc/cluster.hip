@@ -49,6 +49,7 @@ struct ClArgs {
     float *X1, *Y, *G1;                       // published: h1 [64][H], y partials [NWG][64][OMAX], g1 partials [NWG][64][H]
     unsigned* ctr;                            // barrier arrivals (zeroed before the launch)
     unsigned* err;                            // host-visible error word (0 = fine)
+    unsigned long long timeout;               // barrier wait bound (realtime ticks)
     int active_stride;                        // workgroup b works iff b % active_stride == 0 (same-XCD bias)
     unsigned long long* stamps;               // diagnostics (PPO_CLUSTER_STAMPS): wall clock per phase,
                                               // workgroup 0, steps 0..63, 12 slots
@@ -271,7 +272,7 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
             CL_STAMP(2);
             cluster_arrive(a.ctr);
             if (has_next) gather_rows<L>(a, lds, ep_n, kb_n, cur ^ 1);   // the next minibatch, part 1
-            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag, cw);                     // A: every h1 column published
+            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag, cw, a.timeout);                     // A: every h1 column published
             if (!ok) break;
             CL_STAMP(3);
             // every other workgroup's h1 columns (sc1 loads): lane → column quad 4·lane, rows w + 8u,
@@ -324,7 +325,7 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
             CL_STAMP(5);
             cluster_arrive(a.ctr);
             if (has_next) gather_cols<L>(a, lds, cur ^ 1);               // the next minibatch, part 2
-            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag, cw);                     // B: every y partial published
+            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag, cw, a.timeout);                     // B: every y partial published
             if (!ok) break;
             CL_STAMP(6);
             // ---- y = Σ_c partials (fixed order) + b2; the head, identically in every workgroup ----
@@ -433,7 +434,7 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
                 }
             }
             CL_STAMP(8);
-            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag, cw);                     // C: every g1 partial published
+            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag, cw, a.timeout);                     // C: every g1 partial published
             if (!ok) break;
             CL_STAMP(9);
             // ---- g1[b][j] = Σ_c partials (fixed order) ⊙ 1[h1 > 0], own units ----
@@ -554,20 +555,89 @@ struct Ws { float *X1, *Y, *G1; unsigned* ctr; long cap; };
 Ws g_ws[2] = {};
 unsigned* g_err = nullptr;            // host-mapped error word
 
+// PPO_CLUSTER_STAMPS: one stamp buffer per stream (the phases run concurrently) and the report that
+// phip_cluster_report prints once the phases have joined
+struct StampSlot {
+    unsigned long long* buf = nullptr;
+    int nstamp = 0, policy = 0, total_steps = 0, pending = 0;
+    const char* kind = nullptr;
+    const char* const* names = nullptr;
+};
+StampSlot g_stamps[2];
+
 }  // namespace
+
+namespace clu {
+
+unsigned long long host_timeout_ticks() {
+    if (const char* e = getenv("PPO_CLUSTER_TEST_TIMEOUT"))
+        if (*e && *e != '0') return 0ULL;
+    int dev = 0, khz = 0;
+    PPO_CHECK(hipGetDevice(&dev));
+    PPO_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+    return (unsigned long long)(khz > 0 ? khz : 100000) * 2000ULL;          // 2 s
+}
+
+bool host_grid_fits(const void* kfn, size_t lds, int grid) {
+    int dev = 0, cus = 0, per_cu = 0;
+    PPO_CHECK(hipGetDevice(&dev));
+    PPO_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, TPB, lds) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return (long)per_cu * cus >= 2L * grid;
+}
+
+unsigned long long* host_stamps(int nstamp, const char* kind, const char* const* names, int policy, int total_steps) {
+    StampSlot& s = g_stamps[phip_side_active() ? 1 : 0];
+    if (!s.buf) s.buf = (unsigned long long*)phip_malloc(sizeof(unsigned long long) * 64 * 32);
+    s.nstamp = nstamp; s.kind = kind; s.names = names; s.policy = policy; s.total_steps = total_steps;
+    s.pending = total_steps >= 64;
+    return s.buf;
+}
+
+}  // namespace clu
 
 extern "C" {
 
-// host-visible error of the last cluster phases (nonzero: a barrier timed out — a workgroup of the
-// launch was never resident or a device fault stopped one); cleared by reading
+// diagnostics: the per-sub-phase means (µs, steps 1 … 62) of the phases launched since the last call
+// (PPO_CLUSTER_STAMPS); synchronises, so the host calls it after the phases have joined
+void phip_cluster_report(void) {
+    int dev = 0, khz = 0;
+    for (int i = 0; i < 2; ++i) {
+        StampSlot& s = g_stamps[i];
+        if (!s.pending) continue;
+        s.pending = 0;
+        if (!khz) {
+            PPO_CHECK(hipGetDevice(&dev));
+            PPO_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+        }
+        const double mhz = khz > 0 ? khz / 1000.0 : 100.0;
+        unsigned long long h[64 * 32];
+        phip_d2h(h, s.buf, sizeof(unsigned long long) * 64 * (size_t)s.nstamp);
+        double acc[32] = {0}, tot = 0;
+        for (int st = 1; st < 63; ++st)
+            for (int k = 0; k < s.nstamp; ++k) {
+                const unsigned long long t0 = h[st * s.nstamp + k];
+                const unsigned long long t1 = k < s.nstamp - 1 ? h[st * s.nstamp + k + 1] : h[(st + 1) * s.nstamp];
+                acc[k] += (double)(t1 - t0) / mhz;
+            }
+        fprintf(stderr, "%s %s step (us):", s.kind, s.policy ? "policy" : "value");
+        for (int k = 0; k < s.nstamp; ++k) { fprintf(stderr, " %s %.2f", s.names[k], acc[k] / 62); tot += acc[k] / 62; }
+        fprintf(stderr, " | total %.2f\n", tot);
+    }
+}
+
+// Host-visible error of the cluster phases (nonzero: a barrier timed out — a workgroup of the launch was
+// never resident, or a device fault stopped one).  The word stays set: the update that saw it ends the
+// process (ppo_update dies), since the phase left its parameters and Adam state half-written.
 int phip_cluster_error(void) {
     if (!g_err) return 0;
     const unsigned e = __atomic_load_n(g_err, __ATOMIC_ACQUIRE);
     return e != 0u;
 }
 
-// Returns 0 when launched (or, with n_epochs = 0, when the shape fits); −1 when the network or the
-// minibatch does not fit this path (the caller falls back).
 // the device pointer of the host-mapped error word shared by the cluster kernels (allocated on first
 // use); NULL, with the error recorded, when an earlier launch left it set
 unsigned* phip_cluster_err_dev(void) {
@@ -595,6 +665,22 @@ int phip_cluster_update(const PhipTinyNet* net, const PhipTinyPhase* ph) {
     constexpr int HC = 16, NWG = 256 / HC;                         // 16 workgroups of 16 hidden units
     constexpr size_t bytes = sizeof(float) * (size_t)Lay<256, HC>::TOTAL;
     static_assert(bytes <= 160 * 1024, "cluster: LDS");
+    // one workgroup in every `active_stride`: blocks b and b + 8 are dealt to one XCD (observed,
+    // MI355X_MICROARCH.md § Workgroup dispatch), so stride 8 puts the phase on one XCD, 4 on two, 1 on
+    // all eight; correctness never depends on it (PPO_CLUSTER_STRIDE overrides; 1, 2, 4 or 8)
+    // (value phase — the longer — on one XCD, policy on two: 16 + 8 ≤ 32 CUs wherever they land)
+    int stride = ph->policy ? 4 : 8;
+    if (const char* st = getenv("PPO_CLUSTER_STRIDE")) {
+        const int v = atoi(st);
+        if (v == 1 || v == 2 || v == 4 || v == 8) stride = v;
+    }
+    auto kfn = cluster_phase_kernel<256, HC>;
+    static bool attr = false;
+    if (!attr) {
+        PPO_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+        attr = true;
+    }
+    if (!host_grid_fits((const void*)kfn, bytes, NWG * stride)) return -1;   // not co-resident: multi-launch
     if (ph->n_epochs <= 0 || ph->num_batches <= 0) return 0;     // fit check only
     ClArgs a{};
     a.S = S; a.O = O; a.policy = ph->policy;
@@ -634,50 +720,15 @@ int phip_cluster_update(const PhipTinyNet* net, const PhipTinyPhase* ph) {
     unsigned* d_err = phip_cluster_err_dev();
     if (!d_err) return -2;
     a.X1 = ws.X1; a.Y = ws.Y; a.G1 = ws.G1; a.ctr = ws.ctr; a.err = d_err;
-    // one workgroup in every `active_stride`: blocks b and b + 8 are dealt to one XCD (observed,
-    // MI355X_MICROARCH.md § Workgroup dispatch), so stride 8 puts the phase on one XCD, 4 on two, 1 on
-    // all eight; correctness never depends on it (PPO_CLUSTER_STRIDE overrides; 1, 2, 4 or 8)
-    // (value phase — the longer — on one XCD, policy on two: 16 + 8 ≤ 32 CUs wherever they land)
-    a.active_stride = ph->policy ? 4 : 8;
-    if (const char* st = getenv("PPO_CLUSTER_STRIDE")) {
-        const int v = atoi(st);
-        if (v == 1 || v == 2 || v == 4 || v == 8) a.active_stride = v;
-    }
-    static unsigned long long* stamps = nullptr;
-    const bool want_stamps = getenv("PPO_CLUSTER_STAMPS") != nullptr;
-    if (want_stamps) {
-        if (!stamps) stamps = (unsigned long long*)phip_malloc(sizeof(unsigned long long) * 64 * 12);
-        a.stamps = stamps;
-    }
-    auto kfn = cluster_phase_kernel<256, HC>;
-    static bool attr = false;
-    if (!attr) {
-        PPO_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
-        attr = true;
-    }
+    a.timeout = host_timeout_ticks();
+    a.active_stride = stride;
+    static const char* names[12] = {"gather", "L0", "barrier A", "h1 load", "L1+Y", "barrier B", "head+bwd",
+                                    "G1+gW1 adam", "barrier C", "g1+gW0", "adam", "step->next"};
+    if (getenv("PPO_CLUSTER_STAMPS")) a.stamps = host_stamps(12, "cluster", names, ph->policy, a.total_steps);
     PPO_CHECK(hipMemsetAsync(ws.ctr, 0, 128 * CLU_REPL, ppo::stream()));
     ppo::ProfScope ps(PPO_K_OTHER, 0.0);
     hipLaunchKernelGGL(kfn, dim3(NWG * a.active_stride), dim3(TPB), bytes, ppo::stream(), a);
     PPO_LAUNCH_CHECK();
-    if (want_stamps && a.total_steps >= 64) {               // diagnostics: mean µs per sub-phase, steps 1..63
-        unsigned long long h[64 * 12];
-        phip_d2h(h, stamps, sizeof(h));
-        int dev = 0, khz = 0;
-        PPO_CHECK(hipGetDevice(&dev));
-        PPO_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
-        const double mhz = khz > 0 ? khz / 1000.0 : 100.0;
-        static const char* names[12] = {"gather", "L0", "barrier A", "h1 load", "L1+Y", "barrier B", "head+bwd",
-                                        "G1+gW1 adam", "barrier C", "g1+gW0", "adam", "step->next"};
-        double acc[12] = {0};
-        for (int st = 1; st < 63; ++st)
-            for (int k = 0; k < 12; ++k) {
-                const unsigned long long t0 = h[st * 12 + k], t1 = k < 11 ? h[st * 12 + k + 1] : h[(st + 1) * 12];
-                acc[k] += (double)(t1 - t0) / mhz;
-            }
-        fprintf(stderr, "cluster %s step (us):", ph->policy ? "policy" : "value");
-        for (int k = 0; k < 12; ++k) fprintf(stderr, " %s %.2f", names[k], acc[k] / 62);
-        fprintf(stderr, "\n");
-    }
     return 0;
 }
 

@@ -75,20 +75,26 @@ __device__ __forceinline__ void cluster_arrive(unsigned* ctr) {
 }
 // Wait until all `nwg` workgroups have arrived for barrier number `n` (counting from 0 within the
 // launch; `rank` = the workgroup's index in the phase, picks its replica): the arriving lane polls
-// (sc1 loads + s_sleep), the other waves wait at the workgroup barrier it then joins.  Returns false on timeout (error word set), uniformly for the workgroup.
-__device__ __forceinline__ bool cluster_wait(unsigned* ctr, unsigned* err, unsigned n, int nwg, int* flag_lds, int rank) {
+// (sc1 loads + s_sleep), the other waves wait at the workgroup barrier it then joins.  The wait is
+// bounded in wall-clock time (`timeout` ticks of the constant 100 MHz realtime counter, from the first
+// unsuccessful poll) and ends early when another workgroup has already set the error word.  Returns
+// false on timeout (error word set), uniformly for the workgroup.
+__device__ __forceinline__ bool cluster_wait(unsigned* ctr, unsigned* err, unsigned n, int nwg, int* flag_lds, int rank,
+                                             unsigned long long timeout) {
     if (threadIdx.x == 0) {
         ctr += 32 * (rank % CLU_REPL);                           // this workgroup's replica
         const unsigned target = (unsigned)nwg * (n + 1);
-        unsigned spins = 0;
         int ok = 1;
-        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-            __builtin_amdgcn_s_sleep(CLU_SLEEP);
-            if (++spins > (1u << 22) ||
-                __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
-                __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                ok = 0;
-                break;
+        if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            const unsigned long long t0 = wall_clock64();
+            while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+                __builtin_amdgcn_s_sleep(CLU_SLEEP);
+                if (wall_clock64() - t0 > timeout ||
+                    __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
+                    __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    ok = 0;
+                    break;
+                }
             }
         }
         *flag_lds = ok;
@@ -176,5 +182,17 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
     const float denom = (float)((double)sqrtf(v / bc2) + 1e-8);
     p -= step * m / denom;
 }
+
+// ---- host side, shared by both phase kernels (defined in cluster.hip) ----
+// Barrier wait bound in realtime ticks: 2 s (PPO_CLUSTER_TEST_TIMEOUT=1, a test hook, makes it 0 so
+// the first barrier that is not already complete times out and the error path runs).
+unsigned long long host_timeout_ticks();
+// Co-residency guard: the phase spins at grid barriers, so every workgroup of the launch — and of the
+// other phase running beside it on the side stream — must be resident at once.  True when
+// `2 × grid` blocks of `kfn` with `lds` bytes fit the device's CUs at its occupancy.
+bool host_grid_fits(const void* kfn, size_t lds, int grid);
+// Per-stream diagnostics (PPO_CLUSTER_STAMPS): the stamp buffer of the calling stream, and a pending
+// report printed by phip_cluster_report() after the phases joined (no mid-phase synchronisation).
+unsigned long long* host_stamps(int nstamp, const char* kind, const char* const* names, int policy, int total_steps);
 
 }  // namespace clu

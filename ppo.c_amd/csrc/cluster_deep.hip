@@ -65,6 +65,7 @@ struct DArgs {
     float *X1, *X2, *Y, *G3, *Pa, *Pb;               // hand-offs (X1 [2][64][H], X2 [64][H], Y [NWG][64][OP],
                                                      // G3 [64][GP], Pa / Pb [NWG][64][H])
     unsigned *ctr, *err;
+    unsigned long long timeout;                      // barrier wait bound (realtime ticks)
     int active_stride;
     unsigned long long* stamps;                      // PPO_CLUSTER_STAMPS: workgroup 0, steps 0..63
 };
@@ -399,7 +400,7 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
             CD_STAMP(1);
             cluster_arrive(a.ctr);
             if (has_next) gather_rows(a, lds, ep_n, kb_n, cur ^ 1);     // the next minibatch, part 1
-            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag, cw);          // A: h1 published
+            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag, cw, a.timeout);          // A: h1 published
             if (!ok) break;
             CD_STAMP(2);
             // ---- layer 1: h2ᵀ[j][b] = Σ_k W1[j][k]·h1[b][k] ----
@@ -431,7 +432,7 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
                 pf = *reinterpret_cast<const f32x4*>(a.state + (long)rn[RPW * cw + r] * S + k);
             }
 #endif
-            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag, cw);          // B: h2 published
+            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag, cw, a.timeout);          // B: h2 published
             if (!ok) break;
             CD_STAMP(4);
             // ---- layer 2: h3ᵀ[j][b] = Σ_k W2[j][k]·h2[b][k] (own columns stay in LDS) ----
@@ -462,7 +463,7 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
             }
             CD_STAMP(5);
             cluster_arrive(a.ctr);
-            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag, cw);          // C: y partials published
+            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag, cw, a.timeout);          // C: y partials published
             if (!ok) break;
             CD_STAMP(6);
             if (!a.policy) {
@@ -545,7 +546,7 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
             }
             CD_STAMP(7);
             cluster_arrive(a.ctr);
-            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag, cw);          // D: every row's ∂L/∂y published
+            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag, cw, a.timeout);          // D: every row's ∂L/∂y published
             if (!ok) break;
             CD_STAMP(8);
             // ---- ∂L/∂y of all rows → LDS ----
@@ -612,7 +613,7 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
                 }
             }
             CD_STAMP(10);
-            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag, cw);          // E: P2 published
+            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag, cw, a.timeout);          // E: P2 published
             if (!ok) break;
             CD_STAMP(11);
             // ---- layer 1 backward: g2h = Σ P2 ⊙ 1[h2 > 0]; P1 = g2h·W1[own, :] → Pb; gb1; gW1 as gW2 (its
@@ -640,7 +641,7 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
             // b2, the replicated b3 and log σ — none is read again this step)
             small_adam(a, lds, tid, c0, nsmall, sm, sv, step, st, bc2, false);
             CD_STAMP(13);
-            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag, cw);          // F: P1 published
+            ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag, cw, a.timeout);          // F: P1 published
             if (!ok) break;
             CD_STAMP(14);
             // ---- layer 0 backward: g1h = Σ P1 ⊙ 1[h1 > 0]; gW0[j][s] = Σ_b g1h[b][j]·x[b][s] with Adam
@@ -711,6 +712,20 @@ int phip_cluster_deep_update(const PhipTinyNet* net, const PhipTinyPhase* ph) {
     if (ph->policy && (!net->log_std || !net->m_ls)) return -1;
     constexpr size_t bytes = sizeof(float) * (size_t)L::TOTAL;
     static_assert(bytes <= 160 * 1024, "cluster_deep: LDS");
+    // one workgroup in every `active_stride` (cluster.hip): 2 spreads each phase over four XCDs, so the
+    // value and policy phases (64 workgroups, one per CU) fit wherever they land
+    int stride = 2;
+    if (const char* st = getenv("PPO_CLUSTER_STRIDE")) {
+        const int v = atoi(st);
+        if (v == 1 || v == 2 || v == 4 || v == 8) stride = v;
+    }
+    static bool attr = false;
+    if (!attr) {
+        PPO_CHECK(hipFuncSetAttribute((const void*)cluster_deep_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      (int)bytes));
+        attr = true;
+    }
+    if (!host_grid_fits((const void*)cluster_deep_kernel, bytes, NWG * stride)) return -1;   // multi-launch
     if (ph->n_epochs <= 0 || ph->num_batches <= 0) return 0;     // fit check only
     unsigned* d_err = phip_cluster_err_dev();
     if (!d_err) return -2;
@@ -749,50 +764,16 @@ int phip_cluster_deep_update(const PhipTinyNet* net, const PhipTinyPhase* ph) {
     }
     a.X1 = ws.base; a.X2 = a.X1 + nX1; a.Y = a.X2 + nX2; a.G3 = a.Y + nY; a.Pa = a.G3 + nG3; a.Pb = a.Pa + nP;
     a.ctr = ws.ctr; a.err = d_err;
-    // one workgroup in every `active_stride` (cluster.hip): 2 spreads each phase over four XCDs, so the
-    // value and policy phases (64 workgroups, one per CU) fit wherever they land
-    a.active_stride = 2;
-    if (const char* st = getenv("PPO_CLUSTER_STRIDE")) {
-        const int v = atoi(st);
-        if (v == 1 || v == 2 || v == 4 || v == 8) a.active_stride = v;
-    }
-    static unsigned long long* stamps = nullptr;
-    const bool want_stamps = getenv("PPO_CLUSTER_STAMPS") != nullptr;
-    if (want_stamps) {
-        if (!stamps) stamps = (unsigned long long*)phip_malloc(sizeof(unsigned long long) * 64 * NSTAMP);
-        a.stamps = stamps;
-    }
-    static bool attr = false;
-    if (!attr) {
-        PPO_CHECK(hipFuncSetAttribute((const void*)cluster_deep_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      (int)bytes));
-        attr = true;
-    }
+    a.timeout = host_timeout_ticks();
+    a.active_stride = stride;
+    static const char* names[NSTAMP] = {"L0", "bar A", "L1", "bar B", "L2+Y", "bar C", "head", "bar D",
+                                        "g3+P2", "gW2 adam", "bar E", "g2+P1", "gW1 adam", "bar F",
+                                        "g1 reduce", "gW0 adam", "gb0+b0", "step->next"};
+    if (getenv("PPO_CLUSTER_STAMPS")) a.stamps = host_stamps(NSTAMP, "cluster_deep", names, ph->policy, a.total_steps);
     PPO_CHECK(hipMemsetAsync(ws.ctr, 0, 128 * CLU_REPL, ppo::stream()));
     ppo::ProfScope ps(PPO_K_OTHER, 0.0);
     hipLaunchKernelGGL(cluster_deep_kernel, dim3(NWG * a.active_stride), dim3(TPB), bytes, ppo::stream(), a);
     PPO_LAUNCH_CHECK();
-    if (want_stamps && a.total_steps >= 64) {               // diagnostics: mean µs per sub-phase, steps 1..62
-        unsigned long long h[64 * NSTAMP];
-        phip_d2h(h, stamps, sizeof(h));
-        int dev = 0, khz = 0;
-        PPO_CHECK(hipGetDevice(&dev));
-        PPO_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
-        const double mhz = khz > 0 ? khz / 1000.0 : 100.0;
-        static const char* names[NSTAMP] = {"L0", "bar A", "L1", "bar B", "L2+Y", "bar C", "head", "bar D",
-                                            "g3+P2", "gW2 adam", "bar E", "g2+P1", "gW1 adam", "bar F",
-                                            "g1 reduce", "gW0 adam", "gb0+b0", "step->next"};
-        double acc[NSTAMP] = {0};
-        for (int s = 1; s < 63; ++s)
-            for (int k = 0; k < NSTAMP; ++k) {
-                const unsigned long long t0 = h[s * NSTAMP + k], t1 = k < NSTAMP - 1 ? h[s * NSTAMP + k + 1] : h[(s + 1) * NSTAMP];
-                acc[k] += (double)(t1 - t0) / mhz;
-            }
-        fprintf(stderr, "cluster_deep %s step (us):", ph->policy ? "policy" : "value");
-        double tot = 0;
-        for (int k = 0; k < NSTAMP; ++k) { fprintf(stderr, " %s %.2f", names[k], acc[k] / 62); tot += acc[k] / 62; }
-        fprintf(stderr, " | total %.2f\n", tot);
-    }
     return 0;
 }
 

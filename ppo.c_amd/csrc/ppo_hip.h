@@ -33,6 +33,7 @@ void  phip_side_use(int on);
 int   phip_side_active(void);   /* 1 while launches go to the side stream */
 void  phip_side_join(void);
 void  phip_record_error(const char* msg);
+void  phip_drain(void);                 /* synchronise both streams, ignoring errors (before a fatal exit) */
 
 /* ---------------- dense layers (gemm.hip) ---------------- */
 /* y[m,l] = x[m,n]·W[l,n]ᵀ + b[l], optional ReLU (mat_mul.cu:132-163 + K1/K5 fused) */
@@ -121,6 +122,7 @@ int phip_tiny_update(const PhipTinyNet* net, const PhipTinyPhase* ph);
  * workgroups (cluster.hip; net->wt unused); −1 when it does not fit, −2 after an earlier timeout */
 int phip_cluster_update(const PhipTinyNet* net, const PhipTinyPhase* ph);
 int phip_cluster_error(void);          /* nonzero: a cluster barrier timed out */
+void phip_cluster_report(void);        /* PPO_CLUSTER_STAMPS: print the joined phases' sub-phase means */
 /* S → 512 → 512 → 512 → O (S ≤ 380, S % 4 = 0, O ≤ 20) at B = 64 on 32 cooperating workgroups
  * (cluster_deep.hip); phip_cluster_update dispatches 4-layer networks here */
 int phip_cluster_deep_update(const PhipTinyNet* net, const PhipTinyPhase* ph);
@@ -237,6 +239,7 @@ int  phip_graph_begin(void);                 /* capture the current stream's lau
 void* phip_graph_end(void);                  /* → instantiated executable graph (NULL on failure) */
 void phip_graph_launch(void* exec);          /* replay on the current stream */
 void phip_graph_destroy(void* exec);
+const char* phip_graph_error(void);         /* why the last capture failed (warning text) */
 int  phip_capturing(void);                   /* 1 while a capture is open (profiling scopes stay out) */
 
 void phip_adam_flat_w16(float* p, float* g, float* m, float* v, long n, float lr, float beta1, float beta2,

@@ -12,6 +12,7 @@
 #include <cstring>
 #include <mutex>
 #include <vector>
+#include <unistd.h>
 
 namespace ppo {
 
@@ -30,7 +31,8 @@ void fail(const char* msg, const char* file, int line) {
     // drain work already queued so the process never dies with kernels in flight
     if (g_stream) (void)hipStreamSynchronize(g_stream);
     if (g_side) (void)hipStreamSynchronize(g_side);
-    abort();
+    fflush(stdout);
+    _exit(1);                              // the reference's checks exit(1) (cuda_helper.h:4-16)
 }
 
 void check(hipError_t e, const char* what, const char* file, int line) {
@@ -173,22 +175,50 @@ void phip_prof_end(int slot) {
 
 void phip_init(void) { ensure_device(); }
 
+// why the last capture failed (graph replay is an opt-in speed feature: its failure is a warning with
+// this text, not a recorded library error)
+static char g_graph_err[256] = "";
+const char* phip_graph_error(void) { return g_graph_err; }
+
+static void graph_fail(const char* what, hipError_t e) {
+    snprintf(g_graph_err, sizeof(g_graph_err), "%s: %s", what, hipGetErrorString(e));
+    (void)hipGetLastError();
+}
+
 int phip_graph_begin(void) {
-    if (g_capturing) return -1;
-    if (hipStreamBeginCapture(stream(), hipStreamCaptureModeRelaxed) != hipSuccess) return -1;
+    if (g_capturing) {
+        snprintf(g_graph_err, sizeof(g_graph_err), "hipStreamBeginCapture: a capture is already open");
+        return -1;
+    }
+    const hipError_t e = hipStreamBeginCapture(stream(), hipStreamCaptureModeRelaxed);
+    if (e != hipSuccess) {
+        graph_fail("hipStreamBeginCapture", e);
+        return -1;
+    }
     g_capturing = 1;
     return 0;
 }
 
 void* phip_graph_end(void) {
-    if (!g_capturing) return nullptr;
+    if (!g_capturing) {
+        snprintf(g_graph_err, sizeof(g_graph_err), "hipStreamEndCapture: no capture open");
+        return nullptr;
+    }
     hipGraph_t graph = nullptr;
     g_capturing = 0;
-    if (hipStreamEndCapture(stream(), &graph) != hipSuccess || !graph) return nullptr;
+    hipError_t e = hipStreamEndCapture(stream(), &graph);
+    if (e != hipSuccess || !graph) {
+        graph_fail("hipStreamEndCapture", e != hipSuccess ? e : hipErrorInvalidValue);
+        return nullptr;
+    }
     hipGraphExec_t exec = nullptr;
-    const hipError_t e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+    e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
     (void)hipGraphDestroy(graph);
-    return e == hipSuccess ? (void*)exec : nullptr;
+    if (e != hipSuccess) {
+        graph_fail("hipGraphInstantiate", e);
+        return nullptr;
+    }
+    return (void*)exec;
 }
 
 void phip_graph_launch(void* exec) { PPO_CHECK(hipGraphLaunch((hipGraphExec_t)exec, stream())); }
@@ -256,6 +286,11 @@ void phip_side_join(void) {
     ensure_device();
     PPO_CHECK(hipEventRecord(g_join_ev, g_side));
     PPO_CHECK(hipStreamWaitEvent(g_stream, g_join_ev, 0));
+}
+
+void phip_drain(void) {                   // before a fatal exit: let queued kernels finish, ignore errors
+    if (g_stream) (void)hipStreamSynchronize(g_stream);
+    if (g_side) (void)hipStreamSynchronize(g_side);
 }
 
 void phip_record_error(const char* msg) {

@@ -1,11 +1,17 @@
 /* common.c — host helpers: allocation, fatal errors, HBM staging slots. */
 #include "internal.h"
 
+#include <unistd.h>
+
+/* fatal errors end the process with status 1, as the reference's checks do (cuda_helper.h:4-16,
+ * exit(1)); _exit skips atexit teardown of a HIP runtime that may be in a bad state */
 void die(const char* msg) {
     phip_record_error(msg);
     fprintf(stderr, "libppo: FATAL: %s\n", msg);
     fflush(stderr);
-    abort();
+    phip_drain();                          /* never leave the process with kernels in flight */
+    fflush(stdout);
+    _exit(1);
 }
 
 void* xmalloc(size_t n) {

@@ -35,6 +35,7 @@ typedef struct {
     unsigned long long ro_step;   /* rollout step counter (Philox stream offset) */
     float* stats;                 /* [0] Σ value loss, [1] Σ policy loss */
     long n_v, n_p;
+    long n_graph;                 /* minibatch steps replayed from captured graphs (PPO_GRAPH=1) */
     uint64_t key;                 /* device-shuffle epoch key */
     unsigned long long seed;
     int seeded;
@@ -498,6 +499,16 @@ static int ppo_update_tiny(PPO* ppo, PPODev* d, int B, int n_epochs_policy, int 
         d->n_p += cap_p;
     }
     if (concurrent) phip_side_join();
+    if (cluster) {
+        /* a barrier timeout leaves the phase's parameters and Adam state half-written (the workgroups
+         * leave without their write-back): detect it before this update returns, so no caller reads,
+         * checkpoints or continues from that state */
+        phip_sync();
+        if (phip_cluster_error())
+            die("ppo_update: a multi-workgroup phase (cluster.hip) timed out at a grid barrier; "
+                "the update's parameters and Adam state are incomplete");
+        phip_cluster_report();
+    }
     return 0;
 }
 
@@ -709,7 +720,7 @@ static void capture_steps(StepCtx* c, int ph) {
     if (!gk || (K > 1 && !g1)) {
         /* an opt-in speed feature must not end a training run: warn, drop the graphs, replay nothing */
         fprintf(stderr, "libppo: warning: graph capture of the %s steps failed (%s); running them eagerly\n",
-                ph ? "policy" : "value", ppo_last_error());
+                ph ? "policy" : "value", phip_graph_error());
         phip_graph_destroy(gk);
         phip_graph_destroy(g1);
         ppo->adam_V->time_step = t_v;
@@ -808,6 +819,7 @@ static void ppo_update_body(PPO* ppo, float gamma, int batch_size, int n_epochs_
             if (c.gv && iv >= 1 && iv + 1 < nv) {
                 if (nv - 1 - iv >= c.Kv) { phip_graph_launch(c.gv); done = c.Kv; }
                 else phip_graph_launch(c.gv1 ? c.gv1 : c.gv);
+                d->n_graph += done;
             } else {
                 v_zero = value_step(&c, iv, v_zero, 0);
                 if (iv == 0 && graphs && nv >= 3) capture_steps(&c, 0);
@@ -820,6 +832,7 @@ static void ppo_update_body(PPO* ppo, float gamma, int batch_size, int n_epochs_
             if (c.gp && ip >= 1 && ip + 1 < np) {
                 if (np - 1 - ip >= c.Kp) { phip_graph_launch(c.gp); done = c.Kp; }
                 else phip_graph_launch(c.gp1 ? c.gp1 : c.gp);
+                d->n_graph += done;
             } else {
                 policy_step(&c, ip, &p_zero, &ls_zero, 0);
                 if (ip == 0 && graphs && np >= 3) capture_steps(&c, 1);
@@ -847,7 +860,7 @@ void ppo_reset_stats(void* vppo) {
     PPO* ppo = (PPO*)vppo;
     PPODev* d = dev_ws(ppo, 1);
     phip_memset(d->stats, 0, 4 * sizeof(float));
-    d->n_v = d->n_p = 0;
+    d->n_v = d->n_p = d->n_graph = 0;
 }
 
 void ppo_read_stats(void* vppo, double* out, int n) {
@@ -856,9 +869,9 @@ void ppo_read_stats(void* vppo, double* out, int n) {
     float s[4] = {0, 0, 0, 0}, a[2] = {0, 0};
     phip_d2h(s, d->stats, sizeof(s));
     if (g_adv_stats) phip_d2h(a, g_adv_stats, sizeof(a));
-    double v[8] = {s[0], (double)d->n_v, s[1], (double)d->n_p, compute_entropy_cuda(ppo->policy), a[0], a[1],
-                   (double)g_gae_own_rows};
-    for (int i = 0; i < n && i < 8; i++) out[i] = v[i];
+    double v[9] = {s[0], (double)d->n_v, s[1], (double)d->n_p, compute_entropy_cuda(ppo->policy), a[0], a[1],
+                   (double)g_gae_own_rows, (double)d->n_graph};
+    for (int i = 0; i < n && i < 9; i++) out[i] = v[i];
 }
 
 /* ppo.cu:451-558 */

@@ -143,6 +143,42 @@ def test_cluster_full_update_matches_multilaunch(lib, oracle, shuffle, sizes):
         assert abs(np.linalg.norm(da) / np.linalg.norm(db) - 1) < 0.1, k
 
 
+TIMEOUT_CHILD = r"""
+import ctypes as C, sys
+sys.path[:0] = [sys.argv[1]]
+import ppo_ffi
+lib = ppo_ffi.load()
+assert lib.ppo_set_device(0) == 0
+sizes = [int(s) for s in sys.argv[2].split(",")]
+acts = ["relu"] * (len(sizes) - 2) + ["none"]
+ppo = lib.create_ppo(ppo_ffi.c_strings(acts), ppo_ffi.c_ints(sizes), len(sizes), 4096, 3e-4, 3e-4, 0.95, 0.2,
+                     0.0, 1.0, True)
+lib.ppo_fill_synthetic(ppo, 16, 256, 17, 1.0 / 200)
+lib.ppo_update(ppo, 0.99, 64, 1, 1, 1, 9)
+print("UPDATE RETURNED", flush=True)
+"""
+
+
+@NETS
+def test_cluster_barrier_timeout_fails_loudly(lib, sizes, tmp_path):
+    """A grid-barrier timeout ends the update that launched the phases — not the next update, never
+    silently (the timed-out phase leaves its parameters and Adam state half-written).  The test hook
+    PPO_CLUSTER_TEST_TIMEOUT=1 bounds every barrier wait at 0 ticks: the first workgroup to wait at a
+    barrier that is not complete times out, sets the error word, and every other workgroup leaves at its
+    next wait.  Run in a child process (the update exits it with status 1)."""
+    import subprocess
+    import sys
+
+    env = dict(os.environ, PPO_CLUSTER_TEST_TIMEOUT="1")
+    env.pop("PPO_NO_CLUSTER", None)
+    pkg = os.path.dirname(ppo_ffi.__file__)
+    r = subprocess.run([sys.executable, "-c", TIMEOUT_CHILD, pkg, ",".join(map(str, sizes))], env=env,
+                       capture_output=True, text=True, timeout=120, cwd=tmp_path)
+    assert r.returncode == 1, (r.returncode, r.stdout[-500:], r.stderr[-1500:])
+    assert "timed out at a grid barrier" in r.stderr, r.stderr[-1500:]
+    assert "UPDATE RETURNED" not in r.stdout
+
+
 @pytest.mark.parametrize("phase", ["value", "policy"])
 def test_cluster_drift_like_multilaunch(lib, oracle, phase):
     """C4 networks, 512 value or policy steps (two epochs, the epoch boundary included): the cluster

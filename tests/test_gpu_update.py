@@ -295,10 +295,11 @@ def test_concurrent_value_policy_loops(lib, oracle, shuffle_mode, monkeypatch):
         lib.ppo_reset_stats(ppo)
         oracle.srand(41)
         lib.ppo_update(ppo, 0.99, B, 2, 3, shuffle_mode, 8)
-        st = (C.c_double * 7)()
-        lib.ppo_read_stats(ppo, st, 7)
+        st = (C.c_double * 9)()
+        lib.ppo_read_stats(ppo, st, 9)
         mu, ls = policy_state(lib, ppo)
-        out[mode] = dict(stats=np.array(st[:4]), v=nn_params_packed(lib, ppo.contents.V), mu=mu, ls=ls,
+        out[mode] = dict(stats=np.array(st[:4]), graph_steps=st[8], v=nn_params_packed(lib, ppo.contents.V),
+                         mu=mu, ls=ls,
                          next_rand=oracle.libc().rand(),
                          t=(ppo.contents.adam_V.contents.time_step, ppo.contents.adam_policy.contents.time_step,
                             ppo.contents.adam_entropy.contents.time_step))
@@ -518,6 +519,9 @@ def test_graph_replay_matches_eager(lib, oracle, shuffle_mode, monkeypatch):
     for this combination (fp32, fused value and A ≤ 6 policy heads: step_graphs_ok); the A = 17 wide head
     and the unfused path run eagerly even with PPO_GRAPH=1 (checked below)."""
     sizes, N, B = [17, 256, 256, 6], 4096, 64
+    # this shape at B = 64 would take the single-launch cluster phases (cluster.hip) before the graph
+    # path: force the multi-launch loop so graph replay is what runs (counted below)
+    monkeypatch.setenv("PPO_NO_CLUSTER", "1")
     out = {}
     for mode in ("eager", "graph"):
         if mode == "eager":
@@ -533,15 +537,18 @@ def test_graph_replay_matches_eager(lib, oracle, shuffle_mode, monkeypatch):
         oracle.srand(321)
         lib.ppo_update(ppo, 0.99, B, 1, 2, shuffle_mode, 77)
         lib.ppo_synchronize()
-        st = (C.c_double * 7)()
-        lib.ppo_read_stats(ppo, st, 7)
+        st = (C.c_double * 9)()
+        lib.ppo_read_stats(ppo, st, 9)
         mu, ls = policy_state(lib, ppo)
-        out[mode] = dict(stats=np.array(st[:4]), v=nn_params_packed(lib, ppo.contents.V), mu=mu, ls=ls,
+        out[mode] = dict(stats=np.array(st[:4]), graph_steps=st[8], v=nn_params_packed(lib, ppo.contents.V),
+                         mu=mu, ls=ls,
                          gv=nn_grads_packed(lib, ppo.contents.V), next_rand=oracle.libc().rand(),
                          t=(ppo.contents.adam_V.contents.time_step, ppo.contents.adam_policy.contents.time_step,
                             ppo.contents.adam_entropy.contents.time_step))
         lib.free_ppo(ppo)
     a, b = out["eager"], out["graph"]
+    # every step but each phase's first and last replayed from graphs (no silent eager fallback)
+    assert a["graph_steps"] == 0 and b["graph_steps"] == (2 * N // B - 2) + (N // B - 2), b["graph_steps"]
     assert a["t"] == b["t"] == (2 * N // B, N // B, N // B)
     assert a["next_rand"] == b["next_rand"]
     assert a["stats"][1] == b["stats"][1] and a["stats"][3] == b["stats"][3]
@@ -565,6 +572,7 @@ def test_graph_replay_declines_untested_paths(lib, oracle, case, monkeypatch):
     PPO_GRAPH (split-K off: no atomics anywhere but the log σ sums, which the policy bound covers)."""
     sizes = [376, 512, 512, 17] if case == "wide_head" else [17, 256, 256, 6]
     N, B = 2048, 64
+    monkeypatch.setenv("PPO_NO_CLUSTER", "1")     # the multi-launch loop, where step_graphs_ok decides
     lib.ppo_gemm_tune(-1, 1)
     out = {}
     try:
@@ -580,8 +588,12 @@ def test_graph_replay_declines_untested_paths(lib, oracle, case, monkeypatch):
             mu0, ls0 = policy_state(lib, ppo)
             buf = synthetic_buffer(oracle, sizes, mu0, ls0, N, seed=45, n_envs=4)
             load_buffer(lib, ppo, buf)
+            lib.ppo_reset_stats(ppo)
             lib.ppo_update(ppo, 0.99, B, 1, 1, 1, 78)
             lib.ppo_synchronize()
+            st = (C.c_double * 9)()
+            lib.ppo_read_stats(ppo, st, 9)
+            assert st[1] == st[3] == N // B and st[8] == 0, list(st)    # every step ran, none from a graph
             out[mode] = dict(v=nn_params_packed(lib, ppo.contents.V), mu=policy_state(lib, ppo)[0])
             lib.free_ppo(ppo)
     finally:
