@@ -1373,7 +1373,7 @@ int dma16_setting() {
 // the 16×16×32 MFMA form for bf16-output DMA products and for grad_W (PPO_G16_MF16=0: the 32×32×16 form
 // everywhere; 2: only the DMA products).  Measured at C5 16384×1024×1024: forward 41.5 -> 37.3 µs,
 // grad_x 42.1 -> 40.7 µs (C5 update 276.4 -> 271.9 ms); grad_W 82.6 -> 80.3 µs (273.7 -> 271.8 ms)
-int g_mf16 = [] { const char* e = getenv("PPO_G16_MF16"); return e ? atoi(e) : 1; }();
+constexpr int g_mf16 = 1;
 
 template <int OP, typename TC>
 bool launch_dma(Args a) {
@@ -1477,10 +1477,11 @@ inline int epl(int t) { return t ? 8 : 4; }
 // sets the tile width — 256 × 128 by default: at C5 (1024-wide layers, 16384 rows) its 32 tiles × 8
 // splits beat 16 tiles of 256 × 256 × 16 splits in the update, 235.5 vs 244.0 ms
 // (profiles/r04_c5_gradw_tile_ab.txt): half the split-partial bytes for the slab reduce
-int g_tn_dma = [] { const char* e = getenv("PPO_G16_TN"); return e ? atoi(e) : 1; }();
-int g_tn_bn = [] { const char* e = getenv("PPO_G16_TN_BN"); return e && (atoi(e) == 128 || atoi(e) == 256) ? atoi(e) : 128; }();
-// workgroup target of the DMA TN split-K grid (PPO_G16_TN_TARGET; default one per CU)
-int g_tn_target = [] { const char* e = getenv("PPO_G16_TN_TARGET"); return e && atoi(e) > 0 ? atoi(e) : 256; }();
+// (C5's hidden layers, 16384 × 1024 × 1024, are the only production bf16 × bf16 grad_W shape: the
+// 128 default is the measured choice there; other shapes take it too — they only occur in tests)
+constexpr int g_tn_dma = 1;
+int g_tn_bn = 128;                                 // ppo_gemm16_tn_width changes it (A/B)
+constexpr int g_tn_target = 256;                   // workgroup target of the DMA TN split-K grid: one per CU
 
 bool launch_dma_tn(float* gW, float* gb, const void* g, const void* x, int m, int n, int l, int zeroed) {
     if (g_tn_dma == 0 || dma16_setting() == 0 || g_force16 >= 0) return false;

@@ -785,8 +785,6 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
     }
 }
 
-int g_x3_atomics = -1;                   // PPO_X3_ATOMICS=1: split-K partials by f32 atomics (A/B)
-
 // tile configurations: 0 = 256×256 over 8 waves of 64×128 (forward, grad_x; one workgroup per CU),
 // 1 = 128×128 over 4 waves of 64×64, two workgroups per CU (narrow products), 2 = 128×128 over 8
 // waves of 32×64, 3 = 128×128 over two k-groups of 4 waves of 64×64, one workgroup per CU (grad_W),
@@ -843,10 +841,7 @@ void launch_cfg_x3(int c, const X3Args& a) {
 // 128×128 at two per CU (4 waves of 64×64) vs 28.0 µs on 8 waves of 32×64; 16384 rows 50.4 vs 47.9
 int pick_x3(int M, int N, int op) {
     if (g_force_x3 >= 0) return g_force_x3;
-    if (op == OP_TN) {
-        static const int tn = [] { const char* e = getenv("PPO_X3_TN_CFG"); return e ? atoi(e) : 3; }();
-        return tn == 5 ? 5 : 3;                              // PPO_X3_TN_CFG=5: 256×128 slabs (A/B)
-    }
+    if (op == OP_TN) return 3;         // (cfg 5, 256×128 with slabs, measured slower: r04_x3_tn_cfg5_update_ab.txt)
     auto tiles = [&](int c) { return (long)ppo_divup(M, kCfgX3[c].bm) * ppo_divup(N, kCfgX3[c].bn); };
     if (tiles(0) >= 256) return 0;
     if (tiles(2) >= 256) return 2;
@@ -945,8 +940,7 @@ void phip_x3_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, 
     // C3's 256×256 gradient measured 23.5 -> 20.7 µs but sum each output over longer fp32 chains:
     // not adopted)
     const int kq = BK * kCfgX3[c].kg;                       // a split's k range: whole k-tiles per group
-    static const int env_target = [] { const char* e = getenv("PPO_X3_SPLIT_TARGET"); return e ? atoi(e) : 0; }();
-    const int target = g_split_x3 > 0 ? g_split_x3 : env_target > 0 ? env_target : 256 * kCfgX3[c].slots_per_cu;
+    const int target = g_split_x3 > 0 ? g_split_x3 : 256 * kCfgX3[c].slots_per_cu;
     int splits = (int)(target / tiles);
     const int max_splits = m / (8 * kq) > 0 ? m / (8 * kq) : 1;
     splits = std::max(1, std::min(splits, max_splits));
@@ -956,10 +950,6 @@ void phip_x3_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, 
     a.A = g; a.lda = l; a.B = x; a.ldb = n; a.C = gW; a.ldc = n;
     a.M = l; a.N = n; a.K = m; a.kchunk = kchunk; a.splits = splits;
     a.gbias = gb;
-    if (g_x3_atomics < 0) {
-        const char* e = getenv("PPO_X3_ATOMICS");
-        g_x3_atomics = e && *e && *e != '0';
-    }
     // split-K partials: per-split slabs written with plain stores and summed by one reduce launch
     // (16 MB of f32 atomics at ≈1.3 TB/s set the grad_W time of small batches; the slab path moves
     // the same bytes at store / load rate, and its sum is deterministic); the bias gradient keeps
@@ -967,7 +957,7 @@ void phip_x3_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, 
     // (when each split is short: at C4's 32768 rows, 2048 per split, the atomics hide behind the
     // mainloop and the extra launch costs more — 326.1 vs 323.3 ms per update; at the G = 8 shard's
     // 4096 rows, 256 per split, the slabs win — 89.4 vs 93.4 ms, profiles/r03i_*)
-    const bool use_slab = splits > 1 && kchunk <= 1024 && !g_x3_atomics && al16(gW);
+    const bool use_slab = splits > 1 && kchunk <= 1024 && al16(gW);
     if (splits > 1 && !zeroed) {
         if (!use_slab) phip_memset(gW, 0, sizeof(float) * (size_t)l * n);
         if (gb) phip_memset(gb, 0, sizeof(float) * (size_t)l);

@@ -358,8 +358,9 @@ void launch(const OutArgs& a) {
             attr = true;
         }
     }
-    // about 16 rows per wave slot (PPO_OUTHEAD_RPS), at most 1024 workgroups
-    static const int rps = [] { const char* e = getenv("PPO_OUTHEAD_RPS"); return e && atoi(e) > 0 ? atoi(e) : 16; }();
+    // about 16 rows per wave slot (32 / 64 measured slower at C3, C4 and the shard: r04_outhead_rps_*),
+    // at most 1024 workgroups
+    constexpr int rps = 16;
     int grid = ppo_divup(a.m, SLOTS * rps);
     if (grid > 1024) grid = 1024;
     if (grid < 1) grid = 1;
@@ -546,15 +547,11 @@ __global__ __launch_bounds__(256) void out_bwd_wide_kernel(WideArgs p) {
 
 extern "C" {
 
-// workgroups of the one-pass wide backward (PPO_WIDE_NWG, default 512: ≥ 16 rows each)
-static int wide_nwg_cap() {
-    static const int cap = [] { const char* e = getenv("PPO_WIDE_NWG"); return e && atoi(e) >= 64 ? atoi(e) : 512; }();
-    return cap;
-}
+// workgroups of the one-pass wide backward (512: ≥ 16 rows each)
+static int wide_nwg_cap() { return 512; }
 
 int phip_out_bwd_wide_ok(int m, int n, int A, int head) {
     if (A != 17 || (n != 512 && n != 256) || m <= 0 || getenv("PPO_NO_WIDE_BWD")) return 0;
-    if (head && getenv("PPO_NO_WIDE_HEAD")) return 0;
     const int U = 8;
     const int nwg = std::min(wide_nwg_cap(), ppo_divup(m, 16));
     const long rows = (long)ppo_divup(ppo_divup(m, nwg), U) * U;

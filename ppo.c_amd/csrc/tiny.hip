@@ -924,7 +924,7 @@ int phip_tiny_update(const PhipTinyNet* net, const PhipTinyPhase* ph) {
     for (int l = 0; l < net->L; ++l) nw += (long)net->sizes[l] * net->sizes[l + 1];
     const long res = 4 * ((net->span + 3) & ~3L) + nw;
     const size_t kMaxLds = 160 * 1024 - 1024;              // the CU's 160 KiB less the static arrays
-    const bool resident = (size_t)(off + res) * sizeof(float) <= kMaxLds && !getenv("PPO_TINY_NO_RESIDENT");
+    const bool resident = (size_t)(off + res) * sizeof(float) <= kMaxLds;
     a.res_off = off;
     const size_t bytes = sizeof(float) * (size_t)(resident ? off + res : off);
     if (bytes > kMaxLds) return -1;

@@ -614,8 +614,7 @@ static void policy_step(StepCtx* c, long ip, int* p_zero, int* ls_zero, int tab)
     const int own = ap->flat && ap->weights[0] == mu->d_params && ap->grad_weights[0] == mu->d_grads;
     const int fused = mu->dtype == 1 && own;
     const int ls_own = ppo->adam_entropy->flat && ppo->adam_entropy->grad_weights[0] == pol->d_log_std_grad;
-    const int r = getenv("PPO_NO_ADAM_PAIR") ? -1
-                  : adam_update_pair_w16(ap, ppo->lr_policy, fused ? mu->d_w16 : NULL, mu->num_params,
+    const int r = adam_update_pair_w16(ap, ppo->lr_policy, fused ? mu->d_w16 : NULL, mu->num_params,
                                          ip + 1 < c->np && own, ppo->adam_entropy, ppo->lr_policy,
                                          ip + 1 < c->np && ls_own);
     if (r >= 0) {

@@ -18,9 +18,13 @@ def empty(lib, count, dtype=F32):
 
 
 def gemm_tol(ref, K):
-    """Stated fp32 GEMM tolerance: 1e-4·‖ref‖∞ + 1e-6 for K ≤ 1024, growing as √K beyond."""
+    """Stated fp32 GEMM tolerance: 7e-5·‖ref‖∞ + 1e-6 for K ≤ 1024, growing as √K beyond.
+
+    SURVEY §8c stated 1e-4; round 5 tightened it to the evidence (profiles/r04_gemm_tolerance_margins.tsv,
+    530 checks: the worst err/tol was 0.46 at 1e-4 — the C4 policy gradient, K = 32768 — every other
+    ≤ 0.10), so the worst check now sits at ≈ 0.65 of its bound and a 1.5× regression fails."""
     scale = max(1.0, (K / 1024.0) ** 0.5)
-    return 1e-4 * scale * float(np.abs(ref).max(initial=0.0)) + 1e-6
+    return 7e-5 * scale * float(np.abs(ref).max(initial=0.0)) + 1e-6
 
 
 def assert_gemm_close(got, ref, K, what=""):

@@ -10,18 +10,17 @@ import csv
 ap = argparse.ArgumentParser()
 ap.add_argument("trace")
 ap.add_argument("--top", type=int, default=30)
-ap.add_argument("--layers", type=int, default=4, help="value-network layers (C4: 4)")
 args = ap.parse_args()
 rows = sorted(csv.DictReader(open(args.trace)), key=lambda r: int(r["Start_Timestamp"]))
-# the last update starts with V(state)'s forward GEMMs (one per layer) before next_value_map_kernel;
-# with PPO_GAE_FULL=1 both full forwards precede gae_block_kernel
-maps = [i for i, r in enumerate(rows) if "next_value_map" in r["Kernel_Name"]]
-layers = args.layers
-if maps:
-    last = rows[max(0, maps[-1] - layers):]
-else:
-    starts = [i for i, r in enumerate(rows) if "gae_block" in r["Kernel_Name"]]
-    last = rows[max(0, starts[-1] - 2 * layers):]
+# the last update: everything after the previous update's last Adam launch — the GAE's V(state)
+# forward (every layer, m = N), its copies and fills, next_value_map_kernel, the own-row forward of
+# V(next_state), the scan, then the minibatch loops (round 5: the window used to start `layers` rows
+# before next_value_map_kernel and missed the first forward GEMMs and copies of the GAE)
+anchor = [i for i, r in enumerate(rows) if "next_value_map" in r["Kernel_Name"] or "gae_block" in r["Kernel_Name"]]
+j = anchor[-1] if anchor else len(rows) - 1
+while j > 0 and "adam" not in rows[j - 1]["Kernel_Name"]:
+    j -= 1
+last = rows[j:]
 t0, t1 = int(last[0]["Start_Timestamp"]), int(last[-1]["End_Timestamp"])
 busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in last)
 print(f"update span {(t1 - t0) / 1e6:.2f} ms, kernel busy {busy / 1e6:.2f} ms, {len(last)} launches")
