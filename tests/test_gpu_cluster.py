@@ -6,7 +6,8 @@ ppo_update takes it by itself for these shapes at B = 64 on one GPU; PPO_NO_CLUS
 multi-launch loop.  From identical state both must give the same minibatch gradients (stated fp32 GEMM
 tolerance), the same Adam step counts and host rand() consumption, and over many steps the same
 parameter motion; against the oracle, single steps element by element and the first 16 + 16 steps of
-an update (the bounds of test_short_update_elementwise).
+an update (the bounds of test_short_update_elementwise); over long runs, within the oracle's own
+chaos floor (its self-drift under a re-association of every product, measured live).
 """
 import ctypes as C
 import os
@@ -117,11 +118,55 @@ def test_cluster_first_steps_vs_oracle(lib, oracle, sizes):
     np.testing.assert_allclose(a["stats"][2], ref["sum_policy_loss"], rtol=1e-3, atol=1e-5)
 
 
+def oracle_motion(oracle, a, sizes, lim, n_pol, n_val, mode, ent=0.0):
+    """The oracle's update of run()'s buffer from run()'s initial state (Feistel order, seed 9), its
+    products re-associated per `mode` (oracle_ffi.blas_mode: 0 proper, 1 split-K halves, 2 double
+    products rounded once) — returns (value motion, policy motion).  16 OpenBLAS threads: measured
+    bit-identical to one thread (profiles/r05_oracle_chaos_floor.txt), only faster."""
+    lib = oracle.load(use_openblas=True)
+    oracle.blas_mode(mode)
+    lib.ref_blas_threads(16)
+    try:
+        ref = oracle.ppo_update(sizes, RELU(sizes), a["mu0"], a["ls0"], a["v0"], a["buf"], batch_size=64,
+                                n_epochs_policy=n_pol, n_epochs_value=n_val, shuffle_mode=1, seed=9,
+                                max_value_steps=lim[0], max_policy_steps=lim[1], ent_coeff=ent)
+    finally:
+        oracle.blas_mode(0)
+        lib.ref_blas_threads(1)
+    return ref["v"] - a["v0"], ref["mu"] - a["mu0"]
+
+
+def cos_ratio(d, dr):
+    d, dr = d.astype(np.float64), dr.astype(np.float64)
+    return float(d @ dr / (np.linalg.norm(d) * np.linalg.norm(dr))), float(np.linalg.norm(d) / np.linalg.norm(dr))
+
+
+# Long runs are chaotic: a ReLU mask or clip branch that flips at z ≈ 0 changes a gradient outright and
+# Adam normalises every element, so two valid fp32 evaluations of the same update decorrelate as they
+# go, at a rate that varies with the buffer and the perturbation (tools/chaos_floor.py: C4, 512 policy
+# steps, oracle self-drift cos 0.62 – 1.00 across seeds).  The bound is therefore relative to that floor,
+# measured live on the same buffer and initial state: the oracle against itself with every product
+# re-associated (split-K halves) and in double-precision products (profiles/r05_oracle_chaos_floor.txt,
+# r05_gpu_drift_vs_chaos_floor.txt — on this test's buffer at 512 policy steps: oracle self-drift cos
+# 0.62 / 0.63, multi-launch 0.60, cluster 0.78; at 64 steps 0.989 / 0.991 vs 0.989 / 0.9999).  A GPU path
+# may decorrelate from the oracle at most CHAOS_FACTOR times as much as the oracle does from itself,
+# plus CHAOS_SLACK (one sample of a chaotic process against two):
+# 1 − cos_gpu ≤ CHAOS_FACTOR · (1 − min cos_floor) + CHAOS_SLACK.  A defect outruns it already at 64 steps.
+CHAOS_FACTOR, CHAOS_SLACK = 2.0, 0.02
+
+
+def assert_within_chaos_floor(cos_gpu, floor_cos, what):
+    bound = 1 - (CHAOS_FACTOR * (1 - min(floor_cos)) + CHAOS_SLACK)
+    assert cos_gpu >= bound, f"{what}: cos {cos_gpu:.5f} < {bound:.5f} (oracle self-drift floor {floor_cos})"
+
+
 @NETS
 @pytest.mark.parametrize("shuffle", [0, 1])
 def test_cluster_full_update_matches_multilaunch(lib, oracle, shuffle, sizes):
     """a whole update (10 value + 4 policy epochs of 64-row minibatches over 16,384 transitions:
-    2560 + 1024 steps) on both paths: step counts, rand() use, losses and parameter motion"""
+    2560 + 1024 steps) on both paths: step counts, rand() use, losses and parameter motion.  C4: each
+    path's motion against the oracle's update, bounded by the oracle's own chaos floor over the same
+    update (Feistel order; CHAOS_FACTOR, CHAOS_SLACK above)."""
     N, B = 16384, 64
     a = run(lib, sizes, N, B, 4, 10, shuffle, cluster=True)
     b = run(lib, sizes, N, B, 4, 10, shuffle, cluster=False)
@@ -130,17 +175,24 @@ def test_cluster_full_update_matches_multilaunch(lib, oracle, shuffle, sizes):
     assert a["next_rand"] == b["next_rand"]
     assert abs(a["stats"][0] - b["stats"][0]) <= 0.02 * abs(b["stats"][0])
     assert abs(a["stats"][2] - b["stats"][2]) <= 0.05 * abs(b["stats"][2]) + 1e-3
-    # long runs are chaotic (ReLU / clip flips amplify fp32 rounding): the C4 networks drift far faster
-    # — after 512 steps the multi-launch loop itself is at cos 0.95 (value) / 0.64 (policy) against the
-    # oracle — so their parameter motion is checked against the oracle instead
-    # (test_cluster_drift_like_multilaunch), and here only for C3
-    if sizes != C3:
+    if sizes == C3:           # C3 stays near-deterministic (oracle self-drift cos ≥ 0.9995 at 512 steps)
+        for k, k0 in (("v", "v0"), ("mu", "mu0")):
+            cos, ratio = cos_ratio(a[k] - a[k0], b[k] - b[k0])
+            assert cos > 0.95, (k, cos)
+            assert abs(ratio - 1) < 0.1, k
         return
-    for k, k0 in (("v", "v0"), ("mu", "mu0")):
-        da, db = a[k] - a[k0], b[k] - b[k0]
-        cos = float(da @ db / (np.linalg.norm(da) * np.linalg.norm(db)))
-        assert cos > 0.95, (k, cos)
-        assert abs(np.linalg.norm(da) / np.linalg.norm(db) - 1) < 0.1, k
+    if shuffle != 1:          # the oracle floor is measured in the device (Feistel) minibatch order
+        return
+    ref = [oracle_motion(oracle, a, sizes, (-1, -1), 4, 10, mode, ent=0.01) for mode in (0, 1, 2)]
+    for idx, k, k0 in ((0, "v", "v0"), (1, "mu", "mu0")):
+        floor = [cos_ratio(ref[1][idx], ref[0][idx]), cos_ratio(ref[2][idx], ref[0][idx])]
+        spread = max(abs(r - 1) for _, r in floor)
+        for name, x in (("cluster", a), ("multi-launch", b)):
+            cos, ratio = cos_ratio(x[k] - x[k0], ref[0][idx])
+            print(f"C4 full update {k}: {name} vs oracle cos {cos:.5f} ratio {ratio:.4f} | oracle self-drift "
+                  f"split-K {floor[0][0]:.5f} ({floor[0][1]:.4f}) double {floor[1][0]:.5f} ({floor[1][1]:.4f})")
+            assert_within_chaos_floor(cos, [c for c, _ in floor], f"C4 full update {k} {name}")
+            assert abs(ratio - 1) <= spread + 0.1, (k, name, ratio, floor)
 
 
 TIMEOUT_CHILD = r"""
@@ -179,29 +231,26 @@ def test_cluster_barrier_timeout_fails_loudly(lib, sizes, tmp_path):
     assert "UPDATE RETURNED" not in r.stdout
 
 
+@pytest.mark.parametrize("steps", [64, 512])
 @pytest.mark.parametrize("phase", ["value", "policy"])
-def test_cluster_drift_like_multilaunch(lib, oracle, phase):
-    """C4 networks, 512 value or policy steps (two epochs, the epoch boundary included): the cluster
-    path's parameter motion agrees with the oracle's as closely as the multi-launch loop's does
-    (tools/diag_cluster_drift.py: value both ≈ 0.95 at 512 steps, from 1.0000 at 16 — rounding chaos,
-    not a defect, which would separate the two; the clipped policy drifts faster: cluster 0.78,
-    multi-launch 0.64 at 512 steps).  Bound: the cluster path no further from the oracle than the
-    multi-launch loop (cosine within 0.02 or better), motion norms within 10 %."""
-    oracle.load(use_openblas=True)
-    N, B, n = 16384, 64, 512
-    lim, k, ref_k = ((n, 0), "v", "v") if phase == "value" else ((0, n), "mu", "mu")
+def test_long_run_drift_within_oracle_chaos_floor(lib, oracle, phase, steps):
+    """C4 networks, 64 and 512 value or policy steps (two epochs, the epoch boundary included): both GPU
+    B = 64 paths (the cluster phase and the multi-launch loop) against the oracle, bounded by the
+    oracle's own self-drift on the same buffer — the oracle with every product split-K re-associated,
+    and in double-precision products rounded once (CHAOS_FACTOR, CHAOS_SLACK above); motion norms
+    within the floor's norm spread + 0.1.  A defect would outrun the floor already at 64 steps."""
+    N, B = 16384, 64
+    lim, k, idx = ((steps, 0), "v", 0) if phase == "value" else ((0, steps), "mu", 1)
     a = run(lib, C4, N, B, 4, 10, 1, cluster=True, limit=lim, ent=0.0)
     b = run(lib, C4, N, B, 4, 10, 1, cluster=False, limit=lim, ent=0.0)
     assert not a["multi"] and b["multi"]
-    ref = oracle.ppo_update(C4, RELU(C4), a["mu0"], a["ls0"], a["v0"], a["buf"], batch_size=B, n_epochs_policy=4,
-                            n_epochs_value=10, shuffle_mode=1, seed=9, max_value_steps=lim[0], max_policy_steps=lim[1])
-    dr = ref[ref_k] - a[k + "0"]
-    out = []
-    for x in (a, b):
-        d = x[k] - x[k + "0"]
-        out.append((float(d @ dr / (np.linalg.norm(d) * np.linalg.norm(dr))), float(np.linalg.norm(d) / np.linalg.norm(dr))))
-    print(f"C4 512 {phase} steps vs oracle: cluster cos {out[0][0]:.5f} ratio {out[0][1]:.4f}, "
-          f"multi-launch cos {out[1][0]:.5f} ratio {out[1][1]:.4f}")
-    assert out[0][0] > 0.5, out
-    assert out[0][0] >= out[1][0] - 0.02, out
-    assert abs(out[0][1] - 1) < 0.1, out
+    ref = [oracle_motion(oracle, a, C4, lim, 4, 10, mode)[idx] for mode in (0, 1, 2)]
+    floor = [cos_ratio(ref[1], ref[0]), cos_ratio(ref[2], ref[0])]
+    fcos = [c for c, _ in floor]
+    spread = max(abs(r - 1) for _, r in floor)
+    for name, x in (("cluster", a), ("multi-launch", b)):
+        cos, ratio = cos_ratio(x[k] - x[k + "0"], ref[0])
+        print(f"C4 {steps} {phase} steps vs oracle: {name} cos {cos:.5f} ratio {ratio:.4f} | oracle self-drift "
+              f"split-K {floor[0][0]:.5f} ({floor[0][1]:.4f}) double {floor[1][0]:.5f} ({floor[1][1]:.4f})")
+        assert_within_chaos_floor(cos, fcos, f"{name} {phase} {steps}")
+        assert abs(ratio - 1) <= spread + 0.1, (name, ratio, floor)
