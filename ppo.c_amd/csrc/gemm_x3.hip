@@ -61,6 +61,19 @@ struct X3Args {
     int kchunk, splits, tiles_m, tiles_n;
     float* slab;                          // grad_W split-K: per-split partial tiles [splits][M][N] (plain
                                           // stores, summed by slab_reduce_kernel) instead of f32 atomics
+    // value-head fold (the 1-wide output layer y = h·w + b of a value network folded into the last
+    // hidden layer's kernels; neural_network.c nn_value_fold_step):
+    const float* ydot;                    // forward: w — each wave's Σ_cols relu(z)·w per row into ypart
+    float* ypart;                         //   [tiles_n · WARPS_N][M] (slot = column tile · WARPS_N + wave col)
+    // backward: the upper gradient is G(i, c) = g_i·w_c·1[h(i, c) > 0] (g = ∂L/∂y), so with the 0/1 mask
+    // as the operand — exact in one bf16 plane: three plane products instead of six — g and w become row /
+    // column scales: grad_x = diag(g)·(mask·diag(w)·W) (W pre-scaled by the host: the B operand),
+    // grad_W = diag(w)·(maskᵀ·diag(g)·x), grad_b = diag(w)·maskᵀ·g
+    const float* fold_g;                  // g [M batch rows]
+    const float* fold_w;                  // w [units]
+    const unsigned* fold_bits;            // grad_x: the mask words of h [M][fold_wpr]
+    int fold_wpr;
+    float* fold_gw;                       // grad_W (A = h, fp32): + Σ_rows g·h per unit — the output layer's gW
     hipEvent_t ev_start, ev_stop;         // explicit dispatch-stamped events (ppo_prof kernel timing)
 };
 
@@ -122,6 +135,13 @@ struct StageX3 {
     const float* base;                                       // this thread's element (row, k) at k0 = 0
     int row, k;                                              // this thread's first element in the tile
     int ld;
+    // value-head fold (FM, kernel FOLD): a row-contiguous operand's per-row scale — g of the k-tile's
+    // batch rows, one per float4 load (FM 1) — or a k-contiguous operand taken from the 0/1 ReLU′ mask
+    // words of its rows instead of fp32 values (FM 2)
+    const float* sg;
+    float gq[NV];
+    const unsigned* bw_row;
+    unsigned bword;
 
     // src row (k-contiguous: after the gather, clamped into the operand); rows past the end read row
     // Rmax − 1 (their products land in output rows that are never stored)
@@ -142,15 +162,25 @@ struct StageX3 {
             base = p + (long)(ridx ? ridx[gr] : gr) * ld + k;
         }
     }
+    __device__ __forceinline__ void init_fold(const float* __restrict__ g, const unsigned* __restrict__ bits, int wpr,
+                                              int r0, int Rmax) {
+        sg = g;
+        if (!MN && bits) bw_row = bits + (long)min(r0 + row, Rmax - 1) * wpr;
+    }
     // FULL: the whole k-tile lies inside [kbeg, kend) — no clamping
-    template <bool FULL>
+    template <bool FULL, int FM = 0>
     __device__ __forceinline__ void load(int k0, int kend) {
         if (MN) {
 #pragma unroll
             for (int q = 0; q < NV; ++q) {
                 const int dk = FULL ? k0 + q * KSTEP : min(k0 + k + q * KSTEP, kend - 1) - k;
                 v[q] = *reinterpret_cast<const f32x4*>(base + (long)dk * ld);
+                if (FM == 1) gq[q] = sg[k + dk];
             }
+        } else if (FM == 2) {
+            // the thread's 4·NV consecutive k lie in one 32-bit word (16-k tiles, k + 4·NV ≤ 16)
+            const int kk = FULL ? k0 + k : min(k0 + k, kend - 1);
+            bword = bw_row[kk >> 5];
         } else {
 #pragma unroll
             for (int q = 0; q < NV; ++q) {
@@ -159,10 +189,19 @@ struct StageX3 {
             }
         }
     }
+    // FM 2: the mask bits as 0/1 values (exact in one bf16 plane)
+    __device__ __forceinline__ void bits_to_values(int k0) {
+        const unsigned w = bword >> ((k0 + k) & 31);
+#pragma unroll
+        for (int q = 0; q < NV; ++q)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[q][e] = ((w >> (4 * q + e)) & 1u) ? 1.f : 0.f;
+    }
     __device__ __forceinline__ bool kvalid(int q, int k0, int kend) const {
         return MN ? k0 + k + q * KSTEP < kend : k0 + k + 4 * q < kend;
     }
-    template <bool FULL, bool NOSPLIT = false>
+    // ONE: the values are exact in one bf16 plane (0/1 masks): plane 0 only, planes 1 and 2 never read
+    template <bool FULL, bool NOSPLIT = false, bool ONE = false>
     __device__ __forceinline__ void store(unsigned short* img, int k0, int kend) {
         f32x4* vv = v;
         if (!FULL) {
@@ -173,6 +212,7 @@ struct StageX3 {
         // NOSPLIT (timing ablation only): raw bits into the planes, no split VALU
         auto split = [](f32x4 f, u32x2& p0, u32x2& p1, u32x2& p2) {
             if (NOSPLIT) { p0 = p1 = p2 = u32x2{__builtin_bit_cast(unsigned, f[0]), __builtin_bit_cast(unsigned, f[3])}; }
+            else if (ONE) { p0 = u32x2{pack2(f[0], f[1]), pack2(f[2], f[3])}; p1 = p2 = p0; }
             else split4(f, p0, p1, p2);
         };
         if (MN) {
@@ -182,8 +222,10 @@ struct StageX3 {
                 split(vv[q], p0, p1, p2);
                 unsigned short* d = img + mn_off(k + q * KSTEP, row);
                 *reinterpret_cast<u32x2*>(d) = p0;
-                *reinterpret_cast<u32x2*>(d + PLANE) = p1;
-                *reinterpret_cast<u32x2*>(d + 2 * PLANE) = p2;
+                if (!ONE) {
+                    *reinterpret_cast<u32x2*>(d + PLANE) = p1;
+                    *reinterpret_cast<u32x2*>(d + 2 * PLANE) = p2;
+                }
             }
         } else if (NV == 2) {                                 // 8 consecutive k: one ds_write_b128 per plane
             u32x2 a0, a1, a2, b0, b1, b2;
@@ -191,8 +233,10 @@ struct StageX3 {
             split(vv[NV - 1], b0, b1, b2);
             unsigned short* d = img + kc_off(row, k);
             *reinterpret_cast<u32x4*>(d) = u32x4{a0[0], a0[1], b0[0], b0[1]};
-            *reinterpret_cast<u32x4*>(d + PLANE) = u32x4{a1[0], a1[1], b1[0], b1[1]};
-            *reinterpret_cast<u32x4*>(d + 2 * PLANE) = u32x4{a2[0], a2[1], b2[0], b2[1]};
+            if (!ONE) {
+                *reinterpret_cast<u32x4*>(d + PLANE) = u32x4{a1[0], a1[1], b1[0], b1[1]};
+                *reinterpret_cast<u32x4*>(d + 2 * PLANE) = u32x4{a2[0], a2[1], b2[0], b2[1]};
+            }
         } else {
 #pragma unroll
             for (int q = 0; q < NV; ++q) {
@@ -200,8 +244,10 @@ struct StageX3 {
                 split(vv[q], p0, p1, p2);
                 unsigned short* d = img + kc_off(row, k + 4 * q);
                 *reinterpret_cast<u32x2*>(d) = p0;
-                *reinterpret_cast<u32x2*>(d + PLANE) = p1;
-                *reinterpret_cast<u32x2*>(d + 2 * PLANE) = p2;
+                if (!ONE) {
+                    *reinterpret_cast<u32x2*>(d + PLANE) = p1;
+                    *reinterpret_cast<u32x2*>(d + 2 * PLANE) = p2;
+                }
             }
         }
     }
@@ -246,7 +292,7 @@ struct StageX3 {
 // loop version of their own, grad_x's mask words brought into LDS (BM·BN/32 words, free on entry) by
 // one coalesced pass (they were 16 dependent loads per block).  Element stores in the accumulator
 // layout (each wave store: two 128-B row segments).
-template <int OP, int BM, int BN, int TM, int TN, int NTH>
+template <int OP, int BM, int BN, int TM, int TN, int NTH, bool YD = false, bool FG = false>
 __device__ __forceinline__ void x3_epilogue_out(const X3Args& a, f32x16 (&acc)[TM][TN], unsigned short* lds, int m0,
                                                 int n0, int wm, int wn, int tid) {
     constexpr int WM = TM * 32, WN = TN * 32;
@@ -260,18 +306,56 @@ __device__ __forceinline__ void x3_epilogue_out(const X3Args& a, f32x16 (&acc)[T
     constexpr int WPT = BN / 32;                            // mask words per tile row
     unsigned* const mk = reinterpret_cast<unsigned*>(lds);  // images no longer read (last barrier)
     const bool masked = OP == OP_NN && a.bits_in != nullptr;
+    // grad_x fold (FG): the rows' g, a row scale of the product (grad_x = diag(g)·(mask·diag(w)·W))
+    float* const gsh = reinterpret_cast<float*>(mk + BM * WPT);
+    if (FG) {
+        for (int idx = tid; idx < BM; idx += NTH) gsh[idx] = a.fold_g[min(m0 + idx, a.M - 1)];
+    }
     if (masked) {
         for (int idx = tid; idx < BM * WPT; idx += NTH) {
             const int grow = min(m0 + idx / WPT, a.M - 1);
             const int gw = min((n0 >> 5) + idx % WPT, a.wpr - 1);
             mk[idx] = a.bits_in[(long)grow * a.wpr + gw];
         }
-        __syncthreads();
     }
+    if (masked || FG) __syncthreads();
+    // value-head fold (YD): each wave's partial y = Σ over its columns of relu(z)·w, per row — the
+    // wave's 32 rows of block row i summed over its TN column blocks, then over the 32 lanes of each
+    // half-wave, reduce-scattered so that lane r < 16 ends with row e = r of its half
+    constexpr int WARPS_N = BN / WN;
+    float wcol[TN];
+    if constexpr (YD) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            const int col = n0 + wn * WN + j * 32 + r;
+            wcol[j] = col < a.N ? a.ydot[col] : 0.f;
+        }
+    }
+    auto ydot_block = [&](float (&yp)[16], int i) {
+#pragma unroll
+        for (int u = 0; u < 16; ++u) yp[u] += __shfl_xor(yp[u], 16, 64);
+#pragma unroll
+        for (int o = 8; o >= 1; o >>= 1) {
+            const bool up = (r & o) != 0;
+#pragma unroll
+            for (int u = 0; u < o; ++u) {
+                const float send = up ? yp[u] : yp[u + o];
+                const float keep = up ? yp[u + o] : yp[u];
+                yp[u] = keep + __shfl_xor(send, o, 64);
+            }
+        }
+        const int e = r & 15;
+        const int row = m0 + wm * WM + i * 32 + 4 * h + (e & 3) + 8 * (e >> 2);
+        const int slot = (n0 / BN) * WARPS_N + wn;
+        if (r < 16 && row < a.M) a.ypart[(long)slot * a.M + row] = yp[0];
+    };
     auto body = [&](auto BITSc) {
         constexpr bool BITS = decltype(BITSc)::value;
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+        for (int i = 0; i < TM; ++i) {
+            float yp[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) yp[u] = 0.f;
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
                 const int c0 = n0 + wn * WN + j * 32;
@@ -295,12 +379,14 @@ __device__ __forceinline__ void x3_epilogue_out(const X3Args& a, f32x16 (&acc)[T
 #else
                         if (ok) *dst = v;
 #endif
+                        if constexpr (YD) yp[e] += v * wcol[j];
                         if constexpr (BITS) {
                             const unsigned long long bb = __ballot(ok && v > 0.f);
                             const unsigned half = h ? (unsigned)(bb >> 32) : (unsigned)bb;
                             word = r == e ? half : word;
                         }
                     } else {
+                        if (FG) v *= gsh[lr0 + dr];
                         if (masked && !((mk[(lr0 + dr) * WPT + ((c0 - n0) >> 5)] >> r) & 1u)) v = 0.f;
 #ifdef PPO_X3_NTSTORE
                         if (ok) __builtin_nontemporal_store(v, dst);
@@ -314,12 +400,15 @@ __device__ __forceinline__ void x3_epilogue_out(const X3Args& a, f32x16 (&acc)[T
                     if (row < a.M && c0 < a.N) a.bits_out[(long)row * a.wpr + (c0 >> 5)] = word;
                 }
             }
+            if constexpr (YD) ydot_block(yp, i);
+        }
     };
     if (OP == OP_NT && a.bits_out) body(std::true_type{});
     else body(std::false_type{});
 }
 
-template <int OP, int BM, int BN, int WARPS_M, int NTH, int OCC, int KG, int ABL = 0>
+// FOLD: the value-head fold variant (forward: ydot / ypart; grad_x / grad_W: A synthesised from h)
+template <int OP, int BM, int BN, int WARPS_M, int NTH, int OCC, int KG, int ABL = 0, int FOLD = 0>
 __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     constexpr int NTG = NTH / KG;                                  // threads per k-group
     constexpr int NW = NTG / 64, WARPS_N = NW / WARPS_M;
@@ -376,19 +465,29 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     SB sb;
     sa.init(a.A, a.lda, OP == OP_NT ? a.ridx : nullptr, m0, a.M, lt);
     sb.init(a.B, a.ldb, nullptr, n0, a.N, lt);
+    // value-head fold (grad_x: A from the mask words; grad_W: A = h → mask, B = x scaled by g)
+    constexpr bool syn = OP != OP_NT && FOLD != 0;
+    constexpr int FMA_ = !syn ? 0 : OP == OP_NN ? 2 : 1;          // A's fold load mode
+    constexpr int FMB_ = syn && OP == OP_TN ? 1 : 0;              // B's
+    if (syn) {
+        sa.init_fold(a.fold_g, OP == OP_NN ? a.fold_bits : nullptr, a.fold_wpr, m0, a.M);
+        sb.init_fold(a.fold_g, nullptr, 0, n0, a.N);
+    }
     // the fused gather's copy of A's rows: every column tile of a row block stages the same rows, so
     // they share the copy — column tile tn writes the k-tiles with index ≡ tn (mod tiles_n) (one
     // workgroup writing all of it finished its tile ≈ a copy later than the others in a one-round grid)
     const bool do_copy = OP == OP_NT && a.acopy != nullptr;
     // grad_W bias: Σ over this split's k of the A (= g) tile, from the staging registers
     const bool do_bsum = OP == OP_TN && a.gbias != nullptr && tn == 0;
-    f32x4 bs[SA::NV];
+    f32x4 bs[SA::NV], bs3[SA::NV];                     // bs3: the folded output layer's Σ g·h (grad_W fold)
 #pragma unroll
-    for (int q = 0; q < SA::NV; ++q) bs[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int q = 0; q < SA::NV; ++q) bs[q] = bs3[q] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     // fragment registers: plane p of the A (fa) and B (fb) operand tiles of the current k-tile
     bf16x8 fa[3][TM], fb[3][TN];
+    // (fold: A is a 0/1 mask in plane 0 only — its planes 1, 2 and their three products are skipped)
     auto rd_a = [&](const unsigned short* img, int p) {
+        if (syn && p != 0) return;
 #pragma unroll
         for (int i = 0; i < TM; ++i) fa[p][i] = SA::frag(img + p * SA::PLANE, wm * WM + i * 32 + r, lane);
     };
@@ -398,6 +497,7 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     };
     // plane product A_pa·B_pb of the current k-tile (the six with pa + pb ≤ 2)
     auto mm = [&](int pa, int pb) {
+        if (syn && pa != 0) return;
         if (ABL & 1) {               // keep the fragment reads live
 #pragma unroll
             for (int i = 0; i < TM; ++i)
@@ -424,15 +524,35 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     // split + LDS store of the staged tile at k0 (FULL: no k tail); COPY: also the gathered rows
     // COPY (forward, fused gather): also the gathered rows; BSUM (grad_W of a bias): also Σ g — both
     // compile-time, so the mainloop of the workgroups that do neither carries no dead VALU
-    auto stage_a = [&](auto FULLc, auto COPYc, unsigned short* img, int k0) {
+    auto stage_a = [&](auto FULLc, auto COPYc, auto SYNc, unsigned short* img, int k0) {
         constexpr bool FULL = decltype(FULLc)::value, COPY = OP == OP_NT && decltype(COPYc)::value;
         constexpr bool BSUM = OP == OP_TN && decltype(COPYc)::value;
+        constexpr bool SYN = OP != OP_NT && decltype(SYNc)::value;
         if ((ABL & 2) && k0 != kbeg) return;
         if constexpr (COPY) {
             if (((k0 - kbeg) / BK) % a.tiles_n == tn) sa.copy_out(a.acopy, a.K, m0, a.M, k0, kend);
         }
-        sa.template store<FULL, (ABL & 64) != 0>(img, k0, kend);
-        if constexpr (BSUM) {
+        if constexpr (SYN && OP == OP_NN) sa.bits_to_values(k0);
+        if constexpr (SYN && OP == OP_TN) {
+            // A = h: the output layer's Σ g·h and the bias's Σ 1[h > 0]·g (valid batch rows), then the mask
+#pragma unroll
+            for (int q = 0; q < SA::NV; ++q) {
+                const bool ok = FULL || sa.kvalid(q, k0, kend);
+                const float g = sa.gq[q];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const float hv = sa.v[q][e];
+                    const bool on = hv > 0.f;
+                    if (BSUM && ok) {
+                        bs3[q][e] += g * hv;
+                        bs[q][e] += on ? g : 0.f;
+                    }
+                    sa.v[q][e] = on ? 1.f : 0.f;
+                }
+            }
+        }
+        sa.template store<FULL, (ABL & 64) != 0, SYN>(img, k0, kend);
+        if constexpr (BSUM && !SYN) {
 #pragma unroll
             for (int q = 0; q < SA::NV; ++q) bs[q] += sa.v[q];
         }
@@ -440,21 +560,26 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     auto stage_b = [&](auto FULLc, unsigned short* img, int k0) {
         constexpr bool FULL = decltype(FULLc)::value;
         if ((ABL & 2) && k0 != kbeg) return;
+        if constexpr (FMB_ == 1) {                       // grad_W fold: x rows scaled by g
+#pragma unroll
+            for (int q = 0; q < SB::NV; ++q) sb.v[q] *= sb.gq[q];
+        }
         sb.template store<FULL, (ABL & 64) != 0>(img + SA::SIZE, k0, kend);
     };
-    auto load = [&](auto FULLc, int k0) {
+    auto load = [&](auto FULLc, auto SYNc, int k0) {
         constexpr bool FULL = decltype(FULLc)::value;
+        constexpr bool SYN = OP != OP_NT && decltype(SYNc)::value;
         if ((ABL & 8) && k0 != kbeg) return;
-        sa.template load<FULL>(k0, kend);
-        sb.template load<FULL>(k0, kend);
+        sa.template load<FULL, SYN ? FMA_ : 0>(k0, kend);
+        sb.template load<FULL, SYN ? FMB_ : 0>(k0, kend);
     };
     using T = std::true_type;
     using F = std::false_type;
-    auto load_t = [&](int j) {
-        if (is_full(j)) load(T{}, k0_of(j)); else load(F{}, k0_of(j));
+    auto load_t = [&](auto SYNc, int j) {
+        if (is_full(j)) load(T{}, SYNc, k0_of(j)); else load(F{}, SYNc, k0_of(j));
     };
-    auto stage_a_t = [&](auto COPYc, unsigned short* img, int j) {
-        if (is_full(j)) stage_a(T{}, COPYc, img, k0_of(j)); else stage_a(F{}, COPYc, img, k0_of(j));
+    auto stage_a_t = [&](auto COPYc, auto SYNc, unsigned short* img, int j) {
+        if (is_full(j)) stage_a(T{}, COPYc, SYNc, img, k0_of(j)); else stage_a(F{}, COPYc, SYNc, img, k0_of(j));
     };
     auto stage_b_t = [&](unsigned short* img, int j) {
         if (is_full(j)) stage_b(T{}, img, k0_of(j)); else stage_b(F{}, img, k0_of(j));
@@ -498,7 +623,8 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     using I0 = std::integral_constant<int, 0>;
     using I2 = std::integral_constant<int, 2>;
     using I6 = std::integral_constant<int, 6>;
-    auto iter = [&](auto STEADYc, auto COPYc, int j, unsigned short* cur, unsigned short* n1, unsigned short* n2) {
+    auto iter = [&](auto STEADYc, auto COPYc, auto SYNc, int j, unsigned short* cur, unsigned short* n1,
+                    unsigned short* n2) {
         constexpr bool STEADY = decltype(STEADYc)::value;
         const bool has1 = STEADY || j + 1 < NK, has2 = STEADY || j + 2 < NK, has3 = STEADY || j + 3 < NK;
         rd_a(cur, 1);
@@ -510,8 +636,8 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
         if (has1) rd_a(n1, 2);
         region_end(I0{});
         mm(0, 0);
-        if (STEADY) stage_a(T{}, COPYc, n2, k0_of(j + 2));
-        else if (has2) stage_a_t(COPYc, n2, j + 2);
+        if (STEADY) stage_a(T{}, COPYc, SYNc, n2, k0_of(j + 2));
+        else if (has2) stage_a_t(COPYc, SYNc, n2, j + 2);
         region_end(I6{});
         mm(1, 0);
         if (has1) rd_b(n1, 0);
@@ -520,8 +646,8 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
         region_end(I6{});
         mm(0, 2);
         if (has1) rd_b(n1, 2);
-        if (STEADY) load(T{}, k0_of(j + 3));
-        else if (has3) load_t(j + 3);
+        if (STEADY) load(T{}, SYNc, k0_of(j + 3));
+        else if (has3) load_t(SYNc, j + 3);
         region_end(I2{});
         mm(0, 1);
         if (has1) rd_a(n1, 0);
@@ -532,13 +658,13 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
 #endif
         __syncthreads();
     };
-    auto mainloop = [&](auto COPYc) {
+    auto mainloop = [&](auto COPYc, auto SYNc) {
         unsigned short* cur = ring;
         unsigned short* n1 = ring + BUF;
         unsigned short* n2 = ring + 2 * BUF;
-        if (NK > 0) { load_t(0); stage_a_t(COPYc, cur, 0); stage_b_t(cur, 0); }
-        if (NK > 1) { load_t(1); stage_a_t(COPYc, n1, 1); stage_b_t(n1, 1); }
-        if (NK > 2) load_t(2);
+        if (NK > 0) { load_t(SYNc, 0); stage_a_t(COPYc, SYNc, cur, 0); stage_b_t(cur, 0); }
+        if (NK > 1) { load_t(SYNc, 1); stage_a_t(COPYc, SYNc, n1, 1); stage_b_t(n1, 1); }
+        if (NK > 2) load_t(SYNc, 2);
         __syncthreads();
         if (NK > 0) { rd_a(cur, 2); rd_b(cur, 0); rd_b(cur, 2); rd_a(cur, 0); }
         if (ABL & 32) stamp(1);
@@ -553,25 +679,30 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
             unsigned short* const s1 = n1;
             unsigned short* const s2 = n2;
             for (; j + 3 <= steady; j += 3) {
-                iter(T{}, COPYc, j, s0, s1, s2);
-                iter(T{}, COPYc, j + 1, s1, s2, s0);
-                iter(T{}, COPYc, j + 2, s2, s0, s1);
+                iter(T{}, COPYc, SYNc, j, s0, s1, s2);
+                iter(T{}, COPYc, SYNc, j + 1, s1, s2, s0);
+                iter(T{}, COPYc, SYNc, j + 2, s2, s0, s1);
             }
         }
         for (; j < steady; ++j) {
-            iter(T{}, COPYc, j, cur, n1, n2);
+            iter(T{}, COPYc, SYNc, j, cur, n1, n2);
             unsigned short* t = cur; cur = n1; n1 = n2; n2 = t;
         }
         for (; j < NK; ++j) {                                  // the last two or three tiles
-            iter(F{}, COPYc, j, cur, n1, n2);
+            iter(F{}, COPYc, SYNc, j, cur, n1, n2);
             unsigned short* t = cur; cur = n1; n1 = n2; n2 = t;
         }
     };
 #ifdef PPO_X3_PRIO2
     if ((tid >> 6) >= NTH / 128) __builtin_amdgcn_s_setprio(1);   // the second-dispatched half wins VALU arbitration
 #endif
-    if (do_copy || do_bsum) mainloop(T{});                          // (COPYc: the gather copy / Σ g)
-    else mainloop(F{});
+    // (COPYc: the gather copy / Σ g; SYNc: the folded value head's synthesised A)
+    auto run = [&](auto COPYc) {
+        if constexpr (syn) mainloop(COPYc, T{});
+        else mainloop(COPYc, F{});
+    };
+    if (do_copy || do_bsum) run(T{});
+    else run(F{});
 #ifdef PPO_X3_PRIO2
     __builtin_amdgcn_s_setprio(0);
 #endif
@@ -595,8 +726,21 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
             float s = 0.f;
             for (int j = 0; j < S; ++j) s += red[j * BM + tid];
             if (m0 + tid < a.M) {
+                if (syn) s *= a.fold_w[m0 + tid];            // grad_b = diag(w)·maskᵀ·g
                 if (a.splits > 1) atomicAdd(a.gbias + m0 + tid, s);
                 else a.gbias[m0 + tid] = s;
+            }
+        }
+        if constexpr (OP == OP_TN && syn) {           // the folded output layer's gW: the same reduction
+            __syncthreads();
+#pragma unroll
+            for (int q = 1; q < SA::NV; ++q) bs3[0] += bs3[q];
+            *reinterpret_cast<f32x4*>(red + (tid / G) * BM + (tid % G) * 4) = bs3[0];
+            __syncthreads();
+            if (tid < BM) {
+                float s = 0.f;
+                for (int j = 0; j < S; ++j) s += red[j * BM + tid];
+                if (m0 + tid < a.M) atomicAdd(a.fold_gw + m0 + tid, s);
             }
         }
     }
@@ -646,8 +790,9 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
         return;
     }
     if constexpr (OP != OP_TN) {
-        static_assert(BM * (BN / 32) * 4 <= KG * NS * BUF * 2, "x3 epilogue: mask words exceed LDS");
-        x3_epilogue_out<OP, BM, BN, TM, TN, NTH>(a, acc, lds, m0, n0, wm, wn, tid);
+        static_assert(BM * (BN / 32 + 1) * 4 <= KG * NS * BUF * 2, "x3 epilogue: mask words exceed LDS");
+        x3_epilogue_out<OP, BM, BN, TM, TN, NTH, OP == OP_NT && FOLD != 0, OP == OP_NN && FOLD != 0>(a, acc, lds, m0,
+                                                                                                  n0, wm, wn, tid);
         if (ABL & 32) stamp(3);
         return;
     }
@@ -686,6 +831,7 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
                 const int row = r0 + (e & 3) + 8 * (e >> 2);
                 const bool ok = col_ok && row < a.M;
                 float v = acc[i][j][e];
+                if (OP == OP_TN && syn) v *= a.fold_w[row < a.M ? row : a.M - 1];     // grad_W = diag(w)·(…)
                 float* dst = a.C + (long)row * a.ldc + col;
                 if (OP == OP_NT) {
                     v += bcol;
@@ -723,10 +869,13 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
 int g_x3_ablate = -1;
 #endif
 
-template <int OP, int BM, int BN, int WARPS_M, int NTH, int OCC, int KG, int ABL = 0>
+int g_x3_last_slots = 0;                 // the last launch's ypart slots (tiles_n × waves along N)
+
+template <int OP, int BM, int BN, int WARPS_M, int NTH, int OCC, int KG, int ABL = 0, int FOLD = 0>
 void launch_x3(X3Args a) {
     a.tiles_m = ppo_divup(a.M, BM);
     a.tiles_n = ppo_divup(a.N, BN);
+    g_x3_last_slots = a.tiles_n * (NTH / KG / 64 / WARPS_M);
     if (a.splits < 1) a.splits = 1;
     const long grid = (long)a.tiles_m * a.tiles_n * a.splits;
     PPO_REQUIRE(grid > 0 && grid < (1L << 31), "gemm_x3: grid out of range");
@@ -735,7 +884,7 @@ void launch_x3(X3Args a) {
     using SB = StageX3<BN, OP != OP_NT, NTH / KG>;
     constexpr size_t lds = (size_t)KG * 3 * sizeof(unsigned short) * (SA::SIZE + SB::SIZE);   // 3-stage ring
     static_assert(lds <= 160 * 1024, "gemm_x3: LDS images exceed 160 KiB");
-    auto kern = gemm_x3_kernel<OP, BM, BN, WARPS_M, NTH, OCC, KG, ABL>;
+    auto kern = gemm_x3_kernel<OP, BM, BN, WARPS_M, NTH, OCC, KG, ABL, FOLD>;
     if (lds > 64 * 1024) {
         static bool attr = false;                      // once per instantiation
         if (!attr) {
@@ -800,6 +949,18 @@ int g_split_x3 = 0;
 
 template <int OP>
 void launch_cfg_x3(int c, const X3Args& a) {
+    if (a.ydot || a.fold_g) {                      // the value-head fold variants
+        switch (c) {
+            case 0: launch_x3<OP, 256, 256, 4, 512, 2, 1, 0, 1>(a); return;
+            case 2: launch_x3<OP, 128, 128, 4, 512, 2, 1, 0, 1>(a); return;
+            case 4: launch_x3<OP, 64, 64, 2, 256, 4, 1, 0, 1>(a); return;
+            case 5: launch_x3<OP, 256, 128, 4, 512, 2, 1, 0, 1>(a); return;
+            case 3:
+                if constexpr (OP == OP_TN) { launch_x3<OP, 128, 128, 2, 512, 2, 2, 0, 1>(a); return; }
+                [[fallthrough]];
+            default: launch_x3<OP, 128, 128, 2, 256, 2, 1, 0, 1>(a); return;
+        }
+    }
 #ifdef PPO_X3_DIAG
     if (g_x3_ablate < 0) {
         const char* e = getenv("PPO_X3_ABLATE");
@@ -896,35 +1057,67 @@ int phip_x3_supported(int op, int m, int n, int l) {
     return n % 4 == 0 && l % 4 == 0;                           // K = m; g rows l, x rows n
 }
 
-void phip_x3_fwd(float* y, const float* x, const int* ridx, float* xcopy, const float* W, const float* b, int m,
-                 int n, int l, int relu, unsigned* bits) {
-    if (m <= 0 || l <= 0) return;
+// ydot / ypart (value-head fold): each wave's partial y = Σ relu(z)·ydot over its columns, per row, into
+// ypart [slots][m]; returns slots (0 without the fold)
+int phip_x3_fwd_vhead(float* y, const float* x, const int* ridx, float* xcopy, const float* W, const float* b, int m,
+                      int n, int l, int relu, unsigned* bits, const float* ydot, float* ypart) {
+    if (m <= 0 || l <= 0) return 0;
     PPO_REQUIRE(y && x && W && n > 0 && n % 4 == 0 && al16(x) && al16(W), "phip_x3_fwd: unsupported operands");
+    PPO_REQUIRE(!ydot || ypart, "phip_x3_fwd: value-head fold without its partial buffer");
     ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l, ppo::gemm_key(0, 1, m, n, l));
     X3Args a{};
     a.A = x; a.lda = n; a.B = W; a.ldb = n; a.C = y; a.ldc = l;
     a.M = m; a.N = l; a.K = n; a.kchunk = n; a.splits = 1;
     a.bias = b; a.relu = relu; a.ridx = ridx; a.acopy = ridx ? xcopy : nullptr;
     a.bits_out = relu ? bits : nullptr; a.wpr = ppo_divup(l, 32);
+    a.ydot = ydot; a.ypart = ypart;
     launch_cfg_x3<OP_NT>(pick_x3(m, l, OP_NT), a);
+    return ydot ? g_x3_last_slots : 0;
 }
 
-void phip_x3_bwd_x(float* gx, const float* g, const float* W, const unsigned* bits, int m, int n, int l) {
+void phip_x3_fwd(float* y, const float* x, const int* ridx, float* xcopy, const float* W, const float* b, int m,
+                 int n, int l, int relu, unsigned* bits) {
+    (void)phip_x3_fwd_vhead(y, x, ridx, xcopy, W, b, m, n, l, relu, bits, nullptr, nullptr);
+}
+
+// the upper layer's gradient A = g [m, l]; value-head fold (fold_g): A = the 0/1 mask words of h
+// (fold_bits [m][⌈l/32⌉]), W already scaled by the output weights (diag(w)·W), the product scaled by
+// fold_g per row — grad_x = diag(g)·(mask·diag(w)·W) ⊙ the input mask
+void phip_x3_bwd_x_fold(float* gx, const float* g, const unsigned* fold_bits, const float* fold_g, const float* W,
+                        const unsigned* bits, int m, int n, int l) {
     if (m <= 0 || n <= 0) return;
-    PPO_REQUIRE(gx && g && W && l > 0 && l % 4 == 0 && n % 4 == 0 && al16(g) && al16(W),
+    PPO_REQUIRE(gx && (g || fold_bits) && W && l > 0 && l % 4 == 0 && n % 4 == 0 && (!g || al16(g)) && al16(W),
                 "phip_x3_bwd_x: unsupported operands");
+    PPO_REQUIRE(!fold_bits || fold_g, "phip_x3_bwd_x: value-head fold operands");
     ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l, ppo::gemm_key(1, 1, m, n, l));
     X3Args a{};
-    a.A = g; a.lda = l; a.B = W; a.ldb = n; a.C = gx; a.ldc = n;
+    a.A = fold_bits ? W : g; a.lda = l; a.B = W; a.ldb = n; a.C = gx; a.ldc = n;
     a.M = m; a.N = n; a.K = l; a.kchunk = l; a.splits = 1;
     a.bits_in = bits; a.wpr = ppo_divup(n, 32);
+    a.fold_bits = fold_bits; a.fold_wpr = ppo_divup(l, 32); a.fold_g = fold_g;
     launch_cfg_x3<OP_NN>(pick_x3(m, n, OP_NN), a);
 }
 
+void phip_x3_bwd_x(float* gx, const float* g, const float* W, const unsigned* bits, int m, int n, int l) {
+    phip_x3_bwd_x_fold(gx, g, nullptr, nullptr, W, bits, m, n, l);
+}
+
+void phip_x3_bwd_w_fold(float* gW, float* gb, const float* g, const float* fold_g, const float* fold_w,
+                        float* fold_gw, const float* x, int m, int n, int l, int zeroed);
+
 // zeroed: gW / gb already hold zeros (one memset per backward); otherwise they are cleared here
 void phip_x3_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, int n, int l, int zeroed) {
+    phip_x3_bwd_w_fold(gW, gb, g, nullptr, nullptr, nullptr, x, m, n, l, zeroed);
+}
+
+// value-head fold (fold_g): g = h [m, l] (fp32, its mask is the operand), x scaled by fold_g per row, the
+// product and the bias gradient scaled by fold_w per unit — grad_W = diag(w)·(maskᵀ·diag(g)·x), grad_b =
+// diag(w)·maskᵀ·g — and fold_gw [l] (zero on entry) += Σ_rows fold_g·h, the output layer's gW
+void phip_x3_bwd_w_fold(float* gW, float* gb, const float* g, const float* fold_g, const float* fold_w,
+                        float* fold_gw, const float* x, int m, int n, int l, int zeroed) {
     if (l <= 0 || n <= 0) return;
     PPO_REQUIRE(gW && g && x && n % 4 == 0 && l % 4 == 0 && al16(g) && al16(x), "phip_x3_bwd_w: unsupported operands");
+    PPO_REQUIRE(!fold_g || (fold_w && fold_gw && gb), "phip_x3_bwd_w: value-head fold operands");
     ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l, ppo::gemm_key(2, 1, m, n, l));
     if (m <= 0) {
         if (!zeroed) {
@@ -950,6 +1143,7 @@ void phip_x3_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, 
     a.A = g; a.lda = l; a.B = x; a.ldb = n; a.C = gW; a.ldc = n;
     a.M = l; a.N = n; a.K = m; a.kchunk = kchunk; a.splits = splits;
     a.gbias = gb;
+    a.fold_g = fold_g; a.fold_w = fold_w; a.fold_gw = fold_gw;
     // split-K partials: per-split slabs written with plain stores and summed by one reduce launch
     // (16 MB of f32 atomics at ≈1.3 TB/s set the grad_W time of small batches; the slab path moves
     // the same bytes at store / load rate, and its sum is deterministic); the bias gradient keeps

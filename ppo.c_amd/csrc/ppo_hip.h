@@ -79,6 +79,15 @@ void phip_x3_fwd(float* y, const float* x, const int* ridx, float* xcopy, const 
                  int n, int l, int relu, unsigned* bits);
 void phip_x3_bwd_x(float* gx, const float* g, const float* W, const unsigned* bits, int m, int n, int l);
 void phip_x3_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, int n, int l, int zeroed);
+/* value-head fold (nn_value_fold_step): forward partial y dots (returns ypart slots); backward with the
+ * upper gradient g·w·1[h > 0] applied as the 0/1 mask of h with g, w as row / column scales (grad_x:
+ * W pre-scaled by w) and the output layer's gW */
+int  phip_x3_fwd_vhead(float* y, const float* x, const int* ridx, float* xcopy, const float* W, const float* b, int m,
+                       int n, int l, int relu, unsigned* bits, const float* ydot, float* ypart);
+void phip_x3_bwd_x_fold(float* gx, const float* g, const unsigned* fold_bits, const float* fold_g, const float* W,
+                        const unsigned* bits, int m, int n, int l);
+void phip_x3_bwd_w_fold(float* gW, float* gb, const float* h, const float* fold_g, const float* fold_w, float* fold_gw,
+                        const float* x, int m, int n, int l, int zeroed);
 /* dst[i, :] = bf16(src[rows[i], :]) for i < m (S % 4 == 0): layer 0's gather in bf16 mode */
 void phip_gather_rows_bf16(unsigned short* dst, const float* src, const int* rows, int m, int S);
 void phip_f32_to_bf16(unsigned short* dst, const float* src, long count);
@@ -136,6 +145,10 @@ void phip_axpy(float* y, const float* x, long count);
 /* d_loss[0] = Σ(t−y)²/count (written), d_loss_accum[0] += same (if non-NULL);
  * grad = 2(y−t)/count (if non-NULL).  loss.cu:25-83 fused, no host sync. */
 void phip_mse(const float* y, const float* t, long count, float* grad, float* d_loss, float* d_loss_accum);
+/* the folded value head (kernels.hip): y = Σ ypart slots + b, loss += Σ(t−y)²/m, g = 2(y−t)/m, gb += Σ g;
+ * and Ws = diag(w)·W for the hidden layer's grad_x (W [l][n], w [l]) */
+void phip_value_head(const float* ypart, int slots, const float* b, const float* tgt, int m, float* y, float* g,
+                     float* gb, float* d_loss_accum, const float* w, const float* W, float* Ws, int l, int n);
 /* out_head.hip: output layer forward + loss head + output-layer backward in one pass (ppo_update;
  * head 0 = value, A = 1, MSE against tgt; 1 = policy, clipped surrogate); gW / gb / grad_log_std
  * accumulated into zeroed outputs, loss into loss_accum; widths 64…1024, A ∈ {1, 6}; bf16 != 0:

@@ -57,6 +57,9 @@ void nn_backward_dev_z(NeuralNetwork* nn, const float* d_grad_out, int m, int wa
                        long reduce_extra);
 /* the output layer fused with the loss head (head 0 value / MSE, 1 policy), see neural_network.c */
 int  nn_out_head_ok(const NeuralNetwork* nn, int head);
+int  nn_value_fold_ok(const NeuralNetwork* nn, int m);
+void nn_value_fold_step(NeuralNetwork* nn, const float* d_x, const int* d_rows, float* d_xcopy, int m, int grads_zero,
+                        long reduce_extra, const float* tgt, float* loss_accum);
 int  nn_policy_wide_ok(const NeuralNetwork* nn, int m);
 void nn_policy_wide_step(NeuralNetwork* nn, const float* d_x, const int* d_rows, float* d_xcopy, int m,
                          int grads_zero, long reduce_extra, const float* log_std, const float* action,

@@ -294,16 +294,20 @@ void lin_bwd_w(float* gW, const float* g, const float* x, int m, int n, int l) {
     else phip_linear_bwd_w(gW, NULL, g, x, m, n, l);
 }
 
+/* value-head fold (nn_value_fold_step): the forward's last layer also forms the partial dots of the
+ * 1-wide output layer (w) into ypart, and reports their slot count */
+typedef struct { const float* w; float* ypart; int slots; } FoldFwd;
+
 /* forward through the first `upto` linear layers (fp32 storage; upto = L: the whole network) */
 static void nn_forward_dev_upto(NeuralNetwork* nn, const float* d_x, const int* d_rows, float* d_xcopy, int m,
-                                int upto);
+                                int upto, FoldFwd* fold);
 
 void nn_forward_dev_rows(NeuralNetwork* nn, const float* d_x, const int* d_rows, float* d_xcopy, int m) {
-    nn_forward_dev_upto(nn, d_x, d_rows, d_xcopy, m, nn->num_layers - 1);
+    nn_forward_dev_upto(nn, d_x, d_rows, d_xcopy, m, nn->num_layers - 1, NULL);
 }
 
 static void nn_forward_dev_upto(NeuralNetwork* nn, const float* d_x, const int* d_rows, float* d_xcopy, int m,
-                                int upto) {
+                                int upto, FoldFwd* fold) {
     nn_ensure_act(nn, m);
     const int L = nn->num_layers - 1;
     if (nn->dtype == 1) {
@@ -320,7 +324,11 @@ static void nn_forward_dev_upto(NeuralNetwork* nn, const float* d_x, const int* 
         Layer* ly = &nn->layers[i];
         float* out = nn->layers[i + 1].d_input;
         const int n = ly->input_size, l = ly->output_size;
-        if (use_x3_layer(m, n, l) && phip_x3_supported(0, m, n, l)) {
+        if (fold && i == upto - 1) {            /* nn_value_fold_ok: the x3 engine takes this layer */
+            fold->slots = phip_x3_fwd_vhead(out, in, i == 0 ? d_rows : NULL, i == 0 ? d_xcopy : NULL, ly->d_weights,
+                                            ly->d_biases, m, n, l, nn_is_relu(nn, i), act_bits(nn, i + 1), fold->w,
+                                            fold->ypart);
+        } else if (use_x3_layer(m, n, l) && phip_x3_supported(0, m, n, l)) {
             phip_x3_fwd(out, in, i == 0 ? d_rows : NULL, i == 0 ? d_xcopy : NULL, ly->d_weights, ly->d_biases, m, n,
                         l, nn_is_relu(nn, i), act_bits(nn, i + 1));
         } else if (i == 0 && d_rows) {
@@ -354,18 +362,22 @@ void nn_backward_dev(NeuralNetwork* nn, const float* d_grad_out, int m, int want
     nn_backward_dev_z(nn, d_grad_out, m, want_grad_x0, 0, -1);
 }
 
+/* value-head fold: the backward's top layer (top - 1) takes its upper gradient g·w·1[h > 0] from g,
+ * w and h's mask (nn_value_fold_step) */
+typedef struct { const float* g; const float* w; const float* Ws; float* gw_out; } FoldBwd;
+
 static void nn_backward_dev_top(NeuralNetwork* nn, const float* d_grad_out, int m, int want_grad_x0,
-                                int grads_zero, long reduce_extra, int top);
+                                int grads_zero, long reduce_extra, int top, const FoldBwd* fold);
 
 void nn_backward_dev_z(NeuralNetwork* nn, const float* d_grad_out, int m, int want_grad_x0, int grads_zero,
                        long reduce_extra) {
-    nn_backward_dev_top(nn, d_grad_out, m, want_grad_x0, grads_zero, reduce_extra, nn->num_layers - 1);
+    nn_backward_dev_top(nn, d_grad_out, m, want_grad_x0, grads_zero, reduce_extra, nn->num_layers - 1, NULL);
 }
 
 /* backward through layers top-1 … 0, starting from the gradient at layer top's input (top = L: the
  * whole network, from the output gradient; top = L-1: the output layer's backward already ran) */
 static void nn_backward_dev_top(NeuralNetwork* nn, const float* d_grad_out, int m, int want_grad_x0,
-                                int grads_zero, long reduce_extra, int top) {
+                                int grads_zero, long reduce_extra, int top, const FoldBwd* fold) {
     nn_ensure_grad(nn, m);
     const int L = nn->num_layers - 1;
     const float* g = d_grad_out;
@@ -412,7 +424,16 @@ static void nn_backward_dev_top(NeuralNetwork* nn, const float* d_grad_out, int 
         const int want_gx = i > 0 || want_grad_x0;
         const int relu_in = i > 0 && nn_is_relu(nn, i - 1);
         const unsigned* bits = relu_in && nn->bits_m == m ? act_bits(nn, i) : NULL;   /* this forward's bits */
-        if (i == L - 1 && want_gx && (!relu_in || bits) &&
+        if (fold && i == top - 1) {
+            /* grad_W = diag(w)·(maskᵀ·diag(g)·x), grad_b = diag(w)·maskᵀ·g, the output layer's gW = Σ g·h;
+             * grad_x = diag(g)·(mask·diag(w)·W) ⊙ the input mask (gemm_x3.hip) */
+            const float* h = nn->layers[i + 1].d_input;
+            phip_x3_bwd_w_fold(ly->d_grad_weights, ly->d_grad_biases, h, fold->g, fold->w, fold->gw_out, x, m, n, l, 1);
+            if (want_gx) {
+                if (relu_in && !bits) die("nn_value_fold_step: the forward's ReLU′ bits are missing");
+                phip_x3_bwd_x_fold(ly->d_grad_x, NULL, act_bits(nn, i + 1), fold->g, fold->Ws, bits, m, n, l);
+            }
+        } else if (i == L - 1 && want_gx && (!relu_in || bits) &&
             phip_out_bwd_wide(ly->d_grad_weights, ly->d_grad_biases, ly->d_grad_x, g, x, ly->d_weights, relu_in, m, n,
                               l)) {
             /* wide output layer (A = 17): grad_x and grad_W in one pass over the rows (out_head.hip) */
@@ -455,18 +476,71 @@ void nn_out_head_step(NeuralNetwork* nn, int head, const float* d_x, const int* 
                       const float* adv, const float* old_lp, float eps, float ent_coeff, float* grad_log_std,
                       float* loss_accum) {
     const int L = nn->num_layers - 1;
-    nn_forward_dev_upto(nn, d_x, d_rows, d_xcopy, m, L - 1);
+    nn_forward_dev_upto(nn, d_x, d_rows, d_xcopy, m, L - 1, NULL);
     nn_ensure_grad(nn, m);
     if (!grads_zero) phip_memset(nn->d_grads, 0, sizeof(float) * (size_t)nn->num_params);
     Layer* ly = &nn->layers[L - 1];
     const int b16 = nn->dtype == 1;            /* bf16 mode: bf16 activation / gradient, the W shadow */
+
     phip_out_head(head, b16, ly->d_input, nn_is_relu(nn, L - 2), b16 ? (const void*)(nn->d_w16 + nn->param_offset[L - 1])
                                                                      : (const void*)ly->d_weights,
                   ly->d_biases, m, ly->input_size, ly->output_size, tgt, log_std, action, adv, old_lp, eps, ent_coeff,
                   nn->layers[L].d_input, ly->d_grad_x, ly->d_grad_weights, ly->d_grad_biases, grad_log_std,
                   loss_accum);
     nn->d_output = nn->layers[L].d_input;
-    nn_backward_dev_top(nn, ly->d_grad_x, m, 0, 1, reduce_extra, L - 1);
+    nn_backward_dev_top(nn, ly->d_grad_x, m, 0, 1, reduce_extra, L - 1, NULL);
+}
+
+/* The value network's 1-wide output layer and MSE head folded into its last hidden layer's x3
+ * kernels (fp32, identity output after a ReLU hidden layer, the x3 engine at this m, no
+ * deterministic-GEMM request; PPO_VALUE_FOLD=0 disables it, read per call).  With h = relu(z) the
+ * last hidden activation, y = h·w + b and g = ∂L/∂y, the head's upper gradient is G = g·w·1[h > 0] —
+ * rank one — so it is never formed: the forward's epilogue leaves partial dots of h·w, one small kernel
+ * makes y, the loss, g, the output bias gradient and diag(w)·W, and the hidden layer's backward GEMMs take
+ * the 0/1 mask of h as their operand (one bf16 plane: three MFMA plane products instead of six) with g
+ * and w as row / column scales (gemm_x3.hip FOLD). */
+int nn_value_fold_ok(const NeuralNetwork* nn, int m) {
+    const char* e = getenv("PPO_VALUE_FOLD");
+    if ((e && e[0] == '0') || phip_gemm_deterministic()) return 0;     /* atomics in the gradient sums */
+    const int L = nn->num_layers - 1;
+    if (nn->dtype != 0 || L < 2 || nn->output_size != 1 || nn_is_relu(nn, L - 1) || !nn_is_relu(nn, L - 2)) return 0;
+    const Layer* hid = &nn->layers[L - 2];
+    const int n = hid->input_size, l = hid->output_size;
+    return use_x3_layer(m, n, l) && phip_x3_supported(0, m, n, l) && phip_x3_supported(1, m, n, l) &&
+           phip_x3_supported(2, m, n, l);
+}
+
+static float* g_fold_ws = NULL;       /* ypart [slots][m] | g [m] | diag(w)·W [l][n] */
+static size_t g_fold_cap = 0;
+
+void nn_value_fold_step(NeuralNetwork* nn, const float* d_x, const int* d_rows, float* d_xcopy, int m, int grads_zero,
+                        long reduce_extra, const float* tgt, float* loss_accum) {
+    const int L = nn->num_layers - 1;
+    Layer* hid = &nn->layers[L - 2];
+    Layer* out = &nn->layers[L - 1];
+    const int n = hid->input_size, l = hid->output_size;
+    const size_t mp = ((size_t)m + 3) & ~(size_t)3;
+    const size_t slots_max = 2 * (size_t)((l + 63) / 64);     /* column tiles (≥ 64 wide) × 2 waves along N */
+    const size_t need = slots_max * mp + mp + (size_t)l * n;
+    if (need > g_fold_cap) {
+        phip_free(g_fold_ws);
+        g_fold_ws = (float*)phip_malloc(sizeof(float) * need);
+        g_fold_cap = need;
+    }
+    float* ypart = g_fold_ws;
+    float* g = ypart + slots_max * mp;
+    float* Ws = g + mp;
+    FoldFwd ff = {out->d_weights, ypart, 0};
+    nn_forward_dev_upto(nn, d_x, d_rows, d_xcopy, m, L - 1, &ff);
+    if (ff.slots <= 0 || (size_t)ff.slots > slots_max) die("nn_value_fold_step: unexpected partial-dot slots");
+    nn_ensure_grad(nn, m);
+    if (!grads_zero) phip_memset(nn->d_grads, 0, sizeof(float) * (size_t)nn->num_params);
+    /* ypart rows are at stride m (phip_x3_fwd_vhead) */
+    phip_value_head(ypart, ff.slots, out->d_biases, tgt, m, nn->layers[L].d_input, g, out->d_grad_biases, loss_accum,
+                    out->d_weights, hid->d_weights, Ws, l, n);
+    nn->d_output = nn->layers[L].d_input;
+    const FoldBwd fb = {g, out->d_weights, Ws, out->d_grad_weights};
+    nn_backward_dev_top(nn, NULL, m, 0, 1, reduce_extra, L - 1, &fb);
 }
 
 /* The A = 17 policy network (C4): its output layer's backward fused with the policy head
@@ -496,7 +570,7 @@ void nn_policy_wide_step(NeuralNetwork* nn, const float* d_x, const int* d_rows,
                                    loss_accum, ly->d_input, ly->d_weights, nn_is_relu(nn, L - 2), ly->d_grad_weights,
                                    ly->d_grad_biases, ly->d_grad_x, m, ly->input_size, ly->output_size))
         die("nn_policy_wide_step: the wide head declined a shape nn_policy_wide_ok accepted");
-    nn_backward_dev_top(nn, ly->d_grad_x, m, 0, 1, reduce_extra, L - 1);
+    nn_backward_dev_top(nn, ly->d_grad_x, m, 0, 1, reduce_extra, L - 1, NULL);
 }
 
 /* neural_network.cu:74-105: copies the input into layers[0].d_input first. */

@@ -518,7 +518,7 @@ static int ppo_update_tiny(PPO* ppo, PPODev* d, int B, int n_epochs_policy, int 
 typedef struct {
     PPO* ppo;
     PPODev* d;
-    int B, S, A, limit, num_batches, comm, fuse_v, fuse_p, wide_p;
+    int B, S, A, limit, num_batches, comm, fuse_v, fuse_p, wide_p, fold_v;
     const int *perms_v, *perms_p;
     const uint64_t *keys_v, *keys_p;
     long nv, np;
@@ -550,7 +550,9 @@ static int value_step(StepCtx* c, long iv, int v_zero, int tab) {
     }
     /* with a communicator: gradients all-reduced in per-layer buckets as the backward produces them
      * (comm.hip's comm stream), joined before Adam */
-    if (c->fuse_v) {       /* output layer + MSE + output-layer backward in one pass (out_head.hip) */
+    if (c->fold_v && !tab) {   /* output layer + MSE folded into the last hidden layer (nn_value_fold_step) */
+        nn_value_fold_step(V, buf->state_p, d->rows, d->states, B, v_zero, c->comm ? 0 : -1, d->tgt, d->stats + 0);
+    } else if (c->fuse_v) {    /* output layer + MSE + output-layer backward in one pass (out_head.hip) */
         nn_out_head_step(V, 0, buf->state_p, d->rows, d->states, B, v_zero, c->comm ? 0 : -1, d->tgt, NULL, NULL,
                          NULL, NULL, 0.f, 0.f, NULL, d->stats + 0);
     } else {
@@ -654,7 +656,7 @@ static int step_graphs_ok(const StepCtx* c) {
         return 0;
     /* only the combination tests/test_gpu_update.py replays against eager launches: fp32 networks with
      * the fused output heads (value A = 1, policy A <= 6) */
-    if (ppo->V->dtype != 0 || ppo->policy->mu->dtype != 0 || !c->fuse_v || !c->fuse_p) return 0;
+    if (ppo->V->dtype != 0 || ppo->policy->mu->dtype != 0 || !c->fuse_v || !c->fuse_p || c->fold_v) return 0;
     return 1;
 }
 
@@ -796,8 +798,8 @@ static void ppo_update_body(PPO* ppo, float gamma, int batch_size, int n_epochs_
     if (concurrent) phip_side_fork();
     const int fuse_p = nn_out_head_ok(mu, 1);
     StepCtx c = {ppo, d, B, S, A, limit, num_batches, comm, nn_out_head_ok(V, 0), fuse_p,
-                 !fuse_p && nn_policy_wide_ok(mu, B), perms_v, perms_p, keys_v, keys_p, nv, np, NULL, NULL, NULL,
-                 NULL, 16, 1, 1};
+                 !fuse_p && nn_policy_wide_ok(mu, B), nn_value_fold_ok(V, B), perms_v, perms_p, keys_v, keys_p, nv, np,
+                 NULL, NULL, NULL, NULL, 16, 1, 1};
     {
         const char* ge = getenv("PPO_GRAPH_STEPS");
         if (ge && atoi(ge) > 0) c.K = atoi(ge);
