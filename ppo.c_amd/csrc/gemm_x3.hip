@@ -332,19 +332,27 @@ __device__ __forceinline__ void x3_epilogue_out(const X3Args& a, f32x16 (&acc)[T
         }
     }
     auto ydot_block = [&](float (&yp)[16], int i) {
+        // the two 16-lane rows of each half-wave add (lane i ↔ i ^ 16), then a reduce-scatter within each
+        // row on DPP moves (pairs i ↔ 15 − i, 7 − i, i ^ 2, i ^ 1: each pair keeps the half its higher
+        // member's bit selects), so lane i ends with value index i & 15
 #pragma unroll
         for (int u = 0; u < 16; ++u) yp[u] += __shfl_xor(yp[u], 16, 64);
+        const int li = lane & 15;
+        auto level = [&](auto CTRLc, auto Oc) {
+            constexpr int CTRL = decltype(CTRLc)::value, O = decltype(Oc)::value;
+            const bool up = (li & O) != 0;
 #pragma unroll
-        for (int o = 8; o >= 1; o >>= 1) {
-            const bool up = (r & o) != 0;
-#pragma unroll
-            for (int u = 0; u < o; ++u) {
-                const float send = up ? yp[u] : yp[u + o];
-                const float keep = up ? yp[u + o] : yp[u];
-                yp[u] = keep + __shfl_xor(send, o, 64);
+            for (int u = 0; u < O; ++u) {
+                const float send = up ? yp[u] : yp[u + O];
+                const float keep = up ? yp[u + O] : yp[u];
+                yp[u] = keep + ppo::dpp_mov<CTRL>(send);
             }
-        }
-        const int e = r & 15;
+        };
+        level(std::integral_constant<int, 0x140>{}, std::integral_constant<int, 8>{});   // row_mirror
+        level(std::integral_constant<int, 0x141>{}, std::integral_constant<int, 4>{});   // row_half_mirror
+        level(std::integral_constant<int, 0x4E>{}, std::integral_constant<int, 2>{});    // quad_perm [2,3,0,1]
+        level(std::integral_constant<int, 0xB1>{}, std::integral_constant<int, 1>{});    // quad_perm [1,0,3,2]
+        const int e = li;
         const int row = m0 + wm * WM + i * 32 + 4 * h + (e & 3) + 8 * (e >> 2);
         const int slot = (n0 / BN) * WARPS_N + wn;
         if (r < 16 && row < a.M) a.ypart[(long)slot * a.M + row] = yp[0];
@@ -1176,7 +1184,8 @@ int ppo_gemm_x3_tune(int force_cfg, int splitk_target) {
 }
 
 // average device µs of one launch (op 0 forward + bias + ReLU + bits, 1 grad_x with bits, 2 grad_W
-// + bias grad (split-K from zero), 3 forward without activation); cfg −1 = automatic
+// + bias grad (split-K from zero), 3 forward without activation, 4 – 6 the value-head fold variants of
+// 0 – 2); cfg −1 = automatic
 double ppo_bench_gemm_x3(int op, int m, int n, int l, int iters, int cfg, int splitk_target) {
     ppo::ensure_device();
     const size_t sx = (size_t)m * n, sw = (size_t)l * n, sy = (size_t)m * l;
@@ -1194,10 +1203,17 @@ double ppo_bench_gemm_x3(int op, int m, int n, int l, int iters, int cfg, int sp
     const int saved = g_force_x3, saved_split = g_split_x3;
     g_force_x3 = cfg;
     g_split_x3 = splitk_target;
+    // ops 4 – 6: the value-head fold variants (forward with the partial dots; grad_x from the mask words
+    // with the g row scale; grad_W from h with g / w scales and the output layer's gW)
+    float* fold = (op >= 4) ? (float*)phip_malloc(4 * ((size_t)m * (2 * ppo_divup(l, 64) + 1) + (size_t)l)) : nullptr;
+    if (fold) phip_fill_uniform(fold, (long)m * (2 * ppo_divup(l, 64) + 1) + l, 5, -0.1f, 0.1f);
     auto run = [&]() {
         if (op == 0) phip_x3_fwd(y, x, nullptr, nullptr, W, b, m, n, l, 1, bits);
         else if (op == 3) phip_x3_fwd(y, x, nullptr, nullptr, W, b, m, n, l, 0, nullptr);
         else if (op == 1) phip_x3_bwd_x(x, y, W, bits, m, n, l);
+        else if (op == 4) phip_x3_fwd_vhead(y, x, nullptr, nullptr, W, b, m, n, l, 1, bits, fold, fold + l);
+        else if (op == 5) phip_x3_bwd_x_fold(x, nullptr, bits, fold, W, bits, m, n, l);
+        else if (op == 6) phip_x3_bwd_w_fold(gw, b, y, fold, fold + m, fold + m + l, x, m, n, l, 0);
         else phip_x3_bwd_w(gw, b, y, x, m, n, l, 0);
     };
     for (int i = 0; i < 3; ++i) run();
@@ -1214,7 +1230,7 @@ double ppo_bench_gemm_x3(int op, int m, int n, int l, int iters, int cfg, int sp
     PPO_CHECK(hipEventDestroy(e1));
     g_force_x3 = saved;
     g_split_x3 = saved_split;
-    phip_free(x); phip_free(W); phip_free(y); phip_free(b); phip_free(gw); phip_free(bits);
+    phip_free(x); phip_free(W); phip_free(y); phip_free(b); phip_free(gw); phip_free(bits); phip_free(fold);
     return 1000.0 * ms / (iters > 0 ? iters : 1);
 }
 
