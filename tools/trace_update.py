@@ -20,7 +20,9 @@ anchor = [i for i, r in enumerate(rows) if "next_value_map" in r["Kernel_Name"] 
 j = anchor[-1] if anchor else len(rows) - 1
 while j > 0 and "adam" not in rows[j - 1]["Kernel_Name"]:
     j -= 1
-last = rows[j:]
+# … up to its last Adam launch (a bench run's rollout measurement may follow the update)
+end = max((i for i in range(j, len(rows)) if "adam" in rows[i]["Kernel_Name"]), default=len(rows) - 1)
+last = rows[j:end + 1]
 t0, t1 = int(last[0]["Start_Timestamp"]), int(last[-1]["End_Timestamp"])
 busy = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in last)
 print(f"update span {(t1 - t0) / 1e6:.2f} ms, kernel busy {busy / 1e6:.2f} ms, {len(last)} launches")
