@@ -12,13 +12,15 @@ ap.add_argument("trace")
 ap.add_argument("--top", type=int, default=30)
 args = ap.parse_args()
 rows = sorted(csv.DictReader(open(args.trace)), key=lambda r: int(r["Start_Timestamp"]))
-# the last update: everything after the previous update's last Adam launch — the GAE's V(state)
-# forward (every layer, m = N), its copies and fills, next_value_map_kernel, the own-row forward of
-# V(next_state), the scan, then the minibatch loops (round 5: the window used to start `layers` rows
-# before next_value_map_kernel and missed the first forward GEMMs and copies of the GAE)
+# the last update: from the GAE's V(state) forward (every layer, m = N) with its copies and fills,
+# next_value_map_kernel, the own-row forward of V(next_state), the scan, then the minibatch loops
+# (round 5: the window used to start `layers` rows before next_value_map_kernel and missed the first
+# forward GEMMs and copies of the GAE)
 anchor = [i for i, r in enumerate(rows) if "next_value_map" in r["Kernel_Name"] or "gae_block" in r["Kernel_Name"]]
 j = anchor[-1] if anchor else len(rows) - 1
-while j > 0 and "adam" not in rows[j - 1]["Kernel_Name"]:
+# walk back over the GAE's forward GEMMs and its copies / fills (a rollout or the previous update's
+# Adam ends the walk)
+while j > 0 and any(t in rows[j - 1]["Kernel_Name"] for t in ("gemm", "rocclr", "fill", "copy")):
     j -= 1
 # … up to its last Adam launch (a bench run's rollout measurement may follow the update)
 end = max((i for i in range(j, len(rows)) if "adam" in rows[i]["Kernel_Name"]), default=len(rows) - 1)
