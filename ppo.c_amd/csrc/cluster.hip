@@ -50,7 +50,7 @@ struct ClArgs {
     unsigned* ctr;                            // barrier arrivals (zeroed before the launch)
     unsigned* err;                            // host-visible error word (0 = fine)
     unsigned long long timeout;               // barrier wait bound (realtime ticks)
-    int active_stride;                        // workgroup b works iff b % active_stride == 0 (same-XCD bias)
+    int active_stride, active_offset;         // workgroup b works iff b % stride == offset (same-XCD bias)
     unsigned long long* stamps;               // diagnostics (PPO_CLUSTER_STAMPS): wall clock per phase,
                                               // workgroup 0, steps 0..63, 12 slots
 };
@@ -191,8 +191,12 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
     using L = Lay<H, HC>;
     constexpr int HP = L::HP, HCP = L::HCP;
     constexpr int SMALL_SLOTS = small_slots<HC>();
-    if ((int)blockIdx.x % a.active_stride) return;
-    const int cw = (int)blockIdx.x / a.active_stride;            // this workgroup's unit block
+    if ((int)blockIdx.x % a.active_stride != a.active_offset) return;
+    const int cw = (int)blockIdx.x / a.active_stride;
+    // diagnostics (PPO_CLUSTER_STAMPS): where this workgroup runs — XCC id, HW_ID (CU / SH / SE fields)
+    if (a.stamps && threadIdx.x == 0)
+        a.stamps[64 * 32 + cw] = ((unsigned long long)__builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11)) << 32) |
+                                 __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));            // this workgroup's unit block
     const int c0 = cw * HC;
     extern __shared__ float lds[];
     int* flag = reinterpret_cast<int*>(lds + L::flag);
@@ -558,8 +562,8 @@ unsigned* g_err = nullptr;            // host-mapped error word
 // PPO_CLUSTER_STAMPS: one stamp buffer per stream (the phases run concurrently) and the report that
 // phip_cluster_report prints once the phases have joined
 struct StampSlot {
-    unsigned long long* buf = nullptr;
-    int nstamp = 0, policy = 0, total_steps = 0, pending = 0;
+    unsigned long long* buf = nullptr;                // [64 steps][32 stamps] | [64 workgroups] placement
+    int nstamp = 0, policy = 0, total_steps = 0, pending = 0, nwg = 0;
     const char* kind = nullptr;
     const char* const* names = nullptr;
 };
@@ -589,10 +593,11 @@ bool host_grid_fits(const void* kfn, size_t lds, int grid) {
     return (long)per_cu * cus >= 2L * grid;
 }
 
-unsigned long long* host_stamps(int nstamp, const char* kind, const char* const* names, int policy, int total_steps) {
+unsigned long long* host_stamps(int nstamp, const char* kind, const char* const* names, int policy, int total_steps,
+                                int nwg) {
     StampSlot& s = g_stamps[phip_side_active() ? 1 : 0];
-    if (!s.buf) s.buf = (unsigned long long*)phip_malloc(sizeof(unsigned long long) * 64 * 32);
-    s.nstamp = nstamp; s.kind = kind; s.names = names; s.policy = policy; s.total_steps = total_steps;
+    if (!s.buf) s.buf = (unsigned long long*)phip_malloc(sizeof(unsigned long long) * (64 * 32 + 64));
+    s.nstamp = nstamp; s.kind = kind; s.names = names; s.policy = policy; s.total_steps = total_steps; s.nwg = nwg;
     s.pending = total_steps >= 64;
     return s.buf;
 }
@@ -626,6 +631,19 @@ void phip_cluster_report(void) {
         fprintf(stderr, "%s %s step (us):", s.kind, s.policy ? "policy" : "value");
         for (int k = 0; k < s.nstamp; ++k) { fprintf(stderr, " %s %.2f", s.names[k], acc[k] / 62); tot += acc[k] / 62; }
         fprintf(stderr, " | total %.2f\n", tot);
+        // placement: per workgroup XCC id and HW_ID's CU [11:8] / SH [12] / SE [14:13] fields
+        unsigned long long pl[64];
+        phip_d2h(pl, s.buf + 64 * 32, sizeof(unsigned long long) * (size_t)s.nwg);
+        int per_xcc[16] = {0};
+        fprintf(stderr, "%s %s placement (xcc.se.sh.cu):", s.kind, s.policy ? "policy" : "value");
+        for (int w = 0; w < s.nwg; ++w) {
+            const unsigned xcc = (unsigned)(pl[w] >> 32) & 15u, hw = (unsigned)pl[w];
+            per_xcc[xcc]++;
+            fprintf(stderr, " %u.%u.%u.%u", xcc, (hw >> 13) & 3u, (hw >> 12) & 1u, (hw >> 8) & 15u);
+        }
+        fprintf(stderr, " | per XCC:");
+        for (int x = 0; x < 8; ++x) fprintf(stderr, " %d", per_xcc[x]);
+        fprintf(stderr, "\n");
     }
 }
 
@@ -722,9 +740,12 @@ int phip_cluster_update(const PhipTinyNet* net, const PhipTinyPhase* ph) {
     a.X1 = ws.X1; a.Y = ws.Y; a.G1 = ws.G1; a.ctr = ws.ctr; a.err = d_err;
     a.timeout = host_timeout_ticks();
     a.active_stride = stride;
+    // stride 8 puts a phase on one XCD (blocks b, b + 8 share one); the policy phase then takes XCD 4
+    // so the two concurrent phases never share CUs
+    a.active_offset = stride == 8 && ph->policy ? 4 : 0;
     static const char* names[12] = {"gather", "L0", "barrier A", "h1 load", "L1+Y", "barrier B", "head+bwd",
                                     "G1+gW1 adam", "barrier C", "g1+gW0", "adam", "step->next"};
-    if (getenv("PPO_CLUSTER_STAMPS")) a.stamps = host_stamps(12, "cluster", names, ph->policy, a.total_steps);
+    if (getenv("PPO_CLUSTER_STAMPS")) a.stamps = host_stamps(12, "cluster", names, ph->policy, a.total_steps, NWG);
     PPO_CHECK(hipMemsetAsync(ws.ctr, 0, 128 * CLU_REPL, ppo::stream()));
     ppo::ProfScope ps(PPO_K_OTHER, 0.0);
     hipLaunchKernelGGL(kfn, dim3(NWG * a.active_stride), dim3(TPB), bytes, ppo::stream(), a);

@@ -193,6 +193,7 @@ unsigned long long host_timeout_ticks();
 bool host_grid_fits(const void* kfn, size_t lds, int grid);
 // Per-stream diagnostics (PPO_CLUSTER_STAMPS): the stamp buffer of the calling stream, and a pending
 // report printed by phip_cluster_report() after the phases joined (no mid-phase synchronisation).
-unsigned long long* host_stamps(int nstamp, const char* kind, const char* const* names, int policy, int total_steps);
+unsigned long long* host_stamps(int nstamp, const char* kind, const char* const* names, int policy, int total_steps,
+                                int nwg);
 
 }  // namespace clu

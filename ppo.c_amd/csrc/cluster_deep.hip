@@ -66,7 +66,7 @@ struct DArgs {
                                                      // G3 [64][GP], Pa / Pb [NWG][64][H])
     unsigned *ctr, *err;
     unsigned long long timeout;                      // barrier wait bound (realtime ticks)
-    int active_stride;
+    int active_stride, active_offset;                // workgroup b works iff b % stride == offset
     unsigned long long* stamps;                      // PPO_CLUSTER_STAMPS: workgroup 0, steps 0..63
 };
 
@@ -317,8 +317,12 @@ __device__ __forceinline__ void publish_partial(int tid, __amdgpu_buffer_rsrc_t 
     } while (0)
 
 __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
-    if ((int)blockIdx.x % a.active_stride) return;
+    if ((int)blockIdx.x % a.active_stride != a.active_offset) return;
     const int cw = (int)blockIdx.x / a.active_stride;
+    // diagnostics (PPO_CLUSTER_STAMPS): where this workgroup runs — XCC id, HW_ID (CU / SH / SE fields)
+    if (a.stamps && threadIdx.x == 0)
+        a.stamps[64 * 32 + cw] = ((unsigned long long)__builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11)) << 32) |
+                                 __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));
     const int c0 = cw * HC;
     extern __shared__ float lds[];
     int* flag = reinterpret_cast<int*>(lds + L::flag);
@@ -766,10 +770,14 @@ int phip_cluster_deep_update(const PhipTinyNet* net, const PhipTinyPhase* ph) {
     a.ctr = ws.ctr; a.err = d_err;
     a.timeout = host_timeout_ticks();
     a.active_stride = stride;
+    // stride 8 puts a phase on one XCD (blocks b, b + 8 share one); the policy phase then takes XCD 4
+    // so the two concurrent phases never share CUs
+    a.active_offset = stride == 8 && ph->policy ? 4 : 0;
     static const char* names[NSTAMP] = {"L0", "bar A", "L1", "bar B", "L2+Y", "bar C", "head", "bar D",
                                         "g3+P2", "gW2 adam", "bar E", "g2+P1", "gW1 adam", "bar F",
                                         "g1 reduce", "gW0 adam", "gb0+b0", "step->next"};
-    if (getenv("PPO_CLUSTER_STAMPS")) a.stamps = host_stamps(NSTAMP, "cluster_deep", names, ph->policy, a.total_steps);
+    if (getenv("PPO_CLUSTER_STAMPS"))
+        a.stamps = host_stamps(NSTAMP, "cluster_deep", names, ph->policy, a.total_steps, NWG);
     PPO_CHECK(hipMemsetAsync(ws.ctr, 0, 128 * CLU_REPL, ppo::stream()));
     ppo::ProfScope ps(PPO_K_OTHER, 0.0);
     hipLaunchKernelGGL(cluster_deep_kernel, dim3(NWG * a.active_stride), dim3(TPB), bytes, ppo::stream(), a);
