@@ -286,7 +286,7 @@ struct StageX3 {
 // ---------------------------------------------------------------------------------------------
 // ABL (timing ablations, results wrong; PPO_X3_ABLATE, -DPPO_X3_DIAG builds, cfgs 0 and 3): 1 = no
 // MFMAs, 2 = no split / LDS stores, 4 = no epilogue stores, 8 = no global loads after the prologue,
-// 32 = stamps, 64 = no split (raw bits stored to the planes)
+// 32 = stamps, 64 = no split (raw bits stored to the planes), 128 = every other k-tile barrier skipped
 // forward / grad_x epilogue: 32×32 accumulator block (i, j): lane (r, h) holds column r, rows
 // 4h + (e&3) + 8(e>>2).  Branch-free per element: the bias loads hoisted, the ReLU′-bit ballots in a
 // loop version of their own, grad_x's mask words brought into LDS (BM·BN/32 words, free on entry) by
@@ -664,7 +664,7 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
 #ifdef PPO_X3_PRIO
         __builtin_amdgcn_s_setprio(0);
 #endif
-        __syncthreads();
+        if (!((ABL & 128) && (j & 1))) __syncthreads();      // (ABL 128, timing only: every other barrier)
     };
     auto mainloop = [&](auto COPYc, auto SYNc) {
         unsigned short* cur = ring;
@@ -951,7 +951,11 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
 // tail drains under the second round's mainloop)
 struct CfgX3 { int bm, bn, kg, slots_per_cu; };
 constexpr CfgX3 kCfgX3[] = {{256, 256, 1, 1}, {128, 128, 1, 2}, {128, 128, 1, 1}, {128, 128, 2, 1}, {64, 64, 1, 4},
-                            {256, 128, 1, 1}};
+                            {256, 128, 1, 1}
+#ifdef PPO_X3_DIAG
+                            , {64, 64, 1, 8}, {64, 64, 1, 8}, {128, 64, 1, 4}, {128, 64, 1, 4}
+#endif
+};
 int g_force_x3 = -1;
 int g_split_x3 = 0;
 
@@ -988,8 +992,18 @@ void launch_cfg_x3(int c, const X3Args& a) {
             case 8: run(std::integral_constant<int, 8>{}); return;
             case 32: run(std::integral_constant<int, 32>{}); return;
             case 64: run(std::integral_constant<int, 64>{}); return;
+            case 128: run(std::integral_constant<int, 128>{}); return;
             default: break;
         }
+    }
+    // small-tile shape candidates (timing only): 6 = 64×64 over 2 waves of 32×64, 7 = 64×64 over 2 waves
+    // of 64×32, 8 = 128×64 over 4 waves of 64×32, 9 = 128×64 over 4 waves of 32×64
+    switch (c) {
+        case 6: launch_x3<OP, 64, 64, 2, 128, 8, 1>(a); return;
+        case 7: launch_x3<OP, 64, 64, 1, 128, 8, 1>(a); return;
+        case 8: launch_x3<OP, 128, 64, 2, 256, 4, 1>(a); return;
+        case 9: launch_x3<OP, 128, 64, 4, 256, 4, 1>(a); return;
+        default: break;
     }
 #endif
     switch (c) {

@@ -47,6 +47,12 @@ typedef struct {
     int* ctr;                     /* [2] step counters, [2] tickets (as unsigned) */
     PhipStepArgs* h_tab;
     long h_tab_cap;
+    /* phase gathers: every minibatch step's row indices and per-row inputs of a whole phase, gathered
+     * by one launch per epoch before the loops (value: rows, targets; policy: rows, actions, old
+     * log-probs, advantages) — step iv reads its B rows at iv·B */
+    int* ph_rows[2];
+    float *ph_tgt, *ph_act, *ph_olp, *ph_adv;
+    long ph_cap[2];
 } PPODev;
 
 static float* g_v = NULL;         /* V(state), V(next_state) for compute_gae_cuda */
@@ -128,6 +134,8 @@ static void free_dev_ws(PPO* ppo) {
     phip_free(d->rows_p); phip_free(d->states_p);
     for (int i = 0; i < 3; i++) phip_free(d->tiny_steps[i]);
     phip_free(d->tab[0]); phip_free(d->tab[1]); phip_free(d->ctr);
+    phip_free(d->ph_rows[0]); phip_free(d->ph_rows[1]); phip_free(d->ph_tgt); phip_free(d->ph_act);
+    phip_free(d->ph_olp); phip_free(d->ph_adv);
     free(d->h_tab);
     free(d);
     ppo->dev = NULL;
@@ -526,6 +534,7 @@ typedef struct {
     void *gv1, *gp1;              /* … and of one step (the remainder) */
     int K;                        /* requested steps per graph (PPO_GRAPH_STEPS, default 16) */
     long Kv, Kp;                  /* steps per graph as captured */
+    int phg;                      /* the phases' inputs were gathered up front (PPODev ph_*) */
 } StepCtx;
 
 /* value step iv (tab: the step-table form captured into a graph: gather and Adam read their
@@ -537,9 +546,14 @@ static int value_step(StepCtx* c, long iv, int v_zero, int tab) {
     TrajectoryBuffer* buf = ppo->buffer;
     NeuralNetwork* V = ppo->V;
     const int B = c->B;
+    const int* rows = d->rows;
+    const float* tgt = d->tgt;
     if (tab) {
         phip_gather_rows_tab(d->tab[0], d->ctr + 0, c->perms_v, c->limit, B, c->A, buf->action_p, buf->logprob_p,
                              buf->advantage_p, buf->adv_target_p, NULL, NULL, NULL, d->tgt, d->rows);
+    } else if (c->phg) {
+        rows = d->ph_rows[0] + iv * B;
+        tgt = d->ph_tgt + iv * B;
     } else {
         const int j = (int)(iv / c->num_batches), k = (int)(iv % c->num_batches);
         const int* perm = c->perms_v ? c->perms_v + (long)j * c->limit : NULL;
@@ -551,13 +565,13 @@ static int value_step(StepCtx* c, long iv, int v_zero, int tab) {
     /* with a communicator: gradients all-reduced in per-layer buckets as the backward produces them
      * (comm.hip's comm stream), joined before Adam */
     if (c->fold_v && !tab) {   /* output layer + MSE folded into the last hidden layer (nn_value_fold_step) */
-        nn_value_fold_step(V, buf->state_p, d->rows, d->states, B, v_zero, c->comm ? 0 : -1, d->tgt, d->stats + 0);
+        nn_value_fold_step(V, buf->state_p, rows, d->states, B, v_zero, c->comm ? 0 : -1, tgt, d->stats + 0);
     } else if (c->fuse_v) {    /* output layer + MSE + output-layer backward in one pass (out_head.hip) */
-        nn_out_head_step(V, 0, buf->state_p, d->rows, d->states, B, v_zero, c->comm ? 0 : -1, d->tgt, NULL, NULL,
+        nn_out_head_step(V, 0, buf->state_p, rows, d->states, B, v_zero, c->comm ? 0 : -1, tgt, NULL, NULL,
                          NULL, NULL, 0.f, 0.f, NULL, d->stats + 0);
     } else {
-        nn_forward_dev_rows(V, buf->state_p, d->rows, d->states, B);
-        phip_mse(V->d_output, d->tgt, B, d->gv, NULL, d->stats + 0);
+        nn_forward_dev_rows(V, buf->state_p, rows, d->states, B);
+        phip_mse(V->d_output, tgt, B, d->gv, NULL, d->stats + 0);
         nn_backward_dev_z(V, d->gv, B, 0, v_zero, c->comm ? 0 : -1);
     }
     phip_allreduce_join();
@@ -575,9 +589,16 @@ static void policy_step(StepCtx* c, long ip, int* p_zero, int* ls_zero, int tab)
     GaussianPolicy* pol = ppo->policy;
     NeuralNetwork* mu = pol->mu;
     const int B = c->B, A = c->A;
+    const int* rows = d->rows_p;
+    const float *act = d->actions, *olp = d->old_lp, *adv = d->adv;
     if (tab) {
         phip_gather_rows_tab(d->tab[1], d->ctr + 1, c->perms_p, c->limit, B, A, buf->action_p, buf->logprob_p,
                              buf->advantage_p, buf->adv_target_p, d->actions, d->old_lp, d->adv, NULL, d->rows_p);
+    } else if (c->phg) {
+        rows = d->ph_rows[1] + ip * B;
+        act = d->ph_act + ip * B * A;
+        olp = d->ph_olp + ip * B;
+        adv = d->ph_adv + ip * B;
     } else {
         const int j = (int)(ip / c->num_batches), k = (int)(ip % c->num_batches);
         const int* perm = c->perms_p ? c->perms_p + (long)j * c->limit : NULL;
@@ -588,17 +609,17 @@ static void policy_step(StepCtx* c, long ip, int* p_zero, int* ls_zero, int tab)
     /* μ grads + (top bucket) the log σ gradient behind them */
     if (c->fuse_p) {       /* output layer + clipped surrogate + output-layer backward (out_head.hip) */
         if (!*ls_zero) phip_memset(pol->d_log_std_grad, 0, sizeof(float) * (size_t)A);
-        nn_out_head_step(mu, 1, buf->state_p, d->rows_p, d->states_p, B, *p_zero, c->comm ? align4(A) : -1, NULL,
-                         pol->d_log_std, d->actions, d->adv, d->old_lp, ppo->epsilon, ppo->ent_coeff,
+        nn_out_head_step(mu, 1, buf->state_p, rows, d->states_p, B, *p_zero, c->comm ? align4(A) : -1, NULL,
+                         pol->d_log_std, act, adv, olp, ppo->epsilon, ppo->ent_coeff,
                          pol->d_log_std_grad, d->stats + 1);
     } else if (c->wide_p) { /* A = 17: policy head + output-layer backward in one pass (out_head.hip) */
         if (!*ls_zero) phip_memset(pol->d_log_std_grad, 0, sizeof(float) * (size_t)A);
-        nn_policy_wide_step(mu, buf->state_p, d->rows_p, d->states_p, B, *p_zero, c->comm ? align4(A) : -1,
-                            pol->d_log_std, d->actions, d->adv, d->old_lp, ppo->epsilon, ppo->ent_coeff,
+        nn_policy_wide_step(mu, buf->state_p, rows, d->states_p, B, *p_zero, c->comm ? align4(A) : -1,
+                            pol->d_log_std, act, adv, olp, ppo->epsilon, ppo->ent_coeff,
                             pol->d_log_std_grad, d->stats + 1);
     } else {
-        nn_forward_dev_rows(mu, buf->state_p, d->rows_p, d->states_p, B);
-        phip_policy_head(mu->d_output, pol->d_log_std, d->actions, d->adv, d->old_lp, B, A, ppo->epsilon,
+        nn_forward_dev_rows(mu, buf->state_p, rows, d->states_p, B);
+        phip_policy_head(mu->d_output, pol->d_log_std, act, adv, olp, B, A, ppo->epsilon,
                          ppo->ent_coeff, d->gmu, pol->d_log_std_grad, d->stats + 1, *ls_zero);
         nn_backward_dev_z(mu, d->gmu, B, 0, *p_zero, c->comm ? align4(A) : -1);
     }
@@ -735,6 +756,47 @@ static void capture_steps(StepCtx* c, int ph) {
 static void ppo_update_body(PPO* ppo, float gamma, int batch_size, int n_epochs_policy, int n_epochs_value,
                             int shuffle_mode, unsigned long long seed);
 
+/* the phases' minibatch inputs, gathered before the loops: the rows of epoch j's steps are one gather
+ * of num_batches·B consecutive list positions (step k's slot i is position k·B + i, modulo the buffer
+ * length, as the per-step gather takes it — trajectory_buffer.cu get_batch), so ph_rows[p] + iv·B holds
+ * exactly the rows step iv would have gathered */
+static void phase_gather(StepCtx* c) {
+    PPO* ppo = c->ppo;
+    PPODev* d = c->d;
+    TrajectoryBuffer* buf = ppo->buffer;
+    const long B = c->B, A = c->A, per = (long)c->num_batches * B;
+    for (int ph = 0; ph < 2; ph++) {
+        const long n = ph ? c->np : c->nv;
+        if (n <= 0) continue;
+        if (n * B > d->ph_cap[ph]) {
+            phip_free(d->ph_rows[ph]);
+            d->ph_rows[ph] = (int*)phip_malloc(sizeof(int) * (size_t)(n * B));
+            if (ph) {
+                phip_free(d->ph_act); phip_free(d->ph_olp); phip_free(d->ph_adv);
+                d->ph_act = (float*)phip_malloc(sizeof(float) * (size_t)(n * B * A));
+                d->ph_olp = (float*)phip_malloc(sizeof(float) * (size_t)(n * B));
+                d->ph_adv = (float*)phip_malloc(sizeof(float) * (size_t)(n * B));
+            } else {
+                phip_free(d->ph_tgt);
+                d->ph_tgt = (float*)phip_malloc(sizeof(float) * (size_t)(n * B));
+            }
+            d->ph_cap[ph] = n * B;
+        }
+        const int* perms = ph ? c->perms_p : c->perms_v;
+        const uint64_t* keys = ph ? c->keys_p : c->keys_v;
+        for (long j = 0; j * c->num_batches < n; j++) {
+            const long steps = n - j * c->num_batches < c->num_batches ? n - j * c->num_batches : c->num_batches;
+            const long o = j * per;
+            if (steps * B >= (1L << 31)) die("ppo_update: a phase epoch exceeds 2^31 rows");
+            phip_gather_rows(perms ? perms + j * c->limit : NULL, keys[j], 0, c->limit, (int)(steps * B), c->S, c->A,
+                             buf->state_p, buf->action_p, buf->logprob_p, buf->advantage_p, buf->adv_target_p, NULL,
+                             ph ? d->ph_act + o * A : NULL, ph ? d->ph_olp + o : NULL, ph ? d->ph_adv + o : NULL,
+                             ph ? NULL : d->ph_tgt + o, d->ph_rows[ph] + o);
+        }
+    }
+    c->phg = 1;
+}
+
 void ppo_update(void* vppo, float gamma, int batch_size, int n_epochs_policy, int n_epochs_value, int shuffle_mode,
                 unsigned long long seed) {
     PPO* ppo = (PPO*)vppo;
@@ -795,11 +857,10 @@ static void ppo_update_body(PPO* ppo, float gamma, int batch_size, int n_epochs_
     const int* perms_p = phase_perms(ppo, d, shuffle_mode, n_epochs_policy, limit, 1, keys_p);
     const char* serial_env = getenv("PPO_SERIAL");
     const int concurrent = nv > 0 && np > 0 && !(serial_env && *serial_env && *serial_env != '0');
-    if (concurrent) phip_side_fork();
     const int fuse_p = nn_out_head_ok(mu, 1);
     StepCtx c = {ppo, d, B, S, A, limit, num_batches, comm, nn_out_head_ok(V, 0), fuse_p,
                  !fuse_p && nn_policy_wide_ok(mu, B), nn_value_fold_ok(V, B), perms_v, perms_p, keys_v, keys_p, nv, np,
-                 NULL, NULL, NULL, NULL, 16, 1, 1};
+                 NULL, NULL, NULL, NULL, 16, 1, 1, 0};
     {
         const char* ge = getenv("PPO_GRAPH_STEPS");
         if (ge && atoi(ge) > 0) c.K = atoi(ge);
@@ -808,6 +869,10 @@ static void ppo_update_body(PPO* ppo, float gamma, int batch_size, int n_epochs_
      * step runs eagerly — workspaces allocated, gradients cleared — and the last one too, so the
      * caller can read its gradients) */
     const int graphs = step_graphs_ok(&c);
+    /* eager steps: every step's gathered inputs up front (one launch per epoch instead of one per
+     * step; on libppo's stream before the fork, so both loops see them) */
+    if (!graphs) phase_gather(&c);
+    if (concurrent) phip_side_fork();
     long iv = 0, ip = 0;
     /* gradients cleared by the previous Adam step (not after a loop's last step: a caller may read
      * the last minibatch's gradients after the update) */
