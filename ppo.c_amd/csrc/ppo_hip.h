@@ -86,13 +86,6 @@ int  phip_x3_fwd_vhead(float* y, const float* x, const int* ridx, float* xcopy, 
                        int n, int l, int relu, unsigned* bits, const float* ydot, float* ypart);
 void phip_x3_bwd_x_fold(float* gx, const float* g, const unsigned* fold_bits, const float* fold_g, const float* W,
                         const unsigned* bits, int m, int n, int l);
-/* narrow.hip: the input layer of networks with ≤ 32 inputs (l % 64 == 0) on the VALU — forward with the
- * fused row gather (+ copy), ReLU and bits; grad_W / grad_b by per-workgroup f32 atomics (zero on entry
- * unless zeroed == 0) */
-int phip_narrow_supported(int m, int n, int l);
-void phip_narrow_fwd(float* y, const float* x, const int* ridx, float* xcopy, const float* W, const float* b, int m,
-                     int n, int l, int relu, unsigned* bits);
-void phip_narrow_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, int n, int l, int zeroed);
 void phip_x3_bwd_w_fold(float* gW, float* gb, const float* h, const float* fold_g, const float* fold_w, float* fold_gw,
                         const float* x, int m, int n, int l, int zeroed);
 /* dst[i, :] = bf16(src[rows[i], :]) for i < m (S % 4 == 0): layer 0's gather in bf16 mode */

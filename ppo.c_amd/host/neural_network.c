@@ -273,9 +273,6 @@ static int use_x3(int m) { return m > 1024 && ppo_gemm_f32_engine(-1) == 1; }
 /* per layer: the 1- and A-wide output layers are latency-bound skinny products where the exact
  * kernels (and their paired backward launch) measure faster (profiles/r01_x3_sweep.txt) */
 static int use_x3_layer(int m, int n, int l) { return use_x3(m) && n > 32 && l > 32; }
-/* the input layer of a network with ≤ 32 inputs at minibatch sizes: narrow.hip's VALU kernels (the GEMM
- * engines' k-tiles would be mostly padding and their fixed latency the cost) */
-static int use_narrow(int m, int n, int l) { return m > 1024 && phip_narrow_supported(m, n, l); }
 /* the reference-API products (mat_mul*_cuda, layers.c) through the same engine choice (fp32 storage).
  * Callers may pass any valid device pointer (a row or element offset into a buffer); the x3 kernels
  * need 16-B aligned operands, so an unaligned operand routes to the exact family, which has a scalar
@@ -334,9 +331,6 @@ static void nn_forward_dev_upto(NeuralNetwork* nn, const float* d_x, const int* 
         } else if (use_x3_layer(m, n, l) && phip_x3_supported(0, m, n, l)) {
             phip_x3_fwd(out, in, i == 0 ? d_rows : NULL, i == 0 ? d_xcopy : NULL, ly->d_weights, ly->d_biases, m, n,
                         l, nn_is_relu(nn, i), act_bits(nn, i + 1));
-        } else if (i == 0 && use_narrow(m, n, l)) {
-            phip_narrow_fwd(out, in, d_rows, d_xcopy, ly->d_weights, ly->d_biases, m, n, l, nn_is_relu(nn, i),
-                            act_bits(nn, i + 1));
         } else if (i == 0 && d_rows) {
             phip_linear_fwd_gather(out, in, d_rows, d_xcopy, ly->d_weights, ly->d_biases, m, n, l, nn_is_relu(nn, i),
                                    act_bits(nn, i + 1));
@@ -443,8 +437,6 @@ static void nn_backward_dev_top(NeuralNetwork* nn, const float* d_grad_out, int 
             phip_out_bwd_wide(ly->d_grad_weights, ly->d_grad_biases, ly->d_grad_x, g, x, ly->d_weights, relu_in, m, n,
                               l)) {
             /* wide output layer (A = 17): grad_x and grad_W in one pass over the rows (out_head.hip) */
-        } else if (i == 0 && !want_gx && use_narrow(m, n, l) && !phip_gemm_deterministic()) {
-            phip_narrow_bwd_w(ly->d_grad_weights, ly->d_grad_biases, g, x, m, n, l, 1);
         } else if (use_x3_layer(m, n, l) && phip_x3_supported(2, m, n, l)) {
             phip_x3_bwd_w(ly->d_grad_weights, ly->d_grad_biases, g, x, m, n, l, 1);
             if (want_gx && (!relu_in || bits)) phip_x3_bwd_x(ly->d_grad_x, g, ly->d_weights, bits, m, n, l);

@@ -13,4 +13,10 @@ for rep in 1 2; do
     done
     echo "ablate 128: $(PPO_LIB=$D PPO_X3_ABLATE=128 GEMM_ENGINE=x3 timeout -k 5 60 python tools/gemm_one.py $s 4 100)"
   done
+  # grad_W (split-K + slab reduce): 128x128 two k-groups (cfg 3, production) vs 64x64 (cfg 4)
+  for s in "2 4096 512 512" "2 8192 256 256" "2 4096 376 512"; do
+    for c in 3 4; do
+      PPO_LIB=$D GEMM_ENGINE=x3 timeout -k 5 60 python tools/gemm_one.py $s $c 100
+    done
+  done
 done
