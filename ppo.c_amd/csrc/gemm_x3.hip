@@ -951,11 +951,7 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
 // tail drains under the second round's mainloop)
 struct CfgX3 { int bm, bn, kg, slots_per_cu; };
 constexpr CfgX3 kCfgX3[] = {{256, 256, 1, 1}, {128, 128, 1, 2}, {128, 128, 1, 1}, {128, 128, 2, 1}, {64, 64, 1, 4},
-                            {256, 128, 1, 1}
-#ifdef PPO_X3_DIAG
-                            , {64, 64, 1, 8}, {64, 64, 1, 8}, {128, 64, 1, 4}, {128, 64, 1, 4}
-#endif
-};
+                            {256, 128, 1, 1}};
 int g_force_x3 = -1;
 int g_split_x3 = 0;
 
@@ -995,15 +991,6 @@ void launch_cfg_x3(int c, const X3Args& a) {
             case 128: run(std::integral_constant<int, 128>{}); return;
             default: break;
         }
-    }
-    // small-tile shape candidates (timing only): 6 = 64×64 over 2 waves of 32×64, 7 = 64×64 over 2 waves
-    // of 64×32, 8 = 128×64 over 4 waves of 64×32, 9 = 128×64 over 4 waves of 32×64
-    switch (c) {
-        case 6: launch_x3<OP, 64, 64, 2, 128, 8, 1>(a); return;
-        case 7: launch_x3<OP, 64, 64, 1, 128, 8, 1>(a); return;
-        case 8: launch_x3<OP, 128, 64, 2, 256, 4, 1>(a); return;
-        case 9: launch_x3<OP, 128, 64, 4, 256, 4, 1>(a); return;
-        default: break;
     }
 #endif
     switch (c) {
