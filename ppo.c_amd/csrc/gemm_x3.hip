@@ -74,8 +74,46 @@ struct X3Args {
     const unsigned* fold_bits;            // grad_x: the mask words of h [M][fold_wpr]
     int fold_wpr;
     float* fold_gw;                       // grad_W (A = h, fp32): + Σ_rows g·h per unit — the output layer's gW
+    // grad_x carrying the previous grad_W's split-K reduction (phip_x3_defer_reduce): workgroups
+    // gemm_wgs … gemm_wgs + red_wgs − 1 sum red_splits slabs of red_n floats (stride red_stride) into red_out
+    const float* red_slab; float* red_out;
+    long red_n, red_stride;
+    int red_splits, red_wgs, gemm_wgs;
     hipEvent_t ev_start, ev_stop;         // explicit dispatch-stamped events (ppo_prof kernel timing)
 };
+
+// the split-K slab sum of ONE reduce workgroup of NTH threads, in slab_reduce_kernel<4>'s order (four split
+// groups, each summing its splits in order, the groups' partials added in order): NTH/4 float4 columns per
+// workgroup, so the result is bitwise that of the standalone reduce
+template <int NTH>
+__device__ __forceinline__ void x3_slab_reduce_block(const X3Args& a, int blk, float* part) {
+    typedef float f32x4_ __attribute__((ext_vector_type(4)));
+    constexpr int Q = 4, C = NTH / Q;
+    const int c = threadIdx.x % C, q = threadIdx.x / C;
+    const long n4 = (a.red_n + 3) >> 2, s4 = a.red_stride >> 2;
+    const long i = (long)blk * C + c;
+    const int per = (a.red_splits + Q - 1) / Q;
+    const int s0 = q * per, s1 = min(a.red_splits, s0 + per);
+    const f32x4_* __restrict__ sv = reinterpret_cast<const f32x4_*>(a.red_slab);
+    f32x4_ acc = {0.f, 0.f, 0.f, 0.f};
+    if (i < n4) {
+#pragma unroll 8
+        for (int sp = s0; sp < s1; ++sp) acc += sv[(long)sp * s4 + i];
+    }
+    f32x4_* pv = reinterpret_cast<f32x4_*>(part);
+    if (q) pv[(q - 1) * C + c] = acc;
+    __syncthreads();
+    if (q == 0 && i < n4) {
+#pragma unroll
+        for (int v = 0; v < Q - 1; ++v) acc += pv[v * C + c];
+        if (4 * i + 4 <= a.red_n) {
+            reinterpret_cast<f32x4_*>(a.red_out)[i] = acc;
+        } else {
+            for (int e = 0; e < 4; ++e)
+                if (4 * i + e < a.red_n) a.red_out[4 * i + e] = acc[e];
+        }
+    }
+}
 
 // fp32 → bf16 round to nearest even (NaN stays NaN): v_cvt_pk_bf16_f32
 __device__ __forceinline__ unsigned pack2(float lo, float hi) {
@@ -432,9 +470,17 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     constexpr int NS = 3;                                          // LDS ring stages
     extern __shared__ __attribute__((aligned(16))) unsigned short lds[];     // KG × NS × BUF
 
+    // grad_x launches may carry the previous grad_W's slab reduce in extra workgroups past the tiles
+    if constexpr (OP == OP_NN) {
+        if (a.red_wgs && (int)blockIdx.x >= a.gemm_wgs) {
+            x3_slab_reduce_block<NTH>(a, (int)blockIdx.x - a.gemm_wgs, reinterpret_cast<float*>(lds));
+            return;
+        }
+    }
+
     // XCD-aware remap: hardware deals blocks round-robin over the 8 XCDs; give each XCD a
     // contiguous range of linear tiles (n fastest), so tiles sharing an A panel share an L2
-    const int nwg = gridDim.x, b = blockIdx.x;
+    const int nwg = (OP == OP_NN && a.red_wgs) ? a.gemm_wgs : (int)gridDim.x, b = blockIdx.x;
     const int xcd = b & 7, qq = nwg >> 3, rr = nwg & 7;
     const int t = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (b >> 3);
     const int tn = t % a.tiles_n;
@@ -885,8 +931,14 @@ void launch_x3(X3Args a) {
     a.tiles_n = ppo_divup(a.N, BN);
     g_x3_last_slots = a.tiles_n * (NTH / KG / 64 / WARPS_M);
     if (a.splits < 1) a.splits = 1;
-    const long grid = (long)a.tiles_m * a.tiles_n * a.splits;
+    long grid = (long)a.tiles_m * a.tiles_n * a.splits;
     PPO_REQUIRE(grid > 0 && grid < (1L << 31), "gemm_x3: grid out of range");
+    if (a.red_wgs) {
+        a.red_wgs = (int)ppo_divup((a.red_n + 3) / 4, NTH / 4);    // NTH/4 float4 columns per reduce workgroup
+        PPO_REQUIRE(OP == OP_NN && NTH >= 256 && grid + a.red_wgs < (1L << 31), "gemm_x3: carried reduce");
+        a.gemm_wgs = (int)grid;
+        grid += a.red_wgs;
+    }
     PPO_REQUIRE(a.kchunk % (KG * BK) == 0 || a.splits == 1, "gemm_x3: split-K chunk vs k-groups");
     using SA = StageX3<BM, OP == OP_TN, NTH / KG>;
     using SB = StageX3<BN, OP != OP_NT, NTH / KG>;
@@ -1052,9 +1104,21 @@ void slab_reduce(const float* slab, float* out, long n, long stride, int splits,
     PPO_LAUNCH_CHECK();
 }
 
+// a grad_W's split-K slab reduce deferred into the grad_x launch that follows it on the same stream
+// (phip_x3_defer_reduce): per stream, as the slab scratch
+struct PendingReduce { const float* slab; float* out; long n, stride; int splits; bool on; };
+static PendingReduce g_pending[2] = {};
+static int g_defer_next = 0;
+
 }  // namespace ppo
 
 extern "C" {
+
+// The next phip_x3_bwd_w(_fold) call on this thread leaves its split-K slab reduce (if it uses slabs) to
+// the next phip_x3_bwd_x(_fold) launch on the same stream, which runs it in extra workgroups beside its
+// tiles: one launch fewer per layer (the caller guarantees that grad_x follows; the next grad_W on the
+// stream refuses to start while a deferred reduce is pending)
+void phip_x3_defer_reduce(int on) { ppo::g_defer_next = on; }
 
 // Shapes the engine takes (neural_network.c routes the rest to the exact fp32 kernels): the k
 // extent and every leading dimension a multiple of 4 floats, 16-B aligned operands, and for
@@ -1104,6 +1168,12 @@ void phip_x3_bwd_x_fold(float* gx, const float* g, const unsigned* fold_bits, co
     a.M = m; a.N = n; a.K = l; a.kchunk = l; a.splits = 1;
     a.bits_in = bits; a.wpr = ppo_divup(n, 32);
     a.fold_bits = fold_bits; a.fold_wpr = ppo_divup(l, 32); a.fold_g = fold_g;
+    ppo::PendingReduce& pr = ppo::g_pending[phip_side_active() ? 1 : 0];
+    if (pr.on) {
+        a.red_slab = pr.slab; a.red_out = pr.out; a.red_n = pr.n; a.red_stride = pr.stride;
+        a.red_splits = pr.splits; a.red_wgs = 1;              // (sized in launch_x3)
+        pr.on = false;
+    }
     launch_cfg_x3<OP_NN>(pick_x3(m, n, OP_NN), a);
 }
 
@@ -1127,6 +1197,10 @@ void phip_x3_bwd_w_fold(float* gW, float* gb, const float* g, const float* fold_
     if (l <= 0 || n <= 0) return;
     PPO_REQUIRE(gW && g && x && n % 4 == 0 && l % 4 == 0 && al16(g) && al16(x), "phip_x3_bwd_w: unsupported operands");
     PPO_REQUIRE(!fold_g || (fold_w && fold_gw && gb), "phip_x3_bwd_w: value-head fold operands");
+    const int defer = ppo::g_defer_next;
+    ppo::g_defer_next = 0;
+    ppo::PendingReduce& pr = ppo::g_pending[phip_side_active() ? 1 : 0];
+    PPO_REQUIRE(!pr.on, "phip_x3_bwd_w: a deferred split-K reduce was never run (phip_x3_defer_reduce without grad_x)");
     ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l, ppo::gemm_key(2, 1, m, n, l));
     if (m <= 0) {
         if (!zeroed) {
@@ -1173,6 +1247,12 @@ void phip_x3_bwd_w_fold(float* gW, float* gb, const float* g, const float* fold_
     hipEvent_t e0 = nullptr, e1 = nullptr;
     const bool timed = ppo::take_kernel_events(&e0, &e1);     // one duration: GEMM start → reduce end
     a.ev_start = timed ? e0 : nullptr;
+    if (defer && splits < 64) {                               // the reduce rides on the next grad_x launch
+        a.ev_stop = timed ? e1 : nullptr;
+        launch_cfg_x3<OP_TN>(c, a);
+        pr = ppo::PendingReduce{a.slab, gW, (long)l * n, (long)l * n, splits, true};
+        return;
+    }
     a.ev_stop = nullptr;
     launch_cfg_x3<OP_TN>(c, a);
     ppo::slab_reduce(a.slab, gW, (long)l * n, (long)l * n, splits, timed ? e1 : nullptr);

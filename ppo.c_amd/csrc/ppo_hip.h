@@ -77,6 +77,9 @@ void phip_linear16_bwd_w(float* gW, float* gb, const void* g, int tg, const void
 int  phip_x3_supported(int op, int m, int n, int l);
 void phip_x3_fwd(float* y, const float* x, const int* ridx, float* xcopy, const float* W, const float* b, int m,
                  int n, int l, int relu, unsigned* bits);
+/* the next phip_x3_bwd_w(_fold) leaves its split-K slab reduce to the next phip_x3_bwd_x(_fold) on the same
+ * stream (extra workgroups of that launch) — the caller guarantees grad_x follows */
+void phip_x3_defer_reduce(int on);
 void phip_x3_bwd_x(float* gx, const float* g, const float* W, const unsigned* bits, int m, int n, int l);
 void phip_x3_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, int n, int l, int zeroed);
 /* value-head fold (nn_value_fold_step): forward partial y dots (returns ypart slots); backward with the

@@ -428,6 +428,7 @@ static void nn_backward_dev_top(NeuralNetwork* nn, const float* d_grad_out, int 
             /* grad_W = diag(w)·(maskᵀ·diag(g)·x), grad_b = diag(w)·maskᵀ·g, the output layer's gW = Σ g·h;
              * grad_x = diag(g)·(mask·diag(w)·W) ⊙ the input mask (gemm_x3.hip) */
             const float* h = nn->layers[i + 1].d_input;
+            phip_x3_defer_reduce(want_gx);                    /* its slab reduce rides on grad_x */
             phip_x3_bwd_w_fold(ly->d_grad_weights, ly->d_grad_biases, h, fold->g, fold->w, fold->gw_out, x, m, n, l, 1);
             if (want_gx) {
                 if (relu_in && !bits) die("nn_value_fold_step: the forward's ReLU′ bits are missing");
@@ -438,8 +439,10 @@ static void nn_backward_dev_top(NeuralNetwork* nn, const float* d_grad_out, int 
                               l)) {
             /* wide output layer (A = 17): grad_x and grad_W in one pass over the rows (out_head.hip) */
         } else if (use_x3_layer(m, n, l) && phip_x3_supported(2, m, n, l)) {
+            const int pair = want_gx && (!relu_in || bits);
+            phip_x3_defer_reduce(pair);                       /* its slab reduce rides on grad_x */
             phip_x3_bwd_w(ly->d_grad_weights, ly->d_grad_biases, g, x, m, n, l, 1);
-            if (want_gx && (!relu_in || bits)) phip_x3_bwd_x(ly->d_grad_x, g, ly->d_weights, bits, m, n, l);
+            if (pair) phip_x3_bwd_x(ly->d_grad_x, g, ly->d_weights, bits, m, n, l);
             else if (want_gx) phip_linear_bwd_x_bits(ly->d_grad_x, g, ly->d_weights, ly->d_input, NULL, m, n, l);
         } else if (want_gx && (!relu_in || bits)) {
             phip_linear_bwd_pair(ly->d_grad_weights, ly->d_grad_biases, ly->d_grad_x, g, x, ly->d_weights, bits, m, n,
