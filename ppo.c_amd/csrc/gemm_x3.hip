@@ -67,13 +67,20 @@ struct X3Args {
     float* ypart;                         //   [tiles_n · WARPS_N][M] (slot = column tile · WARPS_N + wave col)
     // backward: the upper gradient is G(i, c) = g_i·w_c·1[h(i, c) > 0] (g = ∂L/∂y), so with the 0/1 mask
     // as the operand — exact in one bf16 plane: three plane products instead of six — g and w become row /
-    // column scales: grad_x = diag(g)·(mask·diag(w)·W) (W pre-scaled by the host: the B operand),
+    // column scales: grad_x = diag(g)·(mask·diag(w)·W) (W scaled per k-row by w as it is staged),
     // grad_W = diag(w)·(maskᵀ·diag(g)·x), grad_b = diag(w)·maskᵀ·g
     const float* fold_g;                  // g [M batch rows]
-    const float* fold_w;                  // w [units]
+    const float* fold_w;                  // w [units] (grad_x: W's row scale — B = diag(w)·W staged from W)
     const unsigned* fold_bits;            // grad_x: the mask words of h [M][fold_wpr]
     int fold_wpr;
     float* fold_gw;                       // grad_W (A = h, fp32): + Σ_rows g·h per unit — the output layer's gW
+    // grad_W fold carrying the value head (vh_ypart set): each workgroup forms g = 2(y − t)/m of its split's
+    // batch rows from the forward's partial dots (y = Σ_slots ypart + b, slot order as the head kernel) in
+    // LDS before its mainloop; tile (0, 0) of each split also writes y and g and adds the loss / m and the
+    // output bias gradient Σ g (kernels.hip value_head_kernel, which runs instead when LDS is short)
+    const float* vh_ypart; const float* vh_b; const float* vh_t;
+    float* vh_y; float* vh_gb; float* vh_loss;
+    int vh_slots;
     // grad_x carrying the previous grad_W's split-K reduction (phip_x3_defer_reduce): workgroups
     // gemm_wgs … gemm_wgs + red_wgs − 1 sum red_splits slabs of red_n floats (stride red_stride) into red_out
     const float* red_slab; float* red_out;
@@ -519,13 +526,49 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     SB sb;
     sa.init(a.A, a.lda, OP == OP_NT ? a.ridx : nullptr, m0, a.M, lt);
     sb.init(a.B, a.ldb, nullptr, n0, a.N, lt);
-    // value-head fold (grad_x: A from the mask words; grad_W: A = h → mask, B = x scaled by g)
+    // value-head fold (grad_x: A from the mask words, B = W scaled by w per k-row; grad_W: A = h → mask,
+    // B = x scaled by g per k-row)
     constexpr bool syn = OP != OP_NT && FOLD != 0;
     constexpr int FMA_ = !syn ? 0 : OP == OP_NN ? 2 : 1;          // A's fold load mode
-    constexpr int FMB_ = syn && OP == OP_TN ? 1 : 0;              // B's
+    constexpr int FMB_ = syn ? 1 : 0;                             // B's
+    const float* fold_g = a.fold_g;
+    if constexpr (OP == OP_TN && FOLD != 0) {
+        if (a.vh_ypart) {                                         // the value head, carried (X3Args vh_*)
+            float* gl = reinterpret_cast<float*>(lds + KG * NS * BUF);
+            const bool head = tm == 0 && tn == 0;
+            const float bias = a.vh_b[0];
+            float ls = 0.f, sgs = 0.f;
+            for (int rr = tid; rr < kend - kbeg; rr += NTH) {
+                const int row = kbeg + rr;
+                float yv = 0.f;
+                for (int q = 0; q < a.vh_slots; ++q) yv += a.vh_ypart[(long)q * a.K + row];
+                yv += bias;
+                const float tv = a.vh_t[row];
+                const float d = tv - yv;
+                const float gv = 2 * (yv - tv) / (float)a.K;
+                gl[rr] = gv;
+                if (head) {
+                    a.vh_y[row] = yv;
+                    const_cast<float*>(a.fold_g)[row] = gv;
+                    ls += d * d;
+                    sgs += gv;
+                }
+            }
+            if (head) {
+                ls = ppo::wave_sum64(ls);
+                sgs = ppo::wave_sum64(sgs);
+                if (lane == 0) {
+                    atomicAdd(a.vh_gb, sgs);
+                    if (a.vh_loss) atomicAdd(a.vh_loss, ls * (1.0f / (float)a.K));
+                }
+            }
+            __syncthreads();
+            fold_g = gl - kbeg;
+        }
+    }
     if (syn) {
-        sa.init_fold(a.fold_g, OP == OP_NN ? a.fold_bits : nullptr, a.fold_wpr, m0, a.M);
-        sb.init_fold(a.fold_g, nullptr, 0, n0, a.N);
+        sa.init_fold(fold_g, OP == OP_NN ? a.fold_bits : nullptr, a.fold_wpr, m0, a.M);
+        sb.init_fold(OP == OP_NN ? a.fold_w : fold_g, nullptr, 0, n0, a.N);
     }
     // the fused gather's copy of A's rows: every column tile of a row block stages the same rows, so
     // they share the copy — column tile tn writes the k-tiles with index ≡ tn (mod tiles_n) (one
@@ -614,7 +657,7 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     auto stage_b = [&](auto FULLc, unsigned short* img, int k0) {
         constexpr bool FULL = decltype(FULLc)::value;
         if ((ABL & 2) && k0 != kbeg) return;
-        if constexpr (FMB_ == 1) {                       // grad_W fold: x rows scaled by g
+        if constexpr (FMB_ == 1) {                       // fold: x rows scaled by g (grad_W), W rows by w (grad_x)
 #pragma unroll
             for (int q = 0; q < SB::NV; ++q) sb.v[q] *= sb.gq[q];
         }
@@ -942,13 +985,23 @@ void launch_x3(X3Args a) {
     PPO_REQUIRE(a.kchunk % (KG * BK) == 0 || a.splits == 1, "gemm_x3: split-K chunk vs k-groups");
     using SA = StageX3<BM, OP == OP_TN, NTH / KG>;
     using SB = StageX3<BN, OP != OP_NT, NTH / KG>;
-    constexpr size_t lds = (size_t)KG * 3 * sizeof(unsigned short) * (SA::SIZE + SB::SIZE);   // 3-stage ring
-    static_assert(lds <= 160 * 1024, "gemm_x3: LDS images exceed 160 KiB");
+    constexpr size_t lds0 = (size_t)KG * 3 * sizeof(unsigned short) * (SA::SIZE + SB::SIZE);   // 3-stage ring
+    static_assert(lds0 <= 160 * 1024, "gemm_x3: LDS images exceed 160 KiB");
+    size_t lds = lds0;
+    if (OP == OP_TN && FOLD && a.vh_ypart) {           // the carried value head's g of the split's rows
+        if (lds0 + 4 * (size_t)a.kchunk <= 160 * 1024) {
+            lds += 4 * (size_t)a.kchunk;
+        } else {                                       // no room: the head kernel first, g from HBM
+            phip_value_head(a.vh_ypart, a.vh_slots, a.vh_b, a.vh_t, a.K, a.vh_y, const_cast<float*>(a.fold_g), a.vh_gb,
+                            a.vh_loss);
+            a.vh_ypart = nullptr;
+        }
+    }
     auto kern = gemm_x3_kernel<OP, BM, BN, WARPS_M, NTH, OCC, KG, ABL, FOLD>;
     if (lds > 64 * 1024) {
-        static bool attr = false;                      // once per instantiation
+        static bool attr = false;                      // once per instantiation (the whole LDS)
         if (!attr) {
-            PPO_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            PPO_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
             attr = true;
         }
     }
@@ -1154,20 +1207,20 @@ void phip_x3_fwd(float* y, const float* x, const int* ridx, float* xcopy, const 
 }
 
 // the upper layer's gradient A = g [m, l]; value-head fold (fold_g): A = the 0/1 mask words of h
-// (fold_bits [m][⌈l/32⌉]), W already scaled by the output weights (diag(w)·W), the product scaled by
-// fold_g per row — grad_x = diag(g)·(mask·diag(w)·W) ⊙ the input mask
-void phip_x3_bwd_x_fold(float* gx, const float* g, const unsigned* fold_bits, const float* fold_g, const float* W,
-                        const unsigned* bits, int m, int n, int l) {
+// (fold_bits [m][⌈l/32⌉]), W scaled per k-row by the output weights fold_w as it is staged (diag(w)·W), the
+// product scaled by fold_g per row — grad_x = diag(g)·(mask·diag(w)·W) ⊙ the input mask
+void phip_x3_bwd_x_fold(float* gx, const float* g, const unsigned* fold_bits, const float* fold_g, const float* fold_w,
+                        const float* W, const unsigned* bits, int m, int n, int l) {
     if (m <= 0 || n <= 0) return;
     PPO_REQUIRE(gx && (g || fold_bits) && W && l > 0 && l % 4 == 0 && n % 4 == 0 && (!g || al16(g)) && al16(W),
                 "phip_x3_bwd_x: unsupported operands");
-    PPO_REQUIRE(!fold_bits || fold_g, "phip_x3_bwd_x: value-head fold operands");
+    PPO_REQUIRE(!fold_bits || (fold_g && fold_w), "phip_x3_bwd_x: value-head fold operands");
     ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l, ppo::gemm_key(1, 1, m, n, l));
     X3Args a{};
     a.A = fold_bits ? W : g; a.lda = l; a.B = W; a.ldb = n; a.C = gx; a.ldc = n;
     a.M = m; a.N = n; a.K = l; a.kchunk = l; a.splits = 1;
     a.bits_in = bits; a.wpr = ppo_divup(n, 32);
-    a.fold_bits = fold_bits; a.fold_wpr = ppo_divup(l, 32); a.fold_g = fold_g;
+    a.fold_bits = fold_bits; a.fold_wpr = ppo_divup(l, 32); a.fold_g = fold_g; a.fold_w = fold_w;
     ppo::PendingReduce& pr = ppo::g_pending[phip_side_active() ? 1 : 0];
     if (pr.on) {
         a.red_slab = pr.slab; a.red_out = pr.out; a.red_n = pr.n; a.red_stride = pr.stride;
@@ -1178,15 +1231,17 @@ void phip_x3_bwd_x_fold(float* gx, const float* g, const unsigned* fold_bits, co
 }
 
 void phip_x3_bwd_x(float* gx, const float* g, const float* W, const unsigned* bits, int m, int n, int l) {
-    phip_x3_bwd_x_fold(gx, g, nullptr, nullptr, W, bits, m, n, l);
+    phip_x3_bwd_x_fold(gx, g, nullptr, nullptr, nullptr, W, bits, m, n, l);
 }
 
-void phip_x3_bwd_w_fold(float* gW, float* gb, const float* g, const float* fold_g, const float* fold_w,
-                        float* fold_gw, const float* x, int m, int n, int l, int zeroed);
+void phip_x3_bwd_w_vhead(float* gW, float* gb, const float* g, float* fold_g, const float* fold_w, float* fold_gw,
+                         const float* x, int m, int n, int l, int zeroed, const float* ypart, int slots, const float* b,
+                         const float* tgt, float* y, float* gb_out, float* loss_accum);
 
 // zeroed: gW / gb already hold zeros (one memset per backward); otherwise they are cleared here
 void phip_x3_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, int n, int l, int zeroed) {
-    phip_x3_bwd_w_fold(gW, gb, g, nullptr, nullptr, nullptr, x, m, n, l, zeroed);
+    phip_x3_bwd_w_vhead(gW, gb, g, nullptr, nullptr, nullptr, x, m, n, l, zeroed, nullptr, 0, nullptr, nullptr, nullptr,
+                        nullptr, nullptr);
 }
 
 // value-head fold (fold_g): g = h [m, l] (fp32, its mask is the operand), x scaled by fold_g per row, the
@@ -1194,7 +1249,17 @@ void phip_x3_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, 
 // diag(w)·maskᵀ·g — and fold_gw [l] (zero on entry) += Σ_rows fold_g·h, the output layer's gW
 void phip_x3_bwd_w_fold(float* gW, float* gb, const float* g, const float* fold_g, const float* fold_w,
                         float* fold_gw, const float* x, int m, int n, int l, int zeroed) {
+    phip_x3_bwd_w_vhead(gW, gb, g, const_cast<float*>(fold_g), fold_w, fold_gw, x, m, n, l, zeroed, nullptr, 0, nullptr,
+                        nullptr, nullptr, nullptr, nullptr);
+}
+
+// + the carried value head (ypart set): g (fold_g, written) from the forward's partial dots, y, the output
+// bias gradient gb_out and the loss, in this launch (X3Args vh_*)
+void phip_x3_bwd_w_vhead(float* gW, float* gb, const float* g, float* fold_g, const float* fold_w, float* fold_gw,
+                         const float* x, int m, int n, int l, int zeroed, const float* ypart, int slots, const float* b,
+                         const float* tgt, float* y, float* gb_out, float* loss_accum) {
     if (l <= 0 || n <= 0) return;
+    PPO_REQUIRE(!ypart || (fold_g && slots > 0 && b && tgt && y && gb_out), "phip_x3_bwd_w: carried value head operands");
     PPO_REQUIRE(gW && g && x && n % 4 == 0 && l % 4 == 0 && al16(g) && al16(x), "phip_x3_bwd_w: unsupported operands");
     PPO_REQUIRE(!fold_g || (fold_w && fold_gw && gb), "phip_x3_bwd_w: value-head fold operands");
     const int defer = ppo::g_defer_next;
@@ -1227,6 +1292,7 @@ void phip_x3_bwd_w_fold(float* gW, float* gb, const float* g, const float* fold_
     a.M = l; a.N = n; a.K = m; a.kchunk = kchunk; a.splits = splits;
     a.gbias = gb;
     a.fold_g = fold_g; a.fold_w = fold_w; a.fold_gw = fold_gw;
+    a.vh_ypart = ypart; a.vh_slots = slots; a.vh_b = b; a.vh_t = tgt; a.vh_y = y; a.vh_gb = gb_out; a.vh_loss = loss_accum;
     // split-K partials: per-split slabs written with plain stores and summed by one reduce launch
     // (16 MB of f32 atomics at ≈1.3 TB/s set the grad_W time of small batches; the slab path moves
     // the same bytes at store / load rate, and its sum is deterministic); the bias gradient keeps
@@ -1293,7 +1359,7 @@ double ppo_bench_gemm_x3(int op, int m, int n, int l, int iters, int cfg, int sp
         else if (op == 3) phip_x3_fwd(y, x, nullptr, nullptr, W, b, m, n, l, 0, nullptr);
         else if (op == 1) phip_x3_bwd_x(x, y, W, bits, m, n, l);
         else if (op == 4) phip_x3_fwd_vhead(y, x, nullptr, nullptr, W, b, m, n, l, 1, bits, fold, fold + l);
-        else if (op == 5) phip_x3_bwd_x_fold(x, nullptr, bits, fold, W, bits, m, n, l);
+        else if (op == 5) phip_x3_bwd_x_fold(x, nullptr, bits, fold, fold + m, W, bits, m, n, l);
         else if (op == 6) phip_x3_bwd_w_fold(gw, b, y, fold, fold + m, fold + m + l, x, m, n, l, 0);
         else phip_x3_bwd_w(gw, b, y, x, m, n, l, 0);
     };

@@ -103,22 +103,16 @@ __global__ void mse_kernel(const float* __restrict__ y, const float* __restrict_
 // layer's per-wave partial dots (gemm_x3 forward epilogue, `slots` partials summed in slot order),
 // the MSE loss (Σ(t − y)² / m, as mse_kernel) and its gradient g = 2(y − t)/m, the output bias gradient
 // Σ g; the output layer's weight gradient and the hidden layer's ∂L/∂z follow in the x3 backward
-// kernels, which take g and w as row / column scales of the 0/1 mask of h.  Blocks ≥ head_blocks write
-// Ws = diag(w)·W (the hidden layer's weights [l][n], row c scaled by w[c]: grad_x's B operand).
+// kernels, which take g and w as row / column scales of the 0/1 mask of h.  Since round 5 the hidden
+// layer's grad_W launch carries this head (gemm_x3.hip X3Args vh_*, the same arithmetic per row); this
+// kernel runs only when that launch has no LDS room for its split's g.
 __global__ void value_head_kernel(const float* __restrict__ ypart, int slots, const float* __restrict__ b,
                                   const float* __restrict__ t, int m, float* __restrict__ y, float* __restrict__ g,
-                                  float* gb, float* d_loss_accum, int head_blocks, const float* __restrict__ w,
-                                  const float* __restrict__ W, float* __restrict__ Ws, long ln, int n) {
+                                  float* gb, float* d_loss_accum) {
     __shared__ float red[TPB / 64];
-    if ((int)blockIdx.x >= head_blocks) {
-        for (long i = (long)(blockIdx.x - head_blocks) * TPB + threadIdx.x; i < ln;
-             i += (long)(gridDim.x - head_blocks) * TPB)
-            Ws[i] = W[i] * w[i / n];
-        return;
-    }
     const float bias = b[0];
     float s = 0.f, sg = 0.f;
-    for (int i = blockIdx.x * TPB + threadIdx.x; i < m; i += head_blocks * TPB) {
+    for (int i = blockIdx.x * TPB + threadIdx.x; i < m; i += gridDim.x * TPB) {
         float yv = 0.f;
         for (int q = 0; q < slots; ++q) yv += ypart[(long)q * m + i];
         yv += bias;
@@ -383,14 +377,12 @@ void phip_axpy(float* y, const float* x, long count) {
 }
 
 void phip_value_head(const float* ypart, int slots, const float* b, const float* tgt, int m, float* y, float* g,
-                     float* gb, float* d_loss_accum, const float* w, const float* W, float* Ws, int l, int n) {
+                     float* gb, float* d_loss_accum) {
     if (m <= 0) return;
-    ppo::ProfScope ps(PPO_K_HEAD, 4.0 * m * (slots + 3) + 8.0 * l * n);
+    ppo::ProfScope ps(PPO_K_HEAD, 4.0 * m * (slots + 3));
     const int hb = std::min(ppo_divup(m, TPB), 256);
-    const long ln = (long)l * n;
-    const int wb = (int)std::min<long>(ppo_divup(ln, TPB * 4L), 256);
-    hipLaunchKernelGGL(value_head_kernel, dim3(hb + wb), dim3(TPB), 0, ppo::stream(), ypart, slots, b, tgt, m, y, g, gb,
-                       d_loss_accum, hb, w, W, Ws, ln, n);
+    hipLaunchKernelGGL(value_head_kernel, dim3(hb), dim3(TPB), 0, ppo::stream(), ypart, slots, b, tgt, m, y, g, gb,
+                       d_loss_accum);
     PPO_LAUNCH_CHECK();
 }
 

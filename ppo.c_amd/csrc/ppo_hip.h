@@ -87,10 +87,15 @@ void phip_x3_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, 
  * W pre-scaled by w) and the output layer's gW */
 int  phip_x3_fwd_vhead(float* y, const float* x, const int* ridx, float* xcopy, const float* W, const float* b, int m,
                        int n, int l, int relu, unsigned* bits, const float* ydot, float* ypart);
-void phip_x3_bwd_x_fold(float* gx, const float* g, const unsigned* fold_bits, const float* fold_g, const float* W,
-                        const unsigned* bits, int m, int n, int l);
+void phip_x3_bwd_x_fold(float* gx, const float* g, const unsigned* fold_bits, const float* fold_g, const float* fold_w,
+                        const float* W, const unsigned* bits, int m, int n, int l);
 void phip_x3_bwd_w_fold(float* gW, float* gb, const float* h, const float* fold_g, const float* fold_w, float* fold_gw,
                         const float* x, int m, int n, int l, int zeroed);
+/* phip_x3_bwd_w_fold carrying the value head: g (into fold_g) from the forward's partial dots ypart [slots][m]
+ * + b against tgt, y, the output bias gradient gb_out and loss_accum (+= loss / m) — value_head_kernel's work */
+void phip_x3_bwd_w_vhead(float* gW, float* gb, const float* h, float* fold_g, const float* fold_w, float* fold_gw,
+                         const float* x, int m, int n, int l, int zeroed, const float* ypart, int slots, const float* b,
+                         const float* tgt, float* y, float* gb_out, float* loss_accum);
 /* dst[i, :] = bf16(src[rows[i], :]) for i < m (S % 4 == 0): layer 0's gather in bf16 mode */
 void phip_gather_rows_bf16(unsigned short* dst, const float* src, const int* rows, int m, int S);
 void phip_f32_to_bf16(unsigned short* dst, const float* src, long count);
@@ -151,7 +156,7 @@ void phip_mse(const float* y, const float* t, long count, float* grad, float* d_
 /* the folded value head (kernels.hip): y = Σ ypart slots + b, loss += Σ(t−y)²/m, g = 2(y−t)/m, gb += Σ g;
  * and Ws = diag(w)·W for the hidden layer's grad_x (W [l][n], w [l]) */
 void phip_value_head(const float* ypart, int slots, const float* b, const float* tgt, int m, float* y, float* g,
-                     float* gb, float* d_loss_accum, const float* w, const float* W, float* Ws, int l, int n);
+                     float* gb, float* d_loss_accum);
 /* out_head.hip: output layer forward + loss head + output-layer backward in one pass (ppo_update;
  * head 0 = value, A = 1, MSE against tgt; 1 = policy, clipped surrogate); gW / gb / grad_log_std
  * accumulated into zeroed outputs, loss into loss_accum; widths 64…1024, A ∈ {1, 6}; bf16 != 0:

@@ -364,7 +364,11 @@ void nn_backward_dev(NeuralNetwork* nn, const float* d_grad_out, int m, int want
 
 /* value-head fold: the backward's top layer (top - 1) takes its upper gradient g·w·1[h > 0] from g,
  * w and h's mask (nn_value_fold_step) */
-typedef struct { const float* g; const float* w; const float* Ws; float* gw_out; } FoldBwd;
+typedef struct {
+    float* g; const float* w; float* gw_out;
+    /* the value head carried by the hidden layer's grad_W launch (phip_x3_bwd_w_vhead) */
+    const float* ypart; int slots; const float* b; const float* tgt; float* y; float* gb; float* loss;
+} FoldBwd;
 
 static void nn_backward_dev_top(NeuralNetwork* nn, const float* d_grad_out, int m, int want_grad_x0,
                                 int grads_zero, long reduce_extra, int top, const FoldBwd* fold);
@@ -429,10 +433,12 @@ static void nn_backward_dev_top(NeuralNetwork* nn, const float* d_grad_out, int 
              * grad_x = diag(g)·(mask·diag(w)·W) ⊙ the input mask (gemm_x3.hip) */
             const float* h = nn->layers[i + 1].d_input;
             phip_x3_defer_reduce(want_gx);                    /* its slab reduce rides on grad_x */
-            phip_x3_bwd_w_fold(ly->d_grad_weights, ly->d_grad_biases, h, fold->g, fold->w, fold->gw_out, x, m, n, l, 1);
+            phip_x3_bwd_w_vhead(ly->d_grad_weights, ly->d_grad_biases, h, fold->g, fold->w, fold->gw_out, x, m, n, l, 1,
+                                fold->ypart, fold->slots, fold->b, fold->tgt, fold->y, fold->gb, fold->loss);
             if (want_gx) {
                 if (relu_in && !bits) die("nn_value_fold_step: the forward's ReLU′ bits are missing");
-                phip_x3_bwd_x_fold(ly->d_grad_x, NULL, act_bits(nn, i + 1), fold->g, fold->Ws, bits, m, n, l);
+                phip_x3_bwd_x_fold(ly->d_grad_x, NULL, act_bits(nn, i + 1), fold->g, fold->w, ly->d_weights, bits, m, n,
+                                   l);
             }
         } else if (i == L - 1 && want_gx && (!relu_in || bits) &&
             phip_out_bwd_wide(ly->d_grad_weights, ly->d_grad_biases, ly->d_grad_x, g, x, ly->d_weights, relu_in, m, n,
@@ -498,10 +504,11 @@ void nn_out_head_step(NeuralNetwork* nn, int head, const float* d_x, const int* 
  * kernels (fp32, identity output after a ReLU hidden layer, the x3 engine at this m, no
  * deterministic-GEMM request; PPO_VALUE_FOLD=0 disables it, read per call).  With h = relu(z) the
  * last hidden activation, y = h·w + b and g = ∂L/∂y, the head's upper gradient is G = g·w·1[h > 0] —
- * rank one — so it is never formed: the forward's epilogue leaves partial dots of h·w, one small kernel
- * makes y, the loss, g, the output bias gradient and diag(w)·W, and the hidden layer's backward GEMMs take
- * the 0/1 mask of h as their operand (one bf16 plane: three MFMA plane products instead of six) with g
- * and w as row / column scales (gemm_x3.hip FOLD). */
+ * rank one — so it is never formed: the forward's epilogue leaves partial dots of h·w, the hidden layer's
+ * grad_W launch forms y, the loss, g and the output bias gradient from them before its mainloop (the head
+ * carried: no launch of its own), and the hidden layer's backward GEMMs take the 0/1 mask of h as their
+ * operand (one bf16 plane: three MFMA plane products instead of six) with g and w as row / column scales
+ * (gemm_x3.hip FOLD; grad_x stages W scaled by w per k-row). */
 int nn_value_fold_ok(const NeuralNetwork* nn, int m) {
     const char* e = getenv("PPO_VALUE_FOLD");
     if ((e && e[0] == '0') || phip_gemm_deterministic()) return 0;     /* atomics in the gradient sums */
@@ -513,7 +520,7 @@ int nn_value_fold_ok(const NeuralNetwork* nn, int m) {
            phip_x3_supported(2, m, n, l);
 }
 
-static float* g_fold_ws = NULL;       /* ypart [slots][m] | g [m] | diag(w)·W [l][n] */
+static float* g_fold_ws = NULL;       /* ypart [slots][m] | g [m] */
 static size_t g_fold_cap = 0;
 
 void nn_value_fold_step(NeuralNetwork* nn, const float* d_x, const int* d_rows, float* d_xcopy, int m, int grads_zero,
@@ -521,10 +528,10 @@ void nn_value_fold_step(NeuralNetwork* nn, const float* d_x, const int* d_rows, 
     const int L = nn->num_layers - 1;
     Layer* hid = &nn->layers[L - 2];
     Layer* out = &nn->layers[L - 1];
-    const int n = hid->input_size, l = hid->output_size;
+    const int l = hid->output_size;
     const size_t mp = ((size_t)m + 3) & ~(size_t)3;
     const size_t slots_max = 2 * (size_t)((l + 63) / 64);     /* column tiles (≥ 64 wide) × 2 waves along N */
-    const size_t need = slots_max * mp + mp + (size_t)l * n;
+    const size_t need = slots_max * mp + mp;
     if (need > g_fold_cap) {
         phip_free(g_fold_ws);
         g_fold_ws = (float*)phip_malloc(sizeof(float) * need);
@@ -532,17 +539,16 @@ void nn_value_fold_step(NeuralNetwork* nn, const float* d_x, const int* d_rows, 
     }
     float* ypart = g_fold_ws;
     float* g = ypart + slots_max * mp;
-    float* Ws = g + mp;
     FoldFwd ff = {out->d_weights, ypart, 0};
     nn_forward_dev_upto(nn, d_x, d_rows, d_xcopy, m, L - 1, &ff);
     if (ff.slots <= 0 || (size_t)ff.slots > slots_max) die("nn_value_fold_step: unexpected partial-dot slots");
     nn_ensure_grad(nn, m);
     if (!grads_zero) phip_memset(nn->d_grads, 0, sizeof(float) * (size_t)nn->num_params);
-    /* ypart rows are at stride m (phip_x3_fwd_vhead) */
-    phip_value_head(ypart, ff.slots, out->d_biases, tgt, m, nn->layers[L].d_input, g, out->d_grad_biases, loss_accum,
-                    out->d_weights, hid->d_weights, Ws, l, n);
+    /* ypart rows are at stride m (phip_x3_fwd_vhead); the head itself runs inside the hidden layer's
+     * grad_W launch (y, g, the output bias gradient, the loss) */
     nn->d_output = nn->layers[L].d_input;
-    const FoldBwd fb = {g, out->d_weights, Ws, out->d_grad_weights};
+    const FoldBwd fb = {g, out->d_weights, out->d_grad_weights, ypart, ff.slots, out->d_biases, tgt,
+                        nn->layers[L].d_input, out->d_grad_biases, loss_accum};
     nn_backward_dev_top(nn, NULL, m, 0, 1, reduce_extra, L - 1, &fb);
 }
 
