@@ -5,13 +5,19 @@
 // a 24-byte Welford triple per update; every minibatch step all-reduces the flat gradient buffer
 // of the network being trained (one call per network).
 //
-// Every collective runs on ONE dedicated comm stream, in host issue order, on ONE communicator:
-// the issuing stream (libppo's main stream for the value loop, its side stream for the policy loop)
-// records an event the comm stream waits on, and then waits on the comm stream's completion event
-// before Adam.  The cross-rank order of collectives is therefore the host order, identical on every
-// rank, so the value and policy loops can run concurrently at world > 1 without a second
-// communicator, and each all-reduce overlaps the other loop's kernels.  PPO_COMM_SELF=1 at world 1
-// builds a one-rank communicator so this exact stream/event/RCCL path runs on a single GPU.
+// Gradient all-reduces (round 5): ONE per minibatch step, over the network's whole flat gradient,
+// issued on the training loop's own stream — the value loop on libppo's main stream with the
+// communicator, the policy loop on its side stream with a second communicator split from it (two
+// loops' collectives never share a communicator, so their relative order on the GPU is free).  No
+// cross-stream events: each all-reduce waits for the backward in stream order and Adam waits for
+// it the same way, while the other loop's kernels run beside it.  (Before: per-layer buckets on one
+// shared comm stream behind event pairs, so each all-reduce overlapped the layers below; the event
+// hand-offs alone cost ≈ 23 µs per step — the G = 8 shard line 69.6 ms without a communicator,
+// 80.1 with a one-rank RCCL communicator and the events, 80.0 with the events and no collective,
+// 70.3 with the collectives in stream order: profiles/r05_comm_inline_ab.txt.)  PPO_COMM_ASYNC=1
+// restores the bucketed comm-stream form.  The per-update collectives (Welford all-gather, limit
+// min, max) stay on the comm stream with an event pair, before the loops start.  PPO_COMM_SELF=1 at
+// world 1 builds a one-rank communicator (and its split) so this exact path runs on a single GPU.
 //
 // PPO_COMM_LOOPBACK=k (k > 1, at world 1): an in-process stand-in for k ranks holding IDENTICAL
 // shards.  ppo_comm_world() reports k, so every world > 1 branch of the update runs (grad_scale
@@ -30,6 +36,8 @@
 
 namespace {
 ncclComm_t g_comm = nullptr;
+ncclComm_t g_comm_side = nullptr;            // the policy loop's communicator (split from g_comm)
+int g_inline = 1;                            // gradient all-reduces in stream order (PPO_COMM_ASYNC=1: 0)
 int g_rank = 0, g_world = 1;
 int g_loopback = 0;                          // k > 1: PPO_COMM_LOOPBACK stand-in for k identical ranks
 int* g_i32 = nullptr;                        // scratch for host-visible integer collectives
@@ -171,6 +179,17 @@ int ppo_comm_init(int rank, int world, const unsigned char* id) {
         phip_record_error(ncclGetErrorString(r));
         return -1;
     }
+    {
+        const char* as = getenv("PPO_COMM_ASYNC");
+        g_inline = !(as && *as && *as != '0');
+    }
+    if (g_inline) {                                     // collective over g_comm: every rank splits
+        r = ncclCommSplit(g_comm, 0, rank, &g_comm_side, nullptr);
+        if (r != ncclSuccess) {
+            phip_record_error(ncclGetErrorString(r));
+            return -1;
+        }
+    }
     g_rank = rank;
     g_world = world;
     return 0;
@@ -189,6 +208,8 @@ void ppo_comm_finalize(void) {
     if (g_comm) {
         phip_sync();
         PPO_CHECK(hipStreamSynchronize(g_comm_stream));
+        if (g_comm_side) ncclCommDestroy(g_comm_side);
+        g_comm_side = nullptr;
         ncclCommDestroy(g_comm);
         g_comm = nullptr;
     }
@@ -198,6 +219,7 @@ void ppo_comm_finalize(void) {
 
 int phip_comm_world(void) { return g_world; }
 int phip_comm_active(void) { return g_comm != nullptr || g_loopback > 1; }
+int phip_comm_inline(void) { return g_inline; }
 int phip_comm_rank(void) { return g_rank; }
 
 void phip_allreduce_sum_f32(float* d_buf, long n) {
@@ -227,6 +249,16 @@ static int g_pending = -1;
 void phip_allreduce_sum_f32_async(float* d_buf, long n) {
     if ((!g_comm && !g_loopback) || n <= 0) return;
     ppo::ProfScope ps(PPO_K_COMM, 4.0 * n);
+    if (g_inline) {                                     // in stream order, the loop's own communicator
+        if (g_loopback) {
+            loopback_allreduce(ppo::stream(), d_buf, n);
+        } else {
+            nccl_check(ncclAllReduce(d_buf, d_buf, (size_t)n, ncclFloat32, ncclSum,
+                                     phip_side_active() ? g_comm_side : g_comm, ppo::stream()),
+                       "ncclAllReduce", __LINE__);
+        }
+        return;
+    }
     int slot;
     hipStream_t cs = comm_enter(&slot);
     if (g_loopback) {

@@ -30,6 +30,7 @@ void  phip_sync(void);                     /* both queues */
  * waits for everything issued so far on the side queue */
 void  phip_side_fork(void);
 void  phip_side_use(int on);
+int   phip_comm_inline(void);   /* gradient all-reduces in stream order, one per step (comm.hip) */
 int   phip_side_active(void);   /* 1 while launches go to the side stream */
 void  phip_side_join(void);
 void  phip_record_error(const char* msg);

@@ -350,10 +350,11 @@ void nn_forward_dev(NeuralNetwork* nn, const float* d_x, int m) { nn_forward_dev
 #define GRAD_BUCKET_FLOATS (256L * 1024)
 
 /* layer i's gradients are queued: all-reduce [param_offset[i], *hi) once it holds a bucket's worth,
- * or at the bottom layer (the flat layout [W0, b0, W1, b1, …] makes every bucket one span) */
+ * or at the bottom layer (the flat layout [W0, b0, W1, b1, …] makes every bucket one span); with the
+ * all-reduces in stream order (comm.hip, the default) only at the bottom: one collective per step */
 static void bucket_flush(NeuralNetwork* nn, int i, long* hi) {
     const long lo = nn->param_offset[i];
-    if (i > 0 && *hi - lo < GRAD_BUCKET_FLOATS) return;
+    if (i > 0 && (*hi - lo < GRAD_BUCKET_FLOATS || phip_comm_inline())) return;
     phip_allreduce_sum_f32_async(nn->d_grads + lo, *hi - lo);
     *hi = lo;
 }
