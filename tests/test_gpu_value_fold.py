@@ -1,6 +1,8 @@
 """The value network's output layer + MSE head folded into its last hidden layer's x3 kernels
 (host/neural_network.c nn_value_fold_step, csrc/gemm_x3.hip FOLD variants, kernels.hip value_head_kernel)
 against the fused output-head pass it replaces (PPO_VALUE_FOLD=0: csrc/out_head.hip), from identical state.
+The head (y, g, loss, output bias gradient) rides on the hidden layer's grad_W launch, or runs as its own
+kernel where that launch has no LDS room for its split's g (the head_fallback case).
 
 Reference semantics: the output layer y = h·w + b (mat_mul.cu:122-163), the MSE loss and its gradient
 g = 2(y − t)/m (loss.cu:5-23), the output layer's backward gW = gᵀ·h, gb = Σ g, ∂L/∂h = g·w (mat_mul.cu:
@@ -28,6 +30,9 @@ CASES = {
     "c3": ([17, 256, 256, 6], 8192, 8192),                 # width 256: 64×64 tiles
     "ragged": ([376, 512, 512, 512, 17], 5000, 2500),     # partial row tiles
     "one_hidden": ([64, 256, 6], 2048, 2048),             # the folded layer is layer 0 (the fused gather)
+    # 8192-row grad_W splits: the split's g does not fit beside the LDS ring, so value_head_kernel runs
+    # first instead of the head carried by grad_W (gemm_x3.hip launch_x3)
+    "head_fallback": ([376, 512, 512, 512, 17], 131072, 131072),
 }
 
 
