@@ -185,9 +185,11 @@ int ppo_comm_init(int rank, int world, const unsigned char* id) {
     }
     if (g_inline) {                                     // collective over g_comm: every rank splits
         r = ncclCommSplit(g_comm, 0, rank, &g_comm_side, nullptr);
-        if (r != ncclSuccess) {
-            phip_record_error(ncclGetErrorString(r));
-            return -1;
+        if (r != ncclSuccess) {                         // every rank sees the failure: all fall back alike
+            fprintf(stderr, "libppo: ncclCommSplit failed (%s); gradient all-reduces on the comm stream\n",
+                    ncclGetErrorString(r));
+            g_comm_side = nullptr;
+            g_inline = 0;
         }
     }
     g_rank = rank;
