@@ -1300,6 +1300,8 @@ void phip_x3_bwd_w_vhead(float* gW, float* gb, const float* g, float* fold_g, co
     // (when each split is short: at C4's 32768 rows, 2048 per split, the atomics hide behind the
     // mainloop and the extra launch costs more — 326.1 vs 323.3 ms per update; at the G = 8 shard's
     // 4096 rows, 256 per split, the slabs win — 89.4 vs 93.4 ms, profiles/r03i_*)
+    // (C4 re-measured in round 5 with the reduce carried by grad_x: slabs 306.4 vs atomics 302.4 ms,
+    // profiles/r05_c4_gradw_slab_rejected.txt)
     const bool use_slab = splits > 1 && kchunk <= 1024 && al16(gW);
     if (splits > 1 && !zeroed) {
         if (!use_slab) phip_memset(gW, 0, sizeof(float) * (size_t)l * n);
