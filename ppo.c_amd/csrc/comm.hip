@@ -192,6 +192,18 @@ int ppo_comm_init(int rank, int world, const unsigned char* id) {
             g_inline = 0;
         }
     }
+    if (g_comm_side) {
+        // one collective on each communicator here, in the same order on every rank, so that RCCL's
+        // runtime peer connections (set up by a communicator's first collective) are all in place
+        // before the two training loops start issuing on them from two streams in interleaved order
+        float* w = (float*)phip_malloc(sizeof(float));
+        nccl_check(ncclAllReduce(w, w, 1, ncclFloat32, ncclSum, g_comm, g_comm_stream), "ncclAllReduce(warm)",
+                   __LINE__);
+        nccl_check(ncclAllReduce(w, w, 1, ncclFloat32, ncclSum, g_comm_side, g_comm_stream), "ncclAllReduce(warm)",
+                   __LINE__);
+        PPO_CHECK(hipStreamSynchronize(g_comm_stream));
+        phip_free(w);
+    }
     g_rank = rank;
     g_world = world;
     return 0;
