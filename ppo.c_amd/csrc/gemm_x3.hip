@@ -1116,6 +1116,8 @@ void launch_cfg_x3(int c, const X3Args& a) {
 // 128×128 at two per CU (4 waves of 64×64) vs 28.0 µs on 8 waves of 32×64; 16384 rows 50.4 vs 47.9
 int pick_x3(int M, int N, int op) {
     if (g_force_x3 >= 0) return g_force_x3;
+    // (256×128 tiles in two rounds for C4's forward or grad_x, the second round's mainloop under the
+    // first round's store tail: 322.3 / 313.3 vs 305.4 ms, profiles/r05_x3_cfg5_rounds_rejected.txt)
     if (op == OP_TN) return 3;         // (cfg 5, 256×128 with slabs, measured slower: r04_x3_tn_cfg5_update_ab.txt)
     auto tiles = [&](int c) { return (long)ppo_divup(M, kCfgX3[c].bm) * ppo_divup(N, kCfgX3[c].bn); };
     if (tiles(0) >= 256) return 0;
