@@ -1304,6 +1304,8 @@ void phip_x3_bwd_w_vhead(float* gW, float* gb, const float* g, float* fold_g, co
     // 4096 rows, 256 per split, the slabs win — 89.4 vs 93.4 ms, profiles/r03i_*)
     // (C4 re-measured in round 5 with the reduce carried by grad_x: slabs 306.4 vs atomics 302.4 ms,
     // profiles/r05_c4_gradw_slab_rejected.txt)
+    // (the shard's input-layer grad_W, whose reduce has no grad_x to ride on, with 16-adder atomics instead:
+    // 75.3 vs 73.2 ms, profiles/r05_shard_input_gradw_atomics_rejected.txt)
     const bool use_slab = splits > 1 && kchunk <= 1024 && al16(gW);
     if (splits > 1 && !zeroed) {
         if (!use_slab) phip_memset(gW, 0, sizeof(float) * (size_t)l * n);
