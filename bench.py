@@ -415,7 +415,8 @@ def main():
                    "per_rank_shard_of": shard_of if shard_of > 1 else None,
                    "parallelism": f"dp{world}",
                    "emulated_world": args.emulate_world if (world == 1 and args.emulate_world > 1) else None,
-                   "comm": "rccl-self (1-rank rehearsal)" if comm_self else ("rccl" if world > 1 else "none"),
+                   "comm": ("rccl-self (1-rank rehearsal)" if comm_self else ("rccl" if world > 1 else "none")) +
+                           (f"; gradient all-reduce {LIB.ppo_comm_mode().decode()}" if world > 1 or comm_self else ""),
                    "shuffle": "device-feistel" if args.shuffle else "host-rand"},
         "updates_per_sec": 1.0 / t_update,
         "rollout_env_steps_per_sec": (world * N / t_rollout) if t_rollout else None,
@@ -498,6 +499,15 @@ def main():
                               "algorithmic_flop_per_launch": tot_work / max(1, sum(sh["launches"] for sh in shapes)),
                               "serial_update_ms": 1000.0 * serial[5],
                               "concurrent_class_tflops": conc, "concurrent_class_frac": conc / peak}
+    if (world > 1 or comm_self) and "comm" in kernels:
+        # the gradient all-reduce as the serialised pass timed it (issuing stream ready -> collective
+        # done, per minibatch step): at world > 1 this is the exposed xGMI time SCALE runs pay per step
+        steps = 14 * (N // B)
+        result["comm"] = {"mode": LIB.ppo_comm_mode().decode(),
+                          "ms_per_update": kernels["comm"]["ms_per_update"],
+                          "us_per_minibatch_step": 1000.0 * kernels["comm"]["ms_per_update"] / steps,
+                          "collectives_per_update": kernels["comm"]["launches_per_update"],
+                          "replica_check": os.environ.get("PPO_REPLICA_CHECK", "1") != "0" and world > 1}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(LIB, ppo, S, H, A, N, B)
         result["cpu_baseline"]["gpu_over_cpu"] = result["value"] / result["cpu_baseline"]["value"]

@@ -94,6 +94,8 @@ typedef struct {
     long   dev_version;     /* bumped by every HBM parameter update */
     long   host_version;    /* dev_version the host mirrors (weights and extra floats) last matched */
     long   host_version_w;  /* dev_version the host weight mirrors last matched (a weights-only sync) */
+    float* d_fold_ws;       /* value-head fold scratch (nn_value_fold_step): partial dots [slots][m] | g [m] */
+    long   fold_ws_cap;     /* floats */
 } NeuralNetwork;
 
 typedef struct {

@@ -20,7 +20,14 @@ extern "C" {
 
 /* PPO / GaussianPolicy objects are passed as void* so this header stands alone. */
 
-/* ---------------- device & errors ---------------- */
+/* ---------------- device & errors ----------------
+ * Fatal errors (a failed HIP/RCCL call, a grid-barrier timeout of the B = 64 phases, a replica-check
+ * mismatch, a stalled collective past PPO_COMM_TIMEOUT_S) END THE EMBEDDING PROCESS with status 1, as
+ * the reference's checks do (cuda_helper.h:4-16, exit(1)) — but through _exit(1): after a device fault
+ * the HIP runtime's own teardown can hang, so atexit handlers and buffered stdio of the host language
+ * (e.g. Python's) do not run.  libppo prints the message to stderr and records it for ppo_last_error
+ * first.  Callers that must decide for themselves use the entry points that return a status
+ * (ppo_comm_init, ppo_comm_check_replicas, ppo_set_device, …). */
 int         ppo_device_count(void);              /* HIP devices visible (0 without a GPU) */
 int         ppo_set_device(int device);          /* 0 on success */
 const char* ppo_last_error(void);                /* first HIP/RCCL error recorded, "" if none */
@@ -62,7 +69,20 @@ int  ppo_comm_loopback_peers(const double* welford, const int* limits, int count
 /* an all-reduce of a span inside [d_local_base, d_local_base + n) adds the peers' values at the same
  * offset from d_peers (device, [k−1][n], rank order) instead of the k-fold identical sum; ≤ 4 spans */
 int  ppo_comm_loopback_peer_grads(const float* d_local_base, const float* d_peers, long n);
+/* the parameter hashes of ranks 1…k−1 for the replica check (host [k−1]) */
+int  ppo_comm_loopback_peer_hash(const unsigned long long* hashes, int count);
 void ppo_comm_loopback_clear(void);                      /* forget every registered peer contribution */
+/* the gradient all-reduce form in use: "none", "inline: …" (default: one all-reduce per step in each
+ * loop's stream, a communicator per loop) or "bucketed: …" (PPO_COMM_ASYNC=1, or after a failed split) */
+const char* ppo_comm_mode(void);
+/* Replica check (SURVEY §8e "verify with a periodic checksum all-reduce"): every rank hashes its
+ * parameters (μ, log σ, V: 64-bit, bit-exact), the hashes are all-gathered and compared.  Returns 0
+ * when every rank holds rank 0's parameters, −1 otherwise (ppo_last_error names the ranks).
+ * Synchronises (bounded: PPO_COMM_TIMEOUT_S).  ppo_update runs it at world > 1 after every
+ * PPO_REPLICA_CHECK-th update (default 1; 0 = off) and ends the process on a mismatch. */
+int  ppo_comm_check_replicas(void* ppo);
+/* this rank's parameter hash (as the replica check computes it; synchronises) */
+unsigned long long ppo_param_hash(void* ppo);
 
 /* ---------------- the PPO update ---------------- */
 enum { PPO_SHUFFLE_HOST_RAND = 0,   /* reference shuffle_buffer: swap(i, rand()%N), host rand() */

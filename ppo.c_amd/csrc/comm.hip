@@ -3,21 +3,38 @@
 // The reference has no multi-GPU code.  libppo shards the rollout buffer by whole
 // environments: GAE needs no exchange; advantage statistics need one all-gather of
 // a 24-byte Welford triple per update; every minibatch step all-reduces the flat gradient buffer
-// of the network being trained (one call per network).
+// of the network being trained (one call per network); replicated Adam keeps the parameters equal,
+// which a per-update replica check verifies (a 64-bit parameter hash all-gathered and compared).
 //
-// Gradient all-reduces (round 5): ONE per minibatch step, over the network's whole flat gradient,
-// issued on the training loop's own stream — the value loop on libppo's main stream with the
-// communicator, the policy loop on its side stream with a second communicator split from it (two
-// loops' collectives never share a communicator, so their relative order on the GPU is free).  No
-// cross-stream events: each all-reduce waits for the backward in stream order and Adam waits for
-// it the same way, while the other loop's kernels run beside it.  (Before: per-layer buckets on one
-// shared comm stream behind event pairs, so each all-reduce overlapped the layers below; the event
-// hand-offs alone cost ≈ 23 µs per step — the G = 8 shard line 69.6 ms without a communicator,
-// 80.1 with a one-rank RCCL communicator and the events, 80.0 with the events and no collective,
-// 70.3 with the collectives in stream order: profiles/r05_comm_inline_ab.txt.)  PPO_COMM_ASYNC=1
-// restores the bucketed comm-stream form.  The per-update collectives (Welford all-gather, limit
-// min, max) stay on the comm stream with an event pair, before the loops start.  PPO_COMM_SELF=1 at
-// world 1 builds a one-rank communicator (and its split) so this exact path runs on a single GPU.
+// Gradient all-reduces (default, "inline"): ONE per minibatch step, over the network's whole flat
+// gradient, issued on the training loop's own stream — the value loop on libppo's main stream with
+// the communicator, the policy loop on its side stream with a second communicator split from it.
+// No cross-stream events: each all-reduce waits for the backward in stream order and Adam waits for
+// it the same way, while the other loop's kernels run beside it (the event hand-offs of the bucketed
+// form cost ≈ 23 µs per step: profiles/r05_comm_inline_ab.txt).  PPO_COMM_ASYNC=1 selects the
+// bucketed form: per-layer buckets on ONE comm stream over ONE communicator in host issue order,
+// each overlapping the layers below, joined by events before Adam.
+//
+// Why two communicators on two streams cannot deadlock (DESIGN.md §6 states it in full):
+//  * the only kernels that wait for other kernels are RCCL's (the B = 64 grid-barrier phases never
+//    run at world > 1: ppo_update_tiny); GEMMs, heads and Adam finish unconditionally;
+//  * each communicator's collectives are issued from ONE stream in program order, and the host
+//    interleaves the two loops by a fixed rule (iv·np ≤ ip·nv, host/ppo.c) that does not depend on
+//    timing, so every rank submits the same total order of collectives — also the order a shared
+//    hardware queue would serialise them in;
+//  * every communicator is created with ncclConfig_t.maxCTAs = kMaxCTAs (32; PPO_COMM_MAX_CTAS), so
+//    the two collectives that can be in flight at once need ≤ 64 workgroups of 256 CUs: once the
+//    finite kernels beside them drain, both are resident, whatever else is queued.
+//  By induction over that total order the earliest unfinished collective becomes resident on every
+//  rank and completes.  The split's success is agreed over ranks (a min all-reduce) before any rank
+//  uses it; on any failure every rank falls back to the bucketed single-communicator form.
+// Diagnosis: phip_comm_wait() bounds every host wait of the data-parallel path (replica check,
+// barrier) by PPO_COMM_TIMEOUT_S (default 600 s) and polls ncclCommGetAsyncError; a stall or an RCCL
+// error aborts both communicators and fails loudly naming the rank, the pending streams and the mode.
+//
+// The per-update collectives (Welford all-gather, limit min, replica hashes) stay on the comm stream
+// with an event pair, outside the loops.  PPO_COMM_SELF=1 at world 1 builds a one-rank communicator
+// (and its split) so this exact path runs on a single GPU.
 //
 // PPO_COMM_LOOPBACK=k (k > 1, at world 1): an in-process stand-in for k ranks holding IDENTICAL
 // shards.  ppo_comm_world() reports k, so every world > 1 branch of the update runs (grad_scale
@@ -25,14 +42,17 @@
 // is the exact k-fold sum of identical buffers (×k on the comm stream) and the all-gather
 // replicates the local block k times.  For k a power of two an update must equal the 1-GPU update.
 // Disagreeing ranks (tests): ppo_comm_loopback_peers() supplies ranks 1…k−1's Welford triples and
-// buffer limits, ppo_comm_loopback_peer_grads() their gradient buffers — the all-gather then
-// delivers [own, peers…], the min runs over [own, peers…] and an all-reduce over a registered span
-// adds the peers' values, so rank 0 of a k-rank job with different shards runs in one process.
+// buffer limits, ppo_comm_loopback_peer_grads() their gradient buffers, ppo_comm_loopback_peer_hash()
+// their parameter hashes — the all-gather then delivers [own, peers…], the min runs over [own, peers…]
+// and an all-reduce over a registered span adds the peers' values, so rank 0 of a k-rank job with
+// different shards runs in one process.
 #include "dev.h"
 #include "../../include/ppo_ext.h"
 
 #include <rccl/rccl.h>
+#include <chrono>
 #include <cstring>
+#include <unistd.h>
 
 namespace {
 ncclComm_t g_comm = nullptr;
@@ -139,6 +159,43 @@ void nccl_check(ncclResult_t r, const char* what, int line) {
     snprintf(buf, sizeof(buf), "%s failed: %s", what, ncclGetErrorString(r));
     ppo::fail(buf, __FILE__, line);
 }
+
+// workgroups per collective (ncclConfig_t.maxCTAs) — the co-residency bound of the deadlock argument
+constexpr int kMaxCTAs = 32;
+int comm_max_ctas() {
+    const char* e = getenv("PPO_COMM_MAX_CTAS");
+    const int v = e ? atoi(e) : 0;
+    return v >= 1 && v <= 64 ? v : kMaxCTAs;
+}
+
+double comm_timeout_s() {
+    const char* e = getenv("PPO_COMM_TIMEOUT_S");
+    const double v = e ? atof(e) : 0.0;
+    return v > 0 ? v : 600.0;
+}
+
+// replica check: 64-bit hash of parameter bits, Σ mix(index, bits) mod 2^64 (order-independent, so the
+// grid's atomics give the same value on every rank for the same bits)
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__global__ void param_hash_kernel(const unsigned* __restrict__ p, long n, unsigned long long base,
+                                  unsigned long long* __restrict__ out) {
+    unsigned long long acc = 0;
+    for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256)
+        acc += mix64(((base + (unsigned long long)i) << 32) ^ p[i]);
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    __shared__ unsigned long long part[4];
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(out, ((part[0] + part[1]) + part[2]) + part[3]);
+}
+unsigned long long* g_hash = nullptr;          // device [1 + world]: own hash at [0], the all-gather after it
+unsigned long long g_peer_hash[64];
+int g_peer_hash_set = 0;
 }  // namespace
 
 extern "C" {
@@ -158,6 +215,10 @@ int ppo_comm_init(int rank, int world, const unsigned char* id) {
     const bool self_comm = world <= 1 && self && *self && *self != '0';
     const char* lb = getenv("PPO_COMM_LOOPBACK");
     const int k = lb ? atoi(lb) : 0;
+    {
+        const char* as = getenv("PPO_COMM_ASYNC");
+        g_inline = !(as && *as && *as != '0');
+    }
     if (world <= 1 && k > 1) {
         if (g_comm || g_loopback) { phip_record_error("ppo_comm_init: communicator already initialised"); return -1; }
         comm_stream_init();
@@ -174,20 +235,36 @@ int ppo_comm_init(int rank, int world, const unsigned char* id) {
     else { phip_record_error("ppo_comm_init: null unique id at world > 1"); return -1; }
     if (world <= 1) { world = 1; rank = 0; }
     comm_stream_init();
-    ncclResult_t r = ncclCommInitRank(&g_comm, world, uid, rank);
+    // every communicator capped at maxCTAs workgroups per collective (the co-residency bound of the
+    // two-communicator deadlock argument, header comment); blocking calls
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 1;
+    cfg.maxCTAs = comm_max_ctas();
+    ncclResult_t r = ncclCommInitRankConfig(&g_comm, world, uid, rank, &cfg);
     if (r != ncclSuccess) {
         phip_record_error(ncclGetErrorString(r));
+        g_comm = nullptr;
         return -1;
     }
-    {
-        const char* as = getenv("PPO_COMM_ASYNC");
-        g_inline = !(as && *as && *as != '0');
-    }
     if (g_inline) {                                     // collective over g_comm: every rank splits
-        r = ncclCommSplit(g_comm, 0, rank, &g_comm_side, nullptr);
-        if (r != ncclSuccess) {                         // every rank sees the failure: all fall back alike
-            fprintf(stderr, "libppo: ncclCommSplit failed (%s); gradient all-reduces on the comm stream\n",
-                    ncclGetErrorString(r));
+        ncclConfig_t scfg = NCCL_CONFIG_INITIALIZER;
+        scfg.blocking = 1;
+        scfg.maxCTAs = comm_max_ctas();
+        r = ncclCommSplit(g_comm, 0, rank, &g_comm_side, &scfg);
+        // the ranks agree on the outcome (min over g_comm) before any of them uses the side
+        // communicator: one failing rank sends every rank to the bucketed single-communicator form
+        int* ok = (int*)phip_malloc(sizeof(int));
+        const int mine = r == ncclSuccess && g_comm_side != nullptr;
+        phip_h2d(ok, &mine, sizeof(int));
+        nccl_check(ncclAllReduce(ok, ok, 1, ncclInt32, ncclMin, g_comm, ppo::stream()), "ncclAllReduce(split agree)",
+                   __LINE__);
+        int all = 0;
+        phip_d2h(&all, ok, sizeof(int));
+        phip_free(ok);
+        if (!all) {
+            fprintf(stderr, "libppo: rank %d: ncclCommSplit %s on %s; gradient all-reduces on the comm stream\n",
+                    rank, mine ? "succeeded here but failed" : ncclGetErrorString(r), mine ? "another rank" : "this rank");
+            if (g_comm_side) ncclCommDestroy(g_comm_side);
             g_comm_side = nullptr;
             g_inline = 0;
         }
@@ -227,6 +304,8 @@ void ppo_comm_finalize(void) {
         ncclCommDestroy(g_comm);
         g_comm = nullptr;
     }
+    if (g_hash) { phip_free(g_hash); g_hash = nullptr; }
+    g_inline = 1;
     g_rank = 0;
     g_world = 1;
 }
@@ -330,10 +409,113 @@ double ppo_comm_max_f64(double v) {
     return out;
 }
 
+// Bounded host wait for everything libppo queued (main, side and comm streams): polls the streams and
+// RCCL's asynchronous error state; a stall past PPO_COMM_TIMEOUT_S or an RCCL error aborts the
+// communicators and fails loudly — a hung collective becomes a diagnosable exit, not a silent hang.
+void phip_comm_wait(const char* what) {
+    const double limit = comm_timeout_s();
+    const auto t0 = std::chrono::steady_clock::now();
+    unsigned spins = 0;
+    for (;;) {
+        int pending = ppo::streams_pending();
+        if (g_comm_stream) {
+            const hipError_t e = hipStreamQuery(g_comm_stream);
+            if (e == hipErrorNotReady) pending |= 4;
+            else PPO_CHECK(e);
+        }
+        if (!pending) return;
+        ncclResult_t ae = ncclSuccess, as = ncclSuccess;
+        if (g_comm) (void)ncclCommGetAsyncError(g_comm, &ae);
+        if (g_comm_side) (void)ncclCommGetAsyncError(g_comm_side, &as);
+        const bool rccl_err = (ae != ncclSuccess && ae != ncclInProgress) || (as != ncclSuccess && as != ncclInProgress);
+        const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (rccl_err || s > limit) {
+            char buf[400];
+            snprintf(buf, sizeof(buf),
+                     "rank %d/%d: %s: %s after %.0f s (pending:%s%s%s; gradient all-reduces %s; RCCL: %s / %s); "
+                     "communicators aborted",
+                     g_rank, g_world, what, rccl_err ? "RCCL error" : "no progress", s, pending & 1 ? " main" : "",
+                     pending & 2 ? " side" : "", pending & 4 ? " comm" : "",
+                     g_inline ? "inline (per-loop communicators)" : "bucketed (comm stream)", ncclGetErrorString(ae),
+                     ncclGetErrorString(as));
+            if (g_comm_side) ncclCommAbort(g_comm_side);
+            if (g_comm) ncclCommAbort(g_comm);
+            g_comm_side = g_comm = nullptr;
+            ppo::fail(buf, __FILE__, __LINE__);
+        }
+        if (++spins > 64) usleep(50);
+    }
+}
+
 void ppo_comm_barrier(void) {
-    phip_sync();
+    phip_comm_wait("ppo_comm_barrier (queued work)");
     (void)ppo_comm_max_f64(0.0);
     phip_sync();
+}
+
+// replica check (ppo_comm_check_replicas): this rank's parameter hash
+void phip_param_hash(const float* const* spans, const long* lens, int nspans) {
+    if (!g_hash) g_hash = (unsigned long long*)phip_malloc(sizeof(unsigned long long) * (size_t)(1 + (g_world > 64 ? g_world : 64)));
+    phip_memset(g_hash, 0, sizeof(unsigned long long));
+    unsigned long long base = 0;
+    for (int i = 0; i < nspans; i++) {
+        if (!spans[i] || lens[i] <= 0) continue;
+        int grid = ppo_divup(lens[i], 256);
+        if (grid > 1024) grid = 1024;
+        hipLaunchKernelGGL(param_hash_kernel, dim3(grid), dim3(256), 0, ppo::stream(), (const unsigned*)spans[i],
+                           lens[i], base, g_hash);
+        PPO_LAUNCH_CHECK();
+        base += (unsigned long long)lens[i];
+    }
+    // the value stays on the device (g_hash[0]); phip_comm_check_hash gathers and reads it
+}
+
+// all-gather of every rank's hash (in g_hash[0]) over the communicator, a bounded wait, then the
+// comparison: 0 if all equal, −1 with a message naming the ranks that differ from rank 0
+int phip_comm_check_hash(int gather, unsigned long long* own, char* msg, int cap) {
+    if (!g_hash) return 0;
+    const int k = !gather ? 1 : g_world > 64 ? 64 : g_world;
+    if (gather && g_comm && g_world > 1) {
+        int slot;
+        hipStream_t cs = comm_enter(&slot);
+        nccl_check(ncclAllGather(g_hash, g_hash + 1, 1, ncclUint64, g_comm, cs), "ncclAllGather(replica hash)",
+                   __LINE__);
+        comm_leave(slot);
+    }
+    phip_comm_wait(gather ? "replica check" : "parameter hash");
+    unsigned long long h[65];
+    phip_d2h(h, g_hash, sizeof(unsigned long long) * (size_t)(1 + k));
+    if (own) *own = h[0];
+    if (!(gather && g_comm && g_world > 1)) {     // loopback / one rank: [own, own…] or the registered peers
+        for (int r = 0; r < k; r++) h[1 + r] = r == 0 || !g_peer_hash_set ? h[0] : g_peer_hash[r - 1];
+    }
+    int bad = 0, len = 0;
+    if (msg && cap > 0) msg[0] = 0;
+    for (int r = 1; r < k; r++) {
+        if (h[1 + r] == h[1]) continue;
+        bad++;
+        if (msg && len < cap)
+            len += snprintf(msg + len, (size_t)(cap - len), "%srank %d hash %016llx != rank 0 hash %016llx",
+                            bad > 1 ? "; " : "", r, h[1 + r], h[1]);
+    }
+    return bad ? -1 : 0;
+}
+
+int ppo_comm_loopback_peer_hash(const unsigned long long* hashes, int count) {
+    if (g_loopback < 2 || count != g_loopback - 1 || count > 63 || !hashes) {
+        phip_record_error("ppo_comm_loopback_peer_hash: needs PPO_COMM_LOOPBACK=k and count = k - 1 (< 64)");
+        return -1;
+    }
+    for (int r = 0; r < count; r++) g_peer_hash[r] = hashes[r];
+    g_peer_hash_set = 1;
+    return 0;
+}
+
+const char* ppo_comm_mode(void) {
+    if (g_loopback > 1) return g_inline ? "loopback (in-process ranks), inline" : "loopback (in-process ranks), bucketed";
+    if (!g_comm) return "none";
+    return g_inline ? "inline: one all-reduce per step in each loop's stream, per-loop communicators"
+                    : "bucketed: per-layer all-reduces on one comm stream, one communicator, event-joined";
 }
 
 // min over ranks of a host integer (synchronous; a few µs per call).  The update uses it to agree
@@ -361,6 +543,7 @@ int phip_comm_min_i32(int v) {
 }
 
 void ppo_comm_loopback_clear(void) {
+    g_peer_hash_set = 0;
     if (g_peer_welford) { phip_sync(); phip_free(g_peer_welford); }
     g_peer_welford = nullptr;
     g_peer_welford_n = 0;

@@ -18,6 +18,9 @@ hipStream_t stream();                       // libppo's stream (created on first
 void        ensure_device();                // aborts with a clear message without a HIP device
 void        check(hipError_t e, const char* what, const char* file, int line);
 void        fail(const char* msg, const char* file, int line);   // records + aborts
+// bit 0: libppo's main stream still has work queued, bit 1: the side stream (hipStreamQuery; an
+// error other than "not ready" is fatal).  For bounded waits (comm.hip's watchdog).
+int         streams_pending();
 
 // Per-launch timing: begin() records a start event when profiling is on; end()
 // records the stop event and attributes `work` (FLOPs or bytes) to class k.

@@ -1370,8 +1370,8 @@ int dma16_setting() {
     }
     return g_dma16;
 }
-// the 16×16×32 MFMA form for bf16-output DMA products and for grad_W (PPO_G16_MF16=0: the 32×32×16 form
-// everywhere; 2: only the DMA products).  Measured at C5 16384×1024×1024: forward 41.5 -> 37.3 µs,
+// the 16×16×32 MFMA form for bf16-output DMA products and for grad_W (the round-2 PPO_G16_MF16 switch
+// is gone: the 32×32×16 form remains only where this one does not apply).  Measured at C5 16384×1024×1024: forward 41.5 -> 37.3 µs,
 // grad_x 42.1 -> 40.7 µs (C5 update 276.4 -> 271.9 ms); grad_W 82.6 -> 80.3 µs (273.7 -> 271.8 ms)
 constexpr int g_mf16 = 1;
 

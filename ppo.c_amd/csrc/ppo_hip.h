@@ -303,6 +303,14 @@ void phip_allreduce_sum_f32(float* d_buf, long n);
 void phip_allreduce_sum_f32_async(float* d_buf, long n);
 void phip_allreduce_join(void);
 void phip_allgather_f64(const double* d_send, double* d_recv, long n_per_rank);
+/* bounded host wait for every libppo stream (PPO_COMM_TIMEOUT_S, RCCL async errors polled): a stall
+ * or an RCCL error aborts the communicators and fails loudly, naming `what` */
+void phip_comm_wait(const char* what);
+/* replica check: this rank's parameter hash into a device word (Σ mix(index, bits) over the spans,
+ * indices running on across spans), then an all-gather over ranks, a bounded wait and the comparison —
+ * 0 if every rank's hash equals rank 0's, −1 with the differing ranks in msg; own ← this rank's hash */
+void phip_param_hash(const float* const* spans, const long* lens, int nspans);
+int  phip_comm_check_hash(int gather, unsigned long long* own, char* msg, int cap);   /* gather 0: own only */
 
 /* ---------------- profiling ---------------- */
 /* host C wrappers bracket launches: slot = phip_prof_begin(cls, work); ...; phip_prof_end(slot) */

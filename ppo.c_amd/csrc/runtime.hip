@@ -72,6 +72,18 @@ hipStream_t stream() {
     return g_use_side ? g_side : g_stream;
 }
 
+int streams_pending() {
+    ensure_device();
+    int mask = 0;
+    const hipStream_t s[2] = {g_stream, g_side};
+    for (int i = 0; i < 2; i++) {
+        const hipError_t e = hipStreamQuery(s[i]);
+        if (e == hipErrorNotReady) mask |= 1 << i;
+        else if (e != hipSuccess) check(e, "hipStreamQuery", __FILE__, __LINE__);
+    }
+    return mask;
+}
+
 // ---------------- per-launch event timing ----------------
 struct ProfSlot { hipEvent_t a, b; int k; double work; long long key; int ext; };   // ext: 1 awaiting, 2 stamped
 static bool                  g_prof_on = false;

@@ -521,9 +521,6 @@ int nn_value_fold_ok(const NeuralNetwork* nn, int m) {
            phip_x3_supported(2, m, n, l);
 }
 
-static float* g_fold_ws = NULL;       /* ypart [slots][m] | g [m] */
-static size_t g_fold_cap = 0;
-
 void nn_value_fold_step(NeuralNetwork* nn, const float* d_x, const int* d_rows, float* d_xcopy, int m, int grads_zero,
                         long reduce_extra, const float* tgt, float* loss_accum) {
     const int L = nn->num_layers - 1;
@@ -533,12 +530,12 @@ void nn_value_fold_step(NeuralNetwork* nn, const float* d_x, const int* d_rows, 
     const size_t mp = ((size_t)m + 3) & ~(size_t)3;
     const size_t slots_max = 2 * (size_t)((l + 63) / 64);     /* column tiles (≥ 64 wide) × 2 waves along N */
     const size_t need = slots_max * mp + mp;
-    if (need > g_fold_cap) {
-        phip_free(g_fold_ws);
-        g_fold_ws = (float*)phip_malloc(sizeof(float) * need);
-        g_fold_cap = need;
+    if ((long)need > nn->fold_ws_cap) {        /* the network's own scratch, freed with it */
+        phip_free(nn->d_fold_ws);
+        nn->d_fold_ws = (float*)phip_malloc(sizeof(float) * need);
+        nn->fold_ws_cap = (long)need;
     }
-    float* ypart = g_fold_ws;
+    float* ypart = nn->d_fold_ws;
     float* g = ypart + slots_max * mp;
     FoldFwd ff = {out->d_weights, ypart, 0};
     nn_forward_dev_upto(nn, d_x, d_rows, d_xcopy, m, L - 1, &ff);
@@ -692,6 +689,7 @@ void free_neural_network(NeuralNetwork* nn) {
     phip_free(nn->d_act_bits);
     phip_free(nn->d_w16);
     phip_free(nn->d_tiny_wt);
+    phip_free(nn->d_fold_ws);
     phip_free(nn->d_params);
     phip_free(nn->d_grads);
     nn_registry_remove(nn);

@@ -562,8 +562,8 @@ static int value_step(StepCtx* c, long iv, int v_zero, int tab) {
         phip_gather_rows(perm, c->keys_v[j], k * B, c->limit, B, c->S, c->A, buf->state_p, buf->action_p,
                          buf->logprob_p, buf->advantage_p, buf->adv_target_p, NULL, NULL, NULL, NULL, d->tgt, d->rows);
     }
-    /* with a communicator: gradients all-reduced in per-layer buckets as the backward produces them
-     * (comm.hip's comm stream), joined before Adam */
+    /* with a communicator: the gradients all-reduced after the backward (comm.hip: one all-reduce in
+     * this stream by default; PPO_COMM_ASYNC=1 per-layer buckets on the comm stream), joined before Adam */
     if (c->fold_v && !tab) {   /* output layer + MSE folded into the last hidden layer (nn_value_fold_step) */
         nn_value_fold_step(V, buf->state_p, rows, d->states, B, v_zero, c->comm ? 0 : -1, tgt, d->stats + 0);
     } else if (c->fuse_v) {    /* output layer + MSE + output-layer backward in one pass (out_head.hip) */
@@ -797,12 +797,51 @@ static void phase_gather(StepCtx* c) {
     c->phg = 1;
 }
 
+/* the replica check's parameter spans in HBM: μ, log σ, V */
+static void replica_hash(PPO* ppo) {
+    GaussianPolicy* pol = ppo->policy;
+    const float* spans[3] = {pol->mu->d_params, pol->d_log_std, ppo->V->d_params};
+    const long lens[3] = {pol->mu->num_params, pol->action_size, ppo->V->num_params};
+    phip_param_hash(spans, lens, 3);
+}
+
+unsigned long long ppo_param_hash(void* vppo) {
+    unsigned long long h = 0;
+    replica_hash((PPO*)vppo);
+    char msg[8];
+    (void)phip_comm_check_hash(0, &h, msg, 0);    /* this rank's hash only: no collective */
+    return h;
+}
+
+int ppo_comm_check_replicas(void* vppo) {
+    replica_hash((PPO*)vppo);
+    char msg[400];
+    if (phip_comm_check_hash(1, NULL, msg, (int)sizeof(msg)) == 0) return 0;
+    char buf[480];
+    snprintf(buf, sizeof(buf), "replica check: parameters differ across ranks: %s", msg);
+    phip_record_error(buf);
+    return -1;
+}
+
+/* PPO_REPLICA_CHECK=K: the replica check after every K-th update at world > 1 (default 1, 0 = off) */
+static int replica_check_due(void) {
+    static long n = 0;
+    const char* e = getenv("PPO_REPLICA_CHECK");
+    const long k = e && *e ? atol(e) : 1;
+    if (k <= 0) return 0;
+    return ++n % k == 0;
+}
+
 void ppo_update(void* vppo, float gamma, int batch_size, int n_epochs_policy, int n_epochs_value, int shuffle_mode,
                 unsigned long long seed) {
     PPO* ppo = (PPO*)vppo;
     ppo_update_body(ppo, gamma, batch_size, n_epochs_policy, n_epochs_value, shuffle_mode, seed);
     ppo->V->dev_version++;               /* HBM parameters moved (also by the single-workgroup path) */
     ppo->policy->mu->dev_version++;
+    /* replicated Adam must leave every rank with the same parameters; a rank that drifted
+     * would otherwise train on its own weights silently */
+    if (phip_comm_world() > 1 && replica_check_due() && ppo_comm_check_replicas(ppo) != 0)
+        die(ppo_last_error());
 }
 
 static void ppo_update_body(PPO* ppo, float gamma, int batch_size, int n_epochs_policy, int n_epochs_value,
@@ -844,9 +883,10 @@ static void ppo_update_body(PPO* ppo, float gamma, int batch_size, int n_epochs_
      * side stream (own workspaces), issued interleaved.  Every network sees exactly the reference's
      * sequence of minibatches and Adam steps; epochs' shuffles are drawn up front in the
      * reference's order (value epochs first).  PPO_SERIAL=1 runs them one after the other.  Under
-     * data parallelism (world > 1) both loops hand their gradient all-reduces to comm.hip's single
-     * comm stream in this host issue order, identical on every rank, so they stay concurrent and
-     * each collective overlaps the other loop's kernels. */
+     * data parallelism (world > 1) each loop issues one gradient all-reduce per step in its own
+     * stream on its own communicator (comm.hip; PPO_COMM_ASYNC=1: per-layer buckets on one comm
+     * stream).  The interleave below is a fixed function of (iv, ip, nv, np), never of timing, so
+     * every rank issues the same total order of collectives — half of comm.hip's deadlock argument. */
     long nv = (long)n_epochs_value * num_batches, np = (long)n_epochs_policy * num_batches;
     if (d->max_v >= 0 && nv > d->max_v) nv = d->max_v;
     if (d->max_p >= 0 && np > d->max_p) np = d->max_p;

@@ -43,7 +43,8 @@ class NeuralNetwork(C.Structure):
                 ("bits_m", C.c_int), ("dtype", C.c_int), ("x0_dtype", C.c_int), ("d_w16", C.c_void_p),
                 ("d_tiny_wt", c_float_p), ("tiny_wt_cap", C.c_long),
                 ("h_sync", c_float_p), ("dev_version", C.c_long),
-                ("host_version", C.c_long), ("host_version_w", C.c_long)]
+                ("host_version", C.c_long), ("host_version_w", C.c_long),
+                ("d_fold_ws", c_float_p), ("fold_ws_cap", C.c_long)]
 
 
 class GaussianPolicy(C.Structure):
@@ -136,6 +137,10 @@ _SIGS = {
     "ppo_comm_loopback_peers": (C.c_int, [_P, _P, C.c_int]),
     "ppo_comm_loopback_peer_grads": (C.c_int, [_P, _P, C.c_long]),
     "ppo_comm_loopback_clear": (None, []),
+    "ppo_comm_loopback_peer_hash": (C.c_int, [_P, C.c_int]),
+    "ppo_comm_mode": (C.c_char_p, []),
+    "ppo_comm_check_replicas": (C.c_int, [_P]),
+    "ppo_param_hash": (C.c_ulonglong, [_P]),
     "ppo_gae_state": (C.c_long, [_P, _P, _P, C.c_long]),
     "ppo_comm_barrier": (None, []),
     "ppo_comm_max_f64": (C.c_double, [C.c_double]),

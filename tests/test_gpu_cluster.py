@@ -152,12 +152,20 @@ def cos_ratio(d, dr):
 # may decorrelate from the oracle at most CHAOS_FACTOR times as much as the oracle does from itself,
 # plus CHAOS_SLACK (one sample of a chaotic process against two):
 # 1 − cos_gpu ≤ CHAOS_FACTOR · (1 − min cos_floor) + CHAOS_SLACK.  A defect outruns it already at 64 steps.
-CHAOS_FACTOR, CHAOS_SLACK = 2.0, 0.02
+# Round 6: CHAOS_FACTOR 2.0 → 1.25 — the measured GPU drift is 1.05× (512 policy steps, multi-launch) and
+# 1.16× (the whole update's μ) the oracle's own; every check prints its margin (1 − cos_gpu) / (1 − floor)
+# (profiles/r06_chaos_margins.txt).  And an absolute floor where the oracle's is low: at 512 steps a GPU
+# path must keep cos ≥ CHAOS_ABS_MIN against the oracle whatever the floor.
+CHAOS_FACTOR, CHAOS_SLACK, CHAOS_ABS_MIN = 1.25, 0.02, 0.5
 
 
 def assert_within_chaos_floor(cos_gpu, floor_cos, what):
     bound = 1 - (CHAOS_FACTOR * (1 - min(floor_cos)) + CHAOS_SLACK)
+    margin = (1 - cos_gpu) / max(1e-12, 1 - min(floor_cos))
+    print(f"CHAOS_MARGIN {what}: 1-cos {1 - cos_gpu:.5f} floor 1-cos {1 - min(floor_cos):.5f} margin {margin:.3f} "
+          f"(allowed {CHAOS_FACTOR} + slack)")
     assert cos_gpu >= bound, f"{what}: cos {cos_gpu:.5f} < {bound:.5f} (oracle self-drift floor {floor_cos})"
+    assert cos_gpu >= CHAOS_ABS_MIN, f"{what}: cos {cos_gpu:.5f} < absolute minimum {CHAOS_ABS_MIN}"
 
 
 @NETS
@@ -231,10 +239,10 @@ def test_cluster_barrier_timeout_fails_loudly(lib, sizes, tmp_path):
     assert "UPDATE RETURNED" not in r.stdout
 
 
-@pytest.mark.parametrize("steps", [64, 512])
+@pytest.mark.parametrize("steps", [64, 128, 512])
 @pytest.mark.parametrize("phase", ["value", "policy"])
 def test_long_run_drift_within_oracle_chaos_floor(lib, oracle, phase, steps):
-    """C4 networks, 64 and 512 value or policy steps (two epochs, the epoch boundary included): both GPU
+    """C4 networks, 64, 128 and 512 value or policy steps (two epochs, the epoch boundary included): both GPU
     B = 64 paths (the cluster phase and the multi-launch loop) against the oracle, bounded by the
     oracle's own self-drift on the same buffer — the oracle with every product split-K re-associated,
     and in double-precision products rounded once (CHAOS_FACTOR, CHAOS_SLACK above); motion norms

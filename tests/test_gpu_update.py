@@ -316,20 +316,35 @@ def test_concurrent_value_policy_loops(lib, oracle, shuffle_mode, monkeypatch):
         assert (err > 1e-6).mean() < 0.02, (k, (err > 1e-6).mean())
 
 
-def test_comm_stream_rehearsal(lib, oracle, monkeypatch):
-    """The data-parallel path on one GPU: a one-rank RCCL communicator (PPO_COMM_SELF=1) routes every
-    gradient all-reduce through comm.hip's comm stream (issuing stream -> event -> comm stream ->
-    event -> Adam) while the value and policy loops run concurrently, exactly as at world > 1.  The
-    one-rank sum is the identity, so the update must equal the update without a communicator: value
-    network bit for bit (split-K forced off), policy within the log σ-gradient atomics bound."""
+@pytest.mark.parametrize("comm,async_", [("self", "0"), ("self", "1"), ("loopback2", "0"), ("loopback2", "1")])
+def test_comm_rehearsal(lib, oracle, comm, async_, monkeypatch):
+    """The data-parallel path on one GPU, in both gradient all-reduce forms, while the value and policy
+    loops run concurrently, exactly as at world > 1:
+      * inline (default): one all-reduce per step in each loop's own stream, a communicator per loop
+        (the policy loop's split from the value loop's), Adam behind it in stream order;
+      * bucketed (PPO_COMM_ASYNC=1, also the fallback when the split fails on any rank): per-layer
+        buckets on comm.hip's comm stream over one communicator (issuing stream -> event -> comm
+        stream -> event -> Adam).
+    comm = "self": a one-rank RCCL communicator (PPO_COMM_SELF=1) — the one-rank sum is the identity;
+    comm = "loopback2": two identical in-process ranks (PPO_COMM_LOOPBACK=2) — the sum is 2·g and Adam
+    applies ½, exact in binary.  Either way the update must equal the update without a communicator:
+    value network bit for bit (split-K forced off), policy within the log σ-gradient atomics bound; the
+    per-update replica check runs (loopback: world 2) and passes."""
     sizes, N, B = [17, 256, 256, 6], 4096, 512
     lib.ppo_gemm_tune(-1, 1)
     monkeypatch.delenv("PPO_SERIAL", raising=False)
     out = {}
     for mode in ("plain", "comm"):
         if mode == "comm":
-            monkeypatch.setenv("PPO_COMM_SELF", "1")
+            monkeypatch.setenv("PPO_COMM_ASYNC", async_)
+            if comm == "self":
+                monkeypatch.setenv("PPO_COMM_SELF", "1")
+            else:
+                monkeypatch.setenv("PPO_COMM_LOOPBACK", "2")
             assert lib.ppo_comm_init(0, 1, None) == 0, lib.ppo_last_error()
+            want = "bucketed" if async_ == "1" else "inline"
+            assert want in lib.ppo_comm_mode().decode(), lib.ppo_comm_mode()
+            assert lib.ppo_comm_world() == (2 if comm == "loopback2" else 1)
         ppo = make_ppo(lib, oracle, sizes, N)
         mu0, ls0 = policy_state(lib, ppo)
         buf = synthetic_buffer(oracle, sizes, mu0, ls0, N, seed=5, n_envs=8)
@@ -344,6 +359,8 @@ def test_comm_stream_rehearsal(lib, oracle, monkeypatch):
         lib.free_ppo(ppo)
         if mode == "comm":
             lib.ppo_comm_finalize()
+            for k in ("PPO_COMM_SELF", "PPO_COMM_LOOPBACK", "PPO_COMM_ASYNC"):
+                monkeypatch.delenv(k, raising=False)
     lib.ppo_gemm_tune(-1, 0)
     a, b = out["plain"], out["comm"]
     np.testing.assert_allclose(a["stats"], b["stats"], rtol=1e-5, atol=1e-6)

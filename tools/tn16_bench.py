@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
-"""bf16 grad_W (C5 shapes) per launch: the LDS-DMA TN tile (automatic; PPO_G16_TN_BN forces its width)
-against the register-staged split-K kernel (cfg 6 forced).
+"""bf16 grad_W (C5 shapes) per launch: the LDS-DMA TN tile (width 128 by default; --bn 256 sets it
+through ppo_gemm16_tn_width) against the register-staged split-K kernel (cfg 6 forced).
 
-    python tools/tn16_bench.py [m n l ...]
+    python tools/tn16_bench.py [--bn 128|256] [m n l ...]
 """
 import os
 import sys
@@ -12,8 +12,12 @@ import ppo_ffi  # noqa: E402
 
 lib = ppo_ffi.load()
 lib.ppo_set_device(0)
-args = [int(v) for v in sys.argv[1:]] or [16384, 1024, 1024, 4096, 1024, 1024, 16384, 384, 512]
-bn = os.environ.get("PPO_G16_TN_BN", "auto")
+argv = sys.argv[1:]
+bn = 128
+if argv[:1] == ["--bn"]:
+    bn, argv = int(argv[1]), argv[2:]
+lib.ppo_gemm16_tn_width(bn)
+args = [int(v) for v in argv] or [16384, 1024, 1024, 4096, 1024, 1024, 16384, 384, 512]
 for i in range(0, len(args), 3):
     m, n, l = args[i:i + 3]
     lib.ppo_bench_gemm16(2, m, n, l, 200, -1, 0)                 # settle the clock
