@@ -182,7 +182,10 @@ constexpr int small_slots() { return (HC * (20 + 2 + 16) + 32 + TPB - 1) / TPB; 
 
 #define CL_STAMP(slot)                                                                          \
     do {                                                                                        \
-        if (a.stamps && cw == 0 && tid == 0 && step < 64) a.stamps[step * 12 + (slot)] = wall_clock64(); \
+        if (a.stamps && cw == 0 && tid == 0 && step < 64) {                                     \
+            a.stamps[step * 12 + (slot)] = wall_clock64();                                       \
+            a.stamps[CLU_STAMP_CLK + step * 12 + (slot)] = __builtin_amdgcn_s_memtime();         \
+        }                                                                                        \
     } while (0)
 
 template <int H, int HC>
@@ -596,7 +599,7 @@ bool host_grid_fits(const void* kfn, size_t lds, int grid) {
 unsigned long long* host_stamps(int nstamp, const char* kind, const char* const* names, int policy, int total_steps,
                                 int nwg) {
     StampSlot& s = g_stamps[phip_side_active() ? 1 : 0];
-    if (!s.buf) s.buf = (unsigned long long*)phip_malloc(sizeof(unsigned long long) * (64 * 32 + 64));
+    if (!s.buf) s.buf = (unsigned long long*)phip_malloc(sizeof(unsigned long long) * (CLU_STAMP_CLK + 64 * 32));
     s.nstamp = nstamp; s.kind = kind; s.names = names; s.policy = policy; s.total_steps = total_steps; s.nwg = nwg;
     s.pending = total_steps >= 64;
     return s.buf;
@@ -621,16 +624,23 @@ void phip_cluster_report(void) {
         const double mhz = khz > 0 ? khz / 1000.0 : 100.0;
         unsigned long long h[64 * 32];
         phip_d2h(h, s.buf, sizeof(unsigned long long) * 64 * (size_t)s.nstamp);
-        double acc[32] = {0}, tot = 0;
+        // the shader clock beside the wall clock (s_memtime counts core cycles, s_memrealtime 100 MHz ticks):
+        // per sub-phase the mean wall time and the clock it ran at, MHz = Δcycles / Δµs
+        unsigned long long c[64 * 32];
+        phip_d2h(c, s.buf + CLU_STAMP_CLK, sizeof(unsigned long long) * 64 * (size_t)s.nstamp);
+        double acc[32] = {0}, cyc[32] = {0}, tot = 0, tcyc = 0;
         for (int st = 1; st < 63; ++st)
             for (int k = 0; k < s.nstamp; ++k) {
-                const unsigned long long t0 = h[st * s.nstamp + k];
-                const unsigned long long t1 = k < s.nstamp - 1 ? h[st * s.nstamp + k + 1] : h[(st + 1) * s.nstamp];
-                acc[k] += (double)(t1 - t0) / mhz;
+                const int i0 = st * s.nstamp + k, i1 = k < s.nstamp - 1 ? i0 + 1 : (st + 1) * s.nstamp;
+                acc[k] += (double)(h[i1] - h[i0]) / mhz;
+                cyc[k] += (double)(c[i1] - c[i0]);
             }
         fprintf(stderr, "%s %s step (us):", s.kind, s.policy ? "policy" : "value");
-        for (int k = 0; k < s.nstamp; ++k) { fprintf(stderr, " %s %.2f", s.names[k], acc[k] / 62); tot += acc[k] / 62; }
+        for (int k = 0; k < s.nstamp; ++k) { fprintf(stderr, " %s %.2f", s.names[k], acc[k] / 62); tot += acc[k] / 62; tcyc += cyc[k] / 62; }
         fprintf(stderr, " | total %.2f\n", tot);
+        fprintf(stderr, "%s %s shader clock (MHz):", s.kind, s.policy ? "policy" : "value");
+        for (int k = 0; k < s.nstamp; ++k) fprintf(stderr, " %s %.0f", s.names[k], acc[k] > 0 ? cyc[k] / acc[k] : 0.0);
+        fprintf(stderr, " | step %.0f\n", tot > 0 ? tcyc / tot : 0.0);
         // placement: per workgroup XCC id and HW_ID's CU [11:8] / SH [12] / SE [14:13] fields
         unsigned long long pl[64];
         phip_d2h(pl, s.buf + 64 * 32, sizeof(unsigned long long) * (size_t)s.nwg);

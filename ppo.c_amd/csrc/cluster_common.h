@@ -183,6 +183,10 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
     p -= step * m / denom;
 }
 
+// stamp buffer layout (PPO_CLUSTER_STAMPS): [64 steps][≤ 32] s_memrealtime | [64] placement words |
+// [64 steps][≤ 32] s_memtime (the shader clock beside the wall clock, at the same points)
+constexpr int CLU_STAMP_CLK = 64 * 32 + 64;
+
 // ---- host side, shared by both phase kernels (defined in cluster.hip) ----
 // Barrier wait bound in realtime ticks: 2 s (PPO_CLUSTER_TEST_TIMEOUT=1, a test hook, makes it 0 so
 // the first barrier that is not already complete times out and the error path runs).

@@ -313,7 +313,10 @@ __device__ __forceinline__ void publish_partial(int tid, __amdgpu_buffer_rsrc_t 
 
 #define CD_STAMP(slot)                                                                                   \
     do {                                                                                                 \
-        if (a.stamps && cw == 0 && tid == 0 && step < 64) a.stamps[step * NSTAMP + (slot)] = wall_clock64(); \
+        if (a.stamps && cw == 0 && tid == 0 && step < 64) {                                             \
+            a.stamps[step * NSTAMP + (slot)] = wall_clock64();                                           \
+            a.stamps[CLU_STAMP_CLK + step * NSTAMP + (slot)] = __builtin_amdgcn_s_memtime();             \
+        }                                                                                                \
     } while (0)
 
 __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {

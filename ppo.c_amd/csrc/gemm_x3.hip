@@ -58,6 +58,8 @@ struct X3Args {
     const int* ridx; float* acopy;        // forward: fused gather of A's rows + the gathered copy
     unsigned* bits_out; const unsigned* bits_in; int wpr;
     float* gbias;                         // grad_W: bias gradient (Σ over the batch of g)
+    const int* bridx;                     // grad_W: B's batch rows through these indices (x = buffer rows of
+                                          // the minibatch: layer 0 reads them where the forward read them)
     int kchunk, splits, tiles_m, tiles_n;
     float* slab;                          // grad_W split-K: per-split partial tiles [splits][M][N] (plain
                                           // stores, summed by slab_reduce_kernel) instead of f32 atomics
@@ -187,6 +189,10 @@ struct StageX3 {
     float gq[NV];
     const unsigned* bw_row;
     unsigned bword;
+    // row-contiguous operand whose k-rows (batch rows) are gathered: k-row kk is HBM row gt[kk] (an LDS
+    // table of the split's row indices, indexed by the absolute k), column offset gbase
+    const int* gt;
+    const float* gbase;
 
     // src row (k-contiguous: after the gather, clamped into the operand); rows past the end read row
     // Rmax − 1 (their products land in output rows that are never stored)
@@ -207,15 +213,26 @@ struct StageX3 {
             base = p + (long)(ridx ? ridx[gr] : gr) * ld + k;
         }
     }
+    __device__ __forceinline__ void init_gather(const float* __restrict__ p, const int* tbl, int r0, int Rmax) {
+        gt = tbl;
+        gbase = p + min(r0 + row, Rmax - 4);
+    }
     __device__ __forceinline__ void init_fold(const float* __restrict__ g, const unsigned* __restrict__ bits, int wpr,
                                               int r0, int Rmax) {
         sg = g;
         if (!MN && bits) bw_row = bits + (long)min(r0 + row, Rmax - 1) * wpr;
     }
     // FULL: the whole k-tile lies inside [kbeg, kend) — no clamping
-    template <bool FULL, int FM = 0>
+    template <bool FULL, int FM = 0, bool GT = false>
     __device__ __forceinline__ void load(int k0, int kend) {
-        if (MN) {
+        if (MN && GT) {
+#pragma unroll
+            for (int q = 0; q < NV; ++q) {
+                const int kk = FULL ? k0 + k + q * KSTEP : min(k0 + k + q * KSTEP, kend - 1);
+                v[q] = *reinterpret_cast<const f32x4*>(gbase + (long)gt[kk] * ld);
+                if (FM == 1) gq[q] = sg[kk];
+            }
+        } else if (MN) {
 #pragma unroll
             for (int q = 0; q < NV; ++q) {
                 const int dk = FULL ? k0 + q * KSTEP : min(k0 + k + q * KSTEP, kend - 1) - k;
@@ -461,7 +478,7 @@ __device__ __forceinline__ void x3_epilogue_out(const X3Args& a, f32x16 (&acc)[T
 }
 
 // FOLD: the value-head fold variant (forward: ydot / ypart; grad_x / grad_W: A synthesised from h)
-template <int OP, int BM, int BN, int WARPS_M, int NTH, int OCC, int KG, int ABL = 0, int FOLD = 0>
+template <int OP, int BM, int BN, int WARPS_M, int NTH, int OCC, int KG, int ABL = 0, int FOLD = 0, int GATHER = 0>
 __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     constexpr int NTG = NTH / KG;                                  // threads per k-group
     constexpr int NW = NTG / 64, WARPS_N = NW / WARPS_M;
@@ -531,10 +548,19 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     constexpr bool syn = OP != OP_NT && FOLD != 0;
     constexpr int FMA_ = !syn ? 0 : OP == OP_NN ? 2 : 1;          // A's fold load mode
     constexpr int FMB_ = syn ? 1 : 0;                             // B's
+    constexpr bool GB = OP == OP_TN && GATHER != 0;               // B's batch rows through a.bridx
+    static_assert(!GATHER || OP == OP_TN, "x3 gather of B: grad_W only");
     const float* fold_g = a.fold_g;
+    if constexpr (GB) {
+        // the split's row indices → LDS (behind the ring), read by every B load of the mainloop
+        int* tbl = reinterpret_cast<int*>(lds + KG * NS * BUF);
+        for (int i = tid; i < kend - kbeg; i += NTH) tbl[i] = a.bridx[kbeg + i];
+        __syncthreads();
+        sb.init_gather(a.B, tbl - kbeg, n0, a.N);
+    }
     if constexpr (OP == OP_TN && FOLD != 0) {
         if (a.vh_ypart) {                                         // the value head, carried (X3Args vh_*)
-            float* gl = reinterpret_cast<float*>(lds + KG * NS * BUF);
+            float* gl = reinterpret_cast<float*>(lds + KG * NS * BUF) + (GB ? a.kchunk : 0);
             const bool head = tm == 0 && tn == 0;
             const float bias = a.vh_b[0];
             float ls = 0.f, sgs = 0.f;
@@ -668,7 +694,7 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
         constexpr bool SYN = OP != OP_NT && decltype(SYNc)::value;
         if ((ABL & 8) && k0 != kbeg) return;
         sa.template load<FULL, SYN ? FMA_ : 0>(k0, kend);
-        sb.template load<FULL, SYN ? FMB_ : 0>(k0, kend);
+        sb.template load<FULL, SYN ? FMB_ : 0, GB>(k0, kend);
     };
     using T = std::true_type;
     using F = std::false_type;
@@ -968,7 +994,7 @@ int g_x3_ablate = -1;
 
 int g_x3_last_slots = 0;                 // the last launch's ypart slots (tiles_n × waves along N)
 
-template <int OP, int BM, int BN, int WARPS_M, int NTH, int OCC, int KG, int ABL = 0, int FOLD = 0>
+template <int OP, int BM, int BN, int WARPS_M, int NTH, int OCC, int KG, int ABL = 0, int FOLD = 0, int GATHER = 0>
 void launch_x3(X3Args a) {
     a.tiles_m = ppo_divup(a.M, BM);
     a.tiles_n = ppo_divup(a.N, BN);
@@ -988,8 +1014,12 @@ void launch_x3(X3Args a) {
     constexpr size_t lds0 = (size_t)KG * 3 * sizeof(unsigned short) * (SA::SIZE + SB::SIZE);   // 3-stage ring
     static_assert(lds0 <= 160 * 1024, "gemm_x3: LDS images exceed 160 KiB");
     size_t lds = lds0;
+    if (GATHER) {                                      // the split's row-index table (B gathered)
+        lds += 4 * (size_t)a.kchunk;
+        PPO_REQUIRE(lds <= 160 * 1024 && a.bridx, "gemm_x3: gathered grad_W index table exceeds LDS");
+    }
     if (OP == OP_TN && FOLD && a.vh_ypart) {           // the carried value head's g of the split's rows
-        if (lds0 + 4 * (size_t)a.kchunk <= 160 * 1024) {
+        if (lds + 4 * (size_t)a.kchunk <= 160 * 1024) {
             lds += 4 * (size_t)a.kchunk;
         } else {                                       // no room: the head kernel first, g from HBM
             phip_value_head(a.vh_ypart, a.vh_slots, a.vh_b, a.vh_t, a.K, a.vh_y, const_cast<float*>(a.fold_g), a.vh_gb,
@@ -997,7 +1027,7 @@ void launch_x3(X3Args a) {
             a.vh_ypart = nullptr;
         }
     }
-    auto kern = gemm_x3_kernel<OP, BM, BN, WARPS_M, NTH, OCC, KG, ABL, FOLD>;
+    auto kern = gemm_x3_kernel<OP, BM, BN, WARPS_M, NTH, OCC, KG, ABL, FOLD, GATHER>;
     if (lds > 64 * 1024) {
         static bool attr = false;                      // once per instantiation (the whole LDS)
         if (!attr) {
@@ -1060,19 +1090,33 @@ constexpr CfgX3 kCfgX3[] = {{256, 256, 1, 1}, {128, 128, 1, 2}, {128, 128, 1, 1}
 int g_force_x3 = -1;
 int g_split_x3 = 0;
 
+template <int OP, int FOLD, int GATHER>
+void launch_cfg_x3_var(int c, const X3Args& a) {
+    switch (c) {
+        case 0: launch_x3<OP, 256, 256, 4, 512, 2, 1, 0, FOLD, GATHER>(a); return;
+        case 2: launch_x3<OP, 128, 128, 4, 512, 2, 1, 0, FOLD, GATHER>(a); return;
+        case 4: launch_x3<OP, 64, 64, 2, 256, 4, 1, 0, FOLD, GATHER>(a); return;
+        case 5: launch_x3<OP, 256, 128, 4, 512, 2, 1, 0, FOLD, GATHER>(a); return;
+        case 3:
+            if constexpr (OP == OP_TN) { launch_x3<OP, 128, 128, 2, 512, 2, 2, 0, FOLD, GATHER>(a); return; }
+            [[fallthrough]];
+        default: launch_x3<OP, 128, 128, 2, 256, 2, 1, 0, FOLD, GATHER>(a); return;
+    }
+}
+
 template <int OP>
 void launch_cfg_x3(int c, const X3Args& a) {
-    if (a.ydot || a.fold_g) {                      // the value-head fold variants
-        switch (c) {
-            case 0: launch_x3<OP, 256, 256, 4, 512, 2, 1, 0, 1>(a); return;
-            case 2: launch_x3<OP, 128, 128, 4, 512, 2, 1, 0, 1>(a); return;
-            case 4: launch_x3<OP, 64, 64, 2, 256, 4, 1, 0, 1>(a); return;
-            case 5: launch_x3<OP, 256, 128, 4, 512, 2, 1, 0, 1>(a); return;
-            case 3:
-                if constexpr (OP == OP_TN) { launch_x3<OP, 128, 128, 2, 512, 2, 2, 0, 1>(a); return; }
-                [[fallthrough]];
-            default: launch_x3<OP, 128, 128, 2, 256, 2, 1, 0, 1>(a); return;
+    const bool fold = a.ydot || a.fold_g;           // the value-head fold variants
+    if constexpr (OP == OP_TN) {
+        if (a.bridx) {                              // layer 0's grad_W: x rows through the minibatch indices
+            if (fold) launch_cfg_x3_var<OP, 1, 1>(c, a);
+            else launch_cfg_x3_var<OP, 0, 1>(c, a);
+            return;
         }
+    }
+    if (fold) {
+        launch_cfg_x3_var<OP, 1, 0>(c, a);
+        return;
     }
 #ifdef PPO_X3_DIAG
     if (g_x3_ablate < 0) {
@@ -1129,7 +1173,38 @@ inline bool al16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 }  // namespace
 
+namespace {
+// dst[i][:] = src[rows[i]][:] (n % 4 == 0, 16-B aligned rows): the gathered-grad_W fallback for long splits
+__global__ void x3_gather_rows_kernel(float* __restrict__ dst, const float* __restrict__ src, const int* __restrict__ rows,
+                                      long m, int n4) {
+    for (long e = blockIdx.x * 256L + threadIdx.x; e < m * n4; e += (long)gridDim.x * 256) {
+        const long i = e / n4;
+        const int c = (int)(e % n4);
+        reinterpret_cast<f32x4*>(dst)[e] = reinterpret_cast<const f32x4*>(src + (long)rows[i] * 4 * n4)[c];
+    }
+}
+}  // namespace
+
 namespace ppo {
+
+static float* g_xg[2] = {nullptr, nullptr};
+static size_t g_xg_cap[2] = {0, 0};
+float* x3_gather_scratch(size_t floats) {
+    const int s = phip_side_active() ? 1 : 0;
+    if (floats > g_xg_cap[s]) {
+        phip_free(g_xg[s]);
+        g_xg[s] = (float*)phip_malloc(sizeof(float) * floats);
+        g_xg_cap[s] = floats;
+    }
+    return g_xg[s];
+}
+void x3_gather_rows(float* dst, const float* src, const int* rows, long m, int n) {
+    PPO_REQUIRE(n % 4 == 0 && al16(dst) && al16(src), "x3_gather_rows: operands");
+    const long work = m * (n / 4);
+    const int grid = (int)std::min<long>(4096, std::max<long>(1, (work + 255) / 256));
+    hipLaunchKernelGGL(x3_gather_rows_kernel, dim3(grid), dim3(256), 0, stream(), dst, src, rows, m, n / 4);
+    PPO_LAUNCH_CHECK();
+}
 
 // per-stream slab buffers (the value and policy loops run their grad_W launches on two streams)
 static float* g_slab[2] = {nullptr, nullptr};
@@ -1168,6 +1243,10 @@ static int g_defer_next = 0;
 }  // namespace ppo
 
 extern "C" {
+
+void phip_gather_rows_f32(float* dst, const float* src, const int* rows, long m, int n) {
+    ppo::x3_gather_rows(dst, src, rows, m, n);
+}
 
 // The next phip_x3_bwd_w(_fold) call on this thread leaves its split-K slab reduce (if it uses slabs) to
 // the next phip_x3_bwd_x(_fold) launch on the same stream, which runs it in extra workgroups beside its
@@ -1237,13 +1316,20 @@ void phip_x3_bwd_x(float* gx, const float* g, const float* W, const unsigned* bi
 }
 
 void phip_x3_bwd_w_vhead(float* gW, float* gb, const float* g, float* fold_g, const float* fold_w, float* fold_gw,
-                         const float* x, int m, int n, int l, int zeroed, const float* ypart, int slots, const float* b,
-                         const float* tgt, float* y, float* gb_out, float* loss_accum);
+                         const float* x, const int* xrows, int m, int n, int l, int zeroed, const float* ypart,
+                         int slots, const float* b, const float* tgt, float* y, float* gb_out, float* loss_accum);
 
 // zeroed: gW / gb already hold zeros (one memset per backward); otherwise they are cleared here
 void phip_x3_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, int n, int l, int zeroed) {
-    phip_x3_bwd_w_vhead(gW, gb, g, nullptr, nullptr, nullptr, x, m, n, l, zeroed, nullptr, 0, nullptr, nullptr, nullptr,
-                        nullptr, nullptr);
+    phip_x3_bwd_w_vhead(gW, gb, g, nullptr, nullptr, nullptr, x, nullptr, m, n, l, zeroed, nullptr, 0, nullptr, nullptr,
+                        nullptr, nullptr, nullptr);
+}
+
+// layer 0 of a minibatch: x row i is x[xrows[i]] (the buffer rows the forward gathered; no copy)
+void phip_x3_bwd_w_rows(float* gW, float* gb, const float* g, const float* x, const int* xrows, int m, int n, int l,
+                        int zeroed) {
+    phip_x3_bwd_w_vhead(gW, gb, g, nullptr, nullptr, nullptr, x, xrows, m, n, l, zeroed, nullptr, 0, nullptr, nullptr,
+                        nullptr, nullptr, nullptr);
 }
 
 // value-head fold (fold_g): g = h [m, l] (fp32, its mask is the operand), x scaled by fold_g per row, the
@@ -1251,15 +1337,15 @@ void phip_x3_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, 
 // diag(w)·maskᵀ·g — and fold_gw [l] (zero on entry) += Σ_rows fold_g·h, the output layer's gW
 void phip_x3_bwd_w_fold(float* gW, float* gb, const float* g, const float* fold_g, const float* fold_w,
                         float* fold_gw, const float* x, int m, int n, int l, int zeroed) {
-    phip_x3_bwd_w_vhead(gW, gb, g, const_cast<float*>(fold_g), fold_w, fold_gw, x, m, n, l, zeroed, nullptr, 0, nullptr,
-                        nullptr, nullptr, nullptr, nullptr);
+    phip_x3_bwd_w_vhead(gW, gb, g, const_cast<float*>(fold_g), fold_w, fold_gw, x, nullptr, m, n, l, zeroed, nullptr, 0,
+                        nullptr, nullptr, nullptr, nullptr, nullptr);
 }
 
 // + the carried value head (ypart set): g (fold_g, written) from the forward's partial dots, y, the output
 // bias gradient gb_out and the loss, in this launch (X3Args vh_*)
 void phip_x3_bwd_w_vhead(float* gW, float* gb, const float* g, float* fold_g, const float* fold_w, float* fold_gw,
-                         const float* x, int m, int n, int l, int zeroed, const float* ypart, int slots, const float* b,
-                         const float* tgt, float* y, float* gb_out, float* loss_accum) {
+                         const float* x, const int* xrows, int m, int n, int l, int zeroed, const float* ypart,
+                         int slots, const float* b, const float* tgt, float* y, float* gb_out, float* loss_accum) {
     if (l <= 0 || n <= 0) return;
     PPO_REQUIRE(!ypart || (fold_g && slots > 0 && b && tgt && y && gb_out), "phip_x3_bwd_w: carried value head operands");
     PPO_REQUIRE(gW && g && x && n % 4 == 0 && l % 4 == 0 && al16(g) && al16(x), "phip_x3_bwd_w: unsupported operands");
@@ -1293,6 +1379,17 @@ void phip_x3_bwd_w_vhead(float* gW, float* gb, const float* g, float* fold_g, co
     a.A = g; a.lda = l; a.B = x; a.ldb = n; a.C = gW; a.ldc = n;
     a.M = l; a.N = n; a.K = m; a.kchunk = kchunk; a.splits = splits;
     a.gbias = gb;
+    if (xrows) {
+        // x's rows through the minibatch indices: an LDS table of the split's indices (≤ 8 KiB beside the
+        // 144 KiB ring); a longer split gathers the rows into scratch first
+        if (kchunk <= 2048) {
+            a.bridx = xrows;
+        } else {
+            float* xs = ppo::x3_gather_scratch((size_t)m * n);
+            ppo::x3_gather_rows(xs, x, xrows, m, n);
+            a.B = xs;
+        }
+    }
     a.fold_g = fold_g; a.fold_w = fold_w; a.fold_gw = fold_gw;
     a.vh_ypart = ypart; a.vh_slots = slots; a.vh_b = b; a.vh_t = tgt; a.vh_y = y; a.vh_gb = gb_out; a.vh_loss = loss_accum;
     // split-K partials: per-split slabs written with plain stores and summed by one reduce launch

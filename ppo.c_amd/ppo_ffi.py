@@ -44,7 +44,7 @@ class NeuralNetwork(C.Structure):
                 ("d_tiny_wt", c_float_p), ("tiny_wt_cap", C.c_long),
                 ("h_sync", c_float_p), ("dev_version", C.c_long),
                 ("host_version", C.c_long), ("host_version_w", C.c_long),
-                ("d_fold_ws", c_float_p), ("fold_ws_cap", C.c_long)]
+                ("d_fold_ws", c_float_p), ("fold_ws_cap", C.c_long), ("d_x0_rows", C.POINTER(C.c_int))]
 
 
 class GaussianPolicy(C.Structure):
@@ -141,6 +141,7 @@ _SIGS = {
     "ppo_comm_mode": (C.c_char_p, []),
     "ppo_comm_check_replicas": (C.c_int, [_P]),
     "ppo_param_hash": (C.c_ulonglong, [_P]),
+    "ppo_nn_input_rows": (C.c_int, [_P, _P, C.c_int]),
     "ppo_gae_state": (C.c_long, [_P, _P, _P, C.c_long]),
     "ppo_comm_barrier": (None, []),
     "ppo_comm_max_f64": (C.c_double, [C.c_double]),

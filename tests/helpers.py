@@ -37,18 +37,28 @@ def assert_gemm_close(got, ref, K, what=""):
     assert err <= tol, f"{what}: max |err| {err:.3g} > tol {tol:.3g} (K={K})"
 
 
+def nn_input_rows(lib, nn_ptr, m):
+    """Layer 0's input rows of the last device forward (fp32), as the GEMMs read them: the buffer rows
+    through NeuralNetwork.d_x0_rows (x3 engine: no gathered copy) or the gathered copy d_x0."""
+    nn = nn_ptr.contents
+    S = nn.layers[0].input_size
+    out = np.empty((m, S), F32)
+    assert lib.ppo_nn_input_rows(nn_ptr, out.ctypes.data, m) == 0, "no fp32 layer-0 input of m rows"
+    return out
+
+
 def gpu_relu_masks(lib, nn_ptr, x_rows):
     """The ReLU′ masks libppo's last forward used (NeuralNetwork.d_act_bits: one [act_cap_m, ⌈w/32⌉]
     u32 block per layer input, bit c%32 of word c/32), for every hidden layer input, re-ordered to
-    the rows of `x_rows`: the forward's rows are matched to x_rows through the layer-0 input copy
-    (nn.d_x0, the gathered minibatch)."""
+    the rows of `x_rows`: the forward's rows are matched to x_rows through the layer-0 input rows
+    (nn_input_rows: the gathered minibatch)."""
     nn = nn_ptr.contents
     L = nn.num_layers - 1
     sizes = [nn.layers[i].input_size for i in range(L)] + [nn.output_size]
     m, cap = nn.bits_m, nn.act_cap_m
     if m != x_rows.shape[0] or not nn.d_x0 or not nn.d_act_bits:
         return None          # the last forward was not this one (e.g. the single-workgroup path)
-    x0 = ppo_ffi.d2h(lib, nn.d_x0, F32, m * sizes[0]).reshape(m, sizes[0])
+    x0 = nn_input_rows(lib, nn_ptr, m)
     where = {r.tobytes(): i for i, r in enumerate(np.ascontiguousarray(x_rows, F32))}
     order = np.array([where[r.tobytes()] for r in x0])      # forward row j = reference row order[j]
     total = sum(cap * ((s + 31) // 32) for s in sizes)

@@ -20,7 +20,7 @@ import pytest
 
 import ppo_ffi
 from gpu_internal import set_host_buffer
-from helpers import F32, nn_params_packed
+from helpers import nn_input_rows, F32, nn_params_packed
 from test_gpu_update import load_buffer, make_ppo, policy_state, synthetic_buffer
 
 pytestmark = pytest.mark.gpu
@@ -104,7 +104,7 @@ def test_get_batch_bitexact(lib, oracle, n, S, A, B):
 def _gathered_rows(lib, nn_ptr, B, S):
     nn = nn_ptr.contents
     assert nn.bits_m == B and nn.x0_dtype == 0
-    return ppo_ffi.d2h(lib, nn.d_x0, F32, B * S).reshape(B, S)
+    return nn_input_rows(lib, nn_ptr, B)
 
 
 @pytest.mark.parametrize("shuffle_mode", [0, 1])

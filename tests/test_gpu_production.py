@@ -32,8 +32,8 @@ import numpy as np
 import pytest
 
 import ppo_ffi
-from helpers import (F32, assert_gemm_close, assert_normalised_close, assert_rel_close, gpu_relu_masks, nn_grads_packed, nn_params_packed,
-                     oracle_grads_with_masks)
+from helpers import (F32, assert_gemm_close, assert_normalised_close, assert_rel_close, gpu_relu_masks,
+                     nn_grads_packed, nn_input_rows, nn_params_packed, oracle_grads_with_masks)
 from test_gpu_bf16 import bf16, unpack
 from test_gpu_update import adam_first_step, assert_adam_delta, make_ppo, policy_state
 
@@ -234,7 +234,7 @@ def c3(lib, oracle):
 def _gathered(lib, nn_ptr, B, S):
     nn = nn_ptr.contents
     assert nn.bits_m == B and nn.x0_dtype == 0
-    return ppo_ffi.d2h(lib, nn.d_x0, F32, B * S).reshape(B, S)
+    return nn_input_rows(lib, nn_ptr, B)
 
 
 def test_c3_gae_vs_oracle(lib, oracle, c3):

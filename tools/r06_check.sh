@@ -12,5 +12,8 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_cluster.py -x -v -s -k "cha
     --timeout 300 --timeout-method thread > $O/chaos.log 2>&1 || exit 1
 timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gputest.log 2>&1 || exit 1
 timeout -k 10 240 python bench.py --no-cpu-baseline > $O/c4.log 2>&1 || exit 1
+PPO_X0_COPY=1 timeout -k 10 240 python bench.py --no-cpu-baseline --no-rollout > $O/c4_x0copy.log 2>&1 || exit 1
+timeout -k 10 240 python bench.py --no-cpu-baseline --no-rollout > $O/c4_b.log 2>&1 || exit 1
 PPO_COMM_SELF=1 timeout -k 10 240 python bench.py --emulate-world 8 --no-cpu-baseline --no-rollout > $O/shard8.log 2>&1 || exit 1
 PPO_COMM_SELF=1 PPO_COMM_ASYNC=1 timeout -k 10 240 python bench.py --emulate-world 8 --no-cpu-baseline --no-rollout > $O/shard8_async.log 2>&1 || exit 1
+PPO_CLUSTER_STAMPS=1 timeout -k 10 200 python bench.py --config c4 --batch 64 --steps 3 --warmup 1 --no-cpu-baseline --no-rollout --no-kernel-events > $O/c4b64_clock.log 2>&1 || exit 1
