@@ -26,7 +26,9 @@ int         streams_pending();
 // records the stop event and attributes `work` (FLOPs or bytes) to class k.
 struct ProfScope {
     int k; double work; int slot;
-    ProfScope(int k_, double work_, long long key = 0);   // key: shape tag (gemm_key) for per-shape stats
+    // key: shape tag (gemm_key) for per-shape stats; active = false: a scope that records nothing (a
+    // launch handed to a later call, which accounts for it)
+    ProfScope(int k_, double work_, long long key = 0, bool active = true);
     ~ProfScope();
 };
 

@@ -477,9 +477,11 @@ __device__ __forceinline__ void x3_epilogue_out(const X3Args& a, f32x16 (&acc)[T
     else body(std::false_type{});
 }
 
-// FOLD: the value-head fold variant (forward: ydot / ypart; grad_x / grad_W: A synthesised from h)
+// FOLD: the value-head fold variant (forward: ydot / ypart; grad_x / grad_W: A synthesised from h).
+// The body of one workgroup (block b of a grid of `grid` blocks): gemm_x3_kernel runs it for its own
+// grid; gemm_x3_pair_kernel runs a grad_W and a grad_x in one launch (blocks [0, grid_W) and the rest)
 template <int OP, int BM, int BN, int WARPS_M, int NTH, int OCC, int KG, int ABL = 0, int FOLD = 0, int GATHER = 0>
-__global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
+__device__ __forceinline__ void x3_body(const X3Args& a, int b, int grid) {
     constexpr int NTG = NTH / KG;                                  // threads per k-group
     constexpr int NW = NTG / 64, WARPS_N = NW / WARPS_M;
     constexpr int WM = BM / WARPS_M, WN = BN / WARPS_N;
@@ -496,15 +498,15 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
 
     // grad_x launches may carry the previous grad_W's slab reduce in extra workgroups past the tiles
     if constexpr (OP == OP_NN) {
-        if (a.red_wgs && (int)blockIdx.x >= a.gemm_wgs) {
-            x3_slab_reduce_block<NTH>(a, (int)blockIdx.x - a.gemm_wgs, reinterpret_cast<float*>(lds));
+        if (a.red_wgs && b >= a.gemm_wgs) {
+            x3_slab_reduce_block<NTH>(a, b - a.gemm_wgs, reinterpret_cast<float*>(lds));
             return;
         }
     }
 
     // XCD-aware remap: hardware deals blocks round-robin over the 8 XCDs; give each XCD a
     // contiguous range of linear tiles (n fastest), so tiles sharing an A panel share an L2
-    const int nwg = (OP == OP_NN && a.red_wgs) ? a.gemm_wgs : (int)gridDim.x, b = blockIdx.x;
+    const int nwg = (OP == OP_NN && a.red_wgs) ? a.gemm_wgs : grid;
     const int xcd = b & 7, qq = nwg >> 3, rr = nwg & 7;
     const int t = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (b >> 3);
     const int tn = t % a.tiles_n;
@@ -988,6 +990,23 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     if (ABL & 32) stamp(3);
 }
 
+template <int OP, int BM, int BN, int WARPS_M, int NTH, int OCC, int KG, int ABL = 0, int FOLD = 0, int GATHER = 0>
+__global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
+    x3_body<OP, BM, BN, WARPS_M, NTH, OCC, KG, ABL, FOLD, GATHER>(a, (int)blockIdx.x, (int)gridDim.x);
+}
+
+// A layer's grad_W (cfg 3: 128×128, two k-groups) and grad_x (cfg 0: 256×256) in ONE launch of 512-thread
+// workgroups — independent products of the same upper gradient: blocks [0, wg_w) are grad_W's, the rest
+// grad_x's (and its carried split-K reduce).  The hardware deals the blocks in order, so grad_x tiles start
+// on the CUs grad_W tiles leave: grad_W's atomic tail and ramp overlap grad_x's mainloop instead of
+// standing between two launches.  (grad_x blocks b − wg_w keep their XCD: wg_w % 8 == 0.)
+template <int FOLD>
+__global__ __launch_bounds__(512, 2) void gemm_x3_pair_kernel(X3Args aw, X3Args ax, int wg_w) {
+    const int b = (int)blockIdx.x;
+    if (b < wg_w) x3_body<OP_TN, 128, 128, 2, 512, 2, 2, 0, FOLD, 0>(aw, b, wg_w);
+    else x3_body<OP_NN, 256, 256, 4, 512, 2, 1, 0, FOLD, 0>(ax, b - wg_w, (int)gridDim.x - wg_w);
+}
+
 #ifdef PPO_X3_DIAG
 int g_x3_ablate = -1;
 #endif
@@ -1154,6 +1173,41 @@ void launch_cfg_x3(int c, const X3Args& a) {
     }
 }
 
+// grad_W (cfg 3) + grad_x (cfg 0) of one layer in one launch (gemm_x3_pair_kernel)
+void launch_x3_pair(X3Args aw, X3Args ax) {
+    aw.tiles_m = ppo_divup(aw.M, 128);
+    aw.tiles_n = ppo_divup(aw.N, 128);
+    if (aw.splits < 1) aw.splits = 1;
+    const long gw = (long)aw.tiles_m * aw.tiles_n * aw.splits;
+    ax.tiles_m = ppo_divup(ax.M, 256);
+    ax.tiles_n = ppo_divup(ax.N, 256);
+    ax.splits = 1;
+    long gx = (long)ax.tiles_m * ax.tiles_n;
+    if (ax.red_wgs) {
+        ax.red_wgs = (int)ppo_divup((ax.red_n + 3) / 4, 512 / 4);
+        ax.gemm_wgs = (int)gx;
+        gx += ax.red_wgs;
+    }
+    PPO_REQUIRE(gw > 0 && gw % 8 == 0 && gx > 0 && gw + gx < (1L << 31), "gemm_x3 pair: grid");
+    PPO_REQUIRE(aw.kchunk % (2 * BK) == 0 || aw.splits == 1, "gemm_x3 pair: split-K chunk vs k-groups");
+    using SAW = StageX3<128, true, 256>;
+    using SBW = StageX3<128, true, 256>;
+    using SAX = StageX3<256, false, 512>;
+    using SBX = StageX3<256, true, 512>;
+    constexpr size_t ldsw = (size_t)2 * 3 * sizeof(unsigned short) * (SAW::SIZE + SBW::SIZE);
+    constexpr size_t ldsx = (size_t)3 * sizeof(unsigned short) * (SAX::SIZE + SBX::SIZE);
+    constexpr size_t lds = ldsw > ldsx ? ldsw : ldsx;
+    static_assert(lds <= 160 * 1024, "gemm_x3 pair: LDS");
+    auto kern = gemm_x3_pair_kernel<0>;
+    static bool attr = false;
+    if (!attr) {
+        PPO_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        attr = true;
+    }
+    PPO_TIMED_LAUNCH(kern, dim3((unsigned)(gw + gx)), dim3(512), lds, ppo::stream(), aw, ax, (int)gw);
+    PPO_LAUNCH_CHECK();
+}
+
 // forward / grad_x: the largest tile whose grid still gives every CU a workgroup (one round of
 // 256×256 tiles, else 128×128 over 8 waves, one per CU, else 64×64 at up to four per CU).  At the
 // data-parallel shard shapes (profiles/r03_x3_small_shapes.txt): 8192×512×512 forward 32.1 µs on
@@ -1239,6 +1293,18 @@ void slab_reduce(const float* slab, float* out, long n, long stride, int splits,
 struct PendingReduce { const float* slab; float* out; long n, stride; int splits; bool on; };
 static PendingReduce g_pending[2] = {};
 static int g_defer_next = 0;
+// a grad_W held back to run in one launch with the grad_x that follows it (phip_x3_pair_next)
+struct PendingPair { X3Args a; bool on; };
+static PendingPair g_pair[2] = {};
+static int g_pair_next = 0;
+static int g_pair_mode = -1;                 // PPO_X3_PAIR (default 1; 0: two launches, for A/B runs)
+static bool pair_enabled() {
+    if (g_pair_mode < 0) {
+        const char* e = getenv("PPO_X3_PAIR");
+        g_pair_mode = e && e[0] == '0' ? 0 : 1;
+    }
+    return g_pair_mode == 1;
+}
 
 }  // namespace ppo
 
@@ -1253,6 +1319,10 @@ void phip_gather_rows_f32(float* dst, const float* src, const int* rows, long m,
 // tiles: one launch fewer per layer (the caller guarantees that grad_x follows; the next grad_W on the
 // stream refuses to start while a deferred reduce is pending)
 void phip_x3_defer_reduce(int on) { ppo::g_defer_next = on; }
+
+// The next phip_x3_bwd_w call on this thread may hand its launch to the phip_x3_bwd_x that follows (one
+// gemm_x3_pair_kernel launch for both, when both take their default tiles; the caller guarantees grad_x)
+void phip_x3_pair_next(int on) { ppo::g_pair_next = on; }
 
 // Shapes the engine takes (neural_network.c routes the rest to the exact fp32 kernels): the k
 // extent and every leading dimension a multiple of 4 floats, 16-B aligned operands, and for
@@ -1296,7 +1366,16 @@ void phip_x3_bwd_x_fold(float* gx, const float* g, const unsigned* fold_bits, co
     PPO_REQUIRE(gx && (g || fold_bits) && W && l > 0 && l % 4 == 0 && n % 4 == 0 && (!g || al16(g)) && al16(W),
                 "phip_x3_bwd_x: unsupported operands");
     PPO_REQUIRE(!fold_bits || (fold_g && fold_w), "phip_x3_bwd_x: value-head fold operands");
-    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l, ppo::gemm_key(1, 1, m, n, l));
+    ppo::PendingPair& pp = ppo::g_pair[phip_side_active() ? 1 : 0];
+    const int c = pick_x3(m, n, OP_NN);
+    const bool pair = pp.on && c == 0 && !fold_bits;
+    if (pp.on && !pair) {                                     // not pairable after all: grad_W on its own first
+        pp.on = false;
+        ppo::ProfScope pw(PPO_K_GEMM, 2.0 * pp.a.M * pp.a.N * (double)pp.a.K, ppo::gemm_key(2, 1, pp.a.K, pp.a.N, pp.a.M));
+        launch_cfg_x3<OP_TN>(3, pp.a);
+    }
+    // paired: one scope over both products (key op 3 = grad_W + grad_x of one layer)
+    ppo::ProfScope ps(PPO_K_GEMM, (pair ? 4.0 : 2.0) * m * n * l, ppo::gemm_key(pair ? 3 : 1, 1, m, n, l));
     X3Args a{};
     a.A = fold_bits ? W : g; a.lda = l; a.B = W; a.ldb = n; a.C = gx; a.ldc = n;
     a.M = m; a.N = n; a.K = l; a.kchunk = l; a.splits = 1;
@@ -1308,7 +1387,12 @@ void phip_x3_bwd_x_fold(float* gx, const float* g, const unsigned* fold_bits, co
         a.red_splits = pr.splits; a.red_wgs = 1;              // (sized in launch_x3)
         pr.on = false;
     }
-    launch_cfg_x3<OP_NN>(pick_x3(m, n, OP_NN), a);
+    if (pair) {
+        pp.on = false;
+        launch_x3_pair(pp.a, a);
+        return;
+    }
+    launch_cfg_x3<OP_NN>(c, a);
 }
 
 void phip_x3_bwd_x(float* gx, const float* g, const float* W, const unsigned* bits, int m, int n, int l) {
@@ -1352,16 +1436,12 @@ void phip_x3_bwd_w_vhead(float* gW, float* gb, const float* g, float* fold_g, co
     PPO_REQUIRE(!fold_g || (fold_w && fold_gw && gb), "phip_x3_bwd_w: value-head fold operands");
     const int defer = ppo::g_defer_next;
     ppo::g_defer_next = 0;
-    ppo::PendingReduce& pr = ppo::g_pending[phip_side_active() ? 1 : 0];
+    const int pair_req = ppo::g_pair_next;
+    ppo::g_pair_next = 0;
+    const int sidx = phip_side_active() ? 1 : 0;
+    ppo::PendingReduce& pr = ppo::g_pending[sidx];
     PPO_REQUIRE(!pr.on, "phip_x3_bwd_w: a deferred split-K reduce was never run (phip_x3_defer_reduce without grad_x)");
-    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l, ppo::gemm_key(2, 1, m, n, l));
-    if (m <= 0) {
-        if (!zeroed) {
-            phip_memset(gW, 0, sizeof(float) * (size_t)l * n);
-            if (gb) phip_memset(gb, 0, sizeof(float) * (size_t)l);
-        }
-        return;
-    }
+    PPO_REQUIRE(!ppo::g_pair[sidx].on, "phip_x3_bwd_w: a paired grad_W was never launched (phip_x3_pair_next without grad_x)");
     const int c = pick_x3(l, n, OP_TN);
     const long tiles = (long)ppo_divup(l, kCfgX3[c].bm) * ppo_divup(n, kCfgX3[c].bn);
     // split-K over the batch: the grid stays within one round of workgroup slots (256 CUs × the
@@ -1373,8 +1453,22 @@ void phip_x3_bwd_w_vhead(float* gW, float* gb, const float* g, float* fold_g, co
     int splits = (int)(target / tiles);
     const int max_splits = m / (8 * kq) > 0 ? m / (8 * kq) : 1;
     splits = std::max(1, std::min(splits, max_splits));
-    int kchunk = ppo_divup(ppo_divup(m, splits), kq) * kq;
-    splits = ppo_divup(m, kchunk);
+    int kchunk = m > 0 ? ppo_divup(ppo_divup(m, splits), kq) * kq : kq;
+    splits = m > 0 ? ppo_divup(m, kchunk) : 1;
+    const bool use_slab = splits > 1 && kchunk <= 1024 && al16(gW);
+    // one launch with the grad_x that follows (gemm_x3_pair_kernel): the 128×128 two-k-group tile, f32
+    // atomics or a single split (a slab reduce could not run inside the launch that writes the slabs), no
+    // fold (its carried value head writes the g that grad_x reads), no gathered rows (layer 0 has no grad_x)
+    const bool pair = pair_req && ppo::pair_enabled() && m > 0 && c == 3 && !use_slab && !fold_g && !xrows &&
+                      (tiles * splits) % 8 == 0;
+    ppo::ProfScope ps(PPO_K_GEMM, pair ? 0.0 : 2.0 * m * n * l, pair ? 0 : ppo::gemm_key(2, 1, m, n, l), !pair);
+    if (m <= 0) {
+        if (!zeroed) {
+            phip_memset(gW, 0, sizeof(float) * (size_t)l * n);
+            if (gb) phip_memset(gb, 0, sizeof(float) * (size_t)l);
+        }
+        return;
+    }
     X3Args a{};
     a.A = g; a.lda = l; a.B = x; a.ldb = n; a.C = gW; a.ldc = n;
     a.M = l; a.N = n; a.K = m; a.kchunk = kchunk; a.splits = splits;
@@ -1403,10 +1497,13 @@ void phip_x3_bwd_w_vhead(float* gW, float* gb, const float* g, float* fold_g, co
     // profiles/r05_c4_gradw_slab_rejected.txt)
     // (the shard's input-layer grad_W, whose reduce has no grad_x to ride on, with 16-adder atomics instead:
     // 75.3 vs 73.2 ms, profiles/r05_shard_input_gradw_atomics_rejected.txt)
-    const bool use_slab = splits > 1 && kchunk <= 1024 && al16(gW);
     if (splits > 1 && !zeroed) {
         if (!use_slab) phip_memset(gW, 0, sizeof(float) * (size_t)l * n);
         if (gb) phip_memset(gb, 0, sizeof(float) * (size_t)l);
+    }
+    if (pair) {                                               // launched by the next phip_x3_bwd_x
+        ppo::g_pair[sidx] = ppo::PendingPair{a, true};
+        return;
     }
     if (!use_slab) {
         launch_cfg_x3<OP_TN>(c, a);
