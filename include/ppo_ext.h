@@ -31,6 +31,7 @@ extern "C" {
 int         ppo_device_count(void);              /* HIP devices visible (0 without a GPU) */
 int         ppo_set_device(int device);          /* 0 on success */
 const char* ppo_last_error(void);                /* first HIP/RCCL error recorded, "" if none */
+void        ppo_clear_error(void);               /* forget it (after a status-returning call the caller handled) */
 void        ppo_synchronize(void);               /* drain libppo's stream */
 const char* ppo_build_info(void);                /* offload arch, compiler, kernel list */
 /* sizeof of the API structs, for FFI layout checks: Layer, NeuralNetwork,

@@ -1297,13 +1297,9 @@ static int g_defer_next = 0;
 struct PendingPair { X3Args a; bool on; };
 static PendingPair g_pair[2] = {};
 static int g_pair_next = 0;
-static int g_pair_mode = -1;                 // PPO_X3_PAIR (default 1; 0: two launches, for A/B runs)
-static bool pair_enabled() {
-    if (g_pair_mode < 0) {
-        const char* e = getenv("PPO_X3_PAIR");
-        g_pair_mode = e && e[0] == '0' ? 0 : 1;
-    }
-    return g_pair_mode == 1;
+static bool pair_enabled() {                 // PPO_X3_PAIR=0: two launches (A/B runs; read per call)
+    const char* e = getenv("PPO_X3_PAIR");
+    return !(e && e[0] == '0');
 }
 
 }  // namespace ppo

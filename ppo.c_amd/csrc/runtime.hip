@@ -326,6 +326,7 @@ int ppo_set_device(int device) {
 }
 
 const char* ppo_last_error(void) { return g_err; }
+void ppo_clear_error(void) { g_err[0] = 0; }
 void ppo_synchronize(void) { phip_sync(); }
 
 const char* ppo_build_info(void) {

@@ -141,6 +141,7 @@ _SIGS = {
     "ppo_comm_mode": (C.c_char_p, []),
     "ppo_comm_check_replicas": (C.c_int, [_P]),
     "ppo_param_hash": (C.c_ulonglong, [_P]),
+    "ppo_clear_error": (None, []),
     "ppo_nn_input_rows": (C.c_int, [_P, _P, C.c_int]),
     "ppo_gae_state": (C.c_long, [_P, _P, _P, C.c_long]),
     "ppo_comm_barrier": (None, []),
