@@ -26,9 +26,7 @@ int         streams_pending();
 // records the stop event and attributes `work` (FLOPs or bytes) to class k.
 struct ProfScope {
     int k; double work; int slot;
-    // key: shape tag (gemm_key) for per-shape stats; active = false: a scope that records nothing (a
-    // launch handed to a later call, which accounts for it)
-    ProfScope(int k_, double work_, long long key = 0, bool active = true);
+    ProfScope(int k_, double work_, long long key = 0);   // key: shape tag (gemm_key) for per-shape stats
     ~ProfScope();
 };
 
@@ -41,8 +39,7 @@ bool take_kernel_events(hipEvent_t* start, hipEvent_t* stop);
 // out[i] = Σ_s slab[s·stride + i] for i < n in a fixed order (stride % 4 == 0, 16-B aligned slab and
 // out); `stop`: an event recorded by the reduce's dispatch (or null)
 float* slab_scratch(size_t floats);
-// gathered-row fallback of the x3 grad_W (layer 0 with a long split): per-stream scratch and dst[i] = src[rows[i]]
-float* x3_gather_scratch(size_t floats);
+// dst[i] = src[rows[i]] (n floats per row)
 void x3_gather_rows(float* dst, const float* src, const int* rows, long m, int n);
 void slab_reduce(const float* slab, float* out, long n, long stride, int splits, hipEvent_t stop);
 

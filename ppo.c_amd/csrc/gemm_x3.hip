@@ -189,10 +189,13 @@ struct StageX3 {
     float gq[NV];
     const unsigned* bw_row;
     unsigned bword;
-    // row-contiguous operand whose k-rows (batch rows) are gathered: k-row kk is HBM row gt[kk] (an LDS
-    // table of the split's row indices, indexed by the absolute k), column offset gbase
-    const int* gt;
+    // row-contiguous operand whose k-rows (batch rows) are gathered: k-row kk is HBM row gidx[kk], column
+    // offset gbase; each load's row indices arrive one load earlier (gi, prefetched with the previous
+    // tile's operands, so the address of a load never waits on a fresh index load)
+    const int* gidx;
     const float* gbase;
+    int gi[NV];
+    int gstep;                                               // k distance between this group's loads
 
     // src row (k-contiguous: after the gather, clamped into the operand); rows past the end read row
     // Rmax − 1 (their products land in output rows that are never stored)
@@ -213,9 +216,15 @@ struct StageX3 {
             base = p + (long)(ridx ? ridx[gr] : gr) * ld + k;
         }
     }
-    __device__ __forceinline__ void init_gather(const float* __restrict__ p, const int* tbl, int r0, int Rmax) {
-        gt = tbl;
+    __device__ __forceinline__ void init_gather(const float* __restrict__ p, const int* __restrict__ ridx, int r0,
+                                                int Rmax, int k0, int kend, int step) {
+        gidx = ridx;
         gbase = p + min(r0 + row, Rmax - 4);
+        gstep = step;
+        if (k0 < kend) {
+#pragma unroll
+            for (int q = 0; q < NV; ++q) gi[q] = gidx[min(k0 + k + q * KSTEP, kend - 1)];
+        }
     }
     __device__ __forceinline__ void init_fold(const float* __restrict__ g, const unsigned* __restrict__ bits, int wpr,
                                               int r0, int Rmax) {
@@ -229,8 +238,13 @@ struct StageX3 {
 #pragma unroll
             for (int q = 0; q < NV; ++q) {
                 const int kk = FULL ? k0 + k + q * KSTEP : min(k0 + k + q * KSTEP, kend - 1);
-                v[q] = *reinterpret_cast<const f32x4*>(gbase + (long)gt[kk] * ld);
+                v[q] = *reinterpret_cast<const f32x4*>(gbase + (long)gi[q] * ld);
                 if (FM == 1) gq[q] = sg[kk];
+            }
+            const int kn = k0 + gstep;                       // the next load's indices
+            if (kn < kend) {
+#pragma unroll
+                for (int q = 0; q < NV; ++q) gi[q] = gidx[min(kn + k + q * KSTEP, kend - 1)];
             }
         } else if (MN) {
 #pragma unroll
@@ -478,8 +492,8 @@ __device__ __forceinline__ void x3_epilogue_out(const X3Args& a, f32x16 (&acc)[T
 }
 
 // FOLD: the value-head fold variant (forward: ydot / ypart; grad_x / grad_W: A synthesised from h).
-// The body of one workgroup (block b of a grid of `grid` blocks): gemm_x3_kernel runs it for its own
-// grid; gemm_x3_pair_kernel runs a grad_W and a grad_x in one launch (blocks [0, grid_W) and the rest)
+// The body of one workgroup (block b of a grid of `grid` blocks), a device function so that one launch
+// could run several products' tiles (a grad_W + grad_x pair was measured and not kept, see phip_x3_bwd_w)
 template <int OP, int BM, int BN, int WARPS_M, int NTH, int OCC, int KG, int ABL = 0, int FOLD = 0, int GATHER = 0>
 __device__ __forceinline__ void x3_body(const X3Args& a, int b, int grid) {
     constexpr int NTG = NTH / KG;                                  // threads per k-group
@@ -553,16 +567,10 @@ __device__ __forceinline__ void x3_body(const X3Args& a, int b, int grid) {
     constexpr bool GB = OP == OP_TN && GATHER != 0;               // B's batch rows through a.bridx
     static_assert(!GATHER || OP == OP_TN, "x3 gather of B: grad_W only");
     const float* fold_g = a.fold_g;
-    if constexpr (GB) {
-        // the split's row indices → LDS (behind the ring), read by every B load of the mainloop
-        int* tbl = reinterpret_cast<int*>(lds + KG * NS * BUF);
-        for (int i = tid; i < kend - kbeg; i += NTH) tbl[i] = a.bridx[kbeg + i];
-        __syncthreads();
-        sb.init_gather(a.B, tbl - kbeg, n0, a.N);
-    }
+    if constexpr (GB) sb.init_gather(a.B, a.bridx, n0, a.N, kbeg + grp * BK, kend, KG * BK);
     if constexpr (OP == OP_TN && FOLD != 0) {
         if (a.vh_ypart) {                                         // the value head, carried (X3Args vh_*)
-            float* gl = reinterpret_cast<float*>(lds + KG * NS * BUF) + (GB ? a.kchunk : 0);
+            float* gl = reinterpret_cast<float*>(lds + KG * NS * BUF);
             const bool head = tm == 0 && tn == 0;
             const float bias = a.vh_b[0];
             float ls = 0.f, sgs = 0.f;
@@ -995,18 +1003,6 @@ __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
     x3_body<OP, BM, BN, WARPS_M, NTH, OCC, KG, ABL, FOLD, GATHER>(a, (int)blockIdx.x, (int)gridDim.x);
 }
 
-// A layer's grad_W (cfg 3: 128×128, two k-groups) and grad_x (cfg 0: 256×256) in ONE launch of 512-thread
-// workgroups — independent products of the same upper gradient: blocks [0, wg_w) are grad_W's, the rest
-// grad_x's (and its carried split-K reduce).  The hardware deals the blocks in order, so grad_x tiles start
-// on the CUs grad_W tiles leave: grad_W's atomic tail and ramp overlap grad_x's mainloop instead of
-// standing between two launches.  (grad_x blocks b − wg_w keep their XCD: wg_w % 8 == 0.)
-template <int FOLD>
-__global__ __launch_bounds__(512, 2) void gemm_x3_pair_kernel(X3Args aw, X3Args ax, int wg_w) {
-    const int b = (int)blockIdx.x;
-    if (b < wg_w) x3_body<OP_TN, 128, 128, 2, 512, 2, 2, 0, FOLD, 0>(aw, b, wg_w);
-    else x3_body<OP_NN, 256, 256, 4, 512, 2, 1, 0, FOLD, 0>(ax, b - wg_w, (int)gridDim.x - wg_w);
-}
-
 #ifdef PPO_X3_DIAG
 int g_x3_ablate = -1;
 #endif
@@ -1033,10 +1029,7 @@ void launch_x3(X3Args a) {
     constexpr size_t lds0 = (size_t)KG * 3 * sizeof(unsigned short) * (SA::SIZE + SB::SIZE);   // 3-stage ring
     static_assert(lds0 <= 160 * 1024, "gemm_x3: LDS images exceed 160 KiB");
     size_t lds = lds0;
-    if (GATHER) {                                      // the split's row-index table (B gathered)
-        lds += 4 * (size_t)a.kchunk;
-        PPO_REQUIRE(lds <= 160 * 1024 && a.bridx, "gemm_x3: gathered grad_W index table exceeds LDS");
-    }
+    PPO_REQUIRE(!GATHER || a.bridx, "gemm_x3: gathered grad_W without row indices");
     if (OP == OP_TN && FOLD && a.vh_ypart) {           // the carried value head's g of the split's rows
         if (lds + 4 * (size_t)a.kchunk <= 160 * 1024) {
             lds += 4 * (size_t)a.kchunk;
@@ -1173,41 +1166,6 @@ void launch_cfg_x3(int c, const X3Args& a) {
     }
 }
 
-// grad_W (cfg 3) + grad_x (cfg 0) of one layer in one launch (gemm_x3_pair_kernel)
-void launch_x3_pair(X3Args aw, X3Args ax) {
-    aw.tiles_m = ppo_divup(aw.M, 128);
-    aw.tiles_n = ppo_divup(aw.N, 128);
-    if (aw.splits < 1) aw.splits = 1;
-    const long gw = (long)aw.tiles_m * aw.tiles_n * aw.splits;
-    ax.tiles_m = ppo_divup(ax.M, 256);
-    ax.tiles_n = ppo_divup(ax.N, 256);
-    ax.splits = 1;
-    long gx = (long)ax.tiles_m * ax.tiles_n;
-    if (ax.red_wgs) {
-        ax.red_wgs = (int)ppo_divup((ax.red_n + 3) / 4, 512 / 4);
-        ax.gemm_wgs = (int)gx;
-        gx += ax.red_wgs;
-    }
-    PPO_REQUIRE(gw > 0 && gw % 8 == 0 && gx > 0 && gw + gx < (1L << 31), "gemm_x3 pair: grid");
-    PPO_REQUIRE(aw.kchunk % (2 * BK) == 0 || aw.splits == 1, "gemm_x3 pair: split-K chunk vs k-groups");
-    using SAW = StageX3<128, true, 256>;
-    using SBW = StageX3<128, true, 256>;
-    using SAX = StageX3<256, false, 512>;
-    using SBX = StageX3<256, true, 512>;
-    constexpr size_t ldsw = (size_t)2 * 3 * sizeof(unsigned short) * (SAW::SIZE + SBW::SIZE);
-    constexpr size_t ldsx = (size_t)3 * sizeof(unsigned short) * (SAX::SIZE + SBX::SIZE);
-    constexpr size_t lds = ldsw > ldsx ? ldsw : ldsx;
-    static_assert(lds <= 160 * 1024, "gemm_x3 pair: LDS");
-    auto kern = gemm_x3_pair_kernel<0>;
-    static bool attr = false;
-    if (!attr) {
-        PPO_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        attr = true;
-    }
-    PPO_TIMED_LAUNCH(kern, dim3((unsigned)(gw + gx)), dim3(512), lds, ppo::stream(), aw, ax, (int)gw);
-    PPO_LAUNCH_CHECK();
-}
-
 // forward / grad_x: the largest tile whose grid still gives every CU a workgroup (one round of
 // 256×256 tiles, else 128×128 over 8 waves, one per CU, else 64×64 at up to four per CU).  At the
 // data-parallel shard shapes (profiles/r03_x3_small_shapes.txt): 8192×512×512 forward 32.1 µs on
@@ -1228,7 +1186,7 @@ inline bool al16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 }  // namespace
 
 namespace {
-// dst[i][:] = src[rows[i]][:] (n % 4 == 0, 16-B aligned rows): the gathered-grad_W fallback for long splits
+// dst[i][:] = src[rows[i]][:] (n % 4 == 0, 16-B aligned rows): layer 0's input rows for ppo_nn_input_rows
 __global__ void x3_gather_rows_kernel(float* __restrict__ dst, const float* __restrict__ src, const int* __restrict__ rows,
                                       long m, int n4) {
     for (long e = blockIdx.x * 256L + threadIdx.x; e < m * n4; e += (long)gridDim.x * 256) {
@@ -1241,17 +1199,6 @@ __global__ void x3_gather_rows_kernel(float* __restrict__ dst, const float* __re
 
 namespace ppo {
 
-static float* g_xg[2] = {nullptr, nullptr};
-static size_t g_xg_cap[2] = {0, 0};
-float* x3_gather_scratch(size_t floats) {
-    const int s = phip_side_active() ? 1 : 0;
-    if (floats > g_xg_cap[s]) {
-        phip_free(g_xg[s]);
-        g_xg[s] = (float*)phip_malloc(sizeof(float) * floats);
-        g_xg_cap[s] = floats;
-    }
-    return g_xg[s];
-}
 void x3_gather_rows(float* dst, const float* src, const int* rows, long m, int n) {
     PPO_REQUIRE(n % 4 == 0 && al16(dst) && al16(src), "x3_gather_rows: operands");
     const long work = m * (n / 4);
@@ -1293,14 +1240,6 @@ void slab_reduce(const float* slab, float* out, long n, long stride, int splits,
 struct PendingReduce { const float* slab; float* out; long n, stride; int splits; bool on; };
 static PendingReduce g_pending[2] = {};
 static int g_defer_next = 0;
-// a grad_W held back to run in one launch with the grad_x that follows it (phip_x3_pair_next)
-struct PendingPair { X3Args a; bool on; };
-static PendingPair g_pair[2] = {};
-static int g_pair_next = 0;
-static bool pair_enabled() {                 // PPO_X3_PAIR=0: two launches (A/B runs; read per call)
-    const char* e = getenv("PPO_X3_PAIR");
-    return !(e && e[0] == '0');
-}
 
 }  // namespace ppo
 
@@ -1315,10 +1254,6 @@ void phip_gather_rows_f32(float* dst, const float* src, const int* rows, long m,
 // tiles: one launch fewer per layer (the caller guarantees that grad_x follows; the next grad_W on the
 // stream refuses to start while a deferred reduce is pending)
 void phip_x3_defer_reduce(int on) { ppo::g_defer_next = on; }
-
-// The next phip_x3_bwd_w call on this thread may hand its launch to the phip_x3_bwd_x that follows (one
-// gemm_x3_pair_kernel launch for both, when both take their default tiles; the caller guarantees grad_x)
-void phip_x3_pair_next(int on) { ppo::g_pair_next = on; }
 
 // Shapes the engine takes (neural_network.c routes the rest to the exact fp32 kernels): the k
 // extent and every leading dimension a multiple of 4 floats, 16-B aligned operands, and for
@@ -1362,16 +1297,7 @@ void phip_x3_bwd_x_fold(float* gx, const float* g, const unsigned* fold_bits, co
     PPO_REQUIRE(gx && (g || fold_bits) && W && l > 0 && l % 4 == 0 && n % 4 == 0 && (!g || al16(g)) && al16(W),
                 "phip_x3_bwd_x: unsupported operands");
     PPO_REQUIRE(!fold_bits || (fold_g && fold_w), "phip_x3_bwd_x: value-head fold operands");
-    ppo::PendingPair& pp = ppo::g_pair[phip_side_active() ? 1 : 0];
-    const int c = pick_x3(m, n, OP_NN);
-    const bool pair = pp.on && c == 0 && !fold_bits;
-    if (pp.on && !pair) {                                     // not pairable after all: grad_W on its own first
-        pp.on = false;
-        ppo::ProfScope pw(PPO_K_GEMM, 2.0 * pp.a.M * pp.a.N * (double)pp.a.K, ppo::gemm_key(2, 1, pp.a.K, pp.a.N, pp.a.M));
-        launch_cfg_x3<OP_TN>(3, pp.a);
-    }
-    // paired: one scope over both products (key op 3 = grad_W + grad_x of one layer)
-    ppo::ProfScope ps(PPO_K_GEMM, (pair ? 4.0 : 2.0) * m * n * l, ppo::gemm_key(pair ? 3 : 1, 1, m, n, l));
+    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l, ppo::gemm_key(1, 1, m, n, l));
     X3Args a{};
     a.A = fold_bits ? W : g; a.lda = l; a.B = W; a.ldb = n; a.C = gx; a.ldc = n;
     a.M = m; a.N = n; a.K = l; a.kchunk = l; a.splits = 1;
@@ -1383,12 +1309,7 @@ void phip_x3_bwd_x_fold(float* gx, const float* g, const unsigned* fold_bits, co
         a.red_splits = pr.splits; a.red_wgs = 1;              // (sized in launch_x3)
         pr.on = false;
     }
-    if (pair) {
-        pp.on = false;
-        launch_x3_pair(pp.a, a);
-        return;
-    }
-    launch_cfg_x3<OP_NN>(c, a);
+    launch_cfg_x3<OP_NN>(pick_x3(m, n, OP_NN), a);
 }
 
 void phip_x3_bwd_x(float* gx, const float* g, const float* W, const unsigned* bits, int m, int n, int l) {
@@ -1432,12 +1353,8 @@ void phip_x3_bwd_w_vhead(float* gW, float* gb, const float* g, float* fold_g, co
     PPO_REQUIRE(!fold_g || (fold_w && fold_gw && gb), "phip_x3_bwd_w: value-head fold operands");
     const int defer = ppo::g_defer_next;
     ppo::g_defer_next = 0;
-    const int pair_req = ppo::g_pair_next;
-    ppo::g_pair_next = 0;
-    const int sidx = phip_side_active() ? 1 : 0;
-    ppo::PendingReduce& pr = ppo::g_pending[sidx];
+    ppo::PendingReduce& pr = ppo::g_pending[phip_side_active() ? 1 : 0];
     PPO_REQUIRE(!pr.on, "phip_x3_bwd_w: a deferred split-K reduce was never run (phip_x3_defer_reduce without grad_x)");
-    PPO_REQUIRE(!ppo::g_pair[sidx].on, "phip_x3_bwd_w: a paired grad_W was never launched (phip_x3_pair_next without grad_x)");
     const int c = pick_x3(l, n, OP_TN);
     const long tiles = (long)ppo_divup(l, kCfgX3[c].bm) * ppo_divup(n, kCfgX3[c].bn);
     // split-K over the batch: the grid stays within one round of workgroup slots (256 CUs × the
@@ -1452,12 +1369,10 @@ void phip_x3_bwd_w_vhead(float* gW, float* gb, const float* g, float* fold_g, co
     int kchunk = m > 0 ? ppo_divup(ppo_divup(m, splits), kq) * kq : kq;
     splits = m > 0 ? ppo_divup(m, kchunk) : 1;
     const bool use_slab = splits > 1 && kchunk <= 1024 && al16(gW);
-    // one launch with the grad_x that follows (gemm_x3_pair_kernel): the 128×128 two-k-group tile, f32
-    // atomics or a single split (a slab reduce could not run inside the launch that writes the slabs), no
-    // fold (its carried value head writes the g that grad_x reads), no gathered rows (layer 0 has no grad_x)
-    const bool pair = pair_req && ppo::pair_enabled() && m > 0 && c == 3 && !use_slab && !fold_g && !xrows &&
-                      (tiles * splits) % 8 == 0;
-    ppo::ProfScope ps(PPO_K_GEMM, pair ? 0.0 : 2.0 * m * n * l, pair ? 0 : ppo::gemm_key(2, 1, m, n, l), !pair);
+    // (round 6: grad_W and the grad_x that follows as ONE launch, grad_x tiles starting on the CUs grad_W
+    // tiles leave, measured slower at C4 — the pair 178–183 µs vs 91.8 + 79.1 µs apart, the update 315.4 vs
+    // 312.3 ms: profiles/r06_x3_pair_and_x0_ab.txt; not kept)
+    ppo::ProfScope ps(PPO_K_GEMM, 2.0 * m * n * l, ppo::gemm_key(2, 1, m, n, l));
     if (m <= 0) {
         if (!zeroed) {
             phip_memset(gW, 0, sizeof(float) * (size_t)l * n);
@@ -1469,17 +1384,7 @@ void phip_x3_bwd_w_vhead(float* gW, float* gb, const float* g, float* fold_g, co
     a.A = g; a.lda = l; a.B = x; a.ldb = n; a.C = gW; a.ldc = n;
     a.M = l; a.N = n; a.K = m; a.kchunk = kchunk; a.splits = splits;
     a.gbias = gb;
-    if (xrows) {
-        // x's rows through the minibatch indices: an LDS table of the split's indices (≤ 8 KiB beside the
-        // 144 KiB ring); a longer split gathers the rows into scratch first
-        if (kchunk <= 2048) {
-            a.bridx = xrows;
-        } else {
-            float* xs = ppo::x3_gather_scratch((size_t)m * n);
-            ppo::x3_gather_rows(xs, x, xrows, m, n);
-            a.B = xs;
-        }
-    }
+    a.bridx = xrows;                                       // x's rows through the minibatch indices
     a.fold_g = fold_g; a.fold_w = fold_w; a.fold_gw = fold_gw;
     a.vh_ypart = ypart; a.vh_slots = slots; a.vh_b = b; a.vh_t = tgt; a.vh_y = y; a.vh_gb = gb_out; a.vh_loss = loss_accum;
     // split-K partials: per-split slabs written with plain stores and summed by one reduce launch
@@ -1496,10 +1401,6 @@ void phip_x3_bwd_w_vhead(float* gW, float* gb, const float* g, float* fold_g, co
     if (splits > 1 && !zeroed) {
         if (!use_slab) phip_memset(gW, 0, sizeof(float) * (size_t)l * n);
         if (gb) phip_memset(gb, 0, sizeof(float) * (size_t)l);
-    }
-    if (pair) {                                               // launched by the next phip_x3_bwd_x
-        ppo::g_pair[sidx] = ppo::PendingPair{a, true};
-        return;
     }
     if (!use_slab) {
         launch_cfg_x3<OP_TN>(c, a);

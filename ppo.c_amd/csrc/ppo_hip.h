@@ -81,9 +81,6 @@ void phip_x3_fwd(float* y, const float* x, const int* ridx, float* xcopy, const 
 /* the next phip_x3_bwd_w(_fold) leaves its split-K slab reduce to the next phip_x3_bwd_x(_fold) on the same
  * stream (extra workgroups of that launch) — the caller guarantees grad_x follows */
 void phip_x3_defer_reduce(int on);
-/* the next phip_x3_bwd_w may run in one launch with the phip_x3_bwd_x that follows on the same stream
- * (gemm_x3_pair_kernel; PPO_X3_PAIR=0 disables) — the caller guarantees grad_x follows */
-void phip_x3_pair_next(int on);
 void phip_x3_bwd_x(float* gx, const float* g, const float* W, const unsigned* bits, int m, int n, int l);
 void phip_x3_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, int n, int l, int zeroed);
 /* layer 0 of a minibatch: x row i is x[xrows[i]] — the buffer rows the forward read through the same

@@ -132,8 +132,8 @@ static void harvest() {
     g_slots.clear();
 }
 
-ProfScope::ProfScope(int k_, double work_, long long key, bool active) : k(k_), work(work_), slot(-1) {
-    if (active) slot = phip_prof_begin_key(k, work, key);
+ProfScope::ProfScope(int k_, double work_, long long key) : k(k_), work(work_), slot(-1) {
+    slot = phip_prof_begin_key(k, work, key);
 }
 ProfScope::~ProfScope() { phip_prof_end(slot); }
 

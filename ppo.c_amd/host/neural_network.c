@@ -482,7 +482,6 @@ static void nn_backward_dev_top(NeuralNetwork* nn, const float* d_grad_out, int 
         } else if (use_x3_layer(m, n, l) && phip_x3_supported(2, m, n, l)) {
             const int pair = want_gx && (!relu_in || bits);
             phip_x3_defer_reduce(pair);                       /* its slab reduce rides on grad_x */
-            phip_x3_pair_next(pair);                          /* or both in one launch (gemm_x3_pair_kernel) */
             if (i == 0 && x0_rows) phip_x3_bwd_w_rows(ly->d_grad_weights, ly->d_grad_biases, g, x, x0_rows, m, n, l, 1);
             else phip_x3_bwd_w(ly->d_grad_weights, ly->d_grad_biases, g, x, m, n, l, 1);
             if (pair) phip_x3_bwd_x(ly->d_grad_x, g, ly->d_weights, bits, m, n, l);

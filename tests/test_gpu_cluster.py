@@ -156,14 +156,17 @@ def cos_ratio(d, dr):
 # 1.16× (the whole update's μ) the oracle's own; every check prints its margin (1 − cos_gpu) / (1 − floor)
 # (profiles/r06_chaos_margins.txt).  And an absolute floor where the oracle's is low: at 512 steps a GPU
 # path must keep cos ≥ CHAOS_ABS_MIN against the oracle whatever the floor.
-CHAOS_FACTOR, CHAOS_SLACK, CHAOS_ABS_MIN = 1.25, 0.02, 0.5
+# The whole C4 update (3584 steps, 7× the longest step test) keeps more slack: its multi-launch μ margin
+# measured 1.16 (round 5) and 1.22 (round 6, profiles/r06_chaos_margins.txt) — run-to-run spread of a
+# chaotic process whose split-K atomics reorder sums differently on every run.
+CHAOS_FACTOR, CHAOS_SLACK, CHAOS_SLACK_WHOLE, CHAOS_ABS_MIN = 1.25, 0.02, 0.05, 0.5
 
 
-def assert_within_chaos_floor(cos_gpu, floor_cos, what):
-    bound = 1 - (CHAOS_FACTOR * (1 - min(floor_cos)) + CHAOS_SLACK)
+def assert_within_chaos_floor(cos_gpu, floor_cos, what, slack=CHAOS_SLACK):
+    bound = 1 - (CHAOS_FACTOR * (1 - min(floor_cos)) + slack)
     margin = (1 - cos_gpu) / max(1e-12, 1 - min(floor_cos))
     print(f"CHAOS_MARGIN {what}: 1-cos {1 - cos_gpu:.5f} floor 1-cos {1 - min(floor_cos):.5f} margin {margin:.3f} "
-          f"(allowed {CHAOS_FACTOR} + slack)")
+          f"(allowed {CHAOS_FACTOR} + slack {slack})")
     assert cos_gpu >= bound, f"{what}: cos {cos_gpu:.5f} < {bound:.5f} (oracle self-drift floor {floor_cos})"
     assert cos_gpu >= CHAOS_ABS_MIN, f"{what}: cos {cos_gpu:.5f} < absolute minimum {CHAOS_ABS_MIN}"
 
@@ -199,7 +202,7 @@ def test_cluster_full_update_matches_multilaunch(lib, oracle, shuffle, sizes):
             cos, ratio = cos_ratio(x[k] - x[k0], ref[0][idx])
             print(f"C4 full update {k}: {name} vs oracle cos {cos:.5f} ratio {ratio:.4f} | oracle self-drift "
                   f"split-K {floor[0][0]:.5f} ({floor[0][1]:.4f}) double {floor[1][0]:.5f} ({floor[1][1]:.4f})")
-            assert_within_chaos_floor(cos, [c for c, _ in floor], f"C4 full update {k} {name}")
+            assert_within_chaos_floor(cos, [c for c, _ in floor], f"C4 full update {k} {name}", CHAOS_SLACK_WHOLE)
             assert abs(ratio - 1) <= spread + 0.1, (k, name, ratio, floor)
 
 
