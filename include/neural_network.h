@@ -95,8 +95,6 @@ typedef struct {
     long   host_version;    /* dev_version the host mirrors (weights and extra floats) last matched */
     long   host_version_w;  /* dev_version the host weight mirrors last matched (a weights-only sync) */
     float* d_fold_ws;       /* value-head fold scratch (nn_value_fold_step): partial dots [slots][m] | g [m] */
-    const int* d_x0_rows;   /* non-NULL: layer 0's input row i of the last device forward is d_x0[d_x0_rows[i]]
-                             * (x3 engine: the minibatch read through its indices, no gathered copy) */
     long   fold_ws_cap;     /* floats */
 } NeuralNetwork;
 

@@ -137,9 +137,9 @@ void ppo_fill_synthetic(void* ppo, int n_envs, int horizon, unsigned long long s
 void ppo_rollout_device(void* ppo, int n_envs, int horizon, int env_kind, unsigned long long seed);
 
 /* layer 0's input of the last device forward of a NeuralNetwork*, m rows × input_size fp32, to the
- * host: the gathered minibatch rows (read through NeuralNetwork.d_x0_rows when the x3 engine used
- * the buffer rows directly, else the gathered copy d_x0) — for parity tests; synchronises.  bf16 copies
- * (x0_dtype 1) are not converted: returns −1 for them and for m beyond the last forward, else 0. */
+ * host: the gathered minibatch rows the GEMMs read (NeuralNetwork.d_x0) — for parity tests;
+ * synchronises.  bf16 copies (x0_dtype 1) are not converted: returns −1 for them and for m beyond the
+ * last forward, else 0. */
 int ppo_nn_input_rows(void* nn, float* out, int m);
 
 /* ---------------- compute precision ---------------- */

@@ -39,8 +39,6 @@ bool take_kernel_events(hipEvent_t* start, hipEvent_t* stop);
 // out[i] = Σ_s slab[s·stride + i] for i < n in a fixed order (stride % 4 == 0, 16-B aligned slab and
 // out); `stop`: an event recorded by the reduce's dispatch (or null)
 float* slab_scratch(size_t floats);
-// dst[i] = src[rows[i]] (n floats per row)
-void x3_gather_rows(float* dst, const float* src, const int* rows, long m, int n);
 void slab_reduce(const float* slab, float* out, long n, long stride, int splits, hipEvent_t stop);
 
 // shape tag of a GEMM launch: op (0 fwd, 1 grad_x, 2 grad_W, 3 paired bwd) [60..63] | engine [56..59] |

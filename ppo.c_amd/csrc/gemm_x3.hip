@@ -58,8 +58,6 @@ struct X3Args {
     const int* ridx; float* acopy;        // forward: fused gather of A's rows + the gathered copy
     unsigned* bits_out; const unsigned* bits_in; int wpr;
     float* gbias;                         // grad_W: bias gradient (Σ over the batch of g)
-    const int* bridx;                     // grad_W: B's batch rows through these indices (x = buffer rows of
-                                          // the minibatch: layer 0 reads them where the forward read them)
     int kchunk, splits, tiles_m, tiles_n;
     float* slab;                          // grad_W split-K: per-split partial tiles [splits][M][N] (plain
                                           // stores, summed by slab_reduce_kernel) instead of f32 atomics
@@ -157,16 +155,18 @@ __device__ __forceinline__ void split4(f32x4 f, u32x2& p0, u32x2& p1, u32x2& p2)
 // k-group), each owning NV float4 loads per k-tile.
 // MN = the operand is contiguous along its rows (its k is the HBM row).
 // ---------------------------------------------------------------------------------------------
-template <int R, bool MN, int NTH>
+template <int R, bool MN, int NTH, int KB = BK>
 struct StageX3 {
-    static constexpr int NV = R * BK / (4 * NTH);            // float4 loads per thread
-    static_assert(NV >= 1 && R * BK == 4 * NTH * NV, "tile / thread count");
+    static_assert(KB == 16 || KB == 32, "x3 k-tile depth");
+    static constexpr int NV = R * KB / (4 * NTH);            // float4 loads per thread
+    static_assert(NV >= 1 && R * KB == 4 * NTH * NV, "tile / thread count");
     static_assert(R == 64 || R == 128 || R == 256, "x3 operand tile rows");
-    static constexpr int PLANE = R * BK;                     // bf16 elements per plane (unpadded)
+    static constexpr int PLANE = R * KB;                     // bf16 elements per plane (unpadded)
     static constexpr int SIZE = 3 * PLANE;
-    // k-contiguous [row][16]: element (row, k) — the 16-B chunks of rows with bit 3 set are swapped
+    // k-contiguous [row][KB]: element (row, k) — the 16-B chunks of a row XOR-permuted by its 8-row group
+    // (KB 16: the two chunks swapped on odd groups; KB 32: four chunks permuted by the group mod 4)
     __device__ __forceinline__ static int kc_off(int row, int k) {
-        return row * BK + 8 * ((k >> 3) ^ ((row >> 3) & 1)) + (k & 7);
+        return row * KB + 8 * ((k >> 3) ^ ((row >> 3) & (KB / 8 - 1))) + (k & 7);
     }
     // row-contiguous [k][R]: element (k, row) — 32-B segment s of k-row k sits at s ^ sw(k), so the
     // 4 k-rows × 2 segments a 32-lane group of ds_read_b64_tr_b16 touches cover the 8 bank groups
@@ -174,9 +174,9 @@ struct StageX3 {
     __device__ __forceinline__ static int mn_off(int k, int row) {
         return k * R + 16 * ((row >> 4) ^ sw(k)) + (row & 15);
     }
-    static constexpr int TPR = BK / (4 * NV);                // k-contiguous: threads per row
+    static constexpr int TPR = KB / (4 * NV);                // k-contiguous: threads per row
     static constexpr int KSTEP = 4 * NTH / R;                // row-contiguous: k distance of the q-th load
-    static_assert(MN || (TPR >= 1 && NTH * 4 * NV == R * BK), "k-contiguous mapping");
+    static_assert(MN || (TPR >= 1 && NTH * 4 * NV == R * KB), "k-contiguous mapping");
 
     f32x4 v[NV];
     const float* base;                                       // this thread's element (row, k) at k0 = 0
@@ -189,13 +189,6 @@ struct StageX3 {
     float gq[NV];
     const unsigned* bw_row;
     unsigned bword;
-    // row-contiguous operand whose k-rows (batch rows) are gathered: k-row kk is HBM row gidx[kk], column
-    // offset gbase; each load's row indices arrive one load earlier (gi, prefetched with the previous
-    // tile's operands, so the address of a load never waits on a fresh index load)
-    const int* gidx;
-    const float* gbase;
-    int gi[NV];
-    int gstep;                                               // k distance between this group's loads
 
     // src row (k-contiguous: after the gather, clamped into the operand); rows past the end read row
     // Rmax − 1 (their products land in output rows that are never stored)
@@ -216,37 +209,15 @@ struct StageX3 {
             base = p + (long)(ridx ? ridx[gr] : gr) * ld + k;
         }
     }
-    __device__ __forceinline__ void init_gather(const float* __restrict__ p, const int* __restrict__ ridx, int r0,
-                                                int Rmax, int k0, int kend, int step) {
-        gidx = ridx;
-        gbase = p + min(r0 + row, Rmax - 4);
-        gstep = step;
-        if (k0 < kend) {
-#pragma unroll
-            for (int q = 0; q < NV; ++q) gi[q] = gidx[min(k0 + k + q * KSTEP, kend - 1)];
-        }
-    }
     __device__ __forceinline__ void init_fold(const float* __restrict__ g, const unsigned* __restrict__ bits, int wpr,
                                               int r0, int Rmax) {
         sg = g;
         if (!MN && bits) bw_row = bits + (long)min(r0 + row, Rmax - 1) * wpr;
     }
     // FULL: the whole k-tile lies inside [kbeg, kend) — no clamping
-    template <bool FULL, int FM = 0, bool GT = false>
+    template <bool FULL, int FM = 0>
     __device__ __forceinline__ void load(int k0, int kend) {
-        if (MN && GT) {
-#pragma unroll
-            for (int q = 0; q < NV; ++q) {
-                const int kk = FULL ? k0 + k + q * KSTEP : min(k0 + k + q * KSTEP, kend - 1);
-                v[q] = *reinterpret_cast<const f32x4*>(gbase + (long)gi[q] * ld);
-                if (FM == 1) gq[q] = sg[kk];
-            }
-            const int kn = k0 + gstep;                       // the next load's indices
-            if (kn < kend) {
-#pragma unroll
-                for (int q = 0; q < NV; ++q) gi[q] = gidx[min(kn + k + q * KSTEP, kend - 1)];
-            }
-        } else if (MN) {
+        if (MN) {
 #pragma unroll
             for (int q = 0; q < NV; ++q) {
                 const int dk = FULL ? k0 + q * KSTEP : min(k0 + k + q * KSTEP, kend - 1) - k;
@@ -254,7 +225,7 @@ struct StageX3 {
                 if (FM == 1) gq[q] = sg[k + dk];
             }
         } else if (FM == 2) {
-            // the thread's 4·NV consecutive k lie in one 32-bit word (16-k tiles, k + 4·NV ≤ 16)
+            // the thread's 4·NV consecutive k lie in one 32-bit word (k-tiles start at multiples of 16)
             const int kk = FULL ? k0 + k : min(k0 + k, kend - 1);
             bword = bw_row[kk >> 5];
         } else {
@@ -336,16 +307,16 @@ struct StageX3 {
             if (kvalid(q, k0, kend))
                 *reinterpret_cast<f32x4*>(dst + (long)(r0 + row) * ldd + k0 + k + 4 * q) = v[q];
     }
-    // MFMA fragment (32 rows × 16 k, bf16x8 per lane: row `rr`, k = 8h..8h+7) of one plane
-    __device__ __forceinline__ static bf16x8 frag(const unsigned short* plane, int rr, int lane) {
+    // MFMA fragment (32 rows × 16 k of k-half kh, bf16x8 per lane: row `rr`, k = 16kh + 8h..+7) of one plane
+    __device__ __forceinline__ static bf16x8 frag(const unsigned short* plane, int rr, int lane, int kh = 0) {
         const int h = lane >> 5;
-        if (!MN) return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(plane + kc_off(rr, 8 * h)));
+        if (!MN) return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(plane + kc_off(rr, 16 * kh + 8 * h)));
         // hardware transpose: in each 16-lane group lane 4q+p addresses k-row q, rows 4p..4p+3 of
         // the group's 16; lane i receives row i of the 4 k-rows (two reads: k 8h+0..3, 8h+4..7;
         // sw(k + 4) = sw(k), so the second read is 4 k-rows further)
         const int gi = lane & 15, q = gi >> 2, p = gi & 3;
         typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-        const unsigned short* a0 = plane + mn_off(8 * h + q, rr - gi) + 4 * p;
+        const unsigned short* a0 = plane + mn_off(16 * kh + 8 * h + q, rr - gi) + 4 * p;
         const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0));
         const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(a0 + 4 * R));
         const s16x8 f = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
@@ -494,7 +465,7 @@ __device__ __forceinline__ void x3_epilogue_out(const X3Args& a, f32x16 (&acc)[T
 // FOLD: the value-head fold variant (forward: ydot / ypart; grad_x / grad_W: A synthesised from h).
 // The body of one workgroup (block b of a grid of `grid` blocks), a device function so that one launch
 // could run several products' tiles (a grad_W + grad_x pair was measured and not kept, see phip_x3_bwd_w)
-template <int OP, int BM, int BN, int WARPS_M, int NTH, int OCC, int KG, int ABL = 0, int FOLD = 0, int GATHER = 0>
+template <int OP, int BM, int BN, int WARPS_M, int NTH, int OCC, int KG, int ABL = 0, int FOLD = 0, int KB = BK>
 __device__ __forceinline__ void x3_body(const X3Args& a, int b, int grid) {
     constexpr int NTG = NTH / KG;                                  // threads per k-group
     constexpr int NW = NTG / 64, WARPS_N = NW / WARPS_M;
@@ -503,9 +474,10 @@ __device__ __forceinline__ void x3_body(const X3Args& a, int b, int grid) {
     static_assert(TM >= 1 && TN >= 1 && WARPS_M * WARPS_N == NW, "wave tiling");
     static_assert(KG == 1 || OP == OP_TN, "k-groups: grad_W only");
     constexpr bool A_MN = OP == OP_TN, B_MN = OP != OP_NT;
-    using SA = StageX3<BM, A_MN, NTG>;
-    using SB = StageX3<BN, B_MN, NTG>;
+    using SA = StageX3<BM, A_MN, NTG, KB>;
+    using SB = StageX3<BN, B_MN, NTG, KB>;
     constexpr int BUF = SA::SIZE + SB::SIZE;
+    constexpr int KH = KB / 16;                                    // MFMA k-steps (16 k) per k-tile
 
     constexpr int NS = 3;                                          // LDS ring stages
     extern __shared__ __attribute__((aligned(16))) unsigned short lds[];     // KG × NS × BUF
@@ -564,10 +536,7 @@ __device__ __forceinline__ void x3_body(const X3Args& a, int b, int grid) {
     constexpr bool syn = OP != OP_NT && FOLD != 0;
     constexpr int FMA_ = !syn ? 0 : OP == OP_NN ? 2 : 1;          // A's fold load mode
     constexpr int FMB_ = syn ? 1 : 0;                             // B's
-    constexpr bool GB = OP == OP_TN && GATHER != 0;               // B's batch rows through a.bridx
-    static_assert(!GATHER || OP == OP_TN, "x3 gather of B: grad_W only");
     const float* fold_g = a.fold_g;
-    if constexpr (GB) sb.init_gather(a.B, a.bridx, n0, a.N, kbeg + grp * BK, kend, KG * BK);
     if constexpr (OP == OP_TN && FOLD != 0) {
         if (a.vh_ypart) {                                         // the value head, carried (X3Args vh_*)
             float* gl = reinterpret_cast<float*>(lds + KG * NS * BUF);
@@ -617,16 +586,21 @@ __device__ __forceinline__ void x3_body(const X3Args& a, int b, int grid) {
     for (int q = 0; q < SA::NV; ++q) bs[q] = bs3[q] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     // fragment registers: plane p of the A (fa) and B (fb) operand tiles of the current k-tile
-    bf16x8 fa[3][TM], fb[3][TN];
+    bf16x8 fa[3][TM][KH], fb[3][TN][KH];
     // (fold: A is a 0/1 mask in plane 0 only — its planes 1, 2 and their three products are skipped)
     auto rd_a = [&](const unsigned short* img, int p) {
         if (syn && p != 0) return;
 #pragma unroll
-        for (int i = 0; i < TM; ++i) fa[p][i] = SA::frag(img + p * SA::PLANE, wm * WM + i * 32 + r, lane);
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int kh = 0; kh < KH; ++kh) fa[p][i][kh] = SA::frag(img + p * SA::PLANE, wm * WM + i * 32 + r, lane, kh);
     };
     auto rd_b = [&](const unsigned short* img, int p) {
 #pragma unroll
-        for (int j = 0; j < TN; ++j) fb[p][j] = SB::frag(img + SA::SIZE + p * SB::PLANE, wn * WN + j * 32 + r, lane);
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int kh = 0; kh < KH; ++kh)
+                fb[p][j][kh] = SB::frag(img + SA::SIZE + p * SB::PLANE, wn * WN + j * 32 + r, lane, kh);
     };
     // plane product A_pa·B_pb of the current k-tile (the six with pa + pb ≤ 2)
     auto mm = [&](int pa, int pb) {
@@ -635,22 +609,24 @@ __device__ __forceinline__ void x3_body(const X3Args& a, int b, int grid) {
 #pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
-                for (int j = 0; j < TN; ++j) acc[i][j][0] += (float)fa[pa][i][0] + (float)fb[pb][j][1];
+                for (int j = 0; j < TN; ++j) acc[i][j][0] += (float)fa[pa][i][0][0] + (float)fb[pb][j][0][1];
             return;
         }
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+        for (int kh = 0; kh < KH; ++kh)
 #pragma unroll
-            for (int j = 0; j < TN; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[pa][i], fb[pb][j], acc[i][j], 0, 0, 0);
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[pa][i][kh], fb[pb][j][kh], acc[i][j], 0, 0, 0);
     };
 
     // this group's k-tiles: j = 0 … NK−1 at k0 = kbeg + (KG·j + grp)·BK; only the last one can be
     // partial (or, for a k-group past the end, empty: every element masked to zero)
-    const int nkt = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+    const int nkt = kend > kbeg ? (kend - kbeg + KB - 1) / KB : 0;
     const int NK = (nkt + KG - 1) / KG;
-    auto k0_of = [&](int j) { return kbeg + (KG * j + grp) * BK; };
-    auto is_full = [&](int j) { return k0_of(j) + BK <= kend; };
+    auto k0_of = [&](int j) { return kbeg + (KG * j + grp) * KB; };
+    auto is_full = [&](int j) { return k0_of(j) + KB <= kend; };
     const int tail = NK > 0 && !is_full(NK - 1) ? 1 : 0;
     unsigned short* const ring = lds + (KG > 1 ? grp * NS * BUF : 0);
 
@@ -663,7 +639,7 @@ __device__ __forceinline__ void x3_body(const X3Args& a, int b, int grid) {
         constexpr bool SYN = OP != OP_NT && decltype(SYNc)::value;
         if ((ABL & 2) && k0 != kbeg) return;
         if constexpr (COPY) {
-            if (((k0 - kbeg) / BK) % a.tiles_n == tn) sa.copy_out(a.acopy, a.K, m0, a.M, k0, kend);
+            if (((k0 - kbeg) / KB) % a.tiles_n == tn) sa.copy_out(a.acopy, a.K, m0, a.M, k0, kend);
         }
         if constexpr (SYN && OP == OP_NN) sa.bits_to_values(k0);
         if constexpr (SYN && OP == OP_TN) {
@@ -704,7 +680,7 @@ __device__ __forceinline__ void x3_body(const X3Args& a, int b, int grid) {
         constexpr bool SYN = OP != OP_NT && decltype(SYNc)::value;
         if ((ABL & 8) && k0 != kbeg) return;
         sa.template load<FULL, SYN ? FMA_ : 0>(k0, kend);
-        sb.template load<FULL, SYN ? FMB_ : 0, GB>(k0, kend);
+        sb.template load<FULL, SYN ? FMB_ : 0>(k0, kend);
     };
     using T = std::true_type;
     using F = std::false_type;
@@ -743,7 +719,7 @@ __device__ __forceinline__ void x3_body(const X3Args& a, int b, int grid) {
 #endif
         if constexpr (SGB) {
 #pragma unroll
-            for (int q = 0; q < TM * TN; ++q) {
+            for (int q = 0; q < TM * TN * KH; ++q) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
                 if (NVV) __builtin_amdgcn_sched_group_barrier(0x002, NVV, 0);
                 __builtin_amdgcn_sched_group_barrier(0x080, 1, 0);
@@ -998,9 +974,9 @@ __device__ __forceinline__ void x3_body(const X3Args& a, int b, int grid) {
     if (ABL & 32) stamp(3);
 }
 
-template <int OP, int BM, int BN, int WARPS_M, int NTH, int OCC, int KG, int ABL = 0, int FOLD = 0, int GATHER = 0>
+template <int OP, int BM, int BN, int WARPS_M, int NTH, int OCC, int KG, int ABL = 0, int FOLD = 0, int KB = BK>
 __global__ __launch_bounds__(NTH, OCC) void gemm_x3_kernel(X3Args a) {
-    x3_body<OP, BM, BN, WARPS_M, NTH, OCC, KG, ABL, FOLD, GATHER>(a, (int)blockIdx.x, (int)gridDim.x);
+    x3_body<OP, BM, BN, WARPS_M, NTH, OCC, KG, ABL, FOLD, KB>(a, (int)blockIdx.x, (int)gridDim.x);
 }
 
 #ifdef PPO_X3_DIAG
@@ -1009,7 +985,7 @@ int g_x3_ablate = -1;
 
 int g_x3_last_slots = 0;                 // the last launch's ypart slots (tiles_n × waves along N)
 
-template <int OP, int BM, int BN, int WARPS_M, int NTH, int OCC, int KG, int ABL = 0, int FOLD = 0, int GATHER = 0>
+template <int OP, int BM, int BN, int WARPS_M, int NTH, int OCC, int KG, int ABL = 0, int FOLD = 0, int KB = BK>
 void launch_x3(X3Args a) {
     a.tiles_m = ppo_divup(a.M, BM);
     a.tiles_n = ppo_divup(a.N, BN);
@@ -1023,13 +999,12 @@ void launch_x3(X3Args a) {
         a.gemm_wgs = (int)grid;
         grid += a.red_wgs;
     }
-    PPO_REQUIRE(a.kchunk % (KG * BK) == 0 || a.splits == 1, "gemm_x3: split-K chunk vs k-groups");
-    using SA = StageX3<BM, OP == OP_TN, NTH / KG>;
-    using SB = StageX3<BN, OP != OP_NT, NTH / KG>;
+    PPO_REQUIRE(a.kchunk % (KG * KB) == 0 || a.splits == 1, "gemm_x3: split-K chunk vs k-groups");
+    using SA = StageX3<BM, OP == OP_TN, NTH / KG, KB>;
+    using SB = StageX3<BN, OP != OP_NT, NTH / KG, KB>;
     constexpr size_t lds0 = (size_t)KG * 3 * sizeof(unsigned short) * (SA::SIZE + SB::SIZE);   // 3-stage ring
     static_assert(lds0 <= 160 * 1024, "gemm_x3: LDS images exceed 160 KiB");
     size_t lds = lds0;
-    PPO_REQUIRE(!GATHER || a.bridx, "gemm_x3: gathered grad_W without row indices");
     if (OP == OP_TN && FOLD && a.vh_ypart) {           // the carried value head's g of the split's rows
         if (lds + 4 * (size_t)a.kchunk <= 160 * 1024) {
             lds += 4 * (size_t)a.kchunk;
@@ -1039,7 +1014,7 @@ void launch_x3(X3Args a) {
             a.vh_ypart = nullptr;
         }
     }
-    auto kern = gemm_x3_kernel<OP, BM, BN, WARPS_M, NTH, OCC, KG, ABL, FOLD, GATHER>;
+    auto kern = gemm_x3_kernel<OP, BM, BN, WARPS_M, NTH, OCC, KG, ABL, FOLD, KB>;
     if (lds > 64 * 1024) {
         static bool attr = false;                      // once per instantiation (the whole LDS)
         if (!attr) {
@@ -1096,39 +1071,28 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
 // products have 32 tiles of 256×256 — an eighth of the CUs — but 512 of 64×64)
 // 5 = 256×128 over 8 waves of 64×64, one workgroup per CU (two rounds at C4: the first round's store
 // tail drains under the second round's mainloop)
-struct CfgX3 { int bm, bn, kg, slots_per_cu; };
-constexpr CfgX3 kCfgX3[] = {{256, 256, 1, 1}, {128, 128, 1, 2}, {128, 128, 1, 1}, {128, 128, 2, 1}, {64, 64, 1, 4},
-                            {256, 128, 1, 1}};
+// 6 = 64×64 over 4 waves of 32×32 with 32-k tiles (two MFMA k-steps per barrier), two workgroups per CU
+// (the small products' grids: half the k-tile iterations, barriers and staging round trips of cfg 4)
+struct CfgX3 { int bm, bn, kg, slots_per_cu, kb; };
+constexpr CfgX3 kCfgX3[] = {{256, 256, 1, 1, 16}, {128, 128, 1, 2, 16}, {128, 128, 1, 1, 16}, {128, 128, 2, 1, 16},
+                            {64, 64, 1, 4, 16},   {256, 128, 1, 1, 16}, {64, 64, 1, 2, 32}};
 int g_force_x3 = -1;
 int g_split_x3 = 0;
 
-template <int OP, int FOLD, int GATHER>
-void launch_cfg_x3_var(int c, const X3Args& a) {
-    switch (c) {
-        case 0: launch_x3<OP, 256, 256, 4, 512, 2, 1, 0, FOLD, GATHER>(a); return;
-        case 2: launch_x3<OP, 128, 128, 4, 512, 2, 1, 0, FOLD, GATHER>(a); return;
-        case 4: launch_x3<OP, 64, 64, 2, 256, 4, 1, 0, FOLD, GATHER>(a); return;
-        case 5: launch_x3<OP, 256, 128, 4, 512, 2, 1, 0, FOLD, GATHER>(a); return;
-        case 3:
-            if constexpr (OP == OP_TN) { launch_x3<OP, 128, 128, 2, 512, 2, 2, 0, FOLD, GATHER>(a); return; }
-            [[fallthrough]];
-        default: launch_x3<OP, 128, 128, 2, 256, 2, 1, 0, FOLD, GATHER>(a); return;
-    }
-}
-
 template <int OP>
 void launch_cfg_x3(int c, const X3Args& a) {
-    const bool fold = a.ydot || a.fold_g;           // the value-head fold variants
-    if constexpr (OP == OP_TN) {
-        if (a.bridx) {                              // layer 0's grad_W: x rows through the minibatch indices
-            if (fold) launch_cfg_x3_var<OP, 1, 1>(c, a);
-            else launch_cfg_x3_var<OP, 0, 1>(c, a);
-            return;
+    if (a.ydot || a.fold_g) {                      // the value-head fold variants
+        switch (c) {
+            case 0: launch_x3<OP, 256, 256, 4, 512, 2, 1, 0, 1>(a); return;
+            case 2: launch_x3<OP, 128, 128, 4, 512, 2, 1, 0, 1>(a); return;
+            case 4: launch_x3<OP, 64, 64, 2, 256, 4, 1, 0, 1>(a); return;
+            case 5: launch_x3<OP, 256, 128, 4, 512, 2, 1, 0, 1>(a); return;
+            case 6: launch_x3<OP, 64, 64, 2, 256, 2, 1, 0, 1, 32>(a); return;
+            case 3:
+                if constexpr (OP == OP_TN) { launch_x3<OP, 128, 128, 2, 512, 2, 2, 0, 1>(a); return; }
+                [[fallthrough]];
+            default: launch_x3<OP, 128, 128, 2, 256, 2, 1, 0, 1>(a); return;
         }
-    }
-    if (fold) {
-        launch_cfg_x3_var<OP, 1, 0>(c, a);
-        return;
     }
 #ifdef PPO_X3_DIAG
     if (g_x3_ablate < 0) {
@@ -1159,6 +1123,7 @@ void launch_cfg_x3(int c, const X3Args& a) {
         case 2: launch_x3<OP, 128, 128, 4, 512, 2, 1>(a); break;
         case 4: launch_x3<OP, 64, 64, 2, 256, 4, 1>(a); break;
         case 5: launch_x3<OP, 256, 128, 4, 512, 2, 1>(a); break;
+        case 6: launch_x3<OP, 64, 64, 2, 256, 2, 1, 0, 0, 32>(a); break;
         case 3:
             if constexpr (OP == OP_TN) { launch_x3<OP, 128, 128, 2, 512, 2, 2>(a); break; }
             [[fallthrough]];
@@ -1178,34 +1143,16 @@ int pick_x3(int M, int N, int op) {
     auto tiles = [&](int c) { return (long)ppo_divup(M, kCfgX3[c].bm) * ppo_divup(N, kCfgX3[c].bn); };
     if (tiles(0) >= 256) return 0;
     if (tiles(2) >= 256) return 2;
-    return 4;
+    const char* e = getenv("PPO_X3_BK32");                   // PPO_X3_BK32=0: the 16-k small tiles (A/B runs)
+    return (e && e[0] == '0') ? 4 : 6;
 }
 
 inline bool al16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 }  // namespace
 
-namespace {
-// dst[i][:] = src[rows[i]][:] (n % 4 == 0, 16-B aligned rows): layer 0's input rows for ppo_nn_input_rows
-__global__ void x3_gather_rows_kernel(float* __restrict__ dst, const float* __restrict__ src, const int* __restrict__ rows,
-                                      long m, int n4) {
-    for (long e = blockIdx.x * 256L + threadIdx.x; e < m * n4; e += (long)gridDim.x * 256) {
-        const long i = e / n4;
-        const int c = (int)(e % n4);
-        reinterpret_cast<f32x4*>(dst)[e] = reinterpret_cast<const f32x4*>(src + (long)rows[i] * 4 * n4)[c];
-    }
-}
-}  // namespace
-
 namespace ppo {
 
-void x3_gather_rows(float* dst, const float* src, const int* rows, long m, int n) {
-    PPO_REQUIRE(n % 4 == 0 && al16(dst) && al16(src), "x3_gather_rows: operands");
-    const long work = m * (n / 4);
-    const int grid = (int)std::min<long>(4096, std::max<long>(1, (work + 255) / 256));
-    hipLaunchKernelGGL(x3_gather_rows_kernel, dim3(grid), dim3(256), 0, stream(), dst, src, rows, m, n / 4);
-    PPO_LAUNCH_CHECK();
-}
 
 // per-stream slab buffers (the value and policy loops run their grad_W launches on two streams)
 static float* g_slab[2] = {nullptr, nullptr};
@@ -1244,10 +1191,6 @@ static int g_defer_next = 0;
 }  // namespace ppo
 
 extern "C" {
-
-void phip_gather_rows_f32(float* dst, const float* src, const int* rows, long m, int n) {
-    ppo::x3_gather_rows(dst, src, rows, m, n);
-}
 
 // The next phip_x3_bwd_w(_fold) call on this thread leaves its split-K slab reduce (if it uses slabs) to
 // the next phip_x3_bwd_x(_fold) launch on the same stream, which runs it in extra workgroups beside its
@@ -1317,20 +1260,13 @@ void phip_x3_bwd_x(float* gx, const float* g, const float* W, const unsigned* bi
 }
 
 void phip_x3_bwd_w_vhead(float* gW, float* gb, const float* g, float* fold_g, const float* fold_w, float* fold_gw,
-                         const float* x, const int* xrows, int m, int n, int l, int zeroed, const float* ypart,
-                         int slots, const float* b, const float* tgt, float* y, float* gb_out, float* loss_accum);
+                         const float* x, int m, int n, int l, int zeroed, const float* ypart, int slots, const float* b,
+                         const float* tgt, float* y, float* gb_out, float* loss_accum);
 
 // zeroed: gW / gb already hold zeros (one memset per backward); otherwise they are cleared here
 void phip_x3_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, int n, int l, int zeroed) {
-    phip_x3_bwd_w_vhead(gW, gb, g, nullptr, nullptr, nullptr, x, nullptr, m, n, l, zeroed, nullptr, 0, nullptr, nullptr,
-                        nullptr, nullptr, nullptr);
-}
-
-// layer 0 of a minibatch: x row i is x[xrows[i]] (the buffer rows the forward gathered; no copy)
-void phip_x3_bwd_w_rows(float* gW, float* gb, const float* g, const float* x, const int* xrows, int m, int n, int l,
-                        int zeroed) {
-    phip_x3_bwd_w_vhead(gW, gb, g, nullptr, nullptr, nullptr, x, xrows, m, n, l, zeroed, nullptr, 0, nullptr, nullptr,
-                        nullptr, nullptr, nullptr);
+    phip_x3_bwd_w_vhead(gW, gb, g, nullptr, nullptr, nullptr, x, m, n, l, zeroed, nullptr, 0, nullptr, nullptr, nullptr,
+                        nullptr, nullptr);
 }
 
 // value-head fold (fold_g): g = h [m, l] (fp32, its mask is the operand), x scaled by fold_g per row, the
@@ -1338,15 +1274,15 @@ void phip_x3_bwd_w_rows(float* gW, float* gb, const float* g, const float* x, co
 // diag(w)·maskᵀ·g — and fold_gw [l] (zero on entry) += Σ_rows fold_g·h, the output layer's gW
 void phip_x3_bwd_w_fold(float* gW, float* gb, const float* g, const float* fold_g, const float* fold_w,
                         float* fold_gw, const float* x, int m, int n, int l, int zeroed) {
-    phip_x3_bwd_w_vhead(gW, gb, g, const_cast<float*>(fold_g), fold_w, fold_gw, x, nullptr, m, n, l, zeroed, nullptr, 0,
-                        nullptr, nullptr, nullptr, nullptr, nullptr);
+    phip_x3_bwd_w_vhead(gW, gb, g, const_cast<float*>(fold_g), fold_w, fold_gw, x, m, n, l, zeroed, nullptr, 0, nullptr,
+                        nullptr, nullptr, nullptr, nullptr);
 }
 
 // + the carried value head (ypart set): g (fold_g, written) from the forward's partial dots, y, the output
 // bias gradient gb_out and the loss, in this launch (X3Args vh_*)
 void phip_x3_bwd_w_vhead(float* gW, float* gb, const float* g, float* fold_g, const float* fold_w, float* fold_gw,
-                         const float* x, const int* xrows, int m, int n, int l, int zeroed, const float* ypart,
-                         int slots, const float* b, const float* tgt, float* y, float* gb_out, float* loss_accum) {
+                         const float* x, int m, int n, int l, int zeroed, const float* ypart, int slots, const float* b,
+                         const float* tgt, float* y, float* gb_out, float* loss_accum) {
     if (l <= 0 || n <= 0) return;
     PPO_REQUIRE(!ypart || (fold_g && slots > 0 && b && tgt && y && gb_out), "phip_x3_bwd_w: carried value head operands");
     PPO_REQUIRE(gW && g && x && n % 4 == 0 && l % 4 == 0 && al16(g) && al16(x), "phip_x3_bwd_w: unsupported operands");
@@ -1361,7 +1297,7 @@ void phip_x3_bwd_w_vhead(float* gW, float* gb, const float* g, float* fold_g, co
     // configuration's workgroups per CU), each split ≥ 8 k-tiles per k-group.  (64×64 tiles for
     // C3's 256×256 gradient measured 23.5 -> 20.7 µs but sum each output over longer fp32 chains:
     // not adopted)
-    const int kq = BK * kCfgX3[c].kg;                       // a split's k range: whole k-tiles per group
+    const int kq = kCfgX3[c].kb * kCfgX3[c].kg;             // a split's k range: whole k-tiles per group
     const int target = g_split_x3 > 0 ? g_split_x3 : 256 * kCfgX3[c].slots_per_cu;
     int splits = (int)(target / tiles);
     const int max_splits = m / (8 * kq) > 0 ? m / (8 * kq) : 1;
@@ -1384,7 +1320,6 @@ void phip_x3_bwd_w_vhead(float* gW, float* gb, const float* g, float* fold_g, co
     a.A = g; a.lda = l; a.B = x; a.ldb = n; a.C = gW; a.ldc = n;
     a.M = l; a.N = n; a.K = m; a.kchunk = kchunk; a.splits = splits;
     a.gbias = gb;
-    a.bridx = xrows;                                       // x's rows through the minibatch indices
     a.fold_g = fold_g; a.fold_w = fold_w; a.fold_gw = fold_gw;
     a.vh_ypart = ypart; a.vh_slots = slots; a.vh_b = b; a.vh_t = tgt; a.vh_y = y; a.vh_gb = gb_out; a.vh_loss = loss_accum;
     // split-K partials: per-split slabs written with plain stores and summed by one reduce launch

@@ -83,10 +83,6 @@ void phip_x3_fwd(float* y, const float* x, const int* ridx, float* xcopy, const 
 void phip_x3_defer_reduce(int on);
 void phip_x3_bwd_x(float* gx, const float* g, const float* W, const unsigned* bits, int m, int n, int l);
 void phip_x3_bwd_w(float* gW, float* gb, const float* g, const float* x, int m, int n, int l, int zeroed);
-/* layer 0 of a minibatch: x row i is x[xrows[i]] — the buffer rows the forward read through the same
- * indices (no gathered copy) */
-void phip_x3_bwd_w_rows(float* gW, float* gb, const float* g, const float* x, const int* xrows, int m, int n, int l,
-                        int zeroed);
 /* value-head fold (nn_value_fold_step): forward partial y dots (returns ypart slots); backward with the
  * upper gradient g·w·1[h > 0] applied as the 0/1 mask of h with g, w as row / column scales (grad_x:
  * W pre-scaled by w) and the output layer's gW */
@@ -99,10 +95,8 @@ void phip_x3_bwd_w_fold(float* gW, float* gb, const float* h, const float* fold_
 /* phip_x3_bwd_w_fold carrying the value head: g (into fold_g) from the forward's partial dots ypart [slots][m]
  * + b against tgt, y, the output bias gradient gb_out and loss_accum (+= loss / m) — value_head_kernel's work */
 void phip_x3_bwd_w_vhead(float* gW, float* gb, const float* h, float* fold_g, const float* fold_w, float* fold_gw,
-                         const float* x, const int* xrows, int m, int n, int l, int zeroed, const float* ypart,
-                         int slots, const float* b, const float* tgt, float* y, float* gb_out, float* loss_accum);
-/* dst[i, :] = src[rows[i], :] (n % 4 == 0, 16-B aligned) */
-void phip_gather_rows_f32(float* dst, const float* src, const int* rows, long m, int n);
+                         const float* x, int m, int n, int l, int zeroed, const float* ypart, int slots, const float* b,
+                         const float* tgt, float* y, float* gb_out, float* loss_accum);
 /* dst[i, :] = bf16(src[rows[i], :]) for i < m (S % 4 == 0): layer 0's gather in bf16 mode */
 void phip_gather_rows_bf16(unsigned short* dst, const float* src, const int* rows, int m, int S);
 void phip_f32_to_bf16(unsigned short* dst, const float* src, long count);

@@ -294,28 +294,11 @@ void lin_bwd_w(float* gW, const float* g, const float* x, int m, int n, int l) {
     else phip_linear_bwd_w(gW, NULL, g, x, m, n, l);
 }
 
-/* layer 0 reads its minibatch rows through the indices in forward and grad_W alike (no gathered copy):
- * fp32 storage, at least one hidden layer (layer 0 is not the output layer, whose backward paths read a
- * contiguous input), the x3 engine for layer 0's forward and grad_W, a 16-B aligned buffer */
-static int x0_rows_ok(const NeuralNetwork* nn, const float* d_x, int m) {
-    const char* e = getenv("PPO_X0_COPY");
-    if ((e && e[0] == '1') || nn->dtype != 0 || nn->num_layers - 1 < 2 || !al16(d_x)) return 0;
-    const int S = nn->layers[0].input_size, H = nn->layers[0].output_size;
-    return use_x3_layer(m, S, H) && phip_x3_supported(0, m, S, H) && phip_x3_supported(2, m, S, H);
-}
-
 int ppo_nn_input_rows(void* vnn, float* out, int m) {
     NeuralNetwork* nn = (NeuralNetwork*)vnn;
     const int S = nn->layers[0].input_size;
     if (!nn->d_x0 || nn->x0_dtype != 0 || m <= 0 || m > nn->cache_m_forward) return -1;
-    if (!nn->d_x0_rows) {
-        phip_d2h(out, nn->d_x0, sizeof(float) * (size_t)m * S);
-        return 0;
-    }
-    float* tmp = (float*)phip_malloc(sizeof(float) * (size_t)m * S);   /* diagnostic path: its own buffer */
-    phip_gather_rows_f32(tmp, nn->d_x0, nn->d_x0_rows, m, S);
-    phip_d2h(out, tmp, sizeof(float) * (size_t)m * S);
-    phip_free(tmp);
+    phip_d2h(out, nn->d_x0, sizeof(float) * (size_t)m * S);
     return 0;
 }
 
@@ -342,12 +325,9 @@ static void nn_forward_dev_upto(NeuralNetwork* nn, const float* d_x, const int* 
         nn->d_output = nn->layers[L].d_input;
         return;
     }
-    /* layer 0 on the x3 engine reads the minibatch rows through their indices in the forward AND in its
-     * grad_W (phip_x3_bwd_w_rows), so no gathered copy is written (PPO_X0_COPY=1 restores the copy) */
-    const int rows_x0 = d_rows && d_xcopy && x0_rows_ok(nn, d_x, m);
-    nn->d_x0 = d_rows ? (rows_x0 ? d_x : d_xcopy) : d_x;
-    nn->d_x0_rows = rows_x0 ? d_rows : NULL;
-    if (rows_x0) d_xcopy = NULL;
+    /* (round 6: the gathered copy dropped, layer 0's grad_W reading the buffer rows through the indices —
+     * the forward 6 µs faster, the grad_W 9 µs slower on random 1.5 KB rows: profiles/r06_x0_gather_rejected.txt) */
+    nn->d_x0 = d_rows ? d_xcopy : d_x;
     nn->x0_dtype = 0;
     const float* in = d_x;
     for (int i = 0; i < upto; i++) {
@@ -452,13 +432,10 @@ static void nn_backward_dev_top(NeuralNetwork* nn, const float* d_grad_out, int 
      * out as one launch (phip_linear_bwd_pair: grad_x tiles fill the CUs grad_W tiles leave).
      * (measured: grad_W on a second queue beside grad_x was slower than back to back) */
     long hi = nn->num_params + (reduce_extra > 0 ? reduce_extra : 0);
-    const int* x0_rows = nn->d_x0_rows;                 /* layer 0's rows through the minibatch indices */
     for (int i = top - 1; i >= 0; i--) {
         Layer* ly = &nn->layers[i];
         const float* x = i == 0 ? nn->d_x0 : ly->d_input;
         const int n = ly->input_size, l = ly->output_size;
-        if (i == 0 && x0_rows && !(use_x3_layer(m, n, l) && phip_x3_supported(2, m, n, l)))
-            die("nn_backward_dev: layer 0's gathered rows need the x3 grad_W (forward and backward disagree)");
         const int want_gx = i > 0 || want_grad_x0;
         const int relu_in = i > 0 && nn_is_relu(nn, i - 1);
         const unsigned* bits = relu_in && nn->bits_m == m ? act_bits(nn, i) : NULL;   /* this forward's bits */
@@ -467,9 +444,8 @@ static void nn_backward_dev_top(NeuralNetwork* nn, const float* d_grad_out, int 
              * grad_x = diag(g)·(mask·diag(w)·W) ⊙ the input mask (gemm_x3.hip) */
             const float* h = nn->layers[i + 1].d_input;
             phip_x3_defer_reduce(want_gx);                    /* its slab reduce rides on grad_x */
-            phip_x3_bwd_w_vhead(ly->d_grad_weights, ly->d_grad_biases, h, fold->g, fold->w, fold->gw_out, x,
-                                i == 0 ? x0_rows : NULL, m, n, l, 1, fold->ypart, fold->slots, fold->b, fold->tgt,
-                                fold->y, fold->gb, fold->loss);
+            phip_x3_bwd_w_vhead(ly->d_grad_weights, ly->d_grad_biases, h, fold->g, fold->w, fold->gw_out, x, m, n, l, 1,
+                                fold->ypart, fold->slots, fold->b, fold->tgt, fold->y, fold->gb, fold->loss);
             if (want_gx) {
                 if (relu_in && !bits) die("nn_value_fold_step: the forward's ReLU′ bits are missing");
                 phip_x3_bwd_x_fold(ly->d_grad_x, NULL, act_bits(nn, i + 1), fold->g, fold->w, ly->d_weights, bits, m, n,
@@ -482,8 +458,7 @@ static void nn_backward_dev_top(NeuralNetwork* nn, const float* d_grad_out, int 
         } else if (use_x3_layer(m, n, l) && phip_x3_supported(2, m, n, l)) {
             const int pair = want_gx && (!relu_in || bits);
             phip_x3_defer_reduce(pair);                       /* its slab reduce rides on grad_x */
-            if (i == 0 && x0_rows) phip_x3_bwd_w_rows(ly->d_grad_weights, ly->d_grad_biases, g, x, x0_rows, m, n, l, 1);
-            else phip_x3_bwd_w(ly->d_grad_weights, ly->d_grad_biases, g, x, m, n, l, 1);
+            phip_x3_bwd_w(ly->d_grad_weights, ly->d_grad_biases, g, x, m, n, l, 1);
             if (pair) phip_x3_bwd_x(ly->d_grad_x, g, ly->d_weights, bits, m, n, l);
             else if (want_gx) phip_linear_bwd_x_bits(ly->d_grad_x, g, ly->d_weights, ly->d_input, NULL, m, n, l);
         } else if (want_gx && (!relu_in || bits)) {

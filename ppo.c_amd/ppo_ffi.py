@@ -44,7 +44,7 @@ class NeuralNetwork(C.Structure):
                 ("d_tiny_wt", c_float_p), ("tiny_wt_cap", C.c_long),
                 ("h_sync", c_float_p), ("dev_version", C.c_long),
                 ("host_version", C.c_long), ("host_version_w", C.c_long),
-                ("d_fold_ws", c_float_p), ("fold_ws_cap", C.c_long), ("d_x0_rows", C.POINTER(C.c_int))]
+                ("d_fold_ws", c_float_p), ("fold_ws_cap", C.c_long)]
 
 
 class GaussianPolicy(C.Structure):
