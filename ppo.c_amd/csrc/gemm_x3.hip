@@ -1143,8 +1143,14 @@ int pick_x3(int M, int N, int op) {
     auto tiles = [&](int c) { return (long)ppo_divup(M, kCfgX3[c].bm) * ppo_divup(N, kCfgX3[c].bn); };
     if (tiles(0) >= 256) return 0;
     if (tiles(2) >= 256) return 2;
-    const char* e = getenv("PPO_X3_BK32");                   // PPO_X3_BK32=0: the 16-k small tiles (A/B runs)
-    return (e && e[0] == '0') ? 4 : 6;
+    // 32-k small tiles (cfg 6): each launch alone is faster (shard forward 21.1 -> 20.0 µs, C3 14.4 -> 13.5),
+    // but at 72 KiB of LDS per workgroup the other loop's kernels and the carried reduces no longer fit
+    // beside them — the shard update 71.6 -> 73.1 ms, C3 26.8 -> 27.2 with every small product on it
+    // (profiles/r06_x3_bk32_ab.txt); PPO_X3_BK32 = 1 (every small product) / nt (forwards only) / 0 (default)
+    const char* e = getenv("PPO_X3_BK32");
+    if (e && e[0] == '1') return 6;
+    if (e && e[0] == 'n' && op == OP_NT) return 6;
+    return 4;
 }
 
 inline bool al16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
