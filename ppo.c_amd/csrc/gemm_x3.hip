@@ -1139,11 +1139,10 @@ int pick_x3(int M, int N, int op) {
     if (g_force_x3 >= 0) return g_force_x3;
     // (256×128 tiles in two rounds for C4's forward or grad_x, the second round's mainloop under the
     // first round's store tail: 322.3 / 313.3 vs 305.4 ms, profiles/r05_x3_cfg5_rounds_rejected.txt)
-    if (op == OP_TN) {                 // (cfg 5, 256×128 with slabs, measured slower: r04_x3_tn_cfg5_update_ab.txt)
-        const char* e = getenv("PPO_X3_TN_CFG");              // A/B runs: grad_W's tile configuration
-        const int c = e ? atoi(e) : -1;
-        return c >= 0 && c < (int)(sizeof(kCfgX3) / sizeof(kCfgX3[0])) ? c : 3;
-    }
+    // (cfg 5, 256×128 with slabs, measured slower: r04_x3_tn_cfg5_update_ab.txt; cfg 2, one k-group in 72 KiB
+    // so the other loop's kernels fit beside it, fails the accuracy parity — twice as long fp32 chains:
+    // profiles/r06_x3_tn_cfg2_accuracy_rejected.txt)
+    if (op == OP_TN) return 3;
     auto tiles = [&](int c) { return (long)ppo_divup(M, kCfgX3[c].bm) * ppo_divup(N, kCfgX3[c].bn); };
     if (tiles(0) >= 256) return 0;
     if (tiles(2) >= 256) return 2;
