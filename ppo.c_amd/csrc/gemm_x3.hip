@@ -304,8 +304,14 @@ struct StageX3 {
         if (MN || r0 + row >= Rmax) return;
 #pragma unroll
         for (int q = 0; q < NV; ++q)
-            if (kvalid(q, k0, kend))
-                *reinterpret_cast<f32x4*>(dst + (long)(r0 + row) * ldd + k0 + k + 4 * q) = v[q];
+            if (kvalid(q, k0, kend)) {
+                f32x4* p = reinterpret_cast<f32x4*>(dst + (long)(r0 + row) * ldd + k0 + k + 4 * q);
+#ifdef PPO_X3_COPY_NT
+                __builtin_nontemporal_store(v[q], p);
+#else
+                *p = v[q];
+#endif
+            }
     }
     // MFMA fragment (32 rows × 16 k of k-half kh, bf16x8 per lane: row `rr`, k = 16kh + 8h..+7) of one plane
     __device__ __forceinline__ static bf16x8 frag(const unsigned short* plane, int rr, int lane, int kh = 0) {
