@@ -25,6 +25,8 @@
 // applies the same Adam step (bit-identical copies).  GEMMs: v_mfma_f32_16x16x4_f32 (exact fp32).
 #include "cluster_common.h"
 
+#include <vector>
+
 #include <cmath>
 #include <cstdlib>
 
@@ -565,6 +567,8 @@ unsigned* g_err = nullptr;            // host-mapped error word
 // PPO_CLUSTER_STAMPS: one stamp buffer per stream (the phases run concurrently) and the report that
 // phip_cluster_report prints once the phases have joined
 struct StampSlot {
+    unsigned long long* arr = nullptr;                // per-workgroup barrier stamps [64][6][2][arr_nwg] (or null)
+    int arr_nwg = 0, arr_on = 0;
     unsigned long long* buf = nullptr;                // [64 steps][32 stamps] | [64 workgroups] placement
     int nstamp = 0, policy = 0, total_steps = 0, pending = 0, nwg = 0;
     const char* kind = nullptr;
@@ -602,7 +606,20 @@ unsigned long long* host_stamps(int nstamp, const char* kind, const char* const*
     if (!s.buf) s.buf = (unsigned long long*)phip_malloc(sizeof(unsigned long long) * (CLU_STAMP_CLK + 64 * 32));
     s.nstamp = nstamp; s.kind = kind; s.names = names; s.policy = policy; s.total_steps = total_steps; s.nwg = nwg;
     s.pending = total_steps >= 64;
+    s.arr_on = 0;
     return s.buf;
+}
+
+unsigned long long* host_barrier_stamps(int nwg) {
+    StampSlot& s = g_stamps[phip_side_active() ? 1 : 0];
+    if (!s.arr || s.arr_nwg < nwg) {
+        phip_free(s.arr);
+        s.arr = (unsigned long long*)phip_malloc(sizeof(unsigned long long) * 64 * 6 * 2 * (size_t)nwg);
+        s.arr_nwg = nwg;
+    }
+    PPO_CHECK(hipMemsetAsync(s.arr, 0, sizeof(unsigned long long) * 64 * 6 * 2 * (size_t)nwg, ppo::stream()));
+    s.arr_on = 1;
+    return s.arr;
 }
 
 }  // namespace clu
@@ -654,6 +671,50 @@ void phip_cluster_report(void) {
         fprintf(stderr, " | per XCC:");
         for (int x = 0; x < 8; ++x) fprintf(stderr, " %d", per_xcc[x]);
         fprintf(stderr, "\n");
+        if (s.arr_on) {
+            // per barrier over steps 1 … 62: arrival skew (last − first arrival), exit latency (first exit − last
+            // arrival: the hand-off's own propagation), and the workgroups that arrive last most often
+            const int nw = s.arr_nwg;
+            std::vector<unsigned long long> ar((size_t)64 * 6 * 2 * nw);
+            phip_d2h(ar.data(), s.arr, sizeof(unsigned long long) * ar.size());
+            for (int bi = 0; bi < 6; ++bi) {
+                double skew = 0, prop = 0, spread = 0;
+                int n = 0;
+                std::vector<int> last(nw, 0);
+                for (int st = 1; st < 63; ++st) {
+                    const unsigned long long* A0 = &ar[((size_t)(st * 6 + bi) * 2 + 0) * nw];
+                    const unsigned long long* E0 = &ar[((size_t)(st * 6 + bi) * 2 + 1) * nw];
+                    unsigned long long amin = ~0ull, amax = 0, emin = ~0ull, emax = 0;
+                    int wl = 0;
+                    bool any = true;
+                    for (int w = 0; w < nw; ++w) {
+                        if (!A0[w] || !E0[w]) { any = false; break; }
+                        if (A0[w] < amin) amin = A0[w];
+                        if (A0[w] > amax) { amax = A0[w]; wl = w; }
+                        emin = E0[w] < emin ? E0[w] : emin;
+                        emax = E0[w] > emax ? E0[w] : emax;
+                    }
+                    if (!any) continue;
+                    skew += (double)(amax - amin) / mhz;
+                    prop += (double)(emin > amax ? emin - amax : 0) / mhz;
+                    spread += (double)(emax - emin) / mhz;
+                    last[wl]++;
+                    n++;
+                }
+                if (!n) continue;
+                fprintf(stderr, "%s %s barrier %c: arrival skew %.2f us, exit after last arrival %.2f us, exit spread %.2f us;"
+                        " last to arrive:", s.kind, s.policy ? "policy" : "value", 'A' + bi, skew / n, prop / n, spread / n);
+                for (int k = 0; k < 3; ++k) {
+                    int best = 0;
+                    for (int w = 1; w < nw; ++w) if (last[w] > last[best]) best = w;
+                    if (!last[best]) break;
+                    const unsigned xcc = best < 64 ? (unsigned)(pl[best] >> 32) & 15u : 0u;
+                    fprintf(stderr, " wg %d (xcc %u) %d/%d", best, xcc, last[best], n);
+                    last[best] = 0;
+                }
+                fprintf(stderr, "\n");
+            }
+        }
     }
 }
 

@@ -199,5 +199,9 @@ bool host_grid_fits(const void* kfn, size_t lds, int grid);
 // report printed by phip_cluster_report() after the phases joined (no mid-phase synchronisation).
 unsigned long long* host_stamps(int nstamp, const char* kind, const char* const* names, int policy, int total_steps,
                                 int nwg);
+// PPO_CLUSTER_STAMPS=2 (cluster_deep): every workgroup's arrival and exit time at each of the ≤ 6 barriers of
+// steps 0 … 63 ([64][6][2][nwg], zeroed); phip_cluster_report prints the arrival skew, the exit latency
+// after the last arrival and the workgroups that arrive last
+unsigned long long* host_barrier_stamps(int nwg);
 
 }  // namespace clu

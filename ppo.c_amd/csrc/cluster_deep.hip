@@ -68,6 +68,8 @@ struct DArgs {
     unsigned long long timeout;                      // barrier wait bound (realtime ticks)
     int active_stride, active_offset;                // workgroup b works iff b % stride == offset
     unsigned long long* stamps;                      // PPO_CLUSTER_STAMPS: workgroup 0, steps 0..63
+    unsigned long long* arr;                         // PPO_CLUSTER_STAMPS=2: every workgroup's arrival and exit
+                                                     // time at every barrier, steps 0..63 [64][6][2][NWG]
 };
 
 // LDS layout (floats)
@@ -319,6 +321,13 @@ __device__ __forceinline__ void publish_partial(int tid, __amdgpu_buffer_rsrc_t 
         }                                                                                                \
     } while (0)
 
+// per-workgroup barrier stamps (PPO_CLUSTER_STAMPS=2): arrival (after the counter adds) and exit (the
+// wait returned) of barrier bi (A … F = 0 … 5) at step `step`
+#define CD_BAR_STAMP(bi, ex)                                                                              \
+    do {                                                                                                  \
+        if (a.arr && tid == 0 && step < 64) a.arr[((step * 6 + (bi)) * 2 + (ex)) * NWG + cw] = wall_clock64(); \
+    } while (0)
+
 __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
     if ((int)blockIdx.x % a.active_stride != a.active_offset) return;
     const int cw = (int)blockIdx.x / a.active_stride;
@@ -406,9 +415,11 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
             }
             CD_STAMP(1);
             cluster_arrive(a.ctr);
+            CD_BAR_STAMP(0, 0);
             if (has_next) gather_rows(a, lds, ep_n, kb_n, cur ^ 1);     // the next minibatch, part 1
             ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag, cw, a.timeout);          // A: h1 published
             if (!ok) break;
+            CD_BAR_STAMP(0, 1);
             CD_STAMP(2);
             // ---- layer 1: h2ᵀ[j][b] = Σ_k W1[j][k]·h1[b][k] ----
             {
@@ -429,6 +440,7 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
             }
             CD_STAMP(3);
             cluster_arrive(a.ctr);
+            CD_BAR_STAMP(1, 0);
             if (has_next) gather_act(a, lds, cur ^ 1);                   // the next minibatch, part 2
 #ifndef CLU_NO_PREFETCH
             // rows 2cw, 2cw + 1 of the next minibatch from HBM into the caches (each workgroup two, so
@@ -441,6 +453,7 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
 #endif
             ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag, cw, a.timeout);          // B: h2 published
             if (!ok) break;
+            CD_BAR_STAMP(1, 1);
             CD_STAMP(4);
             // ---- layer 2: h3ᵀ[j][b] = Σ_k W2[j][k]·h2[b][k] (own columns stay in LDS) ----
             {
@@ -470,8 +483,10 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
             }
             CD_STAMP(5);
             cluster_arrive(a.ctr);
+            CD_BAR_STAMP(2, 0);
             ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag, cw, a.timeout);          // C: y partials published
             if (!ok) break;
+            CD_BAR_STAMP(2, 1);
             CD_STAMP(6);
             if (!a.policy) {
                 // ---- the value head, replicated: every workgroup reduces all 64 rows' partials (one
@@ -553,8 +568,10 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
             }
             CD_STAMP(7);
             cluster_arrive(a.ctr);
+            CD_BAR_STAMP(3, 0);
             ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag, cw, a.timeout);          // D: every row's ∂L/∂y published
             if (!ok) break;
+            CD_BAR_STAMP(3, 1);
             CD_STAMP(8);
             // ---- ∂L/∂y of all rows → LDS ----
             for (int e = tid; e < BB * (GP / 4); e += TPB) {
@@ -611,6 +628,7 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
                 if (w == NWAVE - 1) colsum64<HC>(lds + L::gh, HCP, HC, 0.f, lds + L::gb2, tid);
                 CD_STAMP(9);
                 cluster_arrive(a.ctr);                                   // (its barrier: W2 reads done)
+                CD_BAR_STAMP(4, 0);
                 pre.apply(tid, a, lds + L::gh, lds + L::W2, HP, g0, H, H, st, bc2, last, 0);
 #pragma unroll 1
                 for (int t = CLU_GW_PRE; t < T12; ++t) {
@@ -622,6 +640,7 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
             CD_STAMP(10);
             ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag, cw, a.timeout);          // E: P2 published
             if (!ok) break;
+            CD_BAR_STAMP(4, 1);
             CD_STAMP(11);
             // ---- layer 1 backward: g2h = Σ P2 ⊙ 1[h2 > 0]; P1 = g2h·W1[own, :] → Pb; gb1; gW1 as gW2 (its
             // first tiles' operands in flight under the reduction and P1) ----
@@ -636,6 +655,7 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
                 if (w == NWAVE - 1) colsum64<HC>(lds + L::gh, HCP, HC, 0.f, lds + L::gb1, tid);
                 CD_STAMP(12);
                 cluster_arrive(a.ctr);
+                CD_BAR_STAMP(5, 0);
                 pre.apply(tid, a, lds + L::gh, lds + L::W1, HP, g0, H, H, st, bc2, last, 0);
 #pragma unroll 1
                 for (int t = CLU_GW_PRE; t < T12; ++t) {
@@ -650,6 +670,7 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
             CD_STAMP(13);
             ok = cluster_wait(a.ctr, a.err, nbar++, NWG, flag, cw, a.timeout);          // F: P1 published
             if (!ok) break;
+            CD_BAR_STAMP(5, 1);
             CD_STAMP(14);
             // ---- layer 0 backward: g1h = Σ P1 ⊙ 1[h1 > 0]; gW0[j][s] = Σ_b g1h[b][j]·x[b][s] with Adam
             // fused; gb0 ----
@@ -779,8 +800,10 @@ int phip_cluster_deep_update(const PhipTinyNet* net, const PhipTinyPhase* ph) {
     static const char* names[NSTAMP] = {"L0", "bar A", "L1", "bar B", "L2+Y", "bar C", "head", "bar D",
                                         "g3+P2", "gW2 adam", "bar E", "g2+P1", "gW1 adam", "bar F",
                                         "g1 reduce", "gW0 adam", "gb0+b0", "step->next"};
-    if (getenv("PPO_CLUSTER_STAMPS"))
+    if (getenv("PPO_CLUSTER_STAMPS")) {
         a.stamps = host_stamps(NSTAMP, "cluster_deep", names, ph->policy, a.total_steps, NWG);
+        if (getenv("PPO_CLUSTER_STAMPS")[0] == '2') a.arr = host_barrier_stamps(NWG);
+    }
     PPO_CHECK(hipMemsetAsync(ws.ctr, 0, 128 * CLU_REPL, ppo::stream()));
     ppo::ProfScope ps(PPO_K_OTHER, 0.0);
     hipLaunchKernelGGL(cluster_deep_kernel, dim3(NWG * a.active_stride), dim3(TPB), bytes, ppo::stream(), a);
