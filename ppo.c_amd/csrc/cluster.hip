@@ -48,7 +48,7 @@ struct ClArgs {
     const float *steps, *steps_ls;            // per step {lr/bc1, bc2}
     float b1, b2, eps, ent_coeff;
     float* stats;
-    float *X1, *Y, *G1;                       // published: h1 [64][H], y partials [NWG][64][OMAX], g1 partials [NWG][64][H]
+    float *X1, *Y, *G1;                       // published: h1 [64][H], y partials [NWG][64][OMAX], g1 partials [NWG][NWG][64][HC]
     unsigned* ctr;                            // barrier arrivals (zeroed before the launch)
     unsigned* err;                            // host-visible error word (0 = fine)
     unsigned long long timeout;               // barrier wait bound (realtime ticks)
@@ -420,7 +420,16 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
             for (int t = w; t < (H / 16) * (BB / 16); t += NWAVE) {
                 const int tk = t / (BB / 16), tb = t % (BB / 16);
                 const f32x4 acc = mm_tile(lds + L::W1 + 16 * tk, 1, HP, lds + L::g2 + 16 * tb * HCP, 1, HCP, HC);
-                st16_sc1(rG1, (cw * BB + 16 * tb + c) * H + 16 * tk + 4 * q, acc);
+                {
+                    // slice-major partials [slice][cw][b][HC] (each workgroup's later read of its own slice
+                    // is one contiguous block; the row-major [cw][b][H] form read HC columns of every 1-KB row)
+                    const int k = 16 * tk + 4 * q;
+#ifdef CLU_G1ROWS
+                    st16_sc1(rG1, (cw * BB + 16 * tb + c) * H + k, acc);
+#else
+                    st16_sc1(rG1, (((k / HC) * NWG + cw) * BB + 16 * tb + c) * HC + k % HC, acc);
+#endif
+                }
             }
             // bias gradient of layer 1 (fixed order)
             if (w == NWAVE - 1) colsum64<HC>(lds + L::g2, HCP, HC, 0.f, lds + L::gb1);
@@ -454,7 +463,12 @@ __global__ __launch_bounds__(TPB) void cluster_phase_kernel(ClArgs a) {
                 const int b = it / (HC / 4), jq = 4 * (it % (HC / 4));
                 f32x4 v[NWG / 2];
 #pragma unroll
-                for (int cc = 0; cc < NWG / 2; ++cc) v[cc] = ld16_sc1(rG1, ((half * (NWG / 2) + cc) * BB + b) * H + c0 + jq);
+                for (int cc = 0; cc < NWG / 2; ++cc)
+#ifdef CLU_G1ROWS
+                    v[cc] = ld16_sc1(rG1, ((half * (NWG / 2) + cc) * BB + b) * H + c0 + jq);
+#else
+                    v[cc] = ld16_sc1(rG1, (((c0 / HC) * NWG + half * (NWG / 2) + cc) * BB + b) * HC + jq);
+#endif
                 f32x4 s = v[0];
 #pragma unroll
                 for (int cc = 1; cc < NWG / 2; ++cc) s += v[cc];
@@ -714,6 +728,49 @@ void phip_cluster_report(void) {
                 }
                 fprintf(stderr, "\n");
             }
+            // per workgroup, the mean length of its own work segment before each barrier (its arrival
+            // minus its exit from the barrier before; A's segment starts at the previous step's F): which
+            // workgroups are slow, in which segment, independent of the other workgroups' hand-off times
+            auto stamp = [&](int st, int bi, int ex, int w) { return ar[((size_t)(st * 6 + bi) * 2 + ex) * nw + w]; };
+            for (int bi = 0; bi < 6; ++bi) {
+                std::vector<double> seg(nw, 0.0);
+                int n = 0;
+                for (int st = 2; st < 63; ++st) {
+                    int ps = st, pb = bi;
+                    for (int k = 1; k <= 5; ++k) {                       // the barrier before (value: no D)
+                        ps = bi - k < 0 ? st - 1 : st;
+                        pb = bi - k < 0 ? bi - k + 6 : bi - k;
+                        if (stamp(ps, pb, 1, 0)) break;
+                    }
+                    bool any = true;
+                    for (int w = 0; w < nw && any; ++w) any = stamp(st, bi, 0, w) && stamp(ps, pb, 1, w);
+                    if (!any) continue;
+                    for (int w = 0; w < nw; ++w) seg[w] += (double)(stamp(st, bi, 0, w) - stamp(ps, pb, 1, w)) / mhz;
+                    n++;
+                }
+                if (!n) continue;
+                fprintf(stderr, "%s %s segment before %c (us per wg):", s.kind, s.policy ? "policy" : "value", 'A' + bi);
+                for (int w = 0; w < nw; ++w) fprintf(stderr, " %.1f", seg[w] / n);
+                fprintf(stderr, "\n");
+                // and each workgroup's mean exit after the first exit: who sees the release late
+                std::vector<double> lat(nw, 0.0);
+                int ne = 0;
+                for (int st = 1; st < 63; ++st) {
+                    unsigned long long emin = ~0ull;
+                    bool any = true;
+                    for (int w = 0; w < nw && any; ++w) {
+                        any = stamp(st, bi, 1, w) != 0;
+                        if (any && stamp(st, bi, 1, w) < emin) emin = stamp(st, bi, 1, w);
+                    }
+                    if (!any) continue;
+                    for (int w = 0; w < nw; ++w) lat[w] += (double)(stamp(st, bi, 1, w) - emin) / mhz;
+                    ne++;
+                }
+                if (!ne) continue;
+                fprintf(stderr, "%s %s exit %c after first exit (us per wg):", s.kind, s.policy ? "policy" : "value", 'A' + bi);
+                for (int w = 0; w < nw; ++w) fprintf(stderr, " %.1f", lat[w] / ne);
+                fprintf(stderr, "\n");
+            }
         }
     }
 }
@@ -801,7 +858,7 @@ int phip_cluster_update(const PhipTinyNet* net, const PhipTinyPhase* ph) {
         phip_free(ws.X1);
         phip_free(ws.ctr);
         ws.X1 = (float*)phip_malloc(sizeof(float) * (size_t)need);
-        ws.ctr = (unsigned*)phip_malloc(128 * CLU_REPL);      // counter replicas
+        ws.ctr = (unsigned*)phip_malloc(CLU_CTR_BYTES);      // counter replicas
         ws.cap = need;
     }
     ws.Y = ws.X1 + (long)BB * 256;
@@ -817,7 +874,7 @@ int phip_cluster_update(const PhipTinyNet* net, const PhipTinyPhase* ph) {
     static const char* names[12] = {"gather", "L0", "barrier A", "h1 load", "L1+Y", "barrier B", "head+bwd",
                                     "G1+gW1 adam", "barrier C", "g1+gW0", "adam", "step->next"};
     if (getenv("PPO_CLUSTER_STAMPS")) a.stamps = host_stamps(12, "cluster", names, ph->policy, a.total_steps, NWG);
-    PPO_CHECK(hipMemsetAsync(ws.ctr, 0, 128 * CLU_REPL, ppo::stream()));
+    PPO_CHECK(hipMemsetAsync(ws.ctr, 0, CLU_CTR_BYTES, ppo::stream()));
     ppo::ProfScope ps(PPO_K_OTHER, 0.0);
     hipLaunchKernelGGL(kfn, dim3(NWG * a.active_stride), dim3(TPB), bytes, ppo::stream(), a);
     PPO_LAUNCH_CHECK();

@@ -11,6 +11,10 @@
 #ifndef CLU_REPL
 #define CLU_REPL 8                                   // barrier counter replicas (128-B lines; ≤ 64)
 #endif
+#ifndef CLU_RSTRIDE
+#define CLU_RSTRIDE 32                               // words between replicas (32: adjacent 128-B lines)
+#endif
+constexpr int CLU_CTR_BYTES = 4 * CLU_RSTRIDE * CLU_REPL;
 #ifndef CLU_SLEEP
 #define CLU_SLEEP 4                                  // s_sleep between barrier polls (× 64 clocks): 32 pollers
                                                      // at 1 slowed every barrier (C4 value step 75 → 69 µs at 4)
@@ -71,7 +75,7 @@ __device__ __forceinline__ void cluster_arrive(unsigned* ctr) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x < CLU_REPL)
-        __hip_atomic_fetch_add(ctr + 32 * threadIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(ctr + CLU_RSTRIDE * threadIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // Wait until all `nwg` workgroups have arrived for barrier number `n` (counting from 0 within the
 // launch; `rank` = the workgroup's index in the phase, picks its replica): the arriving lane polls
@@ -82,7 +86,7 @@ __device__ __forceinline__ void cluster_arrive(unsigned* ctr) {
 __device__ __forceinline__ bool cluster_wait(unsigned* ctr, unsigned* err, unsigned n, int nwg, int* flag_lds, int rank,
                                              unsigned long long timeout) {
     if (threadIdx.x == 0) {
-        ctr += 32 * (rank % CLU_REPL);                           // this workgroup's replica
+        ctr += CLU_RSTRIDE * (rank % CLU_REPL);                         // this workgroup's replica
         const unsigned target = (unsigned)nwg * (n + 1);
         int ok = 1;
         if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {

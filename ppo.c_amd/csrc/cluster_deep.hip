@@ -41,6 +41,27 @@ constexpr int T12 = (H / 16) / NWAVE;                // gW1 / gW2 tiles per wave
 constexpr int T0 = (SPMAX + 15) / 16 / NWAVE;        // gW0 tiles per wave (3)
 constexpr int RPW = BB / NWG;                        // head rows per workgroup (2)
 constexpr int NSTAMP = 18;
+#ifndef CLU_PPAD
+#define CLU_PPAD 0                                   // floats of padding per row of the Pa / Pb partial slabs
+#endif
+constexpr int PH = H + CLU_PPAD;                     // Pa / Pb row pitch
+#ifndef CLU_PSLICE
+#define CLU_PSLICE 1                                 // Pa / Pb slice-major ([slice][p][b][HC]); 0: row-major [p][b][H]
+#endif
+// Slice-major: a workgroup's reduction of its own 16 columns over the 32 partials is one contiguous
+// 128 KB block. Row-major, it read 64 B from every 2-KB row (2,048 loads at one address offset mod 2 KB),
+// and the four slices at offsets 384-511 mod 1024 B (6, 7, 22, 23) were 1.5-1.8 µs slower at barriers A
+// and F in every placement (PPO_CLUSTER_ROT moved the slow workgroups with their slices): the step
+// waits for them. Slice-major: every slice 13.1 / 5.9 µs (was 14.0 / 7.5, slow 15.5 / 9.3); C4 B = 64
+// 9.51-9.69 s per update vs 10.44-10.51 row-major, same box (profiles/r06_c4b64_partial_layout.txt).
+// float offset of partial p's row b, hidden unit slice·HC + j, in a Pa / Pb slab
+__device__ __forceinline__ int pidx(int slice, int p, int b, int j) {
+#if CLU_PSLICE
+    return ((slice * NWG + p) * BB + b) * HC + j;
+#else
+    return (p * BB + b) * PH + slice * HC + j;
+#endif
+}
 #ifndef CLU_GW_PRE
 #define CLU_GW_PRE 1                                 // weight-gradient tiles whose operands load under the P partial
 #endif
@@ -63,10 +84,12 @@ struct DArgs {
     float b1, b2, eps, ent_coeff;
     float* stats;
     float *X1, *X2, *Y, *G3, *Pa, *Pb;               // hand-offs (X1 [2][64][H], X2 [64][H], Y [NWG][64][OP],
-                                                     // G3 [64][GP], Pa / Pb [NWG][64][H])
+                                                     // G3 [64][GP], Pa / Pb [NWG slices][NWG][64][HC])
     unsigned *ctr, *err;
     unsigned long long timeout;                      // barrier wait bound (realtime ticks)
     int active_stride, active_offset;                // workgroup b works iff b % stride == offset
+    int rot;                                         // PPO_CLUSTER_ROT (diagnostic): workgroup cw owns hidden
+                                                     // slice (cw + rot) mod NWG — separates slice from placement
     unsigned long long* stamps;                      // PPO_CLUSTER_STAMPS: workgroup 0, steps 0..63
     unsigned long long* arr;                         // PPO_CLUSTER_STAMPS=2: every workgroup's arrival and exit
                                                      // time at every barrier, steps 0..63 [64][6][2][NWG]
@@ -278,7 +301,7 @@ struct PartialSum {
     __device__ __forceinline__ void load(int tid, __amdgpu_buffer_rsrc_t rP, int c0) {
         const int it = tid & 255, half = tid >> 8, b = it >> 2, jq = 4 * (it & 3);
 #pragma unroll
-        for (int p = 0; p < NWG / 2; ++p) v[p] = ld16_sc1(rP, ((half * (NWG / 2) + p) * BB + b) * H + c0 + jq);
+        for (int p = 0; p < NWG / 2; ++p) v[p] = ld16_sc1(rP, pidx(c0 / HC, half * (NWG / 2) + p, b, jq));
     }
     __device__ __forceinline__ void finish(int tid, const float* hown, float* lds) {
         const int it = tid & 255, half = tid >> 8, b = it >> 2, jq = 4 * (it & 3);
@@ -309,7 +332,7 @@ __device__ __forceinline__ void publish_partial(int tid, __amdgpu_buffer_rsrc_t 
     for (int t = w; t < (H / 16) * (BB / 16); t += NWAVE) {
         const int tk = t >> 2, tb = t & 3;
         const f32x4 acc = mm_tile(W + 16 * tk, 1, HP, lds + L::gh + 16 * tb * HCP, 1, HCP, HC, tid);
-        st16_sc1(rP, (cw * BB + 16 * tb + c) * H + 16 * tk + 4 * q, acc);
+        st16_sc1(rP, pidx(tk, cw, 16 * tb + c, 4 * q), acc);
     }
 }
 
@@ -335,7 +358,7 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
     if (a.stamps && threadIdx.x == 0)
         a.stamps[64 * 32 + cw] = ((unsigned long long)__builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11)) << 32) |
                                  __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));
-    const int c0 = cw * HC;
+    const int c0 = ((cw + a.rot) % NWG) * HC;
     extern __shared__ float lds[];
     int* flag = reinterpret_cast<int*>(lds + L::flag);
     const int tid = threadIdx.x;
@@ -343,7 +366,7 @@ __global__ __launch_bounds__(TPB) void cluster_deep_kernel(DArgs a) {
     const int nsmall = O * HC + 3 * HC + O + (a.policy ? A : 0);
     const auto rX1 = rsrc(a.X1, 2L * BB * H), rX2 = rsrc(a.X2, (long)BB * H);
     const auto rY = rsrc(a.Y, (long)NWG * BB * OP), rG3 = rsrc(a.G3, (long)BB * GP);
-    const auto rPa = rsrc(a.Pa, (long)NWG * BB * H), rPb = rsrc(a.Pb, (long)NWG * BB * H);
+    const auto rPa = rsrc(a.Pa, (long)NWG * BB * PH), rPb = rsrc(a.Pb, (long)NWG * BB * PH);
 
     // ---- phase start: own parameters → LDS, Adam moments → VGPRs ----
     for (int e = tid; e < HC * SPMAX; e += TPB) {
@@ -781,13 +804,13 @@ int phip_cluster_deep_update(const PhipTinyNet* net, const PhipTinyPhase* ph) {
     a.stats = ph->stats;
     Ws& ws = g_ws[phip_side_active() ? 1 : 0];
     const long nX1 = 2L * BB * H, nX2 = (long)BB * H, nY = (long)NWG * BB * OP, nG3 = (long)BB * GP,
-               nP = (long)NWG * BB * H;
+               nP = (long)NWG * BB * PH;
     const long need = nX1 + nX2 + nY + nG3 + 2 * nP;
     if (ws.cap < need) {
         phip_free(ws.base);
         phip_free(ws.ctr);
         ws.base = (float*)phip_malloc(sizeof(float) * (size_t)need);
-        ws.ctr = (unsigned*)phip_malloc(128 * CLU_REPL);      // counter replicas
+        ws.ctr = (unsigned*)phip_malloc(CLU_CTR_BYTES);      // counter replicas
         ws.cap = need;
     }
     a.X1 = ws.base; a.X2 = a.X1 + nX1; a.Y = a.X2 + nX2; a.G3 = a.Y + nY; a.Pa = a.G3 + nG3; a.Pb = a.Pa + nP;
@@ -797,6 +820,7 @@ int phip_cluster_deep_update(const PhipTinyNet* net, const PhipTinyPhase* ph) {
     // stride 8 puts a phase on one XCD (blocks b, b + 8 share one); the policy phase then takes XCD 4
     // so the two concurrent phases never share CUs
     a.active_offset = stride == 8 && ph->policy ? 4 : 0;
+    if (const char* r = getenv("PPO_CLUSTER_ROT")) a.rot = ((atoi(r) % NWG) + NWG) % NWG;
     static const char* names[NSTAMP] = {"L0", "bar A", "L1", "bar B", "L2+Y", "bar C", "head", "bar D",
                                         "g3+P2", "gW2 adam", "bar E", "g2+P1", "gW1 adam", "bar F",
                                         "g1 reduce", "gW0 adam", "gb0+b0", "step->next"};
@@ -804,7 +828,7 @@ int phip_cluster_deep_update(const PhipTinyNet* net, const PhipTinyPhase* ph) {
         a.stamps = host_stamps(NSTAMP, "cluster_deep", names, ph->policy, a.total_steps, NWG);
         if (getenv("PPO_CLUSTER_STAMPS")[0] == '2') a.arr = host_barrier_stamps(NWG);
     }
-    PPO_CHECK(hipMemsetAsync(ws.ctr, 0, 128 * CLU_REPL, ppo::stream()));
+    PPO_CHECK(hipMemsetAsync(ws.ctr, 0, CLU_CTR_BYTES, ppo::stream()));
     ppo::ProfScope ps(PPO_K_OTHER, 0.0);
     hipLaunchKernelGGL(cluster_deep_kernel, dim3(NWG * a.active_stride), dim3(TPB), bytes, ppo::stream(), a);
     PPO_LAUNCH_CHECK();

@@ -306,11 +306,9 @@ struct StageX3 {
         for (int q = 0; q < NV; ++q)
             if (kvalid(q, k0, kend)) {
                 f32x4* p = reinterpret_cast<f32x4*>(dst + (long)(r0 + row) * ldd + k0 + k + 4 * q);
-#ifdef PPO_X3_COPY_NT
-                __builtin_nontemporal_store(v[q], p);
-#else
+// (a non-temporal store here measured slower: the layer-0 forward that reads the copy back from L2
+                // took 99.6-100.2 vs 82.7-82.9 µs, C4 310.3 vs 306.6 ms; profiles/r06_x3_copy_nt_rejected.txt)
                 *p = v[q];
-#endif
             }
     }
     // MFMA fragment (32 rows × 16 k of k-half kh, bf16x8 per lane: row `rr`, k = 16kh + 8h..+7) of one plane

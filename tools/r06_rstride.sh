@@ -1,0 +1,19 @@
+#!/bin/sh
+# r06_rstride.sh TAG — C4 at B = 64: libppo (slice-major partial slabs, counter replicas on adjacent 128-B
+# lines) vs rows (row-major slabs, the round-6 layout) vs rs1k / rs4k (replicas 4 KB / 16 KB apart):
+# stamps of libppo and rs1k, then update times, interleaved twice
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/$1
+mkdir -p $O
+cd $R
+V=$R/ppo.c_amd/lib/variants
+for v in def rs1k; do
+  L=$R/ppo.c_amd/lib/libppo.so; [ $v = def ] || L=$V/libppo_$v.so
+  PPO_LIB=$L PPO_CLUSTER_STAMPS=2 timeout -k 10 200 python bench.py --config c4 --batch 64 --steps 1 --warmup 1 \
+      --no-cpu-baseline --no-rollout --no-kernel-events > $O/st_$v.log 2>&1 || exit 1
+done
+for i in 1 2; do for v in def rows rs1k rs4k; do
+  L=$R/ppo.c_amd/lib/libppo.so; [ $v = def ] || L=$V/libppo_$v.so
+  PPO_LIB=$L timeout -k 10 200 python bench.py --config c4 --batch 64 --steps 2 --warmup 1 \
+      --no-cpu-baseline --no-rollout --no-kernel-events > $O/t_${v}_$i.log 2>&1 || exit 1
+done; done
