@@ -354,7 +354,7 @@ def main():
         cap = 256
         keys, kms, kl, kw = (C.c_longlong * cap)(), (C.c_double * cap)(), (C.c_long * cap)(), (C.c_double * cap)()
         n_sh = min(cap, LIB.ppo_prof_shapes(keys, kms, kl, kw, cap))
-        ops = ["forward", "grad_x", "grad_W", "grad_W+grad_x"]
+        ops = ["forward", "grad_x", "grad_W", "grad_W+grad_x", "forward+head+grad_W+grad_x"]
         engines = ["exact-fp32", "x3", "bf16"]
         issued_sh = (C.c_long * cap)()
         LIB.ppo_prof_shape_issued(keys, issued_sh, n_sh)
@@ -457,7 +457,8 @@ def main():
         if groups:
             g = max(groups.values(), key=lambda v: v["ms"])
             dom = {"op": g["op"], "engine": g["engine"], "template": {"forward": "NT", "grad_x": "NN", "grad_W": "TN",
-                                                                      "grad_W+grad_x": "pair"}.get(g["op"]),
+                                                                      "grad_W+grad_x": "pair",
+                                                                      "forward+head+grad_W+grad_x": "fused"}.get(g["op"]),
                    "launches": g["launches"], "ms": g["ms"], "avg_us": 1000.0 * g["ms"] / g["launches"],
                    "tflops": g["work"] / (g["ms"] * 1e-3) / 1e12,
                    "algorithmic_bytes": g["bytes"] / g["launches"], "shapes": g["shapes"]}

@@ -543,6 +543,223 @@ __global__ __launch_bounds__(256) void out_bwd_wide_kernel(WideArgs p) {
     }
 }
 
+
+// ---------------------------------------------------------------------------------------------------
+// The A = 17 policy network's whole output layer for one minibatch step in ONE pass over the last hidden
+// activation h (round 6; replaces the exact-fp32 forward GEMM and out_bwd_wide_kernel<HEAD>):
+//   μ = h·W3ᵀ + b3 — exact fp32 MFMA (v_mfma_f32_16x16x4_f32) on 16-row blocks of h staged in LDS, K split
+//       over the four waves and their partial tiles summed in a fixed order (mat_mul.cu:122-163);
+//   the policy head on μ — out_bwd_wide_kernel<HEAD>'s per-row arithmetic (policy.cu:67-111, ppo.cu:82-107);
+//   gx = (g·W3) ⊙ 1[h > 0], gW3 += gᵀ·h, gb3 += Σ g (mat_mul.cu:165-217) — thread t owns columns
+//       t·NPT … t·NPT + NPT − 1 with their W3 values and gW3 accumulators in registers, h read from LDS.
+// h leaves HBM once (the separate forward and backward read it twice and round-trip μ): ≈ 8·n bytes per
+// row.  Each workgroup loops over 16-row blocks; its gW3 / gb3 partial goes to its slab (ppo::slab_reduce
+// sums them in order), log σ's gradient and the loss get one f32 atomic per workgroup (as the HEAD path).
+struct FusedArgs {
+    const float* x; const float* W; const float* b; float* mu;    // h [m, n], W3 [A, n], b3 [A], μ out [m, A]
+    float* gx; float* slab; long slab_stride;
+    int m, relu_in, nblk;                                          // nblk: 16-row blocks of the minibatch
+    const float* log_std; const float* action; const float* adv; const float* old_lp;
+    float eps, ent_coeff; float* grad_log_std; float* loss_accum;
+};
+
+constexpr int FR = 16;                                             // rows per block
+#ifndef PPO_FUSED_ABL
+#define PPO_FUSED_ABL 0        // diagnostic builds only: 1 no μ MFMA, 2 no head, 4 no gx / gW3 rows, 8 no h loads
+#endif
+
+template <int NPT>
+constexpr size_t fused_lds_floats() {
+    constexpr int N = 256 * NPT, HPs = N + 4;                      // pitch ≡ 4 (mod 32): 2-way = optimal for
+    return (size_t)FR * HPs + 17 * HPs + 4 * 2 * 256               // the MFMA operand reads
+           + 3 * FR * 20 + 3 * FR;                                 // μ / g, actions, log σ terms; ∂L/∂lp, adv, old lp
+}
+
+template <int NPT>
+__global__ __launch_bounds__(256, 2) void policy_out_fused_kernel(FusedArgs p) {
+    typedef float f32x4v __attribute__((ext_vector_type(4)));
+    constexpr int A = 17, AP = 20, N = 256 * NPT, HPs = N + 4, KW = N / 4;   // KW: k range of one wave
+    constexpr int NPF = FR * (N / 4) / 256;                        // float4 loads of h per thread per block
+    extern __shared__ __attribute__((aligned(16))) float smf[];
+    float* hs = smf;                                               // [FR][HPs] the block's rows of h
+    float* ws = hs + FR * HPs;                                     // [A][HPs] W3
+    float* red = ws + A * HPs;                                     // [wave][tile][lane] f32x4 partial μ tiles
+    float* mus = red + 4 * 2 * 256;                                // [FR][AP] μ, then ∂L/∂μ in place
+    float* acts = mus + FR * AP;                                   // [FR][AP] actions
+    float* lst = acts + FR * AP;                                   // [FR][AP] ∂/∂log σ row terms
+    float* grs = lst + FR * AP;                                    // [FR] ∂L/∂lp
+    float* advs = grs + FR;                                        // [FR] advantage | old log-prob (2 × FR)
+    double* dterm = reinterpret_cast<double*>(red);                // [FR][A] log-prob terms, over the μ tiles
+    __shared__ float lss[32], ess[32], e2s[32], b3s[32];
+    static_assert(sizeof(float) * fused_lds_floats<NPT>() + 4 * 32 * 4 <= 80 * 1024, "two workgroups per CU");
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, k0 = t * NPT;
+    const int c = lane & 15, q = lane >> 4;
+    float Wr[A][NPT], acc[A][NPT];
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+        load_cols<NPT>(p.W + (long)a * N + k0, Wr[a]);
+#pragma unroll
+        for (int u = 0; u < NPT; ++u) acc[a][u] = 0.f;
+    }
+    for (int e = t; e < A * (N / 4); e += 256) {
+        const int a = e / (N / 4), cq = e % (N / 4);
+        *reinterpret_cast<f32x4v*>(ws + a * HPs + 4 * cq) = *reinterpret_cast<const f32x4v*>(p.W + (long)a * N + 4 * cq);
+    }
+    if (t < A) {
+        lss[t] = p.log_std[t];
+        e2s[t] = expf(-2 * p.log_std[t]);
+        ess[t] = expf(p.log_std[t]);
+        b3s[t] = p.b[t];
+    }
+    // the next block's operands in registers while this block computes: h rows, actions, adv / old log-prob
+    f32x4v hpf[NPF];
+    float apf[2], xpf = 0.f;
+    auto prefetch = [&](int blk) {
+        const int r0 = blk * FR, nr = blk < p.nblk ? min(FR, p.m - r0) : 0;
+#pragma unroll
+        for (int v = 0; v < NPF; ++v) {
+            const int e = t + 256 * v, r = e / (N / 4), cq = e % (N / 4);
+            hpf[v] = r < nr ? *reinterpret_cast<const f32x4v*>(p.x + (long)(r0 + r) * N + 4 * cq)
+                            : f32x4v{0.f, 0.f, 0.f, 0.f};
+        }
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+            const int e = t + 256 * v;
+            apf[v] = e < nr * A ? p.action[(long)r0 * A + e] : 0.f;
+        }
+        xpf = t < nr ? p.adv[r0 + t] : (t >= 32 && t < 32 + nr ? p.old_lp[r0 + t - 32] : 0.f);
+    };
+    float gls = 0.f, gbs = 0.f, sv = 0.f;     // threads j < A: log σ and gb3 partials; wave 0's rows: loss terms
+    prefetch(blockIdx.x);
+    for (int blk = blockIdx.x; blk < p.nblk; blk += gridDim.x) {
+        const int r0 = blk * FR, nr = min(FR, p.m - r0);
+        __syncthreads();                                           // the previous block is done with the LDS
+#pragma unroll
+        for (int v = 0; v < NPF; ++v) {
+            const int e = t + 256 * v, r = e / (N / 4), cq = e % (N / 4);
+            if (!(PPO_FUSED_ABL & 8)) *reinterpret_cast<f32x4v*>(hs + r * HPs + 4 * cq) = hpf[v];
+        }
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+            const int e = t + 256 * v;
+            if (e < FR * A) acts[(e / A) * AP + e % A] = apf[v];
+        }
+        if (t < FR) advs[t] = xpf;
+        else if (t >= 32 && t < 32 + FR) advs[FR + t - 32] = xpf;
+        __syncthreads();
+        if (blk + (int)gridDim.x < p.nblk) prefetch(blk + gridDim.x);
+        {   // μ partial tiles of this wave's k range (two interleaved chains per tile): tile 0 = columns
+            // 0 … 15, tile 1 = column 16
+            f32x4v a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0, b0 = a0, b1 = a0;
+            const float* Ar = hs + c * HPs + w * KW + q;
+            const float* B0 = ws + c * HPs + w * KW + q;
+            const float* B1 = ws + 16 * HPs + w * KW + q;
+#pragma unroll 4
+            for (int kk = 0; kk < KW && !(PPO_FUSED_ABL & 1); kk += 8) {
+                const float av = Ar[kk], bv = Ar[kk + 4];
+                a0 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, B0[kk], a0, 0, 0, 0);
+                b0 = __builtin_amdgcn_mfma_f32_16x16x4f32(bv, B0[kk + 4], b0, 0, 0, 0);
+                a1 = __builtin_amdgcn_mfma_f32_16x16x4f32(av, c == 0 ? B1[kk] : 0.f, a1, 0, 0, 0);
+                b1 = __builtin_amdgcn_mfma_f32_16x16x4f32(bv, c == 0 ? B1[kk + 4] : 0.f, b1, 0, 0, 0);
+            }
+            f32x4v* rp = reinterpret_cast<f32x4v*>(red) + w * 2 * 64 + lane;
+            rp[0] = a0 + b0;
+            rp[64] = a1 + b1;
+        }
+        __syncthreads();
+        // μ = Σ over the waves in order + b3; tile element (row r, column cc) sits in lane cc + 16·(r / 4),
+        // component r % 4.  Then each (row, j) term of the log-prob in parallel (the sum stays sequential)
+        for (int e = t; e < FR * A; e += 256) {
+            const int r = e / A, j = e % A, tile = j >> 4, cc = j & 15;
+            const int ln = cc + 16 * (r >> 2), comp = r & 3;
+            float sacc = red[((0 * 2 + tile) * 64 + ln) * 4 + comp];
+#pragma unroll
+            for (int ww = 1; ww < 4; ++ww) sacc += red[((ww * 2 + tile) * 64 + ln) * 4 + comp];
+            const float muv = sacc + b3s[j];
+            mus[r * AP + j] = muv;
+            if (r < nr) p.mu[(long)(r0 + r) * A + j] = muv;       // the network's output
+        }
+        __syncthreads();
+        for (int e = t; e < FR * A; e += 256) {
+            const int r = e / A, j = e % A;
+            const float z = (acts[r * AP + j] - mus[r * AP + j]) / ess[j];
+            dterm[e] = (double)lss[j] + 0.5 * (double)(z * z);     // policy.cu:67-74 (log_prob_row_p)
+        }
+        __syncthreads();
+        if (t < nr && !(PPO_FUSED_ABL & 2)) {                     // the head, one row per thread (wave 0)
+            float lp = (float)(-0.5 * A * (double)logf((float)(2 * M_PI)));
+#pragma unroll
+            for (int j = 0; j < A; ++j) lp = (float)((double)lp - dterm[t * A + j]);
+            float glp;
+            sv += surrogate(advs[t], lp, advs[FR + t], p.eps, p.m, &glp);
+            grs[t] = glp;
+        }
+        __syncthreads();
+        for (int e = t; e < FR * A; e += 256) {                    // log σ row terms; μ → ∂L/∂μ in place
+            const int r = e / A, j = e % A;
+            const float d = acts[r * AP + j] - mus[r * AP + j], gr = r < nr ? grs[r] : 0.f;
+            lst[r * AP + j] = (-1 + d * d * e2s[j]) * gr;
+            mus[r * AP + j] = d * e2s[j] * gr;
+        }
+        __syncthreads();
+        if (t < A && !(PPO_FUSED_ABL & 2)) {                      // ordered sums over the block's rows
+            for (int r = 0; r < nr; ++r) gls += lst[r * AP + t];
+        } else if (t >= 32 && t < 32 + A) {
+            for (int r = 0; r < nr; ++r) gbs += mus[r * AP + t - 32];
+        }
+        for (int r = 0; r < nr && !(PPO_FUSED_ABL & 4); r += 2) {  // two rows at a time (independent chains)
+            const bool two = r + 1 < nr;
+            float gv0[A], gv1[A], xv0[NPT], xv1[NPT];
+#pragma unroll
+            for (int a = 0; a < A; ++a) {
+                gv0[a] = mus[r * AP + a];                          // uniform address: LDS broadcast
+                gv1[a] = two ? mus[(r + 1) * AP + a] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < NPT; ++u) {
+                xv0[u] = hs[r * HPs + k0 + u];
+                xv1[u] = two ? hs[(r + 1) * HPs + k0 + u] : 0.f;
+            }
+            float o0[NPT], o1[NPT];
+#pragma unroll
+            for (int u = 0; u < NPT; ++u) {
+                float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+                for (int a = 0; a < A; ++a) {
+                    s0 = __builtin_fmaf(gv0[a], Wr[a][u], s0);
+                    s1 = __builtin_fmaf(gv1[a], Wr[a][u], s1);
+                }
+                o0[u] = (!p.relu_in || xv0[u] > 0.f) ? s0 : 0.f;
+                o1[u] = (!p.relu_in || xv1[u] > 0.f) ? s1 : 0.f;
+            }
+            store_cols<NPT>(p.gx + (long)(r0 + r) * N + k0, o0);
+            if (two) store_cols<NPT>(p.gx + (long)(r0 + r + 1) * N + k0, o1);
+#pragma unroll
+            for (int a = 0; a < A; ++a)
+#pragma unroll
+                for (int u = 0; u < NPT; ++u)
+                    acc[a][u] = __builtin_fmaf(gv1[a], xv1[u], __builtin_fmaf(gv0[a], xv0[u], acc[a][u]));
+        }
+    }
+    float* __restrict__ out = p.slab + (long)blockIdx.x * p.slab_stride;
+#pragma unroll
+    for (int a = 0; a < A; ++a) store_cols<NPT>(out + a * N + k0, acc[a]);
+    if (t < A) atomicAdd(p.grad_log_std + t, gls + (blockIdx.x == 0 ? -p.ent_coeff : 0.f));     // ppo.cu:436-438 (D4)
+    else if (t >= 32 && t < 32 + A) out[A * N + t - 32] = gbs;
+    if (w == 0) {
+        const float sl = ppo::wave_sum64(sv);
+        if (lane == 0 && p.loss_accum) {
+            float contrib = -sl / p.m;
+            if (blockIdx.x == 0) {
+                float ent = (float)(A * 0.5 * (1 + log(2 * M_PI)));
+                for (int j = 0; j < A; ++j) ent += lss[j];
+                contrib -= p.ent_coeff * ent;
+            }
+            atomicAdd(p.loss_accum, contrib);
+        }
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -590,6 +807,45 @@ int phip_out_bwd_wide(float* gW, float* gb, float* gx, const float* g, const flo
     WideArgs w{};
     w.g = g; w.x = x; w.W = W; w.gx = gx; w.m = m; w.relu_in = relu_in;
     return out_bwd_wide_launch(w, gW, gb, n, A, false);
+}
+
+// the fused policy output layer (policy_out_fused_kernel): 1 when it ran, 0 when the shape is not its
+// (A = 17, n = 256 or 512, the flat gradient layout gb = gW + A·n, 16-B aligned operands)
+int phip_policy_out_fused(const float* x, const float* W, const float* b, float* mu, const float* log_std,
+                          const float* action, const float* adv, const float* old_lp, float eps, float ent_coeff,
+                          float* grad_log_std, float* loss_accum, int relu_in, float* gW, float* gb, float* gx, int m,
+                          int n, int A) {
+    if (A != 17 || (n != 512 && n != 256) || m <= 0 || !b || !mu || !log_std || !action || !adv || !old_lp ||
+        !grad_log_std || gb != gW + (long)A * n)
+        return 0;
+    if ((((uintptr_t)x | (uintptr_t)gx | (uintptr_t)W | (uintptr_t)gW) & 15u) != 0) return 0;
+    ppo::ProfScope ps(PPO_K_GEMM, 6.0 * m * n * A, ppo::gemm_key(4, 0, m, n, A));
+    FusedArgs f{};
+    f.x = x; f.W = W; f.b = b; f.mu = mu; f.gx = gx; f.m = m; f.relu_in = relu_in;
+    f.log_std = log_std; f.action = action; f.adv = adv; f.old_lp = old_lp;
+    f.eps = eps; f.ent_coeff = ent_coeff; f.grad_log_std = grad_log_std; f.loss_accum = loss_accum;
+    f.nblk = ppo_divup(m, FR);
+    // two workgroups per CU (C4: 256 / 512 / 1024 / 2048 workgroups 107 / 74 / 87 / 104 µs)
+    const int nwg = std::min(512, f.nblk);
+    f.slab_stride = ((long)A * n + A + 3) & ~3L;
+    f.slab = ppo::slab_scratch((size_t)nwg * f.slab_stride);
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    const bool timed = ppo::take_kernel_events(&e0, &e1);          // one duration: kernel start → reduce end
+    auto go = [&](auto kern, size_t lds) {
+        static bool attr[2] = {false, false};
+        bool& at = attr[n == 512 ? 1 : 0];
+        if (!at) {
+            PPO_CHECK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+            at = true;
+        }
+        if (timed) hipExtLaunchKernelGGL(kern, dim3(nwg), dim3(256), lds, ppo::stream(), e0, nullptr, 0, f);
+        else hipLaunchKernelGGL(kern, dim3(nwg), dim3(256), lds, ppo::stream(), f);
+    };
+    if (n == 512) go(policy_out_fused_kernel<2>, sizeof(float) * fused_lds_floats<2>());
+    else go(policy_out_fused_kernel<1>, sizeof(float) * fused_lds_floats<1>());
+    PPO_LAUNCH_CHECK();
+    ppo::slab_reduce(f.slab, gW, (long)A * n + A, f.slab_stride, nwg, timed ? e1 : nullptr);
+    return 1;
 }
 
 int phip_policy_head_bwd_wide(const float* mu, const float* log_std, const float* action, const float* adv,

@@ -174,6 +174,10 @@ int  phip_out_bwd_wide(float* gW, float* gb, float* gx, const float* g, const fl
                        int m, int n, int A);
 /* the same pass with the policy head (kernels.hip policy_head_tiled_kernel's arithmetic) computed from μ
  * first: ∂/∂log σ (+ −c_ent) and the loss accumulated into grad_log_std / loss_accum (atomics) */
+int  phip_policy_out_fused(const float* x, const float* W, const float* b, float* mu, const float* log_std,
+                           const float* action, const float* adv, const float* old_lp, float eps, float ent_coeff,
+                           float* grad_log_std, float* loss_accum, int relu_in, float* gW, float* gb, float* gx,
+                           int m, int n, int A);
 int  phip_policy_head_bwd_wide(const float* mu, const float* log_std, const float* action, const float* adv,
                                const float* old_lp, float eps, float ent_coeff, float* grad_log_std,
                                float* loss_accum, const float* x, const float* W, int relu_in, float* gW, float* gb,

@@ -579,10 +579,31 @@ void nn_policy_wide_step(NeuralNetwork* nn, const float* d_x, const int* d_rows,
                          const float* adv, const float* old_lp, float eps, float ent_coeff, float* grad_log_std,
                          float* loss_accum) {
     const int L = nn->num_layers - 1;
+    Layer* ly = &nn->layers[L - 1];
+    /* PPO_POLICY_FUSED (read per call): 1 the one-launch output layer, 0 the two launches, unset: one launch
+     * up to 8192 rows (the G = 8 shard's policy step: 27.1 vs 19.4 + 17.2 µs) and two above (C4's 32768 rows:
+     * 75 vs 42.6 + 19.1 µs — eight 16-row blocks per CU, each a chain of seven barrier-separated phases;
+     * profiles/r06_policy_out_fused_ab.txt) */
+    const char* pf = getenv("PPO_POLICY_FUSED");
+    const int fused = pf && pf[0] ? pf[0] != '0' : m <= 8192;
+    if (fused) {
+        /* the output layer's forward, the head and its backward in one pass over h (out_head.hip
+         * policy_out_fused_kernel): the hidden layers' forward only */
+        nn_forward_dev_upto(nn, d_x, d_rows, d_xcopy, m, L - 1, NULL);
+        nn_ensure_grad(nn, m);
+        if (!grads_zero) phip_memset(nn->d_grads, 0, sizeof(float) * (size_t)nn->num_params);
+        float* mu = nn->layers[L].d_input;
+        if (!phip_policy_out_fused(ly->d_input, ly->d_weights, ly->d_biases, mu, log_std, action, adv, old_lp, eps,
+                                   ent_coeff, grad_log_std, loss_accum, nn_is_relu(nn, L - 2), ly->d_grad_weights,
+                                   ly->d_grad_biases, ly->d_grad_x, m, ly->input_size, ly->output_size))
+            die("nn_policy_wide_step: the fused output layer declined a shape nn_policy_wide_ok accepted");
+        nn->d_output = mu;
+        nn_backward_dev_top(nn, ly->d_grad_x, m, 0, 1, reduce_extra, L - 1, NULL);
+        return;
+    }
     nn_forward_dev_rows(nn, d_x, d_rows, d_xcopy, m);
     nn_ensure_grad(nn, m);
     if (!grads_zero) phip_memset(nn->d_grads, 0, sizeof(float) * (size_t)nn->num_params);
-    Layer* ly = &nn->layers[L - 1];
     if (!phip_policy_head_bwd_wide(nn->d_output, log_std, action, adv, old_lp, eps, ent_coeff, grad_log_std,
                                    loss_accum, ly->d_input, ly->d_weights, nn_is_relu(nn, L - 2), ly->d_grad_weights,
                                    ly->d_grad_biases, ly->d_grad_x, m, ly->input_size, ly->output_size))

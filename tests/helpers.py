@@ -38,8 +38,8 @@ def assert_gemm_close(got, ref, K, what=""):
 
 
 def nn_input_rows(lib, nn_ptr, m):
-    """Layer 0's input rows of the last device forward (fp32), as the GEMMs read them: the buffer rows
-    through NeuralNetwork.d_x0_rows (x3 engine: no gathered copy) or the gathered copy d_x0."""
+    """Layer 0's input rows of the last device forward (fp32), as the GEMMs read them: the gathered copy
+    d_x0 (ppo_nn_input_rows; the caller never reaches into the layout of the gather)."""
     nn = nn_ptr.contents
     S = nn.layers[0].input_size
     out = np.empty((m, S), F32)

@@ -620,15 +620,18 @@ def test_graph_replay_declines_untested_paths(lib, oracle, case, monkeypatch):
     assert err.max() <= 2 * 3e-4 and (err > 1e-6).mean() < 0.02
 
 
-def test_wide_output_backward_matches_pair(lib, oracle, monkeypatch):
-    """The A = 17 policy head fused with the output layer's one-pass backward (out_bwd_wide_kernel<HEAD>:
-    the head from μ in LDS, then grad_x and grad_W / grad_b from one read of x, per-workgroup partials
-    through the slab reduce) against the separate head launch + paired GEMM launch (PPO_NO_WIDE_BWD=1)
-    from identical state: one policy minibatch of the humanoid config, every policy gradient within the
-    GEMM tolerance (the same products summed in another order), the log σ gradient and the loss sums
-    within reduction rounding."""
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_wide_output_backward_matches_pair(lib, oracle, monkeypatch, fused):
+    """The A = 17 policy network's output layer on its one-pass paths — fused = 1 (default): forward, head
+    and backward in one launch (policy_out_fused_kernel: μ by exact fp32 MFMA from h staged in LDS, the
+    head, grad_x and grad_W / grad_b from the same rows); fused = 0 (PPO_POLICY_FUSED=0): the forward GEMM,
+    then the head fused with the one-pass backward (out_bwd_wide_kernel<HEAD>) — against the separate head
+    launch + paired GEMM launch (PPO_NO_WIDE_BWD=1) from identical state: one policy minibatch of the
+    humanoid config, μ and every policy gradient within the GEMM tolerance (the same products summed in
+    another order), the log σ gradient and the loss sums within reduction rounding."""
     sizes, N = CONFIGS["humanoid"]["sizes"], CONFIGS["humanoid"]["N"]
     out = {}
+    monkeypatch.setenv("PPO_POLICY_FUSED", fused)
     for mode in ("1", "0"):
         if mode == "1":
             monkeypatch.setenv("PPO_NO_WIDE_BWD", "1")
@@ -645,9 +648,11 @@ def test_wide_output_backward_matches_pair(lib, oracle, monkeypatch):
         lib.ppo_read_stats(ppo, st, 7)
         pol = ppo.contents.policy.contents
         out[mode] = dict(gmu=nn_grads_packed(lib, pol.mu), stats=np.array(st[:4]),
-                         gls=ppo_ffi.d2h(lib, pol.d_log_std_grad, F32, sizes[-1]))
+                         gls=ppo_ffi.d2h(lib, pol.d_log_std_grad, F32, sizes[-1]),
+                         mu=ppo_ffi.d2h(lib, pol.mu.contents.d_output, F32, N * sizes[-1]))
         lib.free_ppo(ppo)
     a, b = out["1"], out["0"]
+    assert_gemm_close(b["mu"], a["mu"], sizes[-2], "policy output μ (one-pass vs separate forward)")
     assert_gemm_close(b["gmu"], a["gmu"], N, "policy grads (wide backward vs paired GEMM)")
     assert_rel_close(b["gls"], a["gls"], 1e-4, 1e-5 * max(1.0, np.abs(a["gls"]).max()), "log_std grad")
     np.testing.assert_allclose(b["stats"], a["stats"], rtol=1e-5, atol=1e-7)
