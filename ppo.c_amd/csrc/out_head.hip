@@ -18,11 +18,12 @@
 // (the same arithmetic as kernels.hip's mse_kernel / policy_head_kernel given y), and g·W, gᵀ·x use
 // the lane's columns.  gW / gb / grad_logσ / loss: summed over the workgroup's waves through LDS,
 // then one f32 atomic per element per workgroup into outputs that are zero on entry (as the split-K
-// grad_W GEMMs).  The wide policy output (A = 17) keeps the separate launches: one wave per row
-// would need 2·17·8 registers for its weights and accumulators alone (the round-1 fused kernel
-// spilled, 10× slower), and splitting each row over two waves (4 columns per lane, 256 VGPRs, one
-// wave per SIMD) measured slower than the separate launches (C4 update 330 -> 347 ms,
-// profiles/r02_out_head_ab.txt).
+// grad_W GEMMs).  The wide policy output (A = 17) does not fit this layout: one wave per row would
+// need 2·17·8 registers for its weights and accumulators alone (the round-1 fused kernel spilled,
+// 10× slower), and splitting each row over two waves (4 columns per lane, 256 VGPRs, one wave per
+// SIMD) measured slower than the separate launches (C4 update 330 -> 347 ms,
+// profiles/r02_out_head_ab.txt).  It takes out_bwd_wide_kernel (head + backward, thread per column)
+// after the forward GEMM, or policy_out_fused_kernel (forward + head + backward) up to 8192 rows.
 #include "dev.h"
 
 #include <algorithm>
