@@ -620,16 +620,21 @@ def test_graph_replay_declines_untested_paths(lib, oracle, case, monkeypatch):
     assert err.max() <= 2 * 3e-4 and (err > 1e-6).mean() < 0.02
 
 
+@pytest.mark.parametrize("shape", ["humanoid", "narrow_ragged"])
 @pytest.mark.parametrize("fused", ["1", "0"])
-def test_wide_output_backward_matches_pair(lib, oracle, monkeypatch, fused):
+def test_wide_output_backward_matches_pair(lib, oracle, monkeypatch, fused, shape):
     """The A = 17 policy network's output layer on its one-pass paths — fused = 1 (default): forward, head
     and backward in one launch (policy_out_fused_kernel: μ by exact fp32 MFMA from h staged in LDS, the
     head, grad_x and grad_W / grad_b from the same rows); fused = 0 (PPO_POLICY_FUSED=0): the forward GEMM,
     then the head fused with the one-pass backward (out_bwd_wide_kernel<HEAD>) — against the separate head
     launch + paired GEMM launch (PPO_NO_WIDE_BWD=1) from identical state: one policy minibatch of the
-    humanoid config, μ and every policy gradient within the GEMM tolerance (the same products summed in
-    another order), the log σ gradient and the loss sums within reduction rounding."""
-    sizes, N = CONFIGS["humanoid"]["sizes"], CONFIGS["humanoid"]["N"]
+    humanoid config (and a 256-wide network on a ragged 1000-row minibatch: the last 16-row block partial), μ and
+    every policy gradient within the GEMM tolerance (the same products summed in another order), the log σ
+    gradient and the loss sums within reduction rounding."""
+    if shape == "humanoid":
+        sizes, N = CONFIGS["humanoid"]["sizes"], CONFIGS["humanoid"]["N"]
+    else:
+        sizes, N = [17, 256, 256, 17], 1000
     out = {}
     monkeypatch.setenv("PPO_POLICY_FUSED", fused)
     for mode in ("1", "0"):
