@@ -337,7 +337,8 @@ struct StageX3 {
 // ---------------------------------------------------------------------------------------------
 // ABL (timing ablations, results wrong; PPO_X3_ABLATE, -DPPO_X3_DIAG builds, cfgs 0 and 3): 1 = no
 // MFMAs, 2 = no split / LDS stores, 4 = no epilogue stores, 8 = no global loads after the prologue,
-// 32 = stamps, 64 = no split (raw bits stored to the planes), 128 = every other k-tile barrier skipped
+// 32 = stamps, 64 = no split (raw bits stored to the planes), 128 = every other k-tile barrier skipped,
+// 256 / 512 = no B / A fragment reads after the prologue (stale fragments: the LDS read cost)
 // forward / grad_x epilogue: 32×32 accumulator block (i, j): lane (r, h) holds column r, rows
 // 4h + (e&3) + 8(e>>2).  Branch-free per element: the bias loads hoisted, the ReLU′-bit ballots in a
 // loop version of their own, grad_x's mask words brought into LDS (BM·BN/32 words, free on entry) by
@@ -592,14 +593,17 @@ __device__ __forceinline__ void x3_body(const X3Args& a, int b, int grid) {
     // fragment registers: plane p of the A (fa) and B (fb) operand tiles of the current k-tile
     bf16x8 fa[3][TM][KH], fb[3][TN][KH];
     // (fold: A is a 0/1 mask in plane 0 only — its planes 1, 2 and their three products are skipped)
+    bool first_rd = true;                                          // (ABL 256 / 512: the prologue's reads only)
     auto rd_a = [&](const unsigned short* img, int p) {
         if (syn && p != 0) return;
+        if ((ABL & 512) && !first_rd) return;
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int kh = 0; kh < KH; ++kh) fa[p][i][kh] = SA::frag(img + p * SA::PLANE, wm * WM + i * 32 + r, lane, kh);
     };
     auto rd_b = [&](const unsigned short* img, int p) {
+        if ((ABL & 256) && !first_rd) return;
 #pragma unroll
         for (int j = 0; j < TN; ++j)
 #pragma unroll
@@ -780,6 +784,8 @@ __device__ __forceinline__ void x3_body(const X3Args& a, int b, int grid) {
         if (NK > 2) load_t(SYNc, 2);
         __syncthreads();
         if (NK > 0) { rd_a(cur, 2); rd_b(cur, 0); rd_b(cur, 2); rd_a(cur, 0); }
+        if ((ABL & 768) && NK > 0) { rd_a(cur, 1); rd_b(cur, 1); }
+        first_rd = false;
         if (ABL & 32) stamp(1);
         // steady state: tiles j+2 and j+3 exist and are full.  grad_W's loop is unrolled by the ring
         // length, so every ring slot's fragment / staging addresses are loop-invariant registers (no
@@ -1118,6 +1124,9 @@ void launch_cfg_x3(int c, const X3Args& a) {
             case 32: run(std::integral_constant<int, 32>{}); return;
             case 64: run(std::integral_constant<int, 64>{}); return;
             case 128: run(std::integral_constant<int, 128>{}); return;
+            case 256: run(std::integral_constant<int, 256>{}); return;
+            case 512: run(std::integral_constant<int, 512>{}); return;
+            case 768: run(std::integral_constant<int, 768>{}); return;
             default: break;
         }
     }
